@@ -1,0 +1,253 @@
+"""ORACLE — test infrastructure only. NOT part of the product path.
+
+CPU fp32 restatement of the reference CRNN hot path (sherstpasha/RCNN-OCR),
+written from scratch in functional form so every intermediate is reachable.
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import
+this module, and only as the checker / CPU baseline, never as the thing measured
+or shipped. The HIP product path (rcnn-ocr_amd/crnn_hip) never imports it.
+
+Pinned against tests/golden/*.npz, which were produced by running the reference
+itself (tests/golden/make_goldens.py): eval-mode encode + CTC-head logits,
+train-mode loss + gradients, CTC loss/grad values, greedy-decode strings and a
+4-layer 768-hidden BiLSTM stack.
+
+Citations are /root/reference/<file>:<line>.
+Parameters are a dict keyed by the reference's state_dict names
+(model/model.py:166-213, model/seresnet31.py:70-187) + `ctc_head.{weight,bias}`.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Tuple
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from ctc_oracle import ctc_loss_and_grad  # noqa: E402  (oracle/ on sys.path)
+
+BN_EPS = 1e-5
+BN_MOMENTUM = 0.1
+
+# (layer name, blocks, stride, inplanes, planes) — model/seresnet31.py:92-127
+STAGES = [("layer1", 1, 2, 128, 256), ("layer2", 2, 1, 256, 256),
+          ("layer3", 5, 2, 256, 512), ("layer4", 3, 1, 512, 512)]
+
+
+class Ctx:
+    """train flag + BN running-stat updates + recorded intermediates."""
+
+    def __init__(self, train: bool, record: bool = False):
+        self.train = train
+        self.record = record
+        self.acts: Dict[str, torch.Tensor] = {}
+        self.running: Dict[str, torch.Tensor] = {}
+
+    def rec(self, name, t):
+        if self.record:
+            self.acts[name] = t
+
+
+def batchnorm(x, p, prefix, ctx: Ctx):
+    """nn.BatchNorm2d (torch defaults eps=1e-5, momentum=0.1): train mode normalises
+    with the biased batch variance and folds the unbiased one into running_var."""
+    w, b = p[prefix + ".weight"], p[prefix + ".bias"]
+    if ctx.train:
+        n = x.numel() // x.shape[1]
+        mean = x.mean(dim=(0, 2, 3))
+        var = ((x - mean.view(1, -1, 1, 1)) ** 2).mean(dim=(0, 2, 3))
+        with torch.no_grad():
+            rm = p[prefix + ".running_mean"]
+            rv = p[prefix + ".running_var"]
+            ctx.running[prefix + ".running_mean"] = (1 - BN_MOMENTUM) * rm + BN_MOMENTUM * mean.detach()
+            ctx.running[prefix + ".running_var"] = (1 - BN_MOMENTUM) * rv + BN_MOMENTUM * var.detach() * n / max(1, n - 1)
+    else:
+        mean, var = p[prefix + ".running_mean"], p[prefix + ".running_var"]
+    inv = torch.rsqrt(var + BN_EPS)
+    return (x - mean.view(1, -1, 1, 1)) * (inv * w).view(1, -1, 1, 1) + b.view(1, -1, 1, 1)
+
+
+def se_layer(x, p, prefix):
+    """SELayer.forward, model/seresnet31.py:16-20 (reduction 16, no biases)."""
+    y = x.mean(dim=(2, 3))
+    y = torch.relu(y @ p[prefix + ".fc.0.weight"].t())
+    y = torch.sigmoid(y @ p[prefix + ".fc.2.weight"].t())
+    return x * y[:, :, None, None]
+
+
+def se_block(x, p, prefix, stride, has_ds, ctx):
+    """SEBasicBlock.forward, model/seresnet31.py:55-67 (dropblock = Identity at p=0)."""
+    out = F.conv2d(x, p[prefix + ".conv1.weight"], stride=stride, padding=1)
+    out = torch.relu(batchnorm(out, p, prefix + ".bn1", ctx))
+    out = F.conv2d(out, p[prefix + ".conv2.weight"], stride=1, padding=1)
+    out = batchnorm(out, p, prefix + ".bn2", ctx)
+    out = se_layer(out, p, prefix + ".se")
+    if has_ds:
+        idn = F.conv2d(x, p[prefix + ".downsample.0.weight"], stride=stride)
+        idn = batchnorm(idn, p, prefix + ".downsample.1", ctx)
+    else:
+        idn = x
+    return torch.relu(out + idn)
+
+
+def backbone(x, p, ctx):
+    """SEResNet31.forward, model/seresnet31.py:180-187."""
+    x = F.conv2d(x, p["cnn.conv0.0.weight"], padding=1)
+    x = torch.relu(batchnorm(x, p, "cnn.conv0.1", ctx))
+    x = F.conv2d(x, p["cnn.conv0.3.weight"], padding=1)
+    x = torch.relu(batchnorm(x, p, "cnn.conv0.4", ctx))
+    x = F.max_pool2d(x, 2, 2)
+    ctx.rec("stem", x)
+    for name, blocks, stride, inp, planes in STAGES:
+        for i in range(blocks):
+            s = stride if i == 0 else 1
+            has_ds = i == 0 and (stride != 1 or inp != planes)
+            x = se_block(x, p, f"cnn.{name}.{i}", s, has_ds, ctx)
+        ctx.rec(name, x)
+    # conv_out, model/seresnet31.py:129-136
+    x = F.conv2d(x, p["cnn.conv_out.0.weight"], stride=(2, 1), padding=(0, 1))
+    x = torch.relu(batchnorm(x, p, "cnn.conv_out.1", ctx))
+    x = F.conv2d(x, p["cnn.conv_out.3.weight"], stride=1, padding=0)
+    x = torch.relu(batchnorm(x, p, "cnn.conv_out.4", ctx))
+    ctx.rec("cnn_out", x)
+    return x
+
+
+def lstm_direction(x, w_ih, w_hh, b_ih, b_hh, reverse):
+    """nn.LSTM single direction, gate order i,f,g,o; h0 = c0 = 0.
+    Reverse direction runs over the flipped sequence (model/model.py:152-163)."""
+    B, T, _ = x.shape
+    H = w_hh.shape[1]
+    xg = x @ w_ih.t() + b_ih + b_hh
+    h = x.new_zeros(B, H)
+    c = x.new_zeros(B, H)
+    outs = [None] * T
+    order = range(T - 1, -1, -1) if reverse else range(T)
+    for t in order:
+        g = xg[:, t] + h @ w_hh.t()
+        i, f, gg, o = g.split(H, dim=1)
+        c = torch.sigmoid(f) * c + torch.sigmoid(i) * torch.tanh(gg)
+        h = torch.sigmoid(o) * torch.tanh(c)
+        outs[t] = h
+    return torch.stack(outs, dim=1)
+
+
+def bilstm(x, p, prefix):
+    """BidirectionalLSTM.forward, model/model.py:159-163."""
+    r = prefix + ".rnn."
+    hf = lstm_direction(x, p[r + "weight_ih_l0"], p[r + "weight_hh_l0"], p[r + "bias_ih_l0"],
+                        p[r + "bias_hh_l0"], False)
+    hb = lstm_direction(x, p[r + "weight_ih_l0_reverse"], p[r + "weight_hh_l0_reverse"],
+                        p[r + "bias_ih_l0_reverse"], p[r + "bias_hh_l0_reverse"], True)
+    h = torch.cat([hf, hb], dim=2)
+    return h @ p[prefix + ".linear.weight"].t() + p[prefix + ".linear.bias"]
+
+
+def encode(x, p, ctx, num_rnn_layers=2):
+    """RCNN.encode, model/model.py:215-221 (enc_dropout identity: eval or p=0)."""
+    f = backbone(x, p, ctx)
+    seq = f.mean(dim=2).permute(0, 2, 1)       # AdaptiveAvgPool2d((1,None)) + squeeze + permute
+    ctx.rec("seq", seq)
+    for i in range(num_rnn_layers):
+        seq = bilstm(seq, p, f"enc_rnn.{i}")
+        ctx.rec(f"rnn{i}", seq)
+    return seq
+
+
+def head(enc, p):
+    """CTC head: Linear(H -> num_classes)."""
+    return enc @ p["ctc_head.weight"].t() + p["ctc_head.bias"]
+
+
+class _CTC(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits_btc, targets, lengths, reduction, zero_infinity):
+        loss, grad = ctc_loss_and_grad(logits_btc.detach().double().numpy(), targets.numpy(),
+                                       lengths.numpy(), reduction=reduction,
+                                       zero_infinity=zero_infinity)
+        ctx.save_for_backward(torch.from_numpy(grad).to(logits_btc.dtype))
+        return torch.tensor(loss, dtype=logits_btc.dtype)
+
+    @staticmethod
+    def backward(ctx, go):
+        (g,) = ctx.saved_tensors
+        return g * go, None, None, None, None
+
+
+def ctc_loss(logits_btc, targets, lengths, reduction="mean", zero_infinity=True):
+    """F.ctc_loss(log_softmax(logits), blank=0) restated (numpy, float64)."""
+    return _CTC.apply(logits_btc, targets, lengths, reduction, zero_infinity)
+
+
+def greedy_decode(logits_btc) -> List[List[int]]:
+    """training/utils.py:122-150 semantics with an explicit (B,T,C) layout:
+    argmax over C, drop repeats (prev tracks every t, blank included), drop blank 0."""
+    preds = np.asarray(logits_btc).argmax(axis=2)
+    out = []
+    for row in preds:
+        prev, seq = 0, []
+        for p in row:
+            p = int(p)
+            if p != 0 and p != prev:
+                seq.append(p)
+            prev = p
+        out.append(seq)
+    return out
+
+
+def ids_to_text(seqs, itos):
+    """alphabet[p-1] with alphabet = itos[1:] (training/utils.py:146)."""
+    return ["".join(itos[1:][p - 1] for p in s) for s in seqs]
+
+
+def adamw_step(p, g, m, v, step, lr, beta1=0.9, beta2=0.999, eps=1e-8, wd=1e-2):
+    """torch.optim.AdamW update (training/train.py:294-295 option), numpy float64."""
+    p = p * (1 - lr * wd)
+    m = beta1 * m + (1 - beta1) * g
+    v = beta2 * v + (1 - beta2) * g * g
+    bc1 = 1 - beta1 ** step
+    bc2 = 1 - beta2 ** step
+    denom = np.sqrt(v) / math.sqrt(bc2) + eps
+    p = p - (lr / bc1) * m / denom
+    return p, m, v
+
+
+def param_shapes(hidden: int, num_classes: int, num_rnn_layers: int = 2, enc_dim: int = 512
+                 ) -> List[Tuple[str, Tuple[int, ...]]]:
+    """Ordered (name, shape) of the CTC model's state dict (reference key order)."""
+    out = []
+
+    def conv(n, co, ci, kh, kw):
+        out.append((n + ".weight", (co, ci, kh, kw)))
+
+    def bn(n, c):
+        out.extend([(n + ".weight", (c,)), (n + ".bias", (c,)), (n + ".running_mean", (c,)),
+                    (n + ".running_var", (c,)), (n + ".num_batches_tracked", ())])
+
+    conv("cnn.conv0.0", 64, 3, 3, 3); bn("cnn.conv0.1", 64)
+    conv("cnn.conv0.3", 128, 64, 3, 3); bn("cnn.conv0.4", 128)
+    for name, blocks, stride, inp, planes in STAGES:
+        for i in range(blocks):
+            pre = f"cnn.{name}.{i}"
+            ci = inp if i == 0 else planes
+            conv(pre + ".conv1", planes, ci, 3, 3); bn(pre + ".bn1", planes)
+            conv(pre + ".conv2", planes, planes, 3, 3); bn(pre + ".bn2", planes)
+            out.append((pre + ".se.fc.0.weight", (planes // 16, planes)))
+            out.append((pre + ".se.fc.2.weight", (planes, planes // 16)))
+            if i == 0 and (stride != 1 or inp != planes):
+                conv(pre + ".downsample.0", planes, ci, 1, 1); bn(pre + ".downsample.1", planes)
+    conv("cnn.conv_out.0", 512, 512, 2, 2); bn("cnn.conv_out.1", 512)
+    conv("cnn.conv_out.3", 512, 512, 2, 2); bn("cnn.conv_out.4", 512)
+    for l in range(num_rnn_layers):
+        ind = enc_dim if l == 0 else hidden
+        pre = f"enc_rnn.{l}"
+        for sfx in ["", "_reverse"]:
+            out.append((f"{pre}.rnn.weight_ih_l0{sfx}", (4 * hidden, ind)))
+            out.append((f"{pre}.rnn.weight_hh_l0{sfx}", (4 * hidden, hidden)))
+            out.append((f"{pre}.rnn.bias_ih_l0{sfx}", (4 * hidden,)))
+            out.append((f"{pre}.rnn.bias_hh_l0{sfx}", (4 * hidden,)))
+        out.append((f"{pre}.linear.weight", (hidden, 2 * hidden)))
+        out.append((f"{pre}.linear.bias", (hidden,)))
+    out.append(("ctc_head.weight", (num_classes, hidden)))
+    out.append(("ctc_head.bias", (num_classes,)))
+    return out

@@ -1,0 +1,103 @@
+"""Pin the oracle (oracle/) against the reference-generated goldens (CPU only)."""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import crnn_oracle as O
+from ctc_oracle import ctc_loss_and_grad
+from helpers import case_params, load, pixels_to_images, GOLDEN
+
+torch.set_num_threads(min(8, os.cpu_count() or 1))
+
+
+@pytest.mark.parametrize("case", ["b4_32x128_h256", "b4_32x256_h512", "b2_64x256_h256"])
+def test_oracle_encode_eval(case):
+    z = load(f"encode_eval_{case}.npz")
+    p, hidden = case_params(z)
+    x = pixels_to_images(z["pixels"])
+    ctx = O.Ctx(train=False, record=True)
+    with torch.no_grad():
+        enc = O.encode(x, p, ctx)
+        logits = O.head(enc, p)
+    np.testing.assert_allclose(ctx.acts["cnn_out"].numpy(), z["cnn_out"], rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(enc.numpy(), z["enc"], rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(logits.numpy(), z["logits"], rtol=1e-4, atol=1e-4)
+    assert O.greedy_decode(logits.numpy()) == O.greedy_decode(z["logits"])
+
+
+@pytest.mark.parametrize("case", ["b4_32x128_h256", "b3_32x256_h512"])
+def test_oracle_train_grads(case):
+    z = load(f"train_{case}.npz")
+    p, hidden = case_params(z, with_running=False)
+    p = {k: (v.clone().requires_grad_(True) if v.is_floating_point() and "running" not in k else v)
+         for k, v in p.items()}
+    x = pixels_to_images(z["pixels"])
+    ctx = O.Ctx(train=True)
+    logits = O.head(O.encode(x, p, ctx), p)
+    logits.retain_grad()
+    loss = O.ctc_loss(logits, torch.from_numpy(z["targets"]), torch.from_numpy(z["target_lengths"]))
+    loss.backward()
+    assert abs(float(loss.detach()) - float(z["loss"])) < 1e-4 * max(1.0, abs(float(z["loss"])))
+    np.testing.assert_allclose(logits.grad.numpy(), z["dlogits"], rtol=1e-3, atol=1e-6)
+    for name in z["param_names"]:
+        name = str(name)
+        g = p[name].grad.reshape(-1).double().numpy()
+        ref_norm = float(z["gnorm::" + name])
+        assert abs(np.sqrt((g * g).sum()) - ref_norm) <= 2e-3 * ref_norm + 1e-7, name
+        idx = z["gidx::" + name]
+        ref = z["gval::" + name].astype(np.float64)
+        err = np.linalg.norm(g[idx] - ref) / max(np.linalg.norm(ref), 1e-12)
+        assert err < 2e-3, (name, err)
+    for k, v in ctx.running.items():
+        np.testing.assert_allclose(v.numpy(), z["bnrun::" + k], rtol=1e-4, atol=1e-5)
+
+
+def test_oracle_ctc_cases():
+    z = load("ctc_cases.npz")
+    logits_btc = np.transpose(z["logits"], (1, 0, 2))
+    for red in ["mean", "sum", "none"]:
+        for zi in [True, False]:
+            loss, grad = ctc_loss_and_grad(logits_btc, z["labels"], z["target_lengths"],
+                                           reduction=red, zero_infinity=zi)
+            ref = z[f"loss_{red}_{int(zi)}"]
+            np.testing.assert_allclose(np.asarray(loss, dtype=np.float64), ref, rtol=1e-5, atol=1e-5)
+            refg = z[f"grad_{red}_{int(zi)}"]
+            if np.all(np.isfinite(refg)) and np.all(np.isfinite(np.asarray(loss))):
+                np.testing.assert_allclose(np.transpose(grad, (1, 0, 2)), refg, rtol=1e-4, atol=1e-6)
+    loss, grad = ctc_loss_and_grad(np.transpose(z["big_logits"], (1, 0, 2)), z["big_labels"], z["big_tl"])
+    np.testing.assert_allclose(loss, z["big_loss"], rtol=1e-5)
+    np.testing.assert_allclose(np.transpose(grad, (1, 0, 2)), z["big_grad"], rtol=1e-4, atol=1e-7)
+
+
+def test_oracle_decode(itos):
+    z = load("decode.npz")
+    with open(os.path.join(GOLDEN, "decode.json"), encoding="utf-8") as f:
+        ref = json.load(f)
+    seqs = O.greedy_decode(z["logits"])
+    assert seqs == ref["seqs"]
+    assert O.ids_to_text(seqs, itos) == ref["texts"]
+
+
+def test_oracle_bilstm_stack():
+    z = load("bilstm_stack.npz")
+    from crnn_hip.recipe import recipe_state_dict
+    shapes = []
+    for l in range(4):
+        ind = 512 if l == 0 else 768
+        for sfx in ["", "_reverse"]:
+            shapes += [(f"enc_rnn.{l}.rnn.weight_ih_l0{sfx}", (3072, ind)),
+                       (f"enc_rnn.{l}.rnn.weight_hh_l0{sfx}", (3072, 768)),
+                       (f"enc_rnn.{l}.rnn.bias_ih_l0{sfx}", (3072,)),
+                       (f"enc_rnn.{l}.rnn.bias_hh_l0{sfx}", (3072,))]
+        shapes += [(f"enc_rnn.{l}.linear.weight", (768, 1536)), (f"enc_rnn.{l}.linear.bias", (768,))]
+    p = recipe_state_dict(shapes, int(z["seed"]))
+    x = torch.from_numpy(z["x"]).requires_grad_(True)
+    y = x
+    for l in range(4):
+        y = O.bilstm(y, p, f"enc_rnn.{l}")
+    np.testing.assert_allclose(y.detach().numpy(), z["y"], rtol=1e-4, atol=1e-5)
+    (y * torch.from_numpy(z["proj"])).sum().backward()
+    np.testing.assert_allclose(x.grad.numpy(), z["dx"], rtol=1e-3, atol=1e-5)
