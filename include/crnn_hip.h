@@ -1,0 +1,206 @@
+/*
+ * crnn_hip.h — C ABI of the MI355X-native CRNN hot path (libcrnn_hip.so).
+ *
+ * SE-ResNet31 -> height-collapse -> BiLSTM -> CTC, forward and training step,
+ * as hand-written HIP kernels for gfx950. This is the drop-in boundary: the
+ * Python mirror of the reference API (rcnn-ocr_amd/model/model.py RCNN,
+ * inference.py OCRInference, training/train.py run_training) binds these
+ * entry points with ctypes; see INTEGRATION.md.
+ *
+ * Reference interfaces each group replaces (paths relative to the
+ * sherstpasha/RCNN-OCR checkout):
+ *   crnn_conv_*            nn.Conv2d(bias=False)       model/seresnet31.py:37-45, 82-86, 130-134, 153-154
+ *   crnn_bn_*              nn.BatchNorm2d (+ReLU)      model/seresnet31.py:40-45, 83-88, 131-136, 154
+ *   crnn_maxpool_*         nn.MaxPool2d(2,2)           model/seresnet31.py:88
+ *   crnn_se_*              SELayer + residual + ReLU   model/seresnet31.py:5-20, 55-67
+ *   crnn_hpool_*           AdaptiveAvgPool2d((1,None)) + squeeze + permute   model/model.py:191, 216-218
+ *   crnn_lstm_*            nn.LSTM(bidirectional, batch_first)               model/model.py:152-163
+ *   crnn_gemm_*            nn.Linear (BiLSTM output, CTC head)                model/model.py:157,162
+ *   crnn_ctc_*             F.ctc_loss(blank=0) / ctc_greedy_decoder            training/utils.py:122-162
+ *   crnn_adamw             torch.optim.AdamW step                             training/train.py:294-295
+ *
+ * Conventions
+ *   - dtype: CRNN_F32 (parity mode, exact-f32 MFMA) or CRNN_BF16 (perf mode,
+ *     bf16 MFMA); accumulation is always fp32. Parameters, BN statistics,
+ *     LSTM cell state, logits and CTC are fp32 in both modes.
+ *   - Activations are NHWC ([B][H][W][C]); channel counts are multiples of 8.
+ *   - Every buffer is allocated by the caller (device pointers); the library
+ *     never allocates. `stream` is a hipStream_t passed as void*.
+ *   - No host synchronisation inside any call: every entry point is safe to
+ *     capture into a hipGraph.
+ *   - Return value: 0 on success, else a hipError_t-compatible code;
+ *     crnn_last_error_string() describes the last failure (thread-local).
+ */
+#ifndef CRNN_HIP_H
+#define CRNN_HIP_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CRNN_F32 0
+#define CRNN_BF16 1
+
+int crnn_version(void);
+const char* crnn_last_error_string(void);
+
+/* ------------------------------------------------------------------ layout */
+/* fp32 NCHW image batch -> dtype NHWC with channels zero-padded to Cp. */
+int crnn_nchw_to_nhwc(int dtype, const float* x, void* y, int B, int C, int H, int W, int Cp, void* stream);
+/* fp32 -> dtype cast of n contiguous elements. */
+int crnn_cast_f32(int dtype, const float* src, void* dst, long n, void* stream);
+/* conv weight OIHW fp32 -> OHWI dtype with Ci zero-padded to Cip. */
+int crnn_pack_conv_weight(int dtype, const float* w, void* out, int Co, int Ci, int KH, int KW, int Cip, void* stream);
+/* row gather + cast: out[r][c] = src[perm[r]][c] (perm == NULL: identity), rows >= rows_src are zero.
+ * Used for LSTM gate interleave (row 4*j+gate <- gate*H+j) and padded heads. */
+int crnn_pack_rows(int dtype, const float* src, void* out, const int* perm, int rows_out, int rows_src, int cols, void* stream);
+
+/* ------------------------------------------------------------------ conv */
+typedef struct {
+  int B, Hi, Wi, Ci; /* Ci: stored (padded) input channels */
+  int Ho, Wo, Co;
+  int KH, KW, sh, sw, ph, pw;
+  int Ci_real; /* true input channels (<= Ci); 0 means Ci */
+} crnn_conv_desc;
+
+/* y[B][Ho][Wo][Co] = conv(x[B][Hi][Wi][Ci], w[Co][KH][KW][Ci]).
+ * psum/psq (may be NULL): per-channel partial statistics of y from the fp32 accumulators,
+ * [crnn_conv_stat_rows(d)][Co]: psum = sum, psq = sum of squared deviations from the
+ * partial's own mean, each partial covering crnn_conv_stat_rows_per_partial(d) rows;
+ * consumed by crnn_bn_finalize. */
+int crnn_conv_fwd(int dtype, const crnn_conv_desc* d, const void* x, const void* w, void* y, float* psum, float* psq, void* stream);
+int crnn_conv_stat_rows(const crnn_conv_desc* d);
+int crnn_conv_stat_rows_per_partial(const crnn_conv_desc* d);
+/* dx[B][Hi][Wi][Ci] = dgrad(dy) (+= dx if accumulate) (+ dres*(yres>0) if dres != NULL). */
+int crnn_conv_dgrad(int dtype, const crnn_conv_desc* d, const void* dy, const void* w, void* dx, const void* dres, const void* yres, int accumulate, void* stream);
+/* dw_oihw (fp32, reference layout) = beta*dw + wgrad(dy, x); ws = split-K slabs. */
+int crnn_conv_wgrad(int dtype, const crnn_conv_desc* d, const void* dy, const void* x, float* dw_oihw, float* ws, size_t ws_bytes, float beta, void* stream);
+size_t crnn_conv_wgrad_workspace(const crnn_conv_desc* d);
+void crnn_conv_fwd_tile(const crnn_conv_desc* d, int* bm, int* bn);
+void crnn_conv_wgrad_plan(const crnn_conv_desc* d, int* bm, int* bn, int* splits);
+
+/* ------------------------------------------------------------------ batchnorm */
+/* Combine (sum, M2) partials (Chan, in double) -> per-channel affine (scale = gamma*invstd,
+ * shift = beta - mean*scale). train: batch statistics over `count` rows, partial r covering rows
+ * [r*rows_per_partial, ...) (biased var to normalise, unbiased into running_var, momentum
+ * update); eval: running statistics. mean/invstd saved for backward. */
+int crnn_bn_finalize(const float* psum, const float* psq, int rows, long rows_per_partial, int C, long count,
+                     const float* gamma, const float* beta,
+                     float* running_mean, float* running_var, float momentum, float eps, int train,
+                     float* mean, float* invstd, float* scale, float* shift, void* stream);
+/* per-channel (sum, M2) partials of an NHWC tensor [M][C] (for tensors not produced by a conv);
+ * partial r covers ceil(M/rows) rows. */
+int crnn_channel_stats(int dtype, const void* x, long M, int C, float* psum, float* psq, int rows, void* stream);
+/* y = act(z*scale + shift), act = ReLU if relu. */
+int crnn_bn_act(int dtype, const void* z, const float* scale, const float* shift, void* y, long M, int C, int relu, void* stream);
+/* y = maxpool2x2(relu(z*scale+shift)), z [B][H][W][C] -> y [B][H/2][W/2][C]. */
+int crnn_bn_relu_maxpool(int dtype, const void* z, const float* scale, const float* shift, void* y, int B, int H, int W, int C, void* stream);
+/* dy_full[B][H][W][C] = gradient routed to the first max of each 2x2 window of relu(z*scale+shift). */
+int crnn_maxpool_bwd(int dtype, const void* z, const float* scale, const float* shift, const void* dpool, void* dy_full, int B, int H, int W, int C, void* stream);
+
+#define CRNN_BNG_PLAIN 0 /* g = dy                                   */
+#define CRNN_BNG_RELU 1  /* g = dy * (z*scale+shift > 0)             */
+#define CRNN_BNG_RESID 2 /* g = dy * (y > 0)                         */
+#define CRNN_BNG_SE 3    /* g = dy * (y > 0) * s[b][c] + dpool[b][c] */
+typedef struct {
+  const void* dy;
+  const void* z;
+  const float* mean;
+  const float* invstd;
+  const float* scale;
+  const float* shift;
+  const void* y;      /* RESID / SE */
+  const float* s;     /* SE: [B][C] */
+  const float* dpool; /* SE: [B][C], already divided by HW */
+  int mode;
+  long M; /* rows = B*HW */
+  int C;
+  int HW;
+} crnn_bn_bwd_desc;
+/* partials of sum(g), sum(g*xhat) -> [rows][C] each */
+int crnn_bn_bwd_reduce(int dtype, const crnn_bn_bwd_desc* d, float* pg, float* pgx, int rows, void* stream);
+/* -> dgamma, dbeta (written, or added if accumulate), mean_g = sum(g)/count, mean_gx = sum(g xhat)/count */
+int crnn_bn_bwd_finalize(const float* pg, const float* pgx, int rows, int C, long count, float* dgamma, float* dbeta,
+                         float* mean_g, float* mean_gx, int accumulate, void* stream);
+/* dz = scale * (g - mean_g - xhat*mean_gx) */
+int crnn_bn_bwd_apply(int dtype, const crnn_bn_bwd_desc* d, const float* mean_g, const float* mean_gx, void* dz, void* stream);
+int crnn_bn_rows(long M); /* partial rows used by the reduce kernels for M */
+
+/* ------------------------------------------------------------------ SE + residual */
+/* pooled[b][c] = mean_hw(z2*scale+shift) */
+int crnn_se_pool(int dtype, const void* z2, const float* scale, const float* shift, float* pooled, int B, int HW, int C, void* stream);
+/* hid = relu(pooled W1^T) [B][Cr]; s = sigmoid(hid W2^T) [B][C] (fp32; W1 [Cr][C], W2 [C][Cr]) */
+int crnn_se_mlp_fwd(const float* pooled, const float* w1, const float* w2, float* hid, float* s, int B, int C, int Cr, void* stream);
+/* y = relu((z2*scale+shift)*s[b][c] + idn'), idn' = idn*iscale+ishift if iscale else idn */
+int crnn_se_residual_fwd(int dtype, const void* z2, const float* scale, const float* shift, const float* s,
+                         const void* idn, const float* iscale, const float* ishift, void* y, int B, int HW, int C, void* stream);
+/* ds[b][c] = sum_hw dy*(y>0)*(z2*scale+shift) */
+int crnn_se_bwd_reduce(int dtype, const void* dy, const void* y, const void* z2, const float* scale, const float* shift,
+                       float* ds, int B, int HW, int C, void* stream);
+/* SE MLP backward: dsig, dhid (work [B][C] and [B][Cr]), dpool = W1^T dhid / HW; dw1/dw2 (fp32, written) */
+int crnn_se_mlp_bwd(const float* ds, const float* pooled, const float* hid, const float* s, const float* w1, const float* w2,
+                    float* dsig, float* dhid, float* dpool, float* dw1, float* dw2, int B, int C, int Cr, int HW, void* stream);
+
+/* ------------------------------------------------------------------ height collapse */
+/* seq[b][w][c] = mean_h relu(z*scale+shift), z [B][Hh][W][C] */
+int crnn_hpool_fwd(int dtype, const void* z, const float* scale, const float* shift, void* seq, int B, int Hh, int W, int C, void* stream);
+/* dy_full[b][h][w][c] = dseq[b][w][c] / Hh */
+int crnn_hpool_bwd(int dtype, const void* dseq, void* dy_full, int B, int Hh, int W, int C, void* stream);
+
+/* ------------------------------------------------------------------ GEMM (linear layers) */
+/* C[M][N] (ldc) = A[M][K] (lda) . B[N][K]^T (ldb) (+ bias[N]) (+= C if accumulate); C is fp32 if c_f32 else dtype */
+int crnn_gemm_nt(int dtype, const void* A, int lda, const void* B, int ldb, void* C, int ldc, const float* bias,
+                 int M, int N, int K, int c_f32, int accumulate, void* stream);
+/* C[M][N] = A[M][K] . B[K][N] (ldb), N multiple of 8 */
+int crnn_gemm_nn(int dtype, const void* A, int lda, const void* B, int ldb, void* C, int ldc,
+                 int M, int N, int K, int c_f32, int accumulate, void* stream);
+/* C[M][N] fp32 (+)= A[K][M]^T . B[K][N]  (weight gradients; M, N multiples of 8) */
+int crnn_gemm_tn(int dtype, const void* A, int lda, const void* B, int ldb, float* C, int ldc,
+                 int M, int N, int K, int accumulate, void* stream);
+/* out[n] (+)= sum_m X[m][n]  (bias gradients), X dtype or fp32 */
+int crnn_colsum(int dtype, const void* X, int ld, long M, int N, float* out, int accumulate, int x_f32, void* stream);
+
+/* ------------------------------------------------------------------ BiLSTM */
+/* Gate-interleaved ("packed") layout: packed row 4*j+q <-> reference row q*H+j (q = i,f,g,o).
+ * xg   [B][T][2][4H]  x W_ih'^T + b_ih' + b_hh' (dtype)
+ * whh  [2][4H][H]     packed W_hh (dtype)
+ * hseq [B][T][2H]     outputs, forward dir in [0,H), reverse dir in [H,2H) (dtype)
+ * gsv  [2][T][B][4H]  saved post-activation gates (dtype); csv [2][T][B][H] saved cell state (fp32) */
+int crnn_lstm_step_fwd(int dtype, const void* xg, const void* whh, void* hseq, void* gsv, float* csv, int B, int T, int H, int step, void* stream);
+/* BPTT. dgates [2][T][B][4H] (dtype, pre-activation gate grads), dc [2][B][H] fp32 running cell grad.
+ * step 0 initialises (dh_rec = 0, dc = 0); step s>0 runs dh_rec = dgates(step s-1) . W_hh with the
+ * cell backward of step s fused into the GEMM epilogue. */
+int crnn_lstm_step_bwd(int dtype, const void* dhseq, const void* whh, const void* gsv, const float* csv, void* dgates,
+                       float* dc, int B, int T, int H, int step, void* stream);
+/* dW_hh (reference row order, fp32 [2][4H][H]) (+)= sum_t dgates_t^T h_{t-1} */
+int crnn_lstm_dwhh(int dtype, const void* dgates, const void* hseq, float* dwhh, int B, int T, int H, int accumulate, void* stream);
+/* dW_ih (reference row order, fp32 [2][4H][In]) (+)= sum dgates^T x ; x [B][T][In] */
+int crnn_lstm_dwih(int dtype, const void* dgates, const void* x, float* dwih, int B, int T, int H, int In, int accumulate, void* stream);
+/* db (reference order, fp32 [2][4H]) (+)= sum_{t,b} dgates */
+int crnn_lstm_dbias(int dtype, const void* dgates, float* db, int B, int T, int H, int accumulate, void* stream);
+/* dx [B][T][In] (dtype) = sum_dir dgates . W_ih'  (wih packed [2][4H][In]) */
+int crnn_lstm_dx(int dtype, const void* dgates, const void* wih, void* dx, int B, int T, int H, int In, void* stream);
+
+/* ------------------------------------------------------------------ CTC */
+/* Per-sample log-space CTC over logits [B][T][ldc] (fp32, C classes, blank = 0, input length T).
+ * loss[b] = -log p(target_b); dlogits (may be NULL) = grad of the 'mean' reduction
+ * (mean_b loss_b/len_b) wrt logits, with zero_infinity semantics if zero_inf. */
+int crnn_ctc_loss(const float* logits, int ldc, int B, int T, int C, const int* targets, int Lmax, const int* lengths,
+                  float* loss, float* dlogits, int zero_inf, void* stream);
+/* mean_b(loss_b / max(len_b,1)) -> out[0] */
+int crnn_ctc_reduce_mean(const float* loss, const int* lengths, int B, float* out, void* stream);
+/* greedy decode (training/utils.py:122-150 semantics, explicit [B][T] layout):
+ * ids [B][T] collapsed labels (blank & repeats removed), lens [B] */
+int crnn_ctc_greedy(const float* logits, int ldc, int B, int T, int C, int* ids, int* lens, void* stream);
+
+/* ------------------------------------------------------------------ optimiser */
+/* fused AdamW over a flat fp32 buffer; g is multiplied by grad_scale first (DP averaging). */
+int crnn_adamw(float* p, const float* g, float* m, float* v, long n, float lr, float beta1, float beta2, float eps,
+               float weight_decay, int step, float grad_scale, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CRNN_HIP_H */

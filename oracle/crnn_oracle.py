@@ -45,6 +45,8 @@ class Ctx:
 
     def rec(self, name, t):
         if self.record:
+            if t.requires_grad:
+                t.retain_grad()
             self.acts[name] = t
 
 
@@ -103,6 +105,7 @@ def backbone(x, p, ctx):
             s = stride if i == 0 else 1
             has_ds = i == 0 and (stride != 1 or inp != planes)
             x = se_block(x, p, f"cnn.{name}.{i}", s, has_ds, ctx)
+            ctx.rec(f"{name}.{i}", x)
         ctx.rec(name, x)
     # conv_out, model/seresnet31.py:129-136
     x = F.conv2d(x, p["cnn.conv_out.0.weight"], stride=(2, 1), padding=(0, 1))

@@ -1,0 +1,150 @@
+"""ctypes binding of libcrnn_hip.so (include/crnn_hip.h).
+
+The product path is the HIP library; there is no CPU or eager-PyTorch fallback.
+If the shared object is missing or fails to load, every op raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.dirname(HERE)
+LIB_PATH = os.path.join(HERE, "libcrnn_hip.so")
+CSRC = os.path.join(PKG, "csrc")
+
+F32, BF16 = 0, 1
+
+vp = C.c_void_p
+i32 = C.c_int
+i64 = C.c_long
+f32 = C.c_float
+sz = C.c_size_t
+
+
+class ConvDesc(C.Structure):
+    _fields_ = [(n, C.c_int) for n in
+                ("B", "Hi", "Wi", "Ci", "Ho", "Wo", "Co", "KH", "KW", "sh", "sw", "ph", "pw", "Ci_real")]
+
+
+class BnBwdDesc(C.Structure):
+    _fields_ = [("dy", vp), ("z", vp), ("mean", vp), ("invstd", vp), ("scale", vp), ("shift", vp),
+                ("y", vp), ("s", vp), ("dpool", vp), ("mode", C.c_int), ("M", C.c_long),
+                ("C", C.c_int), ("HW", C.c_int)]
+
+
+_SIGS = {
+    "crnn_version": ([], i32),
+    "crnn_last_error_string": ([], C.c_char_p),
+    "crnn_nchw_to_nhwc": ([i32, vp, vp, i32, i32, i32, i32, i32, vp], i32),
+    "crnn_cast_f32": ([i32, vp, vp, i64, vp], i32),
+    "crnn_pack_conv_weight": ([i32, vp, vp, i32, i32, i32, i32, i32, vp], i32),
+    "crnn_pack_rows": ([i32, vp, vp, vp, i32, i32, i32, vp], i32),
+    "crnn_conv_fwd": ([i32, C.POINTER(ConvDesc), vp, vp, vp, vp, vp, vp], i32),
+    "crnn_conv_stat_rows": ([C.POINTER(ConvDesc)], i32),
+    "crnn_conv_stat_rows_per_partial": ([C.POINTER(ConvDesc)], i32),
+    "crnn_conv_dgrad": ([i32, C.POINTER(ConvDesc), vp, vp, vp, vp, vp, i32, vp], i32),
+    "crnn_conv_wgrad": ([i32, C.POINTER(ConvDesc), vp, vp, vp, vp, sz, f32, vp], i32),
+    "crnn_conv_wgrad_workspace": ([C.POINTER(ConvDesc)], sz),
+    "crnn_bn_finalize": ([vp, vp, i32, i64, i32, i64, vp, vp, vp, vp, f32, f32, i32, vp, vp, vp, vp, vp], i32),
+    "crnn_channel_stats": ([i32, vp, i64, i32, vp, vp, i32, vp], i32),
+    "crnn_bn_act": ([i32, vp, vp, vp, vp, i64, i32, i32, vp], i32),
+    "crnn_bn_relu_maxpool": ([i32, vp, vp, vp, vp, i32, i32, i32, i32, vp], i32),
+    "crnn_maxpool_bwd": ([i32, vp, vp, vp, vp, vp, i32, i32, i32, i32, vp], i32),
+    "crnn_bn_bwd_reduce": ([i32, C.POINTER(BnBwdDesc), vp, vp, i32, vp], i32),
+    "crnn_bn_bwd_finalize": ([vp, vp, i32, i32, i64, vp, vp, vp, vp, i32, vp], i32),
+    "crnn_bn_bwd_apply": ([i32, C.POINTER(BnBwdDesc), vp, vp, vp, vp], i32),
+    "crnn_bn_rows": ([i64], i32),
+    "crnn_se_pool": ([i32, vp, vp, vp, vp, i32, i32, i32, vp], i32),
+    "crnn_se_mlp_fwd": ([vp, vp, vp, vp, vp, i32, i32, i32, vp], i32),
+    "crnn_se_residual_fwd": ([i32, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, vp], i32),
+    "crnn_se_bwd_reduce": ([i32, vp, vp, vp, vp, vp, vp, i32, i32, i32, vp], i32),
+    "crnn_se_mlp_bwd": ([vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, vp], i32),
+    "crnn_hpool_fwd": ([i32, vp, vp, vp, vp, i32, i32, i32, i32, vp], i32),
+    "crnn_hpool_bwd": ([i32, vp, vp, i32, i32, i32, i32, vp], i32),
+    "crnn_gemm_nt": ([i32, vp, i32, vp, i32, vp, i32, vp, i32, i32, i32, i32, i32, vp], i32),
+    "crnn_gemm_nn": ([i32, vp, i32, vp, i32, vp, i32, i32, i32, i32, i32, i32, vp], i32),
+    "crnn_gemm_tn": ([i32, vp, i32, vp, i32, vp, i32, i32, i32, i32, i32, vp], i32),
+    "crnn_colsum": ([i32, vp, i32, i64, i32, vp, i32, i32, vp], i32),
+    "crnn_lstm_step_fwd": ([i32, vp, vp, vp, vp, vp, i32, i32, i32, i32, vp], i32),
+    "crnn_lstm_step_bwd": ([i32, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, vp], i32),
+    "crnn_lstm_dwhh": ([i32, vp, vp, vp, i32, i32, i32, i32, vp], i32),
+    "crnn_lstm_dwih": ([i32, vp, vp, vp, i32, i32, i32, i32, i32, vp], i32),
+    "crnn_lstm_dbias": ([i32, vp, vp, i32, i32, i32, i32, vp], i32),
+    "crnn_lstm_dx": ([i32, vp, vp, vp, i32, i32, i32, i32, vp], i32),
+    "crnn_ctc_loss": ([vp, i32, i32, i32, i32, vp, i32, vp, vp, vp, i32, vp], i32),
+    "crnn_ctc_reduce_mean": ([vp, vp, i32, vp, vp], i32),
+    "crnn_ctc_greedy": ([vp, i32, i32, i32, i32, vp, vp, vp], i32),
+    "crnn_adamw": ([vp, vp, vp, vp, i64, f32, f32, f32, f32, f32, i32, f32, vp], i32),
+}
+
+_lib = None
+
+
+def build(force: bool = False, jobs: int = 8) -> str:
+    """Compile libcrnn_hip.so for gfx950 with hipcc (in-tree)."""
+    if force or not os.path.exists(LIB_PATH):
+        subprocess.run(["make", "-C", CSRC, f"-j{jobs}"], check=True)
+    else:
+        subprocess.run(["make", "-C", CSRC, f"-j{jobs}", "-q"], check=False)
+        r = subprocess.run(["make", "-C", CSRC, "-q"], check=False)
+        if r.returncode != 0:
+            subprocess.run(["make", "-C", CSRC, f"-j{jobs}"], check=True)
+    return LIB_PATH
+
+
+def lib():
+    """Load (once) and return the ctypes handle. Raises if the library is missing."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"libcrnn_hip.so not built ({LIB_PATH}); run crnn_hip._lib.build() "
+                               "or `make -C rcnn-ocr_amd/csrc`")
+        h = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+        for name, (args, res) in _SIGS.items():
+            fn = getattr(h, name)
+            fn.argtypes = args
+            fn.restype = res
+        _lib = h
+    return _lib
+
+
+def exported_symbols():
+    return list(_SIGS.keys())
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = lib().crnn_last_error_string()
+        raise RuntimeError(f"{what} failed (hip error {rc}): {msg.decode() if msg else ''}")
+
+
+def call(name: str, *args):
+    rc = getattr(lib(), name)(*args)
+    check(rc, name)
+
+
+def stream_ptr(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def ptr(t) -> int:
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def dtype_code(dt: torch.dtype) -> int:
+    if dt == torch.bfloat16:
+        return BF16
+    if dt == torch.float32:
+        return F32
+    raise ValueError(f"unsupported compute dtype {dt}")
+
+
+def require_device(t: torch.Tensor):
+    if not t.is_cuda:
+        raise RuntimeError("crnn_hip ops run only on a HIP device (no CPU fallback); got a CPU tensor")

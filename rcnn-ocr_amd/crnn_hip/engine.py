@@ -1,0 +1,620 @@
+"""CRNN hot-path engine: forward / backward of SE-ResNet31 -> BiLSTM -> CTC head
+over libcrnn_hip.so. PyTorch supplies device memory and the stream only.
+
+Reference path (sherstpasha/RCNN-OCR):
+  SEResNet31.forward          model/seresnet31.py:180-187
+  SEBasicBlock.forward        model/seresnet31.py:55-67
+  RCNN.encode                 model/model.py:215-221
+  BidirectionalLSTM.forward   model/model.py:159-163
+  + CTC head Linear(H -> C)
+
+Data layout in HBM (all activations NHWC, compute dtype T = bf16 | fp32):
+  input crop  [B][H][W][8]   (3 channels zero-padded to 8)
+  conv output z (pre-BN)     saved for BN backward; BN+ReLU outputs are
+                             recomputed from z wherever a kernel can fuse it
+  sequence    [B][T][512]    == conv_out output [B][1][T][512] (no permute)
+  LSTM        xg [B][T][2][4H], hseq [B][T][2H], gates [2][T][B][4H], c [2][T][B][H] fp32
+  logits      [B*T][Cpad] fp32 (Cpad = C rounded up to 8, zero columns)
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Tuple
+
+import torch
+
+from . import _lib as L
+from ._lib import BnBwdDesc, ConvDesc, call, ptr
+
+BN_EPS = 1e-5
+BN_MOMENTUM = 0.1
+
+# (stage, blocks, stride, inplanes, planes) — model/seresnet31.py:92-127
+STAGES = [("layer1", 1, 2, 128, 256), ("layer2", 2, 1, 256, 256),
+          ("layer3", 5, 2, 256, 512), ("layer4", 3, 1, 512, 512)]
+
+
+def round8(n: int) -> int:
+    return (n + 7) // 8 * 8
+
+
+@dataclass
+class ConvSpec:
+    name: str          # weight key
+    bn: str            # BN prefix
+    ci: int            # stored input channels
+    ci_real: int
+    co: int
+    kh: int
+    kw: int
+    sh: int
+    sw: int
+    ph: int
+    pw: int
+
+    def out_hw(self, h, w):
+        return (h + 2 * self.ph - self.kh) // self.sh + 1, (w + 2 * self.pw - self.kw) // self.sw + 1
+
+    def desc(self, b, h, w) -> ConvDesc:
+        ho, wo = self.out_hw(h, w)
+        return ConvDesc(b, h, w, self.ci, ho, wo, self.co, self.kh, self.kw, self.sh, self.sw,
+                        self.ph, self.pw, self.ci_real)
+
+
+@dataclass
+class BlockSpec:
+    prefix: str
+    conv1: ConvSpec
+    conv2: ConvSpec
+    ds: Optional[ConvSpec]
+    planes: int
+
+
+def backbone_specs():
+    stem0 = ConvSpec("cnn.conv0.0.weight", "cnn.conv0.1", 8, 3, 64, 3, 3, 1, 1, 1, 1)
+    stem1 = ConvSpec("cnn.conv0.3.weight", "cnn.conv0.4", 64, 64, 128, 3, 3, 1, 1, 1, 1)
+    blocks: List[BlockSpec] = []
+    for name, nblk, stride, inp, planes in STAGES:
+        for i in range(nblk):
+            s = stride if i == 0 else 1
+            ci = inp if i == 0 else planes
+            pre = f"cnn.{name}.{i}"
+            c1 = ConvSpec(pre + ".conv1.weight", pre + ".bn1", ci, ci, planes, 3, 3, s, s, 1, 1)
+            c2 = ConvSpec(pre + ".conv2.weight", pre + ".bn2", planes, planes, planes, 3, 3, 1, 1, 1, 1)
+            ds = None
+            if i == 0 and (stride != 1 or inp != planes):
+                ds = ConvSpec(pre + ".downsample.0.weight", pre + ".downsample.1", ci, ci, planes, 1, 1,
+                              s, s, 0, 0)
+            blocks.append(BlockSpec(pre, c1, c2, ds, planes))
+    co0 = ConvSpec("cnn.conv_out.0.weight", "cnn.conv_out.1", 512, 512, 512, 2, 2, 2, 1, 0, 1)
+    co1 = ConvSpec("cnn.conv_out.3.weight", "cnn.conv_out.4", 512, 512, 512, 2, 2, 1, 1, 0, 0)
+    return stem0, stem1, blocks, co0, co1
+
+
+def gate_perm(H: int) -> List[int]:
+    """packed row 4j+q <- reference row q*H+j (i,f,g,o interleaved per unit)."""
+    return [q * H + j for j in range(H) for q in range(4)]
+
+
+class Workspace:
+    """Named device buffers, (re)allocated only when a shape changes: a step
+    at a fixed batch geometry allocates nothing (hipGraph-capturable)."""
+
+    def __init__(self, device):
+        self.device = device
+        self.bufs: Dict[str, torch.Tensor] = {}
+
+    def get(self, name, shape, dtype) -> torch.Tensor:
+        shape = tuple(int(s) for s in shape)
+        t = self.bufs.get(name)
+        if t is None or t.shape != shape or t.dtype != dtype:
+            t = torch.empty(shape, dtype=dtype, device=self.device)
+            self.bufs[name] = t
+        return t
+
+    def nbytes(self):
+        return sum(t.numel() * t.element_size() for t in self.bufs.values())
+
+
+class CRNNEngine:
+    def __init__(self, params: Dict[str, torch.Tensor], buffers: Dict[str, torch.Tensor], hidden: int,
+                 num_classes: int, num_rnn_layers: int = 2, dtype: torch.dtype = torch.bfloat16,
+                 enc_dim: int = 512, version_source=None):
+        self.p = params
+        self.buf = buffers
+        self.H = hidden
+        self.C = num_classes
+        self.Cpad = round8(num_classes)
+        self.nl = num_rnn_layers
+        self.enc_dim = enc_dim
+        self.dtype = dtype
+        self.dt = L.dtype_code(dtype)
+        any_p = next(iter(params.values()))
+        self.device = any_p.device
+        L.require_device(any_p)
+        L.lib()
+        self.stem0, self.stem1, self.blocks, self.co0, self.co1 = backbone_specs()
+        self.ws = Workspace(self.device)
+        self.packed: Dict[str, torch.Tensor] = {}
+        self.perm = torch.tensor(gate_perm(hidden), dtype=torch.int32, device=self.device)
+        self.packed_version = None
+        self.version = 0
+        # in-place edits of the parameters (torch optimizers, load_state_dict) bump the
+        # flat buffer's version counter; kernel-side updates call mark_params_changed()
+        self.version_source = version_source
+        self._saved = None
+        self.debug = False      # when set, backward keeps copies of block-boundary gradients
+        self.dbg: Dict[str, torch.Tensor] = {}
+
+    # ------------------------------------------------------------------ weights
+    def mark_params_changed(self):
+        self.version += 1
+
+    def convs(self):
+        yield self.stem0
+        yield self.stem1
+        for b in self.blocks:
+            yield b.conv1
+            yield b.conv2
+            if b.ds is not None:
+                yield b.ds
+        yield self.co0
+        yield self.co1
+
+    def pack(self):
+        """fp32 reference-layout parameters -> compute-dtype kernel layouts."""
+        ver = (self.version, self.version_source() if self.version_source is not None else 0)
+        if self.packed_version == ver:
+            return
+        s = L.stream_ptr()
+        dt, T = self.dt, self.dtype
+        for cs in self.convs():
+            w = self.p[cs.name]
+            out = self.packed.get(cs.name)
+            if out is None:
+                out = torch.empty((cs.co, cs.kh, cs.kw, cs.ci), dtype=T, device=self.device)
+                self.packed[cs.name] = out
+            call("crnn_pack_conv_weight", dt, ptr(w), ptr(out), cs.co, cs.ci_real, cs.kh, cs.kw, cs.ci, s)
+        H = self.H
+        for l in range(self.nl):
+            pre = f"enc_rnn.{l}"
+            ind = self.enc_dim if l == 0 else H
+            wih = self._pbuf(pre + ".wih", (2, 4 * H, ind), T)
+            whh = self._pbuf(pre + ".whh", (2, 4 * H, H), T)
+            bias = self._pbuf(pre + ".bias", (2, 4 * H), torch.float32)
+            for d, sfx in enumerate(["", "_reverse"]):
+                r = pre + ".rnn."
+                call("crnn_pack_rows", dt, ptr(self.p[r + "weight_ih_l0" + sfx]), ptr(wih[d]), ptr(self.perm),
+                     4 * H, 4 * H, ind, s)
+                call("crnn_pack_rows", dt, ptr(self.p[r + "weight_hh_l0" + sfx]), ptr(whh[d]), ptr(self.perm),
+                     4 * H, 4 * H, H, s)
+                bsum = self.p[r + "bias_ih_l0" + sfx] + self.p[r + "bias_hh_l0" + sfx]
+                call("crnn_pack_rows", L.F32, ptr(bsum), ptr(bias[d]), ptr(self.perm), 4 * H, 4 * H, 1, s)
+            lw = self._pbuf(pre + ".lin", (H, 2 * H), T)
+            call("crnn_cast_f32", dt, ptr(self.p[pre + ".linear.weight"]), ptr(lw), H * 2 * H, s)
+        hw = self._pbuf("head.w", (self.Cpad, H), T)
+        call("crnn_pack_rows", dt, ptr(self.p["ctc_head.weight"]), ptr(hw), None, self.Cpad, self.C, H, s)
+        hb = self._pbuf("head.b", (self.Cpad,), torch.float32, zero=True)
+        hb[: self.C].copy_(self.p["ctc_head.bias"])
+        self.packed_version = ver
+
+    def _pbuf(self, name, shape, dtype, zero=False):
+        t = self.packed.get(name)
+        if t is None:
+            t = (torch.zeros if zero else torch.empty)(shape, dtype=dtype, device=self.device)
+            self.packed[name] = t
+        return t
+
+    # ------------------------------------------------------------------ helpers
+    def _bn_finalize(self, prefix, psum, psq, rows, count, train, tag, rpp=1):
+        C = psum.shape[-1] if psum is not None else self.p[prefix + ".weight"].numel()
+        ws = self.ws
+        mean = ws.get(tag + ".mean", (C,), torch.float32)
+        inv = ws.get(tag + ".inv", (C,), torch.float32)
+        sc = ws.get(tag + ".scale", (C,), torch.float32)
+        sh = ws.get(tag + ".shift", (C,), torch.float32)
+        rm = self.buf[prefix + ".running_mean"]
+        rv = self.buf[prefix + ".running_var"]
+        call("crnn_bn_finalize", ptr(psum) if train else None, ptr(psq) if train else None, rows, rpp, C, count,
+             ptr(self.p[prefix + ".weight"]), ptr(self.p[prefix + ".bias"]),
+             ptr(rm), ptr(rv), BN_MOMENTUM if self.update_running else 0.0, BN_EPS, 1 if train else 0,
+             ptr(mean), ptr(inv), ptr(sc), ptr(sh), L.stream_ptr())
+        if train and self.update_running:
+            nbt = self.buf.get(prefix + ".num_batches_tracked")
+            if nbt is not None:
+                nbt.add_(1)
+        return mean, inv, sc, sh
+
+    def _conv_bn(self, cs: ConvSpec, x, b, h, w, train, tag):
+        """z = conv(x); BN statistics (train) or running stats (eval) -> (z, mean, inv, scale, shift, ho, wo)."""
+        d = cs.desc(b, h, w)
+        ho, wo = d.Ho, d.Wo
+        z = self.ws.get(tag + ".z", (b, ho, wo, cs.co), self.dtype)
+        s = L.stream_ptr()
+        if train:
+            rows = L.lib().crnn_conv_stat_rows(d)
+            psum = self.ws.get("stat.sum", (self._stat_cap,), torch.float32)[: rows * cs.co].view(rows, cs.co)
+            psq = self.ws.get("stat.sq", (self._stat_cap,), torch.float32)[: rows * cs.co].view(rows, cs.co)
+            call("crnn_conv_fwd", self.dt, d, ptr(x), ptr(self.packed[cs.name]), ptr(z), ptr(psum), ptr(psq), s)
+            rpp = L.lib().crnn_conv_stat_rows_per_partial(d)
+            stats = self._bn_finalize(cs.bn, psum, psq, rows, b * ho * wo, True, tag, rpp)
+        else:
+            call("crnn_conv_fwd", self.dt, d, ptr(x), ptr(self.packed[cs.name]), ptr(z), None, None, s)
+            stats = self._bn_finalize(cs.bn, None, None, 0, b * ho * wo, False, tag)
+        return (z,) + stats + (ho, wo)
+
+    def _stat_capacity(self, B, H, W):
+        cap = 0
+        lib = L.lib()
+
+        def upd(cs, h, w):
+            nonlocal cap
+            d = cs.desc(B, h, w)
+            cap = max(cap, lib.crnn_conv_stat_rows(d) * cs.co)
+            return d.Ho, d.Wo
+
+        h, w = upd(self.stem0, H, W)
+        h, w = upd(self.stem1, h, w)
+        h, w = h // 2, w // 2
+        for blk in self.blocks:
+            h1, w1 = upd(blk.conv1, h, w)
+            upd(blk.conv2, h1, w1)
+            if blk.ds is not None:
+                upd(blk.ds, h, w)
+            h, w = h1, w1
+        h, w = upd(self.co0, h, w)
+        upd(self.co1, h, w)
+        return cap
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, images: torch.Tensor, train: bool, update_running: bool = True,
+                save_for_backward: bool = False) -> torch.Tensor:
+        """images [B,3,H,W] fp32 (reference NCHW input) -> logits [B,T,C] fp32 (view)."""
+        L.require_device(images)
+        self.pack()
+        self.update_running = update_running
+        images = images.contiguous().float()
+        B, Cin, H, W = images.shape
+        if Cin != 3:
+            raise ValueError("expected 3-channel crops")
+        ws, dt, T = self.ws, self.dt, self.dtype
+        s = L.stream_ptr()
+        self._stat_cap = self._stat_capacity(B, H, W) if train else 0
+        sv = {}
+
+        x0 = ws.get("in", (B, H, W, 8), T)
+        call("crnn_nchw_to_nhwc", dt, ptr(images), ptr(x0), B, 3, H, W, 8, s)
+        # stem (model/seresnet31.py:81-89)
+        z0, m0, i0, sc0, sh0, h, w = self._conv_bn(self.stem0, x0, B, H, W, train, "s0")
+        a0 = ws.get("s0.a", (B, h, w, 64), T)
+        call("crnn_bn_act", dt, ptr(z0), ptr(sc0), ptr(sh0), ptr(a0), B * h * w, 64, 1, s)
+        z1, m1, i1, sc1, sh1, h, w = self._conv_bn(self.stem1, a0, B, h, w, train, "s1")
+        if h % 2 or w % 2:
+            raise ValueError("stem maxpool expects even H and W")
+        xp = ws.get("s1.pool", (B, h // 2, w // 2, 128), T)
+        call("crnn_bn_relu_maxpool", dt, ptr(z1), ptr(sc1), ptr(sh1), ptr(xp), B, h, w, 128, s)
+        sv["stem"] = dict(x0=x0, z0=z0, m0=m0, i0=i0, sc0=sc0, sh0=sh0, a0=a0, z1=z1, m1=m1, i1=i1, sc1=sc1,
+                          sh1=sh1, H=H, W=W, h1=h, w1=w)
+        x, h, w = xp, h // 2, w // 2
+        # residual stages
+        blk_saved = []
+        for bi, blk in enumerate(self.blocks):
+            tag = f"b{bi}"
+            P = blk.planes
+            z1b, bm1, bi1, bs1, bh1, ho, wo = self._conv_bn(blk.conv1, x, B, h, w, train, tag + ".c1")
+            a1 = ws.get(tag + ".a1", (B, ho, wo, P), T)
+            call("crnn_bn_act", dt, ptr(z1b), ptr(bs1), ptr(bh1), ptr(a1), B * ho * wo, P, 1, s)
+            z2, bm2, bi2, bs2, bh2, _, _ = self._conv_bn(blk.conv2, a1, B, ho, wo, train, tag + ".c2")
+            HW = ho * wo
+            Cr = P // 16
+            pooled = ws.get(tag + ".pooled", (B, P), torch.float32)
+            hid = ws.get(tag + ".hid", (B, Cr), torch.float32)
+            se = ws.get(tag + ".s", (B, P), torch.float32)
+            call("crnn_se_pool", dt, ptr(z2), ptr(bs2), ptr(bh2), ptr(pooled), B, HW, P, s)
+            call("crnn_se_mlp_fwd", ptr(pooled), ptr(self.p[blk.prefix + ".se.fc.0.weight"]),
+                 ptr(self.p[blk.prefix + ".se.fc.2.weight"]), ptr(hid), ptr(se), B, P, Cr, s)
+            dsv = None
+            if blk.ds is not None:
+                zd, dm, di, dsc, dsh, _, _ = self._conv_bn(blk.ds, x, B, h, w, train, tag + ".ds")
+                dsv = dict(zd=zd, m=dm, i=di, sc=dsc, sh=dsh)
+                idn, isc, ish = zd, dsc, dsh
+            else:
+                idn, isc, ish = x, None, None
+            y = ws.get(tag + ".y", (B, ho, wo, P), T)
+            call("crnn_se_residual_fwd", dt, ptr(z2), ptr(bs2), ptr(bh2), ptr(se), ptr(idn), ptr(isc), ptr(ish),
+                 ptr(y), B, HW, P, s)
+            blk_saved.append(dict(x=x, h=h, w=w, ho=ho, wo=wo, z1=z1b, m1=bm1, i1=bi1, sc1=bs1, sh1=bh1, a1=a1,
+                                  z2=z2, m2=bm2, i2=bi2, sc2=bs2, sh2=bh2, pooled=pooled, hid=hid, s=se, ds=dsv,
+                                  y=y))
+            x, h, w = y, ho, wo
+        sv["blocks"] = blk_saved
+        # conv_out (model/seresnet31.py:129-136) + height collapse (model/model.py:191,216-218)
+        zc0, cm0, ci0, cs0, ch0, h2, w2 = self._conv_bn(self.co0, x, B, h, w, train, "co0")
+        ac0 = ws.get("co0.a", (B, h2, w2, 512), T)
+        call("crnn_bn_act", dt, ptr(zc0), ptr(cs0), ptr(ch0), ptr(ac0), B * h2 * w2, 512, 1, s)
+        zc1, cm1, ci1, cs1, ch1, h3, w3 = self._conv_bn(self.co1, ac0, B, h2, w2, train, "co1")
+        Tn = w3
+        seq = ws.get("seq", (B, Tn, 512), T)
+        call("crnn_hpool_fwd", dt, ptr(zc1), ptr(cs1), ptr(ch1), ptr(seq), B, h3, w3, 512, s)
+        sv["co"] = dict(x=x, h=h, w=w, z0=zc0, m0=cm0, i0=ci0, sc0=cs0, sh0=ch0, a0=ac0, h2=h2, w2=w2, z1=zc1,
+                        m1=cm1, i1=ci1, sc1=cs1, sh1=ch1, h3=h3, w3=w3)
+        # BiLSTM stack (model/model.py:195-198)
+        Hd = self.H
+        xin = seq
+        rnn_saved = []
+        for l in range(self.nl):
+            pre = f"enc_rnn.{l}"
+            ind = xin.shape[-1]
+            xg = ws.get(f"r{l}.xg", (B, Tn, 2, 4 * Hd), T)
+            call("crnn_gemm_nt", dt, ptr(xin), ind, ptr(self.packed[pre + ".wih"]), ind, ptr(xg), 8 * Hd,
+                 ptr(self.packed[pre + ".bias"]), B * Tn, 8 * Hd, ind, 0, 0, s)
+            hseq = ws.get(f"r{l}.hseq", (B, Tn, 2 * Hd), T)
+            gsv = ws.get(f"r{l}.gates", (2, Tn, B, 4 * Hd), T)
+            csv = ws.get(f"r{l}.c", (2, Tn, B, Hd), torch.float32)
+            whh = self.packed[pre + ".whh"]
+            for st in range(Tn):
+                call("crnn_lstm_step_fwd", dt, ptr(xg), ptr(whh), ptr(hseq), ptr(gsv), ptr(csv), B, Tn, Hd, st, s)
+            out = ws.get(f"r{l}.out", (B, Tn, Hd), T)
+            call("crnn_gemm_nt", dt, ptr(hseq), 2 * Hd, ptr(self.packed[pre + ".lin"]), 2 * Hd, ptr(out), Hd,
+                 ptr(self.p[pre + ".linear.bias"]), B * Tn, Hd, 2 * Hd, 0, 0, s)
+            rnn_saved.append(dict(x=xin, hseq=hseq, gates=gsv, c=csv, out=out))
+            xin = out
+        sv["rnn"] = rnn_saved
+        # enc_dropout (model/model.py:201,220): identity in eval; p=0 supported in train
+        # CTC head
+        logits = ws.get("logits", (B, Tn, self.Cpad), torch.float32)
+        call("crnn_gemm_nt", dt, ptr(xin), Hd, ptr(self.packed["head.w"]), Hd, ptr(logits), self.Cpad,
+             ptr(self.packed["head.b"]), B * Tn, self.Cpad, Hd, 1, 0, s)
+        sv["enc"] = xin
+        sv["B"], sv["T"] = B, Tn
+        self._saved = sv if save_for_backward else None
+        return logits[:, :, : self.C]
+
+    # ------------------------------------------------------------------ CTC
+    def ctc(self, logits_padded: torch.Tensor, targets: torch.Tensor, lengths: torch.Tensor,
+            want_grad: bool = True, zero_infinity: bool = True):
+        """mean-reduced CTC loss (device scalar) and d loss / d logits [B,T,Cpad] (fp32)."""
+        B, Tn, _ = logits_padded.shape
+        ws = self.ws
+        s = L.stream_ptr()
+        tg = targets.to(device=self.device, dtype=torch.int32).contiguous()
+        ln = lengths.to(device=self.device, dtype=torch.int32).contiguous()
+        Lmax = tg.shape[1]
+        loss_b = ws.get("ctc.loss_b", (B,), torch.float32)
+        dlog = ws.get("ctc.dlogits", (B, Tn, self.Cpad), torch.float32) if want_grad else None
+        call("crnn_ctc_loss", ptr(logits_padded), self.Cpad, B, Tn, self.C, ptr(tg), Lmax, ptr(ln), ptr(loss_b),
+             ptr(dlog), 1 if zero_infinity else 0, s)
+        loss = ws.get("ctc.loss", (1,), torch.float32)
+        call("crnn_ctc_reduce_mean", ptr(loss_b), ptr(ln), B, ptr(loss), s)
+        return loss, dlog
+
+    def logits_padded(self):
+        return self.ws.bufs["logits"]
+
+    # ------------------------------------------------------------------ backward
+    def _bn_bwd(self, mode, dy, z, stats, prefix, M, C, HW=1, y=None, se=None, dpool=None, out=None,
+                accumulate_params=False):
+        mean, inv, sc, sh = stats
+        ws = self.ws
+        s = L.stream_ptr()
+        d = BnBwdDesc(ptr(dy), ptr(z), ptr(mean), ptr(inv), ptr(sc), ptr(sh), ptr(y), ptr(se), ptr(dpool), mode,
+                      M, C, HW)
+        rows = L.lib().crnn_bn_rows(M)
+        pg = ws.get("bnb.pg", (1024 * 512,), torch.float32)[: rows * C]
+        pgx = ws.get("bnb.pgx", (1024 * 512,), torch.float32)[: rows * C]
+        call("crnn_bn_bwd_reduce", self.dt, d, ptr(pg), ptr(pgx), rows, s)
+        mg = ws.get("bnb.mg", (512,), torch.float32)
+        mgx = ws.get("bnb.mgx", (512,), torch.float32)
+        call("crnn_bn_bwd_finalize", ptr(pg), ptr(pgx), rows, C, M, ptr(self.g[prefix + ".weight"]),
+             ptr(self.g[prefix + ".bias"]), ptr(mg), ptr(mgx), 1 if accumulate_params else 0, s)
+        call("crnn_bn_bwd_apply", self.dt, d, ptr(mg), ptr(mgx), ptr(out), s)
+        return out
+
+    def _wgrad(self, cs: ConvSpec, dz, x, b, h, w):
+        d = cs.desc(b, h, w)
+        need = L.lib().crnn_conv_wgrad_workspace(d)
+        wsb = self.ws.get("wgrad.ws", (self._wg_cap,), torch.float32)
+        if need > wsb.numel() * 4:
+            raise RuntimeError("wgrad workspace too small")
+        beta = 1.0 if self.accumulate else 0.0
+        call("crnn_conv_wgrad", self.dt, d, ptr(dz), ptr(x), ptr(self.g[cs.name]), ptr(wsb), wsb.numel() * 4,
+             beta, L.stream_ptr())
+
+    def _wgrad_capacity(self, B, H, W):
+        lib = L.lib()
+        cap = 0
+
+        def upd(cs, h, w):
+            nonlocal cap
+            d = cs.desc(B, h, w)
+            cap = max(cap, lib.crnn_conv_wgrad_workspace(d) // 4)
+            return d.Ho, d.Wo
+
+        h, w = upd(self.stem0, H, W)
+        h, w = upd(self.stem1, h, w)
+        h, w = h // 2, w // 2
+        for blk in self.blocks:
+            h1, w1 = upd(blk.conv1, h, w)
+            upd(blk.conv2, h1, w1)
+            if blk.ds is not None:
+                upd(blk.ds, h, w)
+            h, w = h1, w1
+        h, w = upd(self.co0, h, w)
+        upd(self.co1, h, w)
+        return cap
+
+    def backward(self, dlogits: torch.Tensor, grads: Dict[str, torch.Tensor], accumulate: bool = False):
+        """Full backward from d loss / d logits [B,T,Cpad] fp32 into `grads` (fp32, reference layouts)."""
+        sv = self._saved
+        if sv is None:
+            raise RuntimeError("forward(save_for_backward=True) must precede backward")
+        self.g = grads
+        self.accumulate = accumulate
+        ws, dt, T = self.ws, self.dt, self.dtype
+        s = L.stream_ptr()
+        B, Tn, Hd = sv["B"], sv["T"], self.H
+        st = sv["stem"]
+        self._wg_cap = self._wgrad_capacity(B, st["H"], st["W"])
+        acc = 1 if accumulate else 0
+        M = B * Tn
+        # ---- CTC head
+        dlT = ws.get("head.dlT", (B, Tn, self.Cpad), T)
+        call("crnn_cast_f32", dt, ptr(dlogits), ptr(dlT), M * self.Cpad, s)
+        hw_g = ws.get("head.dw", (self.Cpad, Hd), torch.float32)
+        call("crnn_gemm_tn", dt, ptr(dlT), self.Cpad, ptr(sv["enc"]), Hd, ptr(hw_g), Hd, self.Cpad, Hd, M, 0, s)
+        self._store_grad("ctc_head.weight", hw_g[: self.C], accumulate)
+        call("crnn_colsum", L.F32, ptr(dlogits), self.Cpad, M, self.C, ptr(grads["ctc_head.bias"]), acc, 1, s)
+        dx = ws.get("rnn.dx_head", (B, Tn, Hd), T)
+        call("crnn_gemm_nn", dt, ptr(dlT), self.Cpad, ptr(self.packed["head.w"]), Hd, ptr(dx), Hd, M, Hd,
+             self.Cpad, 0, 0, s)
+        # ---- BiLSTM stack, reverse
+        for l in reversed(range(self.nl)):
+            pre = f"enc_rnn.{l}"
+            r = sv["rnn"][l]
+            ind = r["x"].shape[-1]
+            dh = ws.get("rnn.dhseq", (B, Tn, 2 * Hd), T)
+            call("crnn_gemm_nn", dt, ptr(dx), Hd, ptr(self.packed[pre + ".lin"]), 2 * Hd, ptr(dh), 2 * Hd, M,
+                 2 * Hd, Hd, 0, 0, s)
+            call("crnn_gemm_tn", dt, ptr(dx), Hd, ptr(r["hseq"]), 2 * Hd, ptr(grads[pre + ".linear.weight"]),
+                 2 * Hd, Hd, 2 * Hd, M, acc, s)
+            call("crnn_colsum", dt, ptr(dx), Hd, M, Hd, ptr(grads[pre + ".linear.bias"]), acc, 0, s)
+            dg = ws.get("rnn.dgates", (2, Tn, B, 4 * Hd), T)
+            dc = ws.get("rnn.dc", (2, B, Hd), torch.float32)
+            whh = self.packed[pre + ".whh"]
+            for stp in range(Tn):
+                call("crnn_lstm_step_bwd", dt, ptr(dh), ptr(whh), ptr(r["gates"]), ptr(r["c"]), ptr(dg), ptr(dc),
+                     B, Tn, Hd, stp, s)
+            dwhh = ws.get("rnn.dwhh", (2, 4 * Hd, Hd), torch.float32)
+            call("crnn_lstm_dwhh", dt, ptr(dg), ptr(r["hseq"]), ptr(dwhh), B, Tn, Hd, 0, s)
+            dwih = ws.get(f"rnn.dwih{ind}", (2, 4 * Hd, ind), torch.float32)
+            call("crnn_lstm_dwih", dt, ptr(dg), ptr(r["x"]), ptr(dwih), B, Tn, Hd, ind, 0, s)
+            db = ws.get("rnn.db", (2, 4 * Hd), torch.float32)
+            call("crnn_lstm_dbias", dt, ptr(dg), ptr(db), B, Tn, Hd, 0, s)
+            for d, sfx in enumerate(["", "_reverse"]):
+                rr = pre + ".rnn."
+                self._store_grad(rr + "weight_hh_l0" + sfx, dwhh[d], accumulate)
+                self._store_grad(rr + "weight_ih_l0" + sfx, dwih[d], accumulate)
+                self._store_grad(rr + "bias_ih_l0" + sfx, db[d], accumulate)
+                self._store_grad(rr + "bias_hh_l0" + sfx, db[d], accumulate)
+            nxt = ws.get(f"rnn.dx_l{l}", (B, Tn, ind), T)
+            call("crnn_lstm_dx", dt, ptr(dg), ptr(self.packed[pre + ".wih"]), ptr(nxt), B, Tn, Hd, ind, s)
+            dx = nxt
+        dseq = dx  # [B, T, 512]
+        if self.debug:
+            self.dbg["dseq"] = dseq.clone()
+        # ---- conv_out + height collapse
+        co = sv["co"]
+        big = self._scratch_elems(sv)
+        bufA = ws.get("g.A", (big,), T)
+        bufB = ws.get("g.B", (big,), T)
+        bufC = ws.get("g.C", (big,), T)
+        h3, w3 = co["h3"], co["w3"]
+        if h3 == 1:
+            dyf = dseq
+        else:
+            dyf = bufA[: B * h3 * w3 * 512].view(B, h3, w3, 512)
+            call("crnn_hpool_bwd", dt, ptr(dseq), ptr(dyf), B, h3, w3, 512, s)
+        dz = bufB[: B * h3 * w3 * 512]
+        self._bn_bwd(1, dyf, co["z1"], (co["m1"], co["i1"], co["sc1"], co["sh1"]), self.co1.bn, B * h3 * w3, 512,
+                     out=dz, accumulate_params=accumulate)
+        self._wgrad(self.co1, dz, co["a0"], B, co["h2"], co["w2"])
+        da = bufC[: B * co["h2"] * co["w2"] * 512]
+        call("crnn_conv_dgrad", dt, self.co1.desc(B, co["h2"], co["w2"]), ptr(dz), ptr(self.packed[self.co1.name]),
+             ptr(da), None, None, 0, s)
+        dz0 = bufA[: B * co["h2"] * co["w2"] * 512]
+        self._bn_bwd(1, da, co["z0"], (co["m0"], co["i0"], co["sc0"], co["sh0"]), self.co0.bn,
+                     B * co["h2"] * co["w2"], 512, out=dz0, accumulate_params=accumulate)
+        self._wgrad(self.co0, dz0, co["x"], B, co["h"], co["w"])
+        dy = bufB[: B * co["h"] * co["w"] * 512]
+        call("crnn_conv_dgrad", dt, self.co0.desc(B, co["h"], co["w"]), ptr(dz0), ptr(self.packed[self.co0.name]),
+             ptr(dy), None, None, 0, s)
+        # ---- residual blocks, reverse
+        bufs = [bufA, bufB, bufC]
+        cur = 1  # dy lives in bufB
+        for bi in reversed(range(len(self.blocks))):
+            blk = self.blocks[bi]
+            sb = sv["blocks"][bi]
+            P = blk.planes
+            ho, wo, h, w = sb["ho"], sb["wo"], sb["h"], sb["w"]
+            HW = ho * wo
+            Mo = B * HW
+            Cr = P // 16
+            o1, o2 = [k for k in range(3) if k != cur]
+            dyb = bufs[cur][: Mo * P]
+            if self.debug:
+                self.dbg[f"dy.b{bi}"] = dyb.clone().view(B, ho, wo, P)
+            ds = ws.get(f"se.ds{P}", (B, P), torch.float32)
+            call("crnn_se_bwd_reduce", dt, ptr(dyb), ptr(sb["y"]), ptr(sb["z2"]), ptr(sb["sc2"]), ptr(sb["sh2"]),
+                 ptr(ds), B, HW, P, s)
+            dsig = ws.get(f"se.dsig{P}", (B, P), torch.float32)
+            dhid = ws.get(f"se.dhid{P}", (B, Cr), torch.float32)
+            dpool = ws.get(f"se.dpool{P}", (B, P), torch.float32)
+            dw1 = ws.get(f"se.dw1{P}", (Cr, P), torch.float32)
+            dw2 = ws.get(f"se.dw2{P}", (P, Cr), torch.float32)
+            call("crnn_se_mlp_bwd", ptr(ds), ptr(sb["pooled"]), ptr(sb["hid"]), ptr(sb["s"]),
+                 ptr(self.p[blk.prefix + ".se.fc.0.weight"]), ptr(self.p[blk.prefix + ".se.fc.2.weight"]),
+                 ptr(dsig), ptr(dhid), ptr(dpool), ptr(dw1), ptr(dw2), B, P, Cr, HW, s)
+            self._store_grad(blk.prefix + ".se.fc.0.weight", dw1, accumulate)
+            self._store_grad(blk.prefix + ".se.fc.2.weight", dw2, accumulate)
+            dz2 = bufs[o1][: Mo * P]
+            self._bn_bwd(3, dyb, sb["z2"], (sb["m2"], sb["i2"], sb["sc2"], sb["sh2"]), blk.conv2.bn, Mo, P, HW=HW,
+                         y=sb["y"], se=sb["s"], dpool=dpool, out=dz2, accumulate_params=accumulate)
+            self._wgrad(blk.conv2, dz2, sb["a1"], B, ho, wo)
+            da1 = bufs[o2][: Mo * P]
+            call("crnn_conv_dgrad", dt, blk.conv2.desc(B, ho, wo), ptr(dz2), ptr(self.packed[blk.conv2.name]),
+                 ptr(da1), None, None, 0, s)
+            dz1 = bufs[o1][: Mo * P]
+            self._bn_bwd(1, da1, sb["z1"], (sb["m1"], sb["i1"], sb["sc1"], sb["sh1"]), blk.conv1.bn, Mo, P,
+                         out=dz1, accumulate_params=accumulate)
+            self._wgrad(blk.conv1, dz1, sb["x"], B, h, w)
+            Ci = blk.conv1.ci
+            dxb = bufs[o2][: B * h * w * Ci]
+            if blk.ds is None:
+                call("crnn_conv_dgrad", dt, blk.conv1.desc(B, h, w), ptr(dz1), ptr(self.packed[blk.conv1.name]),
+                     ptr(dxb), ptr(dyb), ptr(sb["y"]), 0, s)
+                cur = o2
+            else:
+                call("crnn_conv_dgrad", dt, blk.conv1.desc(B, h, w), ptr(dz1), ptr(self.packed[blk.conv1.name]),
+                     ptr(dxb), None, None, 0, s)
+                dsv = sb["ds"]
+                dzd = bufs[o1][: Mo * P]
+                self._bn_bwd(2, dyb, dsv["zd"], (dsv["m"], dsv["i"], dsv["sc"], dsv["sh"]), blk.ds.bn, Mo, P,
+                             y=sb["y"], out=dzd, accumulate_params=accumulate)
+                self._wgrad(blk.ds, dzd, sb["x"], B, h, w)
+                call("crnn_conv_dgrad", dt, blk.ds.desc(B, h, w), ptr(dzd), ptr(self.packed[blk.ds.name]),
+                     ptr(dxb), None, None, 1, s)
+                cur = o2
+        # ---- stem
+        o1, o2 = [k for k in range(3) if k != cur]
+        dp = bufs[cur]
+        if self.debug:
+            self.dbg["dpool"] = dp[: B * (st["h1"] // 2) * (st["w1"] // 2) * 128].clone()
+        h1, w1 = st["h1"], st["w1"]
+        dyf = bufs[o1][: B * h1 * w1 * 128]
+        call("crnn_maxpool_bwd", dt, ptr(st["z1"]), ptr(st["sc1"]), ptr(st["sh1"]), ptr(dp), ptr(dyf), B, h1, w1,
+             128, s)
+        dz1 = bufs[o2][: B * h1 * w1 * 128]
+        self._bn_bwd(1, dyf, st["z1"], (st["m1"], st["i1"], st["sc1"], st["sh1"]), self.stem1.bn, B * h1 * w1, 128,
+                     out=dz1, accumulate_params=accumulate)
+        self._wgrad(self.stem1, dz1, st["a0"], B, h1, w1)
+        da0 = bufs[o1][: B * h1 * w1 * 64]
+        call("crnn_conv_dgrad", dt, self.stem1.desc(B, h1, w1), ptr(dz1), ptr(self.packed[self.stem1.name]),
+             ptr(da0), None, None, 0, s)
+        dz0 = bufs[cur][: B * h1 * w1 * 64]
+        self._bn_bwd(1, da0, st["z0"], (st["m0"], st["i0"], st["sc0"], st["sh0"]), self.stem0.bn, B * h1 * w1, 64,
+                     out=dz0, accumulate_params=accumulate)
+        self._wgrad(self.stem0, dz0, st["x0"], B, st["H"], st["W"])
+
+    def _scratch_elems(self, sv):
+        st = sv["stem"]
+        B = sv["B"]
+        return B * st["h1"] * st["w1"] * 128
+
+    def _store_grad(self, name, src, accumulate):
+        g = self.g[name]
+        src = src.reshape(g.shape)
+        if accumulate:
+            g.add_(src)
+        else:
+            g.copy_(src)

@@ -1,0 +1,741 @@
+// BatchNorm / ReLU / MaxPool / SE / residual / height-collapse kernels, NHWC.
+//
+// Reference semantics:
+//   nn.BatchNorm2d train/eval (torch defaults eps 1e-5, momentum 0.1)   model/seresnet31.py:40-45
+//   nn.ReLU, nn.MaxPool2d(2,2)                                          model/seresnet31.py:83-88
+//   SELayer: mean_hw -> Linear(C,C/16,no bias) -> ReLU -> Linear(C/16,C) -> sigmoid -> x*s
+//                                                                       model/seresnet31.py:5-20
+//   SEBasicBlock tail: relu(se(bn2(conv2)) + identity|bn_d(conv_d(x)))   model/seresnet31.py:55-67
+//   AdaptiveAvgPool2d((1,None)) + squeeze(2) + permute(0,2,1)           model/model.py:191, 216-218
+// All elementwise passes move 8 channels (16 B bf16 / 32 B f32) per lane.
+#include "common.hpp"
+#include "crnn_internal.hpp"
+
+namespace {
+
+constexpr int NT = 256;
+
+// ------------------------------------------------------------ channel reductions
+// Block b reduces rows [b*rpb, (b+1)*rpb) of an [M][C] tensor into row b of two
+// [rows][C] partial buffers. Threads: cg = C/8 channel groups x (256/cg) row lanes.
+template <class F>
+__global__ __launch_bounds__(NT) void chan_reduce_kernel(F f, long M, int C, long rpb, float* __restrict__ p0,
+                                                         float* __restrict__ p1) {
+  extern __shared__ float red[];  // [2][rl][C]
+  const int cg = C / 8, rl = NT / cg;
+  const int tid = threadIdx.x, c8 = (tid % cg) * 8, r = tid / cg;
+  float a0[8], a1[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) a0[i] = a1[i] = 0.f;
+  const long m0 = blockIdx.x * rpb, m1 = min(M, m0 + rpb);
+  if (r < rl)
+    for (long m = m0 + r; m < m1; m += rl) f(m, c8, a0, a1);
+  if (r < rl) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      red[r * C + c8 + i] = a0[i];
+      red[(rl + r) * C + c8 + i] = a1[i];
+    }
+  }
+  __syncthreads();
+  for (int c = tid; c < C; c += NT) {
+    float s0 = 0.f, s1 = 0.f;
+    for (int q = 0; q < rl; ++q) {
+      s0 += red[q * C + c];
+      s1 += red[(rl + q) * C + c];
+    }
+    p0[(size_t)blockIdx.x * C + c] = s0;
+    p1[(size_t)blockIdx.x * C + c] = s1;
+  }
+}
+
+// (sum, M2) partials of a streamed [M][C] tensor: block-local two-pass (the block's rows
+// are re-read for the second pass, they are L2-resident) — matches the conv epilogue format.
+template <typename T>
+__global__ __launch_bounds__(NT) void chan_stats_kernel(const T* __restrict__ x, long M, int C, long rpb,
+                                                        float* __restrict__ p0, float* __restrict__ p1) {
+  extern __shared__ float red[];  // [rl][C] + [C] block means
+  const int cg = C / 8, rl = NT / cg;
+  const int tid = threadIdx.x, c8 = (tid % cg) * 8, r = tid / cg;
+  const long m0 = blockIdx.x * rpb, m1 = min(M, m0 + rpb);
+  const long n = m1 > m0 ? m1 - m0 : 0;
+  float* mu = red + rl * C;
+  float a[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) a[i] = 0.f;
+  if (r < rl)
+    for (long m = m0 + r; m < m1; m += rl) {
+      float v[8];
+      unpack8<T>(ld8<T>(x + m * C + c8), v);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) a[i] += v[i];
+    }
+  if (r < rl)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) red[r * C + c8 + i] = a[i];
+  __syncthreads();
+  for (int c = tid; c < C; c += NT) {
+    float s = 0.f;
+    for (int q = 0; q < rl; ++q) s += red[q * C + c];
+    p0[(size_t)blockIdx.x * C + c] = s;
+    mu[c] = n > 0 ? s / (float)n : 0.f;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 8; ++i) a[i] = 0.f;
+  if (r < rl)
+    for (long m = m0 + r; m < m1; m += rl) {
+      float v[8];
+      unpack8<T>(ld8<T>(x + m * C + c8), v);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        float d = v[i] - mu[c8 + i];
+        a[i] += d * d;
+      }
+    }
+  __syncthreads();
+  if (r < rl)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) red[r * C + c8 + i] = a[i];
+  __syncthreads();
+  for (int c = tid; c < C; c += NT) {
+    float s = 0.f;
+    for (int q = 0; q < rl; ++q) s += red[q * C + c];
+    p1[(size_t)blockIdx.x * C + c] = s;
+  }
+}
+
+// upstream gradient g of a BN output, by mode (see crnn_hip.h CRNN_BNG_*)
+template <typename T>
+__device__ __forceinline__ void bn_g(const crnn_bn_bwd_desc& d, long m, int c8, const float* zz, float* g) {
+  float dy[8];
+  unpack8<T>(ld8<T>((const T*)d.dy + m * d.C + c8), dy);
+  if (d.mode == CRNN_BNG_PLAIN) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) g[i] = dy[i];
+  } else if (d.mode == CRNN_BNG_RELU) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) g[i] = (zz[i] * d.scale[c8 + i] + d.shift[c8 + i]) > 0.f ? dy[i] : 0.f;
+  } else {
+    float y[8];
+    unpack8<T>(ld8<T>((const T*)d.y + m * d.C + c8), y);
+    if (d.mode == CRNN_BNG_RESID) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) g[i] = y[i] > 0.f ? dy[i] : 0.f;
+    } else {
+      long b = m / d.HW;
+      const float* s = d.s + b * d.C + c8;
+      const float* dp = d.dpool + b * d.C + c8;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) g[i] = (y[i] > 0.f ? dy[i] * s[i] : 0.f) + dp[i];
+    }
+  }
+}
+
+template <typename T> struct BnBwdF {
+  crnn_bn_bwd_desc d;
+  __device__ __forceinline__ void operator()(long m, int c8, float* s, float* q) const {
+    float z[8], g[8];
+    unpack8<T>(ld8<T>((const T*)d.z + m * d.C + c8), z);
+    bn_g<T>(d, m, c8, z, g);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float xh = (z[i] - d.mean[c8 + i]) * d.invstd[c8 + i];
+      s[i] += g[i];
+      q[i] += g[i] * xh;
+    }
+  }
+};
+
+int rows_for(long M) {
+  long r = (M + 63) / 64;
+  if (r > 1024) r = 1024;
+  if (r < 1) r = 1;
+  return (int)r;
+}
+
+template <class F> int chan_reduce(F f, long M, int C, float* p0, float* p1, int rows, hipStream_t st) {
+  if (C % 8 || C / 8 > NT || NT % (C / 8)) return crnn_set_error(hipErrorInvalidValue, "channel reduce: bad C");
+  long rpb = (M + rows - 1) / rows;
+  int rl = NT / (C / 8);
+  size_t sm = (size_t)2 * rl * C * sizeof(float);
+  hipLaunchKernelGGL((chan_reduce_kernel<F>), dim3(rows), dim3(NT), sm, st, f, M, C, rpb, p0, p1);
+  return (int)hipGetLastError();
+}
+
+// ------------------------------------------------------------ finalize (double)
+// partial r covers rows [r*rpp, r*rpp + rpp) of `count`; psum = sum, psq = M2 about the
+// partial's own mean. Chan: M2 = sum M2_r + sum n_r (mean_r - mean)^2.
+__global__ void bn_finalize_kernel(const float* psum, const float* psq, int rows, long rpp, int C, long count,
+                                   const float* gamma, const float* beta, float* rmean, float* rvar,
+                                   float momentum, float eps, int train, float* mean_o, float* inv_o,
+                                   float* scale_o, float* shift_o) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double mean, var;
+  if (train) {
+    double s = 0.0;
+    for (int r = 0; r < rows; ++r) s += psum[(size_t)r * C + c];
+    mean = s / (double)count;
+    double m2 = 0.0;
+    for (int r = 0; r < rows; ++r) {
+      long nr = count - (long)r * rpp;
+      nr = nr < 0 ? 0 : (nr > rpp ? rpp : nr);
+      if (nr == 0) continue;
+      double mr = (double)psum[(size_t)r * C + c] / (double)nr - mean;
+      m2 += (double)psq[(size_t)r * C + c] + (double)nr * mr * mr;
+    }
+    var = m2 / (double)count;
+    if (var < 0.0) var = 0.0;
+    if (rmean) {
+      double unb = count > 1 ? var * (double)count / (double)(count - 1) : var;
+      rmean[c] = (float)((1.0 - momentum) * rmean[c] + momentum * mean);
+      rvar[c] = (float)((1.0 - momentum) * rvar[c] + momentum * unb);
+    }
+  } else {
+    mean = rmean[c];
+    var = rvar[c];
+  }
+  double inv = 1.0 / sqrt(var + (double)eps);
+  double sc = (double)gamma[c] * inv;
+  if (mean_o) mean_o[c] = (float)mean;
+  if (inv_o) inv_o[c] = (float)inv;
+  scale_o[c] = (float)sc;
+  shift_o[c] = (float)((double)beta[c] - mean * sc);
+}
+
+__global__ void bn_bwd_finalize_kernel(const float* pg, const float* pgx, int rows, int C, long count,
+                                       float* dgamma, float* dbeta, float* mean_g, float* mean_gx, int acc) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s = 0.0, q = 0.0;
+  for (int r = 0; r < rows; ++r) {
+    s += pg[(size_t)r * C + c];
+    q += pgx[(size_t)r * C + c];
+  }
+  if (dgamma) dgamma[c] = (float)(acc ? dgamma[c] + q : q);
+  if (dbeta) dbeta[c] = (float)(acc ? dbeta[c] + s : s);
+  mean_g[c] = (float)(s / (double)count);
+  mean_gx[c] = (float)(q / (double)count);
+}
+
+// ------------------------------------------------------------ elementwise
+template <typename T>
+__global__ void bn_act_kernel(const T* __restrict__ z, const float* __restrict__ sc, const float* __restrict__ sh,
+                              T* __restrict__ y, long nvec, int C, int relu) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < nvec; i += (long)gridDim.x * blockDim.x) {
+    int c8 = (int)((i * 8) % C);
+    float v[8];
+    unpack8<T>(ld8<T>(z + i * 8), v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      v[k] = v[k] * sc[c8 + k] + sh[c8 + k];
+      if (relu) v[k] = fmaxf(v[k], 0.f);
+    }
+    st8<T>(y + i * 8, pack8<T>(v));
+  }
+}
+
+template <typename T>
+__global__ void bn_apply_bwd_kernel(crnn_bn_bwd_desc d, const float* __restrict__ mg, const float* __restrict__ mgx,
+                                    T* __restrict__ dz, long nvec) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < nvec; i += (long)gridDim.x * blockDim.x) {
+    long m = (i * 8) / d.C;
+    int c8 = (int)(i * 8 - m * d.C);
+    float z[8], g[8], o[8];
+    unpack8<T>(ld8<T>((const T*)d.z + i * 8), z);
+    bn_g<T>(d, m, c8, z, g);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      int c = c8 + k;
+      float xh = (z[k] - d.mean[c]) * d.invstd[c];
+      o[k] = d.scale[c] * (g[k] - mg[c] - xh * mgx[c]);
+    }
+    st8<T>(dz + i * 8, pack8<T>(o));
+  }
+}
+
+// maxpool 2x2/2 over relu(z*sc+sh); NHWC, one lane = 8 channels of one output pixel
+template <typename T>
+__global__ void bn_relu_maxpool_kernel(const T* __restrict__ z, const float* __restrict__ sc, const float* __restrict__ sh,
+                                       T* __restrict__ y, int B, int H, int W, int C) {
+  const int Ho = H / 2, Wo = W / 2, cg = C / 8;
+  const long n = (long)B * Ho * Wo * cg;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    int c8 = (int)(i % cg) * 8;
+    long p = i / cg;
+    int wo = (int)(p % Wo);
+    long q = p / Wo;
+    int ho = (int)(q % Ho);
+    int b = (int)(q / Ho);
+    float best[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) best[k] = -INFINITY;
+#pragma unroll
+    for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+      for (int dw = 0; dw < 2; ++dw) {
+        float v[8];
+        unpack8<T>(ld8<T>(z + (((size_t)b * H + 2 * ho + dh) * W + 2 * wo + dw) * C + c8), v);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          float a = fmaxf(v[k] * sc[c8 + k] + sh[c8 + k], 0.f);
+          best[k] = a > best[k] ? a : best[k];
+        }
+      }
+    st8<T>(y + (((size_t)b * Ho + ho) * Wo + wo) * C + c8, pack8<T>(best));
+  }
+}
+
+// route d(pool) to the first maximum (scan order h, w — torch's max_pool2d index)
+template <typename T>
+__global__ void maxpool_bwd_kernel(const T* __restrict__ z, const float* __restrict__ sc, const float* __restrict__ sh,
+                                   const T* __restrict__ dp, T* __restrict__ dy, int B, int H, int W, int C) {
+  const int Ho = H / 2, Wo = W / 2, cg = C / 8;
+  const long n = (long)B * Ho * Wo * cg;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    int c8 = (int)(i % cg) * 8;
+    long p = i / cg;
+    int wo = (int)(p % Wo);
+    long q = p / Wo;
+    int ho = (int)(q % Ho);
+    int b = (int)(q / Ho);
+    float a[4][8], best[8], g[8];
+    int arg[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { best[k] = -INFINITY; arg[k] = 0; }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      unpack8<T>(ld8<T>(z + (((size_t)b * H + 2 * ho + (t >> 1)) * W + 2 * wo + (t & 1)) * C + c8), a[t]);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float v = fmaxf(a[t][k] * sc[c8 + k] + sh[c8 + k], 0.f);
+        if (v > best[k]) { best[k] = v; arg[k] = t; }
+      }
+    }
+    unpack8<T>(ld8<T>(dp + (((size_t)b * Ho + ho) * Wo + wo) * C + c8), g);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      float o[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) o[k] = arg[k] == t ? g[k] : 0.f;
+      st8<T>(dy + (((size_t)b * H + 2 * ho + (t >> 1)) * W + 2 * wo + (t & 1)) * C + c8, pack8<T>(o));
+    }
+  }
+}
+
+// ------------------------------------------------------------ SE
+// per-sample spatial reduction: out[b][c] = scale_out * sum_hw f(b, hw, c8)
+template <class F>
+__global__ __launch_bounds__(NT) void sample_reduce_kernel(F f, int HW, int C, float* __restrict__ out, float mul) {
+  extern __shared__ float red[];
+  const int cg = C / 8, rl = NT / cg;
+  const int tid = threadIdx.x, c8 = (tid % cg) * 8, r = tid / cg;
+  const int b = blockIdx.x;
+  float a[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) a[i] = 0.f;
+  if (r < rl)
+    for (int hw = r; hw < HW; hw += rl) f(b, hw, c8, a);
+  if (r < rl) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) red[r * C + c8 + i] = a[i];
+  }
+  __syncthreads();
+  for (int c = tid; c < C; c += NT) {
+    float s = 0.f;
+    for (int q = 0; q < rl; ++q) s += red[q * C + c];
+    out[(size_t)b * C + c] = s * mul;
+  }
+}
+
+template <typename T> struct SePoolF {
+  const T* z;
+  const float* sc;
+  const float* sh;
+  int HW, C;
+  __device__ __forceinline__ void operator()(int b, int hw, int c8, float* a) const {
+    float v[8];
+    unpack8<T>(ld8<T>(z + ((size_t)b * HW + hw) * C + c8), v);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a[i] += v[i] * sc[c8 + i] + sh[c8 + i];
+  }
+};
+
+template <typename T> struct SeBwdF {
+  const T* dy;
+  const T* y;
+  const T* z;
+  const float* sc;
+  const float* sh;
+  int HW, C;
+  __device__ __forceinline__ void operator()(int b, int hw, int c8, float* a) const {
+    size_t o = ((size_t)b * HW + hw) * C + c8;
+    float d[8], yy[8], v[8];
+    unpack8<T>(ld8<T>(dy + o), d);
+    unpack8<T>(ld8<T>(y + o), yy);
+    unpack8<T>(ld8<T>(z + o), v);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a[i] += yy[i] > 0.f ? d[i] * (v[i] * sc[c8 + i] + sh[c8 + i]) : 0.f;
+  }
+};
+
+__global__ void se_mlp_fwd_kernel(const float* __restrict__ pooled, const float* __restrict__ w1,
+                                  const float* __restrict__ w2, float* __restrict__ hid, float* __restrict__ s,
+                                  int C, int Cr) {
+  extern __shared__ float sm[];  // pooled[C], hid[Cr]
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  float* p = sm;
+  float* h = sm + C;
+  for (int c = tid; c < C; c += blockDim.x) p[c] = pooled[(size_t)b * C + c];
+  __syncthreads();
+  for (int r = wid; r < Cr; r += blockDim.x / 64) {
+    float acc = 0.f;
+    for (int c = lane; c < C; c += 64) acc += p[c] * w1[(size_t)r * C + c];
+    acc = wave_sum(acc);
+    if (lane == 0) {
+      h[r] = fmaxf(acc, 0.f);
+      hid[(size_t)b * Cr + r] = h[r];
+    }
+  }
+  __syncthreads();
+  for (int c = tid; c < C; c += blockDim.x) {
+    float acc = 0.f;
+    for (int r = 0; r < Cr; ++r) acc += h[r] * w2[(size_t)c * Cr + r];
+    s[(size_t)b * C + c] = 1.f / (1.f + expf(-acc));
+  }
+}
+
+__global__ void se_mlp_bwd_kernel(const float* __restrict__ ds, const float* __restrict__ hid,
+                                  const float* __restrict__ s, const float* __restrict__ w1,
+                                  const float* __restrict__ w2, float* __restrict__ dsig, float* __restrict__ dhid,
+                                  float* __restrict__ dpool, int C, int Cr, float inv_hw) {
+  extern __shared__ float sm[];  // dsig[C], dhid[Cr]
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  float* dg = sm;
+  float* dh = sm + C;
+  for (int c = tid; c < C; c += blockDim.x) {
+    float sv = s[(size_t)b * C + c];
+    float v = ds[(size_t)b * C + c] * sv * (1.f - sv);
+    dg[c] = v;
+    dsig[(size_t)b * C + c] = v;
+  }
+  __syncthreads();
+  for (int r = wid; r < Cr; r += blockDim.x / 64) {
+    float acc = 0.f;
+    for (int c = lane; c < C; c += 64) acc += dg[c] * w2[(size_t)c * Cr + r];
+    acc = wave_sum(acc);
+    if (lane == 0) {
+      float v = hid[(size_t)b * Cr + r] > 0.f ? acc : 0.f;
+      dh[r] = v;
+      dhid[(size_t)b * Cr + r] = v;
+    }
+  }
+  __syncthreads();
+  for (int c = tid; c < C; c += blockDim.x) {
+    float acc = 0.f;
+    for (int r = 0; r < Cr; ++r) acc += dh[r] * w1[(size_t)r * C + c];
+    dpool[(size_t)b * C + c] = acc * inv_hw;
+  }
+}
+
+// dw2[c][r] = sum_b dsig[b][c] hid[b][r] ; dw1[r][c] = sum_b dhid[b][r] pooled[b][c]
+__global__ void se_wgrad_kernel(const float* __restrict__ dsig, const float* __restrict__ hid,
+                                const float* __restrict__ dhid, const float* __restrict__ pooled,
+                                float* __restrict__ dw1, float* __restrict__ dw2, int B, int C, int Cr) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= C * Cr) return;
+  int c = i % C, r = i / C;
+  float a2 = 0.f, a1 = 0.f;
+  for (int b = 0; b < B; ++b) {
+    a2 += dsig[(size_t)b * C + c] * hid[(size_t)b * Cr + r];
+    a1 += dhid[(size_t)b * Cr + r] * pooled[(size_t)b * C + c];
+  }
+  dw2[(size_t)c * Cr + r] = a2;
+  dw1[(size_t)r * C + c] = a1;
+}
+
+template <typename T>
+__global__ void se_residual_kernel(const T* __restrict__ z, const float* __restrict__ sc, const float* __restrict__ sh,
+                                   const float* __restrict__ s, const T* __restrict__ idn,
+                                   const float* __restrict__ isc, const float* __restrict__ ish, T* __restrict__ y,
+                                   long nvec, int HW, int C) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < nvec; i += (long)gridDim.x * blockDim.x) {
+    long m = (i * 8) / C;
+    int c8 = (int)(i * 8 - m * C);
+    long b = m / HW;
+    float v[8], d[8];
+    unpack8<T>(ld8<T>(z + i * 8), v);
+    unpack8<T>(ld8<T>(idn + i * 8), d);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      int c = c8 + k;
+      float u = (v[k] * sc[c] + sh[c]) * s[b * C + c];
+      float id = isc ? d[k] * isc[c] + ish[c] : d[k];
+      v[k] = fmaxf(u + id, 0.f);
+    }
+    st8<T>(y + i * 8, pack8<T>(v));
+  }
+}
+
+// ------------------------------------------------------------ height collapse
+template <typename T>
+__global__ void hpool_fwd_kernel(const T* __restrict__ z, const float* __restrict__ sc, const float* __restrict__ sh,
+                                 T* __restrict__ seq, int B, int Hh, int W, int C) {
+  const int cg = C / 8;
+  const long n = (long)B * W * cg;
+  const float inv = 1.f / (float)Hh;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    int c8 = (int)(i % cg) * 8;
+    long p = i / cg;
+    int w = (int)(p % W), b = (int)(p / W);
+    float acc[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+    for (int h = 0; h < Hh; ++h) {
+      float v[8];
+      unpack8<T>(ld8<T>(z + (((size_t)b * Hh + h) * W + w) * C + c8), v);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] += fmaxf(v[k] * sc[c8 + k] + sh[c8 + k], 0.f);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] *= inv;
+    st8<T>(seq + ((size_t)b * W + w) * C + c8, pack8<T>(acc));
+  }
+}
+
+template <typename T>
+__global__ void hpool_bwd_kernel(const T* __restrict__ dseq, T* __restrict__ dy, int B, int Hh, int W, int C) {
+  const int cg = C / 8;
+  const long n = (long)B * Hh * W * cg;
+  const float inv = 1.f / (float)Hh;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    int c8 = (int)(i % cg) * 8;
+    long p = i / cg;
+    int w = (int)(p % W);
+    long q = p / W;
+    int b = (int)(q / Hh);
+    float v[8];
+    unpack8<T>(ld8<T>(dseq + ((size_t)b * W + w) * C + c8), v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] *= inv;
+    st8<T>(dy + p * C + c8, pack8<T>(v));
+  }
+}
+
+// ------------------------------------------------------------ layout / packing
+template <typename T>
+__global__ void nchw_to_nhwc_kernel(const float* __restrict__ x, T* __restrict__ y, int B, int C, int H, int W, int Cp) {
+  const long n = (long)B * H * W;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    long b = i / ((long)H * W), hw = i - b * H * W;
+    for (int c = 0; c < Cp; ++c) {
+      float v = c < C ? x[(b * C + c) * H * W + hw] : 0.f;
+      y[i * Cp + c] = fromf<T>(v);
+    }
+  }
+}
+
+template <typename T>
+__global__ void cast_kernel(const float* __restrict__ s, T* __restrict__ d, long n) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    d[i] = fromf<T>(s[i]);
+}
+
+template <typename T>
+__global__ void pack_conv_kernel(const float* __restrict__ w, T* __restrict__ o, int Co, int Ci, int KH, int KW, int Cip) {
+  const long n = (long)Co * KH * KW * Cip;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    int ci = (int)(i % Cip);
+    long t = i / Cip;
+    int kw = (int)(t % KW);
+    t /= KW;
+    int kh = (int)(t % KH);
+    int co = (int)(t / KH);
+    float v = ci < Ci ? w[(((size_t)co * Ci + ci) * KH + kh) * KW + kw] : 0.f;
+    o[i] = fromf<T>(v);
+  }
+}
+
+template <typename T>
+__global__ void pack_rows_kernel(const float* __restrict__ src, T* __restrict__ o, const int* __restrict__ perm,
+                                 int rows_out, int rows_src, int cols) {
+  const long n = (long)rows_out * cols;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    int r = (int)(i / cols), c = (int)(i - (long)r * cols);
+    int sr = perm ? perm[r] : r;
+    float v = (r < rows_src && sr >= 0) ? src[(size_t)sr * cols + c] : 0.f;
+    o[i] = fromf<T>(v);
+  }
+}
+
+#define DISPATCH(dtype, ...)            \
+  if ((dtype) == CRNN_BF16) {           \
+    using T = bf16;                     \
+    __VA_ARGS__;                        \
+  } else {                              \
+    using T = float;                    \
+    __VA_ARGS__;                        \
+  }
+
+}  // namespace
+
+extern "C" {
+
+int crnn_bn_rows(long M) { return rows_for(M); }
+
+int crnn_channel_stats(int dtype, const void* x, long M, int C, float* psum, float* psq, int rows, void* stream) {
+  if (C % 8 || C / 8 > NT || NT % (C / 8)) return crnn_set_error(hipErrorInvalidValue, "channel_stats: bad C");
+  long rpb = (M + rows - 1) / rows;
+  int rl = NT / (C / 8);
+  size_t sm = (size_t)(rl + 1) * C * sizeof(float);
+  DISPATCH(dtype, hipLaunchKernelGGL(chan_stats_kernel<T>, dim3(rows), dim3(NT), sm, (hipStream_t)stream, (const T*)x, M,
+                                     C, rpb, psum, psq));
+  return (int)hipGetLastError();
+}
+
+int crnn_bn_finalize(const float* psum, const float* psq, int rows, long rows_per_partial, int C, long count,
+                     const float* gamma, const float* beta, float* running_mean, float* running_var, float momentum,
+                     float eps, int train, float* mean, float* invstd, float* scale, float* shift, void* stream) {
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 127) / 128), dim3(128), 0, (hipStream_t)stream, psum, psq, rows,
+                     rows_per_partial, C,
+                     count, gamma, beta, running_mean, running_var, momentum, eps, train, mean, invstd, scale, shift);
+  return (int)hipGetLastError();
+}
+
+int crnn_bn_act(int dtype, const void* z, const float* scale, const float* shift, void* y, long M, int C, int relu,
+                void* stream) {
+  long nvec = M * C / 8;
+  DISPATCH(dtype, hipLaunchKernelGGL(bn_act_kernel<T>, dim3(grid_for(nvec)), dim3(256), 0, (hipStream_t)stream,
+                                     (const T*)z, scale, shift, (T*)y, nvec, C, relu));
+  return (int)hipGetLastError();
+}
+
+int crnn_bn_relu_maxpool(int dtype, const void* z, const float* scale, const float* shift, void* y, int B, int H,
+                         int W, int C, void* stream) {
+  long n = (long)B * (H / 2) * (W / 2) * (C / 8);
+  DISPATCH(dtype, hipLaunchKernelGGL(bn_relu_maxpool_kernel<T>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream,
+                                     (const T*)z, scale, shift, (T*)y, B, H, W, C));
+  return (int)hipGetLastError();
+}
+
+int crnn_maxpool_bwd(int dtype, const void* z, const float* scale, const float* shift, const void* dpool,
+                     void* dy_full, int B, int H, int W, int C, void* stream) {
+  if ((H & 1) || (W & 1)) return crnn_set_error(hipErrorInvalidValue, "maxpool_bwd: H and W must be even");
+  long n = (long)B * (H / 2) * (W / 2) * (C / 8);
+  DISPATCH(dtype, hipLaunchKernelGGL(maxpool_bwd_kernel<T>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream,
+                                     (const T*)z, scale, shift, (const T*)dpool, (T*)dy_full, B, H, W, C));
+  return (int)hipGetLastError();
+}
+
+int crnn_bn_bwd_reduce(int dtype, const crnn_bn_bwd_desc* d, float* pg, float* pgx, int rows, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  DISPATCH(dtype, return chan_reduce(BnBwdF<T>{*d}, d->M, d->C, pg, pgx, rows, st));
+}
+
+int crnn_bn_bwd_finalize(const float* pg, const float* pgx, int rows, int C, long count, float* dgamma, float* dbeta,
+                         float* mean_g, float* mean_gx, int accumulate, void* stream) {
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 127) / 128), dim3(128), 0, (hipStream_t)stream, pg, pgx, rows, C,
+                     count, dgamma, dbeta, mean_g, mean_gx, accumulate);
+  return (int)hipGetLastError();
+}
+
+int crnn_bn_bwd_apply(int dtype, const crnn_bn_bwd_desc* d, const float* mean_g, const float* mean_gx, void* dz,
+                      void* stream) {
+  long nvec = d->M * d->C / 8;
+  DISPATCH(dtype, hipLaunchKernelGGL(bn_apply_bwd_kernel<T>, dim3(grid_for(nvec)), dim3(256), 0, (hipStream_t)stream,
+                                     *d, mean_g, mean_gx, (T*)dz, nvec));
+  return (int)hipGetLastError();
+}
+
+int crnn_se_pool(int dtype, const void* z2, const float* scale, const float* shift, float* pooled, int B, int HW, int C,
+                 void* stream) {
+  if (C % 8 || NT % (C / 8)) return crnn_set_error(hipErrorInvalidValue, "se_pool: bad C");
+  size_t sm = (size_t)(NT / (C / 8)) * C * sizeof(float);
+  DISPATCH(dtype, hipLaunchKernelGGL(sample_reduce_kernel<SePoolF<T>>, dim3(B), dim3(NT), sm, (hipStream_t)stream,
+                                     SePoolF<T>{(const T*)z2, scale, shift, HW, C}, HW, C, pooled, 1.f / (float)HW));
+  return (int)hipGetLastError();
+}
+
+int crnn_se_mlp_fwd(const float* pooled, const float* w1, const float* w2, float* hid, float* s, int B, int C, int Cr,
+                    void* stream) {
+  hipLaunchKernelGGL(se_mlp_fwd_kernel, dim3(B), dim3(256), (C + Cr) * sizeof(float), (hipStream_t)stream, pooled, w1,
+                     w2, hid, s, C, Cr);
+  return (int)hipGetLastError();
+}
+
+int crnn_se_residual_fwd(int dtype, const void* z2, const float* scale, const float* shift, const float* s,
+                         const void* idn, const float* iscale, const float* ishift, void* y, int B, int HW, int C,
+                         void* stream) {
+  long nvec = (long)B * HW * C / 8;
+  DISPATCH(dtype, hipLaunchKernelGGL(se_residual_kernel<T>, dim3(grid_for(nvec)), dim3(256), 0, (hipStream_t)stream,
+                                     (const T*)z2, scale, shift, s, (const T*)idn, iscale, ishift, (T*)y, nvec, HW, C));
+  return (int)hipGetLastError();
+}
+
+int crnn_se_bwd_reduce(int dtype, const void* dy, const void* y, const void* z2, const float* scale,
+                       const float* shift, float* ds, int B, int HW, int C, void* stream) {
+  if (C % 8 || NT % (C / 8)) return crnn_set_error(hipErrorInvalidValue, "se_bwd_reduce: bad C");
+  size_t sm = (size_t)(NT / (C / 8)) * C * sizeof(float);
+  DISPATCH(dtype, hipLaunchKernelGGL(sample_reduce_kernel<SeBwdF<T>>, dim3(B), dim3(NT), sm, (hipStream_t)stream,
+                                     SeBwdF<T>{(const T*)dy, (const T*)y, (const T*)z2, scale, shift, HW, C}, HW, C,
+                                     ds, 1.f));
+  return (int)hipGetLastError();
+}
+
+int crnn_se_mlp_bwd(const float* ds, const float* pooled, const float* hid, const float* s, const float* w1,
+                    const float* w2, float* dsig, float* dhid, float* dpool, float* dw1, float* dw2, int B, int C,
+                    int Cr, int HW, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(se_mlp_bwd_kernel, dim3(B), dim3(256), (C + Cr) * sizeof(float), st, ds, hid, s, w1, w2, dsig,
+                     dhid, dpool, C, Cr, 1.f / (float)HW);
+  int n = C * Cr;
+  hipLaunchKernelGGL(se_wgrad_kernel, dim3((n + 255) / 256), dim3(256), 0, st, dsig, hid, dhid, pooled, dw1, dw2, B, C,
+                     Cr);
+  return (int)hipGetLastError();
+}
+
+int crnn_hpool_fwd(int dtype, const void* z, const float* scale, const float* shift, void* seq, int B, int Hh, int W,
+                   int C, void* stream) {
+  long n = (long)B * W * (C / 8);
+  DISPATCH(dtype, hipLaunchKernelGGL(hpool_fwd_kernel<T>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream,
+                                     (const T*)z, scale, shift, (T*)seq, B, Hh, W, C));
+  return (int)hipGetLastError();
+}
+
+int crnn_hpool_bwd(int dtype, const void* dseq, void* dy_full, int B, int Hh, int W, int C, void* stream) {
+  long n = (long)B * Hh * W * (C / 8);
+  DISPATCH(dtype, hipLaunchKernelGGL(hpool_bwd_kernel<T>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream,
+                                     (const T*)dseq, (T*)dy_full, B, Hh, W, C));
+  return (int)hipGetLastError();
+}
+
+int crnn_nchw_to_nhwc(int dtype, const float* x, void* y, int B, int C, int H, int W, int Cp, void* stream) {
+  long n = (long)B * H * W;
+  DISPATCH(dtype, hipLaunchKernelGGL(nchw_to_nhwc_kernel<T>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, x,
+                                     (T*)y, B, C, H, W, Cp));
+  return (int)hipGetLastError();
+}
+
+int crnn_cast_f32(int dtype, const float* src, void* dst, long n, void* stream) {
+  DISPATCH(dtype, hipLaunchKernelGGL(cast_kernel<T>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, src, (T*)dst,
+                                     n));
+  return (int)hipGetLastError();
+}
+
+int crnn_pack_conv_weight(int dtype, const float* w, void* out, int Co, int Ci, int KH, int KW, int Cip, void* stream) {
+  long n = (long)Co * KH * KW * Cip;
+  DISPATCH(dtype, hipLaunchKernelGGL(pack_conv_kernel<T>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, w,
+                                     (T*)out, Co, Ci, KH, KW, Cip));
+  return (int)hipGetLastError();
+}
+
+int crnn_pack_rows(int dtype, const float* src, void* out, const int* perm, int rows_out, int rows_src, int cols,
+                   void* stream) {
+  long n = (long)rows_out * cols;
+  DISPATCH(dtype, hipLaunchKernelGGL(pack_rows_kernel<T>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, src,
+                                     (T*)out, perm, rows_out, rows_src, cols));
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

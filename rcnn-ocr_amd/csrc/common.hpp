@@ -1,0 +1,123 @@
+// Shared types and helpers for the CRNN HIP kernels (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+
+typedef __bf16 bf16;
+typedef bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x8 __attribute__((ext_vector_type(8)));
+
+// 8 elements of T, naturally the unit of a 16 B (bf16) / 32 B (f32) vector access.
+template <typename T> struct VT;
+template <> struct VT<float> { using v8 = f32x8; using v4 = f32x4; };
+template <> struct VT<bf16> { using v8 = bf16x8; using v4 = bf16x4; };
+
+__device__ __forceinline__ float tof(float x) { return x; }
+__device__ __forceinline__ float tof(bf16 x) { return (float)x; }
+template <typename T> __device__ __forceinline__ T fromf(float x);
+template <> __device__ __forceinline__ float fromf<float>(float x) { return x; }
+template <> __device__ __forceinline__ bf16 fromf<bf16>(float x) { return (bf16)x; }
+
+template <typename T>
+__device__ __forceinline__ typename VT<T>::v8 ld8(const T* p) {
+  if constexpr (sizeof(T) == 2) {
+    return *reinterpret_cast<const bf16x8*>(p);
+  } else {
+    f32x4 a = *reinterpret_cast<const f32x4*>(p);
+    f32x4 b = *reinterpret_cast<const f32x4*>(p + 4);
+    f32x8 r;
+    r[0] = a[0]; r[1] = a[1]; r[2] = a[2]; r[3] = a[3];
+    r[4] = b[0]; r[5] = b[1]; r[6] = b[2]; r[7] = b[3];
+    return r;
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ void st8(T* p, const typename VT<T>::v8& v) {
+  if constexpr (sizeof(T) == 2) {
+    *reinterpret_cast<bf16x8*>(p) = v;
+  } else {
+    f32x4 a, b;
+    a[0] = v[0]; a[1] = v[1]; a[2] = v[2]; a[3] = v[3];
+    b[0] = v[4]; b[1] = v[5]; b[2] = v[6]; b[3] = v[7];
+    *reinterpret_cast<f32x4*>(p) = a;
+    *reinterpret_cast<f32x4*>(p + 4) = b;
+  }
+}
+
+template <typename T> __device__ __forceinline__ typename VT<T>::v8 zero8() {
+  typename VT<T>::v8 z;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) z[i] = fromf<T>(0.f);
+  return z;
+}
+
+// 8 elements -> floats, and back
+template <typename T>
+__device__ __forceinline__ void unpack8(const typename VT<T>::v8& v, float* f) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) f[i] = tof(v[i]);
+}
+template <typename T>
+__device__ __forceinline__ typename VT<T>::v8 pack8(const float* f) {
+  typename VT<T>::v8 v;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = fromf<T>(f[i]);
+  return v;
+}
+
+// store 4 consecutive values (n..n+3) of one row
+template <typename T>
+__device__ __forceinline__ void st4(T* p, f32x4 v) {
+  if constexpr (sizeof(T) == 2) {
+    bf16x4 b;
+    b[0] = (bf16)v[0]; b[1] = (bf16)v[1]; b[2] = (bf16)v[2]; b[3] = (bf16)v[3];
+    *reinterpret_cast<bf16x4*>(p) = b;
+  } else {
+    *reinterpret_cast<f32x4*>(p) = v;
+  }
+}
+template <typename T>
+__device__ __forceinline__ f32x4 ld4f(const T* p) {
+  f32x4 r;
+  if constexpr (sizeof(T) == 2) {
+    bf16x4 b = *reinterpret_cast<const bf16x4*>(p);
+    r[0] = (float)b[0]; r[1] = (float)b[1]; r[2] = (float)b[2]; r[3] = (float)b[3];
+  } else {
+    r = *reinterpret_cast<const f32x4*>(p);
+  }
+  return r;
+}
+
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
+__device__ __forceinline__ float tanhf_(float x) {
+  // tanh via exp, saturating for large |x|
+  float e = __expf(-2.f * fabsf(x));
+  float t = (1.f - e) / (1.f + e);
+  return copysignf(t, x);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Bijective XCD-aware remap (cdna_hip_programming.md §5 / T1): consecutive logical
+// tiles land on the same XCD so their shared operand panels hit one L2.
+__device__ __forceinline__ int xcd_remap(int b, int nwg) {
+  const int nx = 8;
+  int xcd = b % nx, q = nwg / nx, r = nwg % nx;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + b / nx;
+}
+
+#define CRNN_CHECK_LAUNCH() return (int)hipGetLastError()

@@ -1,0 +1,210 @@
+// CTC loss (log-space alpha/beta, blank = 0) + greedy decode, and fused AdamW.
+//
+// The reference has no CTC loss; semantics follow
+// torch.nn.functional.ctc_loss(log_softmax(logits), blank=0, reduction='mean',
+// zero_infinity) as restated in oracle/ctc_oracle.py. Greedy decode follows
+// training/utils.py:122-150 (argmax, collapse repeats with prev updated at every
+// t, drop blank) with an explicit [B][T] layout.
+// AdamW follows torch.optim.AdamW (training/train.py:294-295).
+#include <math.h>
+#include "common.hpp"
+#include "crnn_internal.hpp"
+
+namespace {
+
+__device__ __forceinline__ float lse2(float a, float b) {
+  float m = fmaxf(a, b);
+  if (m == -INFINITY) return -INFINITY;
+  return m + logf(__expf(a - m) + __expf(b - m));
+}
+
+// one workgroup per sample
+__global__ __launch_bounds__(256) void ctc_kernel(const float* __restrict__ logits, int ldc, int T, int C,
+                                                  const int* __restrict__ targets, int Lmax,
+                                                  const int* __restrict__ lengths, float* __restrict__ loss,
+                                                  float* __restrict__ dlogits, int zero_inf, float inv_B) {
+  extern __shared__ float sm[];
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nw = blockDim.x / 64;
+  int L = lengths[b];
+  if (L > Lmax) L = Lmax;
+  if (L < 0) L = 0;
+  const int S = 2 * L + 1;
+  float* lse = sm;                    // [T]
+  float* alpha = lse + T;             // [T][S]
+  float* bcur = alpha + (size_t)T * S;  // [S]
+  float* bnxt = bcur + S;             // [S]
+  float* grow = bnxt + S;             // [C]
+  int* ext = (int*)(grow + C);        // [S]
+  const float* lg = logits + (size_t)b * T * ldc;
+
+  for (int t = wid; t < T; t += nw) {
+    float m = -INFINITY;
+    for (int c = lane; c < C; c += 64) m = fmaxf(m, lg[(size_t)t * ldc + c]);
+    m = wave_max(m);
+    float s = 0.f;
+    for (int c = lane; c < C; c += 64) s += __expf(lg[(size_t)t * ldc + c] - m);
+    s = wave_sum(s);
+    if (lane == 0) lse[t] = m + logf(s);
+  }
+  for (int s = tid; s < S; s += blockDim.x) ext[s] = (s & 1) ? targets[(size_t)b * Lmax + (s >> 1)] : 0;
+  __syncthreads();
+#define LP(t, c) (lg[(size_t)(t) * ldc + (c)] - lse[(t)])
+  for (int s = tid; s < S; s += blockDim.x) alpha[s] = s < 2 ? LP(0, ext[s]) : -INFINITY;
+  for (int t = 1; t < T; ++t) {
+    __syncthreads();
+    for (int s = tid; s < S; s += blockDim.x) {
+      const float* ap = alpha + (size_t)(t - 1) * S;
+      float a = ap[s];
+      if (s >= 1) a = lse2(a, ap[s - 1]);
+      if (s >= 2 && ext[s] != 0 && ext[s] != ext[s - 2]) a = lse2(a, ap[s - 2]);
+      alpha[(size_t)t * S + s] = a + LP(t, ext[s]);
+    }
+  }
+  __syncthreads();
+  float ll = alpha[(size_t)(T - 1) * S + S - 1];
+  if (S > 1) ll = lse2(ll, alpha[(size_t)(T - 1) * S + S - 2]);
+  const float nll = -ll;
+  const bool bad = !(nll < INFINITY);
+  if (tid == 0) loss[b] = (bad && zero_inf) ? 0.f : nll;
+  if (dlogits == nullptr) return;
+  float* dl = dlogits + (size_t)b * T * ldc;
+  const float scale = inv_B / (float)(L > 0 ? L : 1);
+  if (bad) {
+    const float fill = zero_inf ? 0.f : NAN;
+    for (int i = tid; i < T * ldc; i += blockDim.x) dl[i] = (i % ldc) < C ? fill : 0.f;
+    return;
+  }
+  for (int s = tid; s < S; s += blockDim.x) bnxt[s] = (s >= S - 2) ? LP(T - 1, ext[s]) : -INFINITY;
+  __syncthreads();
+  for (int t = T - 1; t >= 0; --t) {
+    // beta_t into bcur (bnxt holds beta_{t+1}; at t = T-1 it already is beta_{T-1})
+    for (int s = tid; s < S; s += blockDim.x) {
+      float v;
+      if (t == T - 1) {
+        v = bnxt[s];
+      } else {
+        v = bnxt[s];
+        if (s + 1 < S) v = lse2(v, bnxt[s + 1]);
+        if (s + 2 < S && ext[s] != 0 && ext[s] != ext[s + 2]) v = lse2(v, bnxt[s + 2]);
+        v += LP(t, ext[s]);
+      }
+      bcur[s] = v;
+    }
+    for (int c = tid; c < C; c += blockDim.x) grow[c] = __expf(LP(t, c));
+    __syncthreads();
+    for (int s = tid; s < S; s += blockDim.x) {
+      float e = alpha[(size_t)t * S + s] + bcur[s] - LP(t, ext[s]) - ll;
+      if (e > -INFINITY) atomicAdd(&grow[ext[s]], -__expf(e));
+    }
+    __syncthreads();
+    for (int c = tid; c < ldc; c += blockDim.x) dl[(size_t)t * ldc + c] = c < C ? grow[c] * scale : 0.f;
+    for (int s = tid; s < S; s += blockDim.x) bnxt[s] = bcur[s];
+    __syncthreads();
+  }
+#undef LP
+}
+
+__global__ void ctc_mean_kernel(const float* loss, const int* lengths, int B, float* out) {
+  __shared__ float red[256];
+  float s = 0.f;
+  for (int b = threadIdx.x; b < B; b += blockDim.x) {
+    int L = lengths[b];
+    s += loss[b] / (float)(L > 0 ? L : 1);
+  }
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = red[0] / (float)B;
+}
+
+// one wave per sample: argmax per t (first index on ties), then collapse
+__global__ void greedy_kernel(const float* __restrict__ logits, int ldc, int B, int T, int C, int* __restrict__ ids,
+                              int* __restrict__ lens) {
+  const int b = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (b >= B) return;
+  int prev = 0, n = 0;
+  for (int t = 0; t < T; ++t) {
+    const float* row = logits + ((size_t)b * T + t) * ldc;
+    float bv = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int c = lane; c < C; c += 64) {
+      float v = row[c];
+      if (v > bv || (v == bv && c < bi)) { bv = v; bi = c; }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      float ov = __shfl_xor(bv, o, 64);
+      int oi = __shfl_xor(bi, o, 64);
+      if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+    }
+    if (bi != 0 && bi != prev) {
+      if (lane == 0) ids[(size_t)b * T + n] = bi;
+      ++n;
+    }
+    prev = bi;
+  }
+  for (int i = n + lane; i < T; i += 64) ids[(size_t)b * T + i] = 0;
+  if (lane == 0) lens[b] = n;
+}
+
+__global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                             float* __restrict__ v, long n, float lr, float b1, float b2, float eps, float wd,
+                             float step_size, float inv_sqrt_bc2, float gs) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    float gr = g[i] * gs;
+    float pv = p[i] * (1.f - lr * wd);
+    float mv = m[i];
+    mv = mv + (1.f - b1) * (gr - mv);
+    float vv = v[i] * b2 + (1.f - b2) * gr * gr;
+    float denom = sqrtf(vv) * inv_sqrt_bc2 + eps;
+    pv -= step_size * mv / denom;
+    p[i] = pv;
+    m[i] = mv;
+    v[i] = vv;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int crnn_ctc_loss(const float* logits, int ldc, int B, int T, int C, const int* targets, int Lmax, const int* lengths,
+                  float* loss, float* dlogits, int zero_inf, void* stream) {
+  const int S = 2 * Lmax + 1;
+  size_t sm = ((size_t)T + (size_t)T * S + 2 * S + C) * sizeof(float) + S * sizeof(int);
+  if (sm > 160 * 1024) return crnn_set_error(hipErrorInvalidValue, "ctc_loss: T x (2*Lmax+1) too large for LDS");
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute((const void*)ctc_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(ctc_kernel, dim3(B), dim3(256), sm, (hipStream_t)stream, logits, ldc, T, C, targets, Lmax, lengths,
+                     loss, dlogits, zero_inf, 1.f / (float)B);
+  return (int)hipGetLastError();
+}
+
+int crnn_ctc_reduce_mean(const float* loss, const int* lengths, int B, float* out, void* stream) {
+  hipLaunchKernelGGL(ctc_mean_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, loss, lengths, B, out);
+  return (int)hipGetLastError();
+}
+
+int crnn_ctc_greedy(const float* logits, int ldc, int B, int T, int C, int* ids, int* lens, void* stream) {
+  hipLaunchKernelGGL(greedy_kernel, dim3((B + 3) / 4), dim3(256), 0, (hipStream_t)stream, logits, ldc, B, T, C, ids, lens);
+  return (int)hipGetLastError();
+}
+
+int crnn_adamw(float* p, const float* g, float* m, float* v, long n, float lr, float beta1, float beta2, float eps,
+               float weight_decay, int step, float grad_scale, void* stream) {
+  double bc1 = 1.0 - pow((double)beta1, (double)step);
+  double bc2 = 1.0 - pow((double)beta2, (double)step);
+  float step_size = (float)((double)lr / bc1);
+  float inv_sqrt_bc2 = (float)(1.0 / sqrt(bc2));
+  hipLaunchKernelGGL(adamw_kernel, dim3(grid_for(n, 256, 16384)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n, lr,
+                     beta1, beta2, eps, weight_decay, step_size, inv_sqrt_bc2, grad_scale);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

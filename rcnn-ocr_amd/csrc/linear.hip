@@ -1,0 +1,165 @@
+// Dense products for nn.Linear layers on the hot path (BiLSTM output projection,
+// model/model.py:157,162; CTC head) and their gradients, on the
+// shared MFMA GEMM core.
+#include "gemm.hpp"
+#include "crnn_internal.hpp"
+
+using namespace gemm;
+
+namespace {
+
+template <typename T> struct OutEpi {
+  static constexpr bool kStats = false;
+  void* c;
+  int ldc, M, N, c_f32, accumulate, atomic;
+  const float* bias;
+  __device__ __forceinline__ void store(int m, int n, f32x4 v, int) const {
+    if (m >= M || n >= N) return;
+    if (bias) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] += (n + r < N) ? bias[n + r] : 0.f;
+    }
+    size_t o = (size_t)m * ldc + n;
+    if (c_f32) {
+      float* p = (float*)c + o;
+      if (atomic) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (n + r < N) atomicAdd(p + r, v[r]);
+        return;
+      }
+      if (n + 4 <= N && (ldc % 4) == 0) {
+        if (accumulate) v += *reinterpret_cast<const f32x4*>(p);
+        *reinterpret_cast<f32x4*>(p) = v;
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (n + r < N) p[r] = accumulate ? p[r] + v[r] : v[r];
+      }
+    } else {
+      T* p = (T*)c + o;
+      if (n + 4 <= N && (ldc % 4) == 0) {
+        if (accumulate) v += ld4f<T>(p);
+        st4<T>(p, v);
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (n + r < N) p[r] = fromf<T>(accumulate ? tof(p[r]) + v[r] : v[r]);
+      }
+    }
+  }
+  __device__ __forceinline__ void stats(int, int, f32x4, f32x4) const {}
+};
+
+template <typename T, class LA, class LB>
+int run(const LA& la, const LB& lb, const OutEpi<T>& ep, int M, int N, int K, int splits, hipStream_t st) {
+  long work = (long)M * N;
+  if (M >= 128 && N >= 128 && work >= 128L * 128 * 128) return launch<T, 128, 128>(la, lb, ep, M, N, K, splits, st);
+  if (work >= 64L * 64 * 128) return launch<T, 64, 64>(la, lb, ep, M, N, K, splits, st);
+  return launch<T, 32, 32>(la, lb, ep, M, N, K, splits, st);
+}
+
+template <typename T>
+int gemm_nt_t(const void* A, int lda, const void* B, int ldb, void* C, int ldc, const float* bias, int M, int N, int K,
+              int c_f32, int acc, hipStream_t st) {
+  RowMajorK<T> la{(const T*)A, lda, M, K};
+  RowMajorK<T> lb{(const T*)B, ldb, N, K};
+  OutEpi<T> ep{C, ldc, M, N, c_f32, acc, 0, bias};
+  return run<T>(la, lb, ep, M, N, K, 1, st);
+}
+
+template <typename T>
+int gemm_nn_t(const void* A, int lda, const void* B, int ldb, void* C, int ldc, int M, int N, int K, int c_f32, int acc,
+              hipStream_t st) {
+  RowMajorK<T> la{(const T*)A, lda, M, K};
+  ColMajorK<T> lb{(const T*)B, ldb, N, K};
+  OutEpi<T> ep{C, ldc, M, N, c_f32, acc, 0, nullptr};
+  return run<T>(la, lb, ep, M, N, K, 1, st);
+}
+
+template <typename T>
+int gemm_tn_t(const void* A, int lda, const void* B, int ldb, float* C, int ldc, int M, int N, int K, int acc,
+              hipStream_t st) {
+  ColMajorK<T> la{(const T*)A, lda, M, K};
+  ColMajorK<T> lb{(const T*)B, ldb, N, K};
+  int b = (M >= 128 && N >= 128) ? 128 : (M >= 64 && N >= 64 ? 64 : 32);
+  long tiles = (long)((M + b - 1) / b) * ((N + b - 1) / b);
+  long want = (512 + tiles - 1) / tiles;
+  long maxs = (K + 4 * BK - 1) / (4 * BK);
+  if (want > maxs) want = maxs;
+  if (want < 1) want = 1;
+  int splits = eff_splits(K, (int)want);
+  if (splits > 1 && !acc) {
+    for (int m = 0; m < 1; ++m) {
+      hipError_t e = ldc == N ? hipMemsetAsync(C, 0, (size_t)M * N * sizeof(float), st)
+                              : hipMemset2DAsync(C, (size_t)ldc * sizeof(float), 0, (size_t)N * sizeof(float), M, st);
+      if (e != hipSuccess) return (int)e;
+    }
+  }
+  OutEpi<T> ep{C, ldc, M, N, 1, acc, splits > 1 ? 1 : 0, nullptr};
+  if (b == 128) return launch<T, 128, 128>(la, lb, ep, M, N, K, splits, st);
+  if (b == 64) return launch<T, 64, 64>(la, lb, ep, M, N, K, splits, st);
+  return launch<T, 32, 32>(la, lb, ep, M, N, K, splits, st);
+}
+
+// out[n] += sum over a row chunk; grid (ceil(N/64), row chunks)
+template <typename T>
+__global__ void colsum_kernel(const T* __restrict__ X, int ld, long M, int N, long rpc, float* __restrict__ out) {
+  __shared__ float red[4][64];
+  const int c = threadIdx.x & 63, r = threadIdx.x >> 6;
+  const int n = blockIdx.x * 64 + c;
+  const long m0 = blockIdx.y * rpc, m1 = min(M, m0 + rpc);
+  float s = 0.f;
+  if (n < N)
+    for (long m = m0 + r; m < m1; m += 4) s += tof(X[m * ld + n]);
+  red[r][c] = s;
+  __syncthreads();
+  if (r == 0 && n < N) atomicAdd(out + n, red[0][c] + red[1][c] + red[2][c] + red[3][c]);
+}
+
+}  // namespace
+
+extern "C" {
+
+int crnn_gemm_nt(int dtype, const void* A, int lda, const void* B, int ldb, void* C, int ldc, const float* bias, int M,
+                 int N, int K, int c_f32, int accumulate, void* stream) {
+  if (K % 8 || lda % 8 || ldb % 8) return crnn_set_error(hipErrorInvalidValue, "gemm_nt: K/lda/ldb must be multiples of 8");
+  hipStream_t st = (hipStream_t)stream;
+  return dtype == CRNN_BF16 ? gemm_nt_t<bf16>(A, lda, B, ldb, C, ldc, bias, M, N, K, c_f32, accumulate, st)
+                            : gemm_nt_t<float>(A, lda, B, ldb, C, ldc, bias, M, N, K, c_f32, accumulate, st);
+}
+
+int crnn_gemm_nn(int dtype, const void* A, int lda, const void* B, int ldb, void* C, int ldc, int M, int N, int K,
+                 int c_f32, int accumulate, void* stream) {
+  if (K % 8 || N % 8 || lda % 8 || ldb % 8) return crnn_set_error(hipErrorInvalidValue, "gemm_nn: K/N/ld must be multiples of 8");
+  hipStream_t st = (hipStream_t)stream;
+  return dtype == CRNN_BF16 ? gemm_nn_t<bf16>(A, lda, B, ldb, C, ldc, M, N, K, c_f32, accumulate, st)
+                            : gemm_nn_t<float>(A, lda, B, ldb, C, ldc, M, N, K, c_f32, accumulate, st);
+}
+
+int crnn_gemm_tn(int dtype, const void* A, int lda, const void* B, int ldb, float* C, int ldc, int M, int N, int K,
+                 int accumulate, void* stream) {
+  if (M % 8 || N % 8 || lda % 8 || ldb % 8) return crnn_set_error(hipErrorInvalidValue, "gemm_tn: M/N/ld must be multiples of 8");
+  hipStream_t st = (hipStream_t)stream;
+  return dtype == CRNN_BF16 ? gemm_tn_t<bf16>(A, lda, B, ldb, C, ldc, M, N, K, accumulate, st)
+                            : gemm_tn_t<float>(A, lda, B, ldb, C, ldc, M, N, K, accumulate, st);
+}
+
+int crnn_colsum(int dtype, const void* X, int ld, long M, int N, float* out, int accumulate, int x_f32, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (!accumulate) {
+    hipError_t e = hipMemsetAsync(out, 0, (size_t)N * sizeof(float), st);
+    if (e != hipSuccess) return (int)e;
+  }
+  long chunks = (M + 255) / 256;
+  if (chunks > 512) chunks = 512;
+  long rpc = (M + chunks - 1) / chunks;
+  dim3 grid((N + 63) / 64, (unsigned)chunks);
+  if (x_f32 || dtype != CRNN_BF16)
+    hipLaunchKernelGGL(colsum_kernel<float>, grid, dim3(256), 0, st, (const float*)X, ld, M, N, rpc, out);
+  else
+    hipLaunchKernelGGL(colsum_kernel<bf16>, grid, dim3(256), 0, st, (const bf16*)X, ld, M, N, rpc, out);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

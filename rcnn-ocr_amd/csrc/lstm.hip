@@ -1,0 +1,351 @@
+// Bidirectional LSTM (nn.LSTM(in, H, bidirectional=True, batch_first=True),
+// model/model.py:152-163; gate order i,f,g,o; h0 = c0 = 0) — recurrence and BPTT.
+//
+// The input projection x W_ih^T + b_ih + b_hh for all T and both directions is
+// one GEMM (crnn_gemm_nt) done before the recurrence. Each recurrent step is
+// one MFMA GEMM  h_{t-1} [B x H] . W_hh'^T [H x 4H]  whose epilogue finishes
+// the cell: weights are packed with gate-interleaved rows (packed row 4j+q =
+// reference row q*H+j) so the swapped-MFMA accumulator layout hands every lane
+// the four gate pre-activations (i,f,g,o) of one (b, j) — sigmoid/tanh, the
+// cell update and h are computed in registers with no extra pass.
+// BPTT mirrors it: step s's GEMM dgates_{s-1} . W_hh' produces dh_rec and its
+// epilogue runs the cell backward of step s (again one lane per (b, 4 units)).
+#include "gemm.hpp"
+#include "crnn_internal.hpp"
+
+using namespace gemm;
+
+namespace {
+
+// ---------------------------------------------------------------- forward step
+template <typename T> struct StepFwdEpi {
+  static constexpr bool kStats = false;
+  const T* xg;   // [B][T][2][4H]
+  T* hseq;       // [B][T][2H]
+  T* gsv;        // [2][T][B][4H]
+  float* csv;    // [2][T][B][H]
+  int B, Tn, H, d, t, tp, first;
+  __device__ __forceinline__ void store(int b, int n, f32x4 v, int) const {
+    if (b >= B || n >= 4 * H) return;
+    const int j = n >> 2, H4 = 4 * H;
+    f32x4 x = ld4f<T>(xg + ((size_t)b * Tn + t) * 2 * H4 + d * H4 + n);
+    v += x;
+    float ig = sigmoidf_(v[0]), fg = sigmoidf_(v[1]), gg = tanhf_(v[2]), og = sigmoidf_(v[3]);
+    float cp = first ? 0.f : csv[((size_t)(d * Tn + tp) * B + b) * H + j];
+    float c = fg * cp + ig * gg;
+    float h = og * tanhf_(c);
+    csv[((size_t)(d * Tn + t) * B + b) * H + j] = c;
+    st4<T>(gsv + ((size_t)(d * Tn + t) * B + b) * H4 + n, f32x4{ig, fg, gg, og});
+    hseq[((size_t)b * Tn + t) * 2 * H + d * H + j] = fromf<T>(h);
+  }
+  __device__ __forceinline__ void stats(int, int, f32x4, f32x4) const {}
+};
+
+template <typename T>
+int step_fwd_t(const void* xg, const void* whh, void* hseq, void* gsv, float* csv, int B, int Tn, int H, int s,
+               hipStream_t st) {
+  for (int d = 0; d < 2; ++d) {
+    int t = d == 0 ? s : Tn - 1 - s;
+    int tp = d == 0 ? t - 1 : t + 1;
+    int first = s == 0;
+    // A: h_{t-1} rows b, k = j  (all-zero rows at the first step)
+    RowMajorK<T> la{(const T*)hseq + (size_t)(first ? 0 : tp) * 2 * H + d * H, Tn * 2 * H, first ? 0 : B, H};
+    RowMajorK<T> lb{(const T*)whh + (size_t)d * 4 * H * H, H, 4 * H, H};
+    StepFwdEpi<T> ep{(const T*)xg, (T*)hseq, (T*)gsv, csv, B, Tn, H, d, t, tp, first};
+    int rc;
+    if ((long)B * 4 * H >= 64L * 64 * 256) rc = launch<T, 64, 64>(la, lb, ep, B, 4 * H, H, 1, st);
+    else rc = launch<T, 32, 32>(la, lb, ep, B, 4 * H, H, 1, st);
+    if (rc) return rc;
+  }
+  return 0;
+}
+
+// ---------------------------------------------------------------- backward step
+// cell backward for unit u of (d, t, b), given dh_rec (recurrent part of dh)
+template <typename T>
+__device__ __forceinline__ void cell_bwd(const T* dhseq, const T* gsv, const float* csv, T* dgates, float* dc, int B,
+                                         int Tn, int H, int d, int t, int b, int u, float dh_rec) {
+  const int H4 = 4 * H;
+  const size_t gi = ((size_t)(d * Tn + t) * B + b) * H4 + 4 * u;
+  f32x4 g = ld4f<T>(gsv + gi);
+  float ig = g[0], fg = g[1], gg = g[2], og = g[3];
+  float c = csv[((size_t)(d * Tn + t) * B + b) * H + u];
+  int tf = d == 0 ? t - 1 : t + 1;  // previous time in the forward recurrence
+  bool has_prev = d == 0 ? t > 0 : t < Tn - 1;
+  float cp = has_prev ? csv[((size_t)(d * Tn + tf) * B + b) * H + u] : 0.f;
+  float dh = dh_rec + tof(dhseq[((size_t)b * Tn + t) * 2 * H + d * H + u]);
+  float tc = tanhf_(c);
+  float* dcp = dc + ((size_t)d * B + b) * H + u;
+  float dcv = *dcp + dh * og * (1.f - tc * tc);
+  float do_ = dh * tc;
+  float di = dcv * gg, dg = dcv * ig, df = dcv * cp;
+  *dcp = dcv * fg;
+  st4<T>(dgates + gi, f32x4{di * ig * (1.f - ig), df * fg * (1.f - fg), dg * (1.f - gg * gg), do_ * og * (1.f - og)});
+}
+
+template <typename T> struct StepBwdEpi {
+  static constexpr bool kStats = false;
+  const T* dhseq;
+  const T* gsv;
+  const float* csv;
+  T* dgates;
+  float* dc;
+  int B, Tn, H, d, t;
+  __device__ __forceinline__ void store(int b, int n, f32x4 v, int) const {
+    if (b >= B || n >= H) return;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) cell_bwd<T>(dhseq, gsv, csv, dgates, dc, B, Tn, H, d, t, b, n + r, v[r]);
+  }
+  __device__ __forceinline__ void stats(int, int, f32x4, f32x4) const {}
+};
+
+template <typename T>
+__global__ void bptt_init_kernel(const T* dhseq, const T* gsv, const float* csv, T* dgates, float* dc, int B, int Tn,
+                                 int H) {
+  const long n = 2L * B * H;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    int u = (int)(i % H);
+    long q = i / H;
+    int b = (int)(q % B), d = (int)(q / B);
+    dc[((size_t)d * B + b) * H + u] = 0.f;
+    int t = d == 0 ? Tn - 1 : 0;
+    cell_bwd<T>(dhseq, gsv, csv, dgates, dc, B, Tn, H, d, t, b, u, 0.f);
+  }
+}
+
+template <typename T>
+int step_bwd_t(const void* dhseq, const void* whh, const void* gsv, const float* csv, void* dgates, float* dc, int B,
+               int Tn, int H, int s, hipStream_t st) {
+  if (s == 0) {
+    long n = 2L * B * H;
+    hipLaunchKernelGGL(bptt_init_kernel<T>, dim3(grid_for(n)), dim3(256), 0, st, (const T*)dhseq, (const T*)gsv, csv,
+                       (T*)dgates, dc, B, Tn, H);
+    return (int)hipGetLastError();
+  }
+  for (int d = 0; d < 2; ++d) {
+    int t = d == 0 ? Tn - 1 - s : s;  // time processed now
+    int tn = d == 0 ? t + 1 : t - 1;  // time processed at step s-1
+    RowMajorK<T> la{(const T*)dgates + (size_t)(d * Tn + tn) * B * 4 * H, 4 * H, B, 4 * H};
+    ColMajorK<T> lb{(const T*)whh + (size_t)d * 4 * H * H, H, H, 4 * H};
+    StepBwdEpi<T> ep{(const T*)dhseq, (const T*)gsv, csv, (T*)dgates, dc, B, Tn, H, d, t};
+    int rc;
+    if ((long)B * H >= 64L * 64 * 256) rc = launch<T, 64, 64>(la, lb, ep, B, H, 4 * H, 1, st);
+    else rc = launch<T, 32, 32>(la, lb, ep, B, H, 4 * H, 1, st);
+    if (rc) return rc;
+  }
+  return 0;
+}
+
+// ---------------------------------------------------------------- weight grads
+// A: dgates as rows g' (packed), k = t*B + b : element at dg[k*4H + g']
+// B (dW_hh): h_{t-1} rows j, k = t*B + b
+template <typename T> struct HPrevB {
+  static constexpr bool kRowVec = true;
+  const T* hseq;
+  int B, Tn, H, d;
+  struct Ctx { int j; bool ok; };
+  __device__ __forceinline__ Ctx row_ctx(int r8) const { return Ctx{r8, r8 < H}; }
+  __device__ __forceinline__ typename VT<T>::v8 load(const Ctx& c, int k) const {
+    if (!c.ok || k >= Tn * B) return zero8<T>();
+    int t = k / B, b = k - t * B;
+    int tp = d == 0 ? t - 1 : t + 1;
+    if (tp < 0 || tp >= Tn) return zero8<T>();
+    return ld8<T>(hseq + ((size_t)b * Tn + tp) * 2 * H + d * H + c.j);
+  }
+};
+// B (dW_ih): x rows i, k = t*B + b : x[b][t][i]
+template <typename T> struct XB {
+  static constexpr bool kRowVec = true;
+  const T* x;
+  int B, Tn, In;
+  struct Ctx { int i; bool ok; };
+  __device__ __forceinline__ Ctx row_ctx(int r8) const { return Ctx{r8, r8 < In}; }
+  __device__ __forceinline__ typename VT<T>::v8 load(const Ctx& c, int k) const {
+    if (!c.ok || k >= Tn * B) return zero8<T>();
+    int t = k / B, b = k - t * B;
+    return ld8<T>(x + ((size_t)b * Tn + t) * In + c.i);
+  }
+};
+
+// writes rows in reference gate order: packed row g' = 4j+q -> q*H + j
+struct GateRowEpi {
+  static constexpr bool kStats = false;
+  float* out;  // [4H][N]
+  int H, N, atomic, accumulate;
+  __device__ __forceinline__ void store(int gp, int n, f32x4 v, int) const {
+    if (gp >= 4 * H || n >= N) return;
+    int row = (gp & 3) * H + (gp >> 2);
+    float* p = out + (size_t)row * N + n;
+    if (atomic) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (n + r < N) atomicAdd(p + r, v[r]);
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (n + r < N) p[r] = accumulate ? p[r] + v[r] : v[r];
+    }
+  }
+  __device__ __forceinline__ void stats(int, int, f32x4, f32x4) const {}
+};
+
+template <typename T, class LB>
+int gate_wgrad(const T* dgates_d, const LB& lb, float* out, int B, int Tn, int H, int N, int accumulate, hipStream_t st) {
+  const int K = Tn * B;
+  ColMajorK<T> la{dgates_d, 4 * H, 4 * H, K};
+  const int b = (4 * H >= 128 && N >= 128) ? 128 : 64;
+  long tiles = (long)((4 * H + b - 1) / b) * ((N + b - 1) / b);
+  long want = (256 + tiles - 1) / tiles;
+  long maxs = (K + 4 * BK - 1) / (4 * BK);
+  if (want > maxs) want = maxs;
+  if (want < 1) want = 1;
+  int splits = eff_splits(K, (int)want);
+  if (splits > 1 && !accumulate) {
+    hipError_t e = hipMemsetAsync(out, 0, (size_t)4 * H * N * sizeof(float), st);
+    if (e != hipSuccess) return (int)e;
+  }
+  GateRowEpi ep{out, H, N, splits > 1 ? 1 : 0, accumulate};
+  if (b == 128) return launch<T, 128, 128>(la, lb, ep, 4 * H, N, K, splits, st);
+  return launch<T, 64, 64>(la, lb, ep, 4 * H, N, K, splits, st);
+}
+
+// db[d][q*H+j] = sum_k dgates[d][k][4j+q]
+template <typename T>
+__global__ void dbias_kernel(const T* __restrict__ dg, float* __restrict__ db, int K, int H, long rpc) {
+  __shared__ float red[4][64];
+  const int c = threadIdx.x & 63, r = threadIdx.x >> 6;
+  const int H4 = 4 * H, d = blockIdx.z;
+  const int gp = blockIdx.x * 64 + c;
+  const long k0 = blockIdx.y * rpc, k1 = min((long)K, k0 + rpc);
+  const T* p = dg + (size_t)d * K * H4;
+  float s = 0.f;
+  if (gp < H4)
+    for (long k = k0 + r; k < k1; k += 4) s += tof(p[k * H4 + gp]);
+  red[r][c] = s;
+  __syncthreads();
+  if (r == 0 && gp < H4) {
+    int row = (gp & 3) * H + (gp >> 2);
+    atomicAdd(db + (size_t)d * H4 + row, red[0][c] + red[1][c] + red[2][c] + red[3][c]);
+  }
+}
+
+// dx: A rows m = b*T + t, k = (d, g') -> dgates[(d*T + t)*B + b][g']
+template <typename T> struct DgatesA {
+  static constexpr bool kRowVec = false;
+  const T* dg;
+  int B, Tn, H;
+  struct Ctx { int b, t; bool ok; };
+  __device__ __forceinline__ Ctx row_ctx(int m) const {
+    Ctx c;
+    c.ok = m < B * Tn;
+    int mm = c.ok ? m : 0;
+    c.b = mm / Tn;
+    c.t = mm - c.b * Tn;
+    return c;
+  }
+  __device__ __forceinline__ typename VT<T>::v8 load(const Ctx& c, int k) const {
+    const int H4 = 4 * H;
+    if (!c.ok || k >= 2 * H4) return zero8<T>();
+    int d = k >= H4 ? 1 : 0, gp = k - d * H4;
+    return ld8<T>(dg + ((size_t)(d * Tn + c.t) * B + c.b) * H4 + gp);
+  }
+};
+
+template <typename T> struct StoreEpi {
+  static constexpr bool kStats = false;
+  T* y;
+  int M, N;
+  __device__ __forceinline__ void store(int m, int n, f32x4 v, int) const {
+    if (m < M && n < N) st4<T>(y + (size_t)m * N + n, v);
+  }
+  __device__ __forceinline__ void stats(int, int, f32x4, f32x4) const {}
+};
+
+}  // namespace
+
+extern "C" {
+
+int crnn_lstm_step_fwd(int dtype, const void* xg, const void* whh, void* hseq, void* gsv, float* csv, int B, int T,
+                       int H, int step, void* stream) {
+  if (H % 8) return crnn_set_error(hipErrorInvalidValue, "lstm: H must be a multiple of 8");
+  hipStream_t st = (hipStream_t)stream;
+  return dtype == CRNN_BF16 ? step_fwd_t<bf16>(xg, whh, hseq, gsv, csv, B, T, H, step, st)
+                            : step_fwd_t<float>(xg, whh, hseq, gsv, csv, B, T, H, step, st);
+}
+
+int crnn_lstm_step_bwd(int dtype, const void* dhseq, const void* whh, const void* gsv, const float* csv, void* dgates,
+                       float* dc, int B, int T, int H, int step, void* stream) {
+  if (H % 8) return crnn_set_error(hipErrorInvalidValue, "lstm: H must be a multiple of 8");
+  hipStream_t st = (hipStream_t)stream;
+  return dtype == CRNN_BF16 ? step_bwd_t<bf16>(dhseq, whh, gsv, csv, dgates, dc, B, T, H, step, st)
+                            : step_bwd_t<float>(dhseq, whh, gsv, csv, dgates, dc, B, T, H, step, st);
+}
+
+int crnn_lstm_dwhh(int dtype, const void* dgates, const void* hseq, float* dwhh, int B, int T, int H, int accumulate,
+                   void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  for (int d = 0; d < 2; ++d) {
+    size_t off = (size_t)d * T * B * 4 * H;
+    float* out = dwhh + (size_t)d * 4 * H * H;
+    int rc = dtype == CRNN_BF16
+                 ? gate_wgrad<bf16>((const bf16*)dgates + off, HPrevB<bf16>{(const bf16*)hseq, B, T, H, d}, out, B, T,
+                                    H, H, accumulate, st)
+                 : gate_wgrad<float>((const float*)dgates + off, HPrevB<float>{(const float*)hseq, B, T, H, d}, out, B,
+                                     T, H, H, accumulate, st);
+    if (rc) return rc;
+  }
+  return 0;
+}
+
+int crnn_lstm_dwih(int dtype, const void* dgates, const void* x, float* dwih, int B, int T, int H, int In,
+                   int accumulate, void* stream) {
+  if (In % 8) return crnn_set_error(hipErrorInvalidValue, "lstm: In must be a multiple of 8");
+  hipStream_t st = (hipStream_t)stream;
+  for (int d = 0; d < 2; ++d) {
+    size_t off = (size_t)d * T * B * 4 * H;
+    float* out = dwih + (size_t)d * 4 * H * In;
+    int rc = dtype == CRNN_BF16
+                 ? gate_wgrad<bf16>((const bf16*)dgates + off, XB<bf16>{(const bf16*)x, B, T, In}, out, B, T, H, In,
+                                    accumulate, st)
+                 : gate_wgrad<float>((const float*)dgates + off, XB<float>{(const float*)x, B, T, In}, out, B, T, H,
+                                     In, accumulate, st);
+    if (rc) return rc;
+  }
+  return 0;
+}
+
+int crnn_lstm_dbias(int dtype, const void* dgates, float* db, int B, int T, int H, int accumulate, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (!accumulate) {
+    hipError_t e = hipMemsetAsync(db, 0, (size_t)8 * H * sizeof(float), st);
+    if (e != hipSuccess) return (int)e;
+  }
+  int K = T * B;
+  long chunks = (K + 255) / 256;
+  if (chunks > 128) chunks = 128;
+  long rpc = (K + chunks - 1) / chunks;
+  dim3 grid((4 * H + 63) / 64, (unsigned)chunks, 2);
+  if (dtype == CRNN_BF16)
+    hipLaunchKernelGGL(dbias_kernel<bf16>, grid, dim3(256), 0, st, (const bf16*)dgates, db, K, H, rpc);
+  else
+    hipLaunchKernelGGL(dbias_kernel<float>, grid, dim3(256), 0, st, (const float*)dgates, db, K, H, rpc);
+  return (int)hipGetLastError();
+}
+
+int crnn_lstm_dx(int dtype, const void* dgates, const void* wih, void* dx, int B, int T, int H, int In, void* stream) {
+  if (In % 8) return crnn_set_error(hipErrorInvalidValue, "lstm: In must be a multiple of 8");
+  hipStream_t st = (hipStream_t)stream;
+  const int M = B * T, K = 8 * H;
+  if (dtype == CRNN_BF16) {
+    DgatesA<bf16> la{(const bf16*)dgates, B, T, H};
+    ColMajorK<bf16> lb{(const bf16*)wih, In, In, K};
+    StoreEpi<bf16> ep{(bf16*)dx, M, In};
+    return launch<bf16, 128, 128>(la, lb, ep, M, In, K, 1, st);
+  }
+  DgatesA<float> la{(const float*)dgates, B, T, H};
+  ColMajorK<float> lb{(const float*)wih, In, In, K};
+  StoreEpi<float> ep{(float*)dx, M, In};
+  return launch<float, 64, 64>(la, lb, ep, M, In, K, 1, st);
+}
+
+}  // extern "C"

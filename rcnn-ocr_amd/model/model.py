@@ -1,0 +1,178 @@
+"""RCNN with the reference's API (sherstpasha/RCNN-OCR model/model.py:166-227),
+running SE-ResNet31 -> BiLSTM -> CTC head on the MI355X HIP engine.
+
+    RCNN(num_classes, hidden_size=256, sos_id=1, eos_id=2, pad_id=0, blank_id=3,
+         enc_dropout_p=0.1, dropblock_p=0.0, dropblock_block_size=5,
+         decoder="ctc", num_rnn_layers=2, compute_dtype=torch.bfloat16)
+    .encode(x [B,3,H,W]) -> [B, T=W/8, hidden]        (model/model.py:215-221)
+    .forward(x, text=None, is_train=True, batch_max_length=25) -> CTC logits [B, T, C]
+
+State-dict keys are the reference's (cnn.*, enc_rnn.*) plus ctc_head.{weight,bias}
+(the reference's training head is an attention decoder; this path is CTC).
+Every forward/backward runs in libcrnn_hip.so; there is no CPU path — on a CPU
+tensor the module raises.
+"""
+from __future__ import annotations
+
+from typing import Dict, Optional
+
+import torch
+import torch.nn as nn
+
+from crnn_hip import _lib as L
+from crnn_hip.engine import CRNNEngine, round8
+from model.seresnet31 import SEResNet31
+
+
+class BidirectionalLSTM(nn.Module):
+    """parameter container with the reference's names (model/model.py:151-163)."""
+
+    def __init__(self, input_size, hidden_size, output_size):
+        super().__init__()
+        if output_size != hidden_size:
+            raise NotImplementedError("the HIP BiLSTM stack keeps output_size == hidden_size")
+        self.rnn = nn.LSTM(input_size, hidden_size, bidirectional=True, batch_first=True)
+        self.linear = nn.Linear(hidden_size * 2, output_size)
+
+    def forward(self, x):
+        raise NotImplementedError("BiLSTM layers run inside the HIP engine; call RCNN.encode/forward")
+
+
+class _EncodeFn(torch.autograd.Function):
+    """images -> logits via the engine; backward writes parameter gradients
+    straight into the flat grad buffer (the params' .grad views)."""
+
+    @staticmethod
+    def forward(ctx, anchor, images, model, need_grad):
+        eng = model._engine_for(images)
+        logits = eng.forward(images, train=model.training, save_for_backward=need_grad,
+                             update_running=model.training)
+        ctx.model = model
+        return logits.clone()
+
+    @staticmethod
+    def backward(ctx, grad_logits):
+        model = ctx.model
+        eng = model._engine
+        B, T, C = grad_logits.shape
+        dl = eng.ws.get("autograd.dlogits", (B, T, eng.Cpad), torch.float32)
+        dl[:, :, C:].zero_()
+        dl[:, :, :C].copy_(grad_logits)
+        grads, accumulate = model._grad_views()
+        eng.backward(dl, grads, accumulate=accumulate)
+        return None, None, None, None
+
+
+class RCNN(nn.Module):
+    def __init__(self, num_classes, hidden_size=256, sos_id: int = 1, eos_id: int = 2, pad_id: int = 0,
+                 blank_id: Optional[int] = 3, enc_dropout_p: float = 0.1, dropblock_p: float = 0.0,
+                 dropblock_block_size: int = 5, decoder: str = "ctc", num_rnn_layers: int = 2,
+                 compute_dtype: torch.dtype = torch.bfloat16):
+        super().__init__()
+        if decoder != "ctc":
+            raise NotImplementedError("decoder='attn' (model/model.py:23-148) is outside the MI355X hot path; "
+                                      "SURVEY.md §8(f) next-1")
+        self.num_classes = num_classes
+        self.hidden_size = hidden_size
+        self.sos_id, self.eos_id, self.pad_id, self.blank_id = sos_id, eos_id, pad_id, blank_id
+        self.decoder = decoder
+        self.num_rnn_layers = num_rnn_layers
+        self.compute_dtype = compute_dtype
+        self.cnn = SEResNet31(in_channels=3, out_channels=512, dropblock_p=dropblock_p,
+                              dropblock_block_size=dropblock_block_size)
+        self.pool = nn.AdaptiveAvgPool2d((1, None))
+        enc_dim = self.cnn.out_channels
+        layers = [BidirectionalLSTM(enc_dim, hidden_size, hidden_size)]
+        layers += [BidirectionalLSTM(hidden_size, hidden_size, hidden_size) for _ in range(1, num_rnn_layers)]
+        self.enc_rnn = nn.Sequential(*layers)
+        self.enc_dropout = nn.Dropout(enc_dropout_p)
+        self.ctc_head = nn.Linear(hidden_size, num_classes)
+        self._engine: Optional[CRNNEngine] = None
+        self._flat_param: Optional[torch.Tensor] = None
+        self._flat_grad: Optional[torch.Tensor] = None
+
+    # ------------------------------------------------------------------ engine plumbing
+    def _param_dict(self) -> Dict[str, torch.Tensor]:
+        return {k: v for k, v in self.named_parameters()}
+
+    def _buffer_dict(self) -> Dict[str, torch.Tensor]:
+        return {k: v for k, v in self.named_buffers()}
+
+    def flatten_parameters_(self):
+        """Make every parameter (and its .grad) a view into one fp32 buffer: one fused
+        AdamW launch and one RCCL all-reduce cover the whole model."""
+        params = list(self.parameters())
+        dev = params[0].device
+        n = sum(p.numel() for p in params)
+        if self._flat_param is not None and self._flat_param.device == dev:
+            return
+        flat = torch.empty(n, dtype=torch.float32, device=dev)
+        gflat = torch.zeros(n, dtype=torch.float32, device=dev)
+        off = 0
+        for p in params:
+            k = p.numel()
+            flat[off:off + k].copy_(p.data.reshape(-1))
+            p.data = flat[off:off + k].view_as(p)
+            p.grad = gflat[off:off + k].view_as(p)
+            off += k
+        self._flat_param, self._flat_grad = flat, gflat
+        self._grad_offsets = None
+
+    def _grad_views(self):
+        """(name -> grad tensor, accumulate?) ; re-attaches flat views after zero_grad(set_to_none=True)."""
+        params = list(self.named_parameters())
+        any_none = any(p.grad is None for _, p in params)
+        all_none = all(p.grad is None for _, p in params)
+        if any_none:
+            off = 0
+            for _, p in params:
+                k = p.numel()
+                if p.grad is None:
+                    g = self._flat_grad[off:off + k].view_as(p)
+                    if not all_none:
+                        g.zero_()
+                    p.grad = g
+                off += k
+        return {n: p.grad for n, p in params}, not all_none
+
+    def _engine_for(self, images: torch.Tensor) -> CRNNEngine:
+        L.require_device(images)
+        dev = images.device
+        if self._engine is None or self._engine.device != dev or self._flat_param is None \
+                or self._flat_param.device != dev:
+            if next(self.parameters()).device != dev:
+                raise RuntimeError("model parameters and images must be on the same HIP device")
+            self.flatten_parameters_()
+            self._engine = CRNNEngine(self._param_dict(), self._buffer_dict(), self.hidden_size,
+                                      self.num_classes, self.num_rnn_layers, self.compute_dtype,
+                                      version_source=self._param_version)
+        return self._engine
+
+    def _param_version(self) -> int:
+        # torch optimizers / load_state_dict modify parameters in place, bumping _version
+        return sum(p._version for p in self.parameters())
+
+    def mark_params_changed(self):
+        """call after modifying parameters in place (optimizer steps do this via hooks)."""
+        if self._engine is not None:
+            self._engine.mark_params_changed()
+
+    def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
+        r = super().load_state_dict(state_dict, strict=strict, assign=assign)
+        self.mark_params_changed()
+        return r
+
+    # ------------------------------------------------------------------ reference API
+    def encode(self, x):
+        """RCNN.encode (model/model.py:215-221): [B,3,H,W] -> [B, W/8, hidden] (inference)."""
+        eng = self._engine_for(x)
+        with torch.no_grad():
+            eng.forward(x, train=self.training, save_for_backward=False, update_running=self.training)
+        return eng.ws.bufs[f"r{self.num_rnn_layers - 1}.out"].float().clone()
+
+    def forward(self, x, text=None, is_train=True, batch_max_length=25):
+        """CTC logits [B, T, num_classes] (fp32). `text`/`batch_max_length` are accepted for
+        signature compatibility with the attention head and ignored (CTC is alignment-free)."""
+        self._engine_for(x)
+        anchor = next(self.parameters())
+        return _EncodeFn.apply(anchor, x, self, torch.is_grad_enabled() and anchor.requires_grad)

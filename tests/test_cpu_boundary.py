@@ -1,0 +1,79 @@
+"""CPU-only checks: the C-ABI library loads and exports every symbol include/crnn_hip.h
+declares (no compute calls), the ctypes table matches the header, the Python API keeps
+the reference's state-dict contract, and the HIP path refuses CPU tensors (no fallback)."""
+import os
+import re
+import subprocess
+
+import pytest
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "crnn_hip.h")
+
+
+def header_symbols():
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(crnn_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_library_exports_every_header_symbol():
+    from crnn_hip import _lib as L
+    if not os.path.exists(L.LIB_PATH):
+        L.build()
+    out = subprocess.run(["nm", "-D", "--defined-only", L.LIB_PATH], capture_output=True, text=True, check=True)
+    exported = set(re.findall(r"\bT (crnn_[a-z0-9_]+)", out.stdout))
+    missing = [s for s in header_symbols() if s not in exported]
+    assert not missing, missing
+
+
+def test_ctypes_table_covers_header():
+    from crnn_hip import _lib as L
+    decl = set(header_symbols())
+    bound = set(L.exported_symbols())
+    helpers = {"crnn_conv_fwd_tile", "crnn_conv_wgrad_plan"}
+    assert decl - bound <= helpers, decl - bound - helpers
+    assert bound <= decl
+
+
+def test_library_loads_without_gpu():
+    from crnn_hip import _lib as L
+    h = L.lib()
+    assert h.crnn_version() >= 100
+
+
+def test_state_dict_contract_matches_reference_names():
+    import crnn_oracle as O
+    from model.model import RCNN
+    m = RCNN(num_classes=194, hidden_size=512)
+    got = [(k, tuple(v.shape)) for k, v in m.state_dict().items()]
+    ref = O.param_shapes(512, 194)
+    assert got == ref
+
+
+def test_refuses_cpu_tensors():
+    from model.model import RCNN
+    m = RCNN(num_classes=194, hidden_size=64)
+    with pytest.raises(RuntimeError):
+        m(torch.zeros(1, 3, 32, 64))
+
+
+def test_attention_decoder_is_out_of_scope():
+    from model.model import RCNN
+    with pytest.raises(NotImplementedError):
+        RCNN(num_classes=10, decoder="attn")
+
+
+def test_engine_geometry_matches_reference_shapes():
+    from crnn_hip.engine import backbone_specs
+    stem0, stem1, blocks, co0, co1 = backbone_specs()
+    assert len(blocks) == 11
+    for H, W in [(32, 128), (32, 256), (64, 256), (32, 1024)]:
+        h, w = stem1.out_hw(*stem0.out_hw(H, W))
+        h, w = h // 2, w // 2
+        for b in blocks:
+            h, w = b.conv1.out_hw(h, w)
+        h, w = co1.out_hw(*co0.out_hw(h, w))
+        assert w == W // 8
+        assert h == (1 if H == 32 else 3)

@@ -1,0 +1,388 @@
+"""HIP kernel unit tests (MI355X). Each kernel family vs a plain torch-CPU fp32
+reference of the same op (fp32 mode: tight; bf16 mode: bf16-level tolerance)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _lib():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from crnn_hip import _lib as L
+    L.lib()
+    yield
+
+
+def _L():
+    from crnn_hip import _lib as L
+    return L
+
+
+def relerr(a, b):
+    a = a.double().cpu()
+    b = b.double().cpu()
+    return float((a - b).norm() / max(b.norm(), 1e-30))
+
+
+def to_nhwc(x, cp=None, dtype=torch.float32):
+    x = x.permute(0, 2, 3, 1)
+    if cp is not None and cp > x.shape[-1]:
+        x = F.pad(x, (0, cp - x.shape[-1]))
+    return x.contiguous().to(DEV, dtype)
+
+
+CONVS = [
+    # B, Ci, H, W, Co, k, stride, pad
+    (2, 64, 8, 16, 128, (3, 3), (1, 1), (1, 1)),
+    (2, 128, 8, 16, 256, (3, 3), (2, 2), (1, 1)),
+    (2, 128, 8, 16, 256, (1, 1), (2, 2), (0, 0)),
+    (2, 512, 4, 8, 512, (2, 2), (2, 1), (0, 1)),
+    (3, 512, 2, 9, 512, (2, 2), (1, 1), (0, 0)),
+    (2, 3, 6, 10, 64, (3, 3), (1, 1), (1, 1)),
+    (1, 256, 5, 7, 256, (3, 3), (1, 1), (1, 1)),
+]
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("cfg", CONVS)
+def test_conv_fwd_dgrad_wgrad(cfg, dtype):
+    L = _L()
+    B, Ci, H, W, Co, k, s, p = cfg
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(B, Ci, H, W, generator=g)
+    w = torch.randn(Co, Ci, *k, generator=g) / math.sqrt(Ci * k[0] * k[1])
+    if dtype == torch.bfloat16:
+        x = x.bfloat16().float()
+        w = w.bfloat16().float()
+    y_ref = F.conv2d(x, w, stride=s, padding=p)
+    Ho, Wo = y_ref.shape[2:]
+    dy = torch.randn(y_ref.shape, generator=g)
+    if dtype == torch.bfloat16:
+        dy = dy.bfloat16().float()
+    xr = x.clone().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    F.conv2d(xr, wr, stride=s, padding=p).backward(dy)
+    Cip = max(8, (Ci + 7) // 8 * 8)
+    dt = L.dtype_code(dtype)
+    d = L.ConvDesc(B, H, W, Cip, Ho, Wo, Co, k[0], k[1], s[0], s[1], p[0], p[1], Ci)
+    xd = to_nhwc(x, Cip, dtype)
+    wd = torch.empty(Co, k[0], k[1], Cip, dtype=dtype, device=DEV)
+    st = L.stream_ptr()
+    L.call("crnn_pack_conv_weight", dt, w.to(DEV).data_ptr(), wd.data_ptr(), Co, Ci, k[0], k[1], Cip, st)
+    yd = torch.empty(B, Ho, Wo, Co, dtype=dtype, device=DEV)
+    rows = L.lib().crnn_conv_stat_rows(d)
+    ps = torch.empty(rows, Co, device=DEV)
+    pq = torch.empty(rows, Co, device=DEV)
+    L.call("crnn_conv_fwd", dt, d, xd.data_ptr(), wd.data_ptr(), yd.data_ptr(), ps.data_ptr(), pq.data_ptr(), st)
+    y = yd.float().permute(0, 3, 1, 2).cpu()
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    assert relerr(y, y_ref) < tol
+    # BN stats partials
+    ssum = ps.sum(0).cpu().double()
+    ref_sum = y_ref.sum(dim=(0, 2, 3)).double()
+    assert float((ssum - ref_sum).abs().max()) < 1e-3 * float(y_ref.abs().sum() / Co + 1)
+    # dgrad
+    dyd = to_nhwc(dy, None, dtype)
+    if Ci % 8 == 0:
+        dxd = torch.empty(B, H, W, Cip, dtype=dtype, device=DEV)
+        L.call("crnn_conv_dgrad", dt, d, dyd.data_ptr(), wd.data_ptr(), dxd.data_ptr(), None, None, 0, st)
+        dx = dxd.float().permute(0, 3, 1, 2).cpu()
+        assert relerr(dx, xr.grad) < tol
+    # wgrad
+    need = L.lib().crnn_conv_wgrad_workspace(d)
+    ws = torch.empty(need // 4 + 1, device=DEV)
+    dw = torch.full((Co, Ci, k[0], k[1]), 7.0, device=DEV)
+    L.call("crnn_conv_wgrad", dt, d, dyd.data_ptr(), xd.data_ptr(), dw.data_ptr(), ws.data_ptr(), need, 0.0, st)
+    assert relerr(dw.cpu(), wr.grad) < (1e-5 if dtype == torch.float32 else 1e-2)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("mnk", [(37, 50, 64), (256, 194, 512), (304, 1024, 256), (8, 16, 8), (200, 512, 8192),
+                                 (512, 1024, 4096)])
+def test_gemm_nt_nn_tn(mnk, dtype):
+    L = _L()
+    M, N, K = mnk
+    g = torch.Generator().manual_seed(2)
+    A = torch.randn(M, K, generator=g).to(dtype).float()
+    Bm = torch.randn(N, K, generator=g).to(dtype).float()
+    bias = torch.randn(N, generator=g)
+    dt = L.dtype_code(dtype)
+    st = L.stream_ptr()
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    Ad, Bd = A.to(DEV, dtype), Bm.to(DEV, dtype)
+    C = torch.empty(M, N, device=DEV)
+    L.call("crnn_gemm_nt", dt, Ad.data_ptr(), K, Bd.data_ptr(), K, C.data_ptr(), N, bias.to(DEV).data_ptr(), M, N,
+           K, 1, 0, st)
+    assert relerr(C.cpu(), A @ Bm.t() + bias) < tol
+    if N % 8 == 0:
+        Bk = torch.randn(K, N, generator=g).to(dtype).float()
+        C2 = torch.empty(M, N, dtype=dtype, device=DEV)
+        Bkd = Bk.to(DEV, dtype)
+        L.call("crnn_gemm_nn", dt, Ad.data_ptr(), K, Bkd.data_ptr(), N, C2.data_ptr(), N, M, N, K, 0, 0, st)
+        assert relerr(C2.float().cpu(), A @ Bk) < max(tol, 8e-3)
+    if M % 8 == 0 and N % 8 == 0:
+        At = torch.randn(K, M, generator=g).to(dtype).float()
+        Bt = torch.randn(K, N, generator=g).to(dtype).float()
+        C3 = torch.full((M, N), 3.0, device=DEV)
+        Atd, Btd = At.to(DEV, dtype), Bt.to(DEV, dtype)  # keep both alive across the call
+        L.call("crnn_gemm_tn", dt, Atd.data_ptr(), M, Btd.data_ptr(), N, C3.data_ptr(), N, M, N, K, 0, st)
+        assert relerr(C3.cpu(), At.t() @ Bt) < tol
+
+
+def _pack_lstm(w_ih, w_hh, b_ih, b_hh, H, dtype, L):
+    from crnn_hip.engine import gate_perm
+    perm = torch.tensor(gate_perm(H))
+    wih = torch.stack([w[perm] for w in w_ih]).to(DEV, dtype).contiguous()
+    whh = torch.stack([w[perm] for w in w_hh]).to(DEV, dtype).contiguous()
+    bias = torch.stack([(bi + bh)[perm] for bi, bh in zip(b_ih, b_hh)]).to(DEV).contiguous()
+    return wih, whh, bias
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("BTHI", [(3, 5, 32, 64), (16, 8, 64, 128)])
+def test_bilstm_fwd_bwd(BTHI, dtype):
+    L = _L()
+    import crnn_oracle as O
+    B, T, H, In = BTHI
+    g = torch.Generator().manual_seed(3)
+    k = 1 / math.sqrt(H)
+    w_ih = [(torch.rand(4 * H, In, generator=g) * 2 - 1) * k for _ in range(2)]
+    w_hh = [(torch.rand(4 * H, H, generator=g) * 2 - 1) * k for _ in range(2)]
+    b_ih = [(torch.rand(4 * H, generator=g) * 2 - 1) * k for _ in range(2)]
+    b_hh = [(torch.rand(4 * H, generator=g) * 2 - 1) * k for _ in range(2)]
+    x = torch.randn(B, T, In, generator=g)
+    dh_out = torch.randn(B, T, 2 * H, generator=g)
+    if dtype == torch.bfloat16:
+        w_ih = [w.bfloat16().float() for w in w_ih]
+        w_hh = [w.bfloat16().float() for w in w_hh]
+        x = x.bfloat16().float()
+        dh_out = dh_out.bfloat16().float()
+    # reference (oracle restatement, autograd)
+    ps = [t.clone().requires_grad_(True) for t in w_ih + w_hh + b_ih + b_hh]
+    xr = x.clone().requires_grad_(True)
+    hf = O.lstm_direction(xr, ps[0], ps[2], ps[4], ps[6], False)
+    hb = O.lstm_direction(xr, ps[1], ps[3], ps[5], ps[7], True)
+    href = torch.cat([hf, hb], 2)
+    href.backward(dh_out)
+    # HIP
+    dt = L.dtype_code(dtype)
+    st = L.stream_ptr()
+    wih, whh, bias = _pack_lstm(w_ih, w_hh, b_ih, b_hh, H, dtype, L)
+    xd = x.to(DEV, dtype).contiguous()
+    xg = torch.empty(B, T, 2, 4 * H, dtype=dtype, device=DEV)
+    L.call("crnn_gemm_nt", dt, xd.data_ptr(), In, wih.data_ptr(), In, xg.data_ptr(), 8 * H, bias.data_ptr(),
+           B * T, 8 * H, In, 0, 0, st)
+    hseq = torch.empty(B, T, 2 * H, dtype=dtype, device=DEV)
+    gsv = torch.empty(2, T, B, 4 * H, dtype=dtype, device=DEV)
+    csv = torch.empty(2, T, B, H, device=DEV)
+    for s in range(T):
+        L.call("crnn_lstm_step_fwd", dt, xg.data_ptr(), whh.data_ptr(), hseq.data_ptr(), gsv.data_ptr(),
+               csv.data_ptr(), B, T, H, s, st)
+    tol = 2e-5 if dtype == torch.float32 else 3e-2
+    assert relerr(hseq.float().cpu(), href.detach()) < tol
+    dh = dh_out.to(DEV, dtype).contiguous()
+    dg = torch.empty(2, T, B, 4 * H, dtype=dtype, device=DEV)
+    dc = torch.empty(2, B, H, device=DEV)
+    for s in range(T):
+        L.call("crnn_lstm_step_bwd", dt, dh.data_ptr(), whh.data_ptr(), gsv.data_ptr(), csv.data_ptr(),
+               dg.data_ptr(), dc.data_ptr(), B, T, H, s, st)
+    dwhh = torch.empty(2, 4 * H, H, device=DEV)
+    dwih = torch.empty(2, 4 * H, In, device=DEV)
+    db = torch.empty(2, 4 * H, device=DEV)
+    L.call("crnn_lstm_dwhh", dt, dg.data_ptr(), hseq.data_ptr(), dwhh.data_ptr(), B, T, H, 0, st)
+    L.call("crnn_lstm_dwih", dt, dg.data_ptr(), xd.data_ptr(), dwih.data_ptr(), B, T, H, In, 0, st)
+    L.call("crnn_lstm_dbias", dt, dg.data_ptr(), db.data_ptr(), B, T, H, 0, st)
+    dx = torch.empty(B, T, In, dtype=dtype, device=DEV)
+    L.call("crnn_lstm_dx", dt, dg.data_ptr(), wih.data_ptr(), dx.data_ptr(), B, T, H, In, st)
+    gtol = 1e-4 if dtype == torch.float32 else 5e-2
+    for d in range(2):
+        assert relerr(dwih[d].cpu(), ps[0 + d].grad) < gtol
+        assert relerr(dwhh[d].cpu(), ps[2 + d].grad) < gtol
+        assert relerr(db[d].cpu(), ps[4 + d].grad) < gtol
+    assert relerr(dx.float().cpu(), xr.grad) < gtol
+
+
+def test_ctc_golden_cases():
+    L = _L()
+    from helpers import load
+    from crnn_hip.ctc import ctc_loss
+    z = load("ctc_cases.npz")
+    logits = torch.from_numpy(np.transpose(z["logits"], (1, 0, 2))).contiguous()
+    labels = torch.from_numpy(z["labels"])
+    tl = torch.from_numpy(z["target_lengths"])
+    x = logits.to(DEV).requires_grad_(True)
+    loss = ctc_loss(x, labels, tl, zero_infinity=True)
+    loss.backward()
+    np.testing.assert_allclose(float(loss), float(z["loss_mean_1"]), rtol=1e-5)
+    np.testing.assert_allclose(np.transpose(x.grad.cpu().numpy(), (1, 0, 2)), z["grad_mean_1"], rtol=1e-3, atol=1e-6)
+    big = torch.from_numpy(np.transpose(z["big_logits"], (1, 0, 2))).contiguous().to(DEV).requires_grad_(True)
+    loss = ctc_loss(big, torch.from_numpy(z["big_labels"]), torch.from_numpy(z["big_tl"]))
+    loss.backward()
+    np.testing.assert_allclose(float(loss), float(z["big_loss"]), rtol=1e-5)
+    np.testing.assert_allclose(np.transpose(big.grad.cpu().numpy(), (1, 0, 2)), z["big_grad"], rtol=1e-3, atol=1e-7)
+
+
+def test_ctc_long_sequence_vs_oracle():
+    _L()
+    from ctc_oracle import ctc_loss_and_grad
+    from crnn_hip.ctc import ctc_loss
+    g = torch.Generator().manual_seed(5)
+    B, T, C = 5, 128, 194
+    x = torch.randn(B, T, C, generator=g) * 2
+    tl = torch.tensor([1, 64, 30, 63, 10])
+    tg = torch.randint(3, C, (B, 64), generator=g)
+    ref_loss, ref_grad = ctc_loss_and_grad(x.double().numpy(), tg.numpy(), tl.numpy())
+    xd = x.to(DEV).requires_grad_(True)
+    loss = ctc_loss(xd, tg, tl)
+    loss.backward()
+    np.testing.assert_allclose(float(loss), ref_loss, rtol=1e-4)
+    np.testing.assert_allclose(xd.grad.cpu().numpy(), ref_grad, rtol=2e-3, atol=1e-6)
+
+
+def test_greedy_decode_golden(itos):
+    _L()
+    import json
+    import os
+    from helpers import load, GOLDEN
+    from crnn_hip.ctc import ctc_greedy_decoder
+    z = load("decode.npz")
+    with open(os.path.join(GOLDEN, "decode.json"), encoding="utf-8") as f:
+        ref = json.load(f)
+    texts, seqs = ctc_greedy_decoder(torch.from_numpy(z["logits"]).to(DEV), itos[1:])
+    assert seqs == ref["seqs"]
+    assert texts == ref["texts"]
+
+
+def test_adamw_vs_oracle():
+    L = _L()
+    import crnn_oracle as O
+    g = torch.Generator().manual_seed(6)
+    n = 100003
+    p = torch.randn(n, generator=g)
+    m = torch.zeros(n)
+    v = torch.zeros(n)
+    pd, md, vd = p.to(DEV), m.to(DEV), v.to(DEV)
+    pn, mn, vn = p.double().numpy(), m.double().numpy(), v.double().numpy()
+    for step in range(1, 4):
+        gr = torch.randn(n, generator=g)
+        L.call("crnn_adamw", pd.data_ptr(), gr.to(DEV).data_ptr(), md.data_ptr(), vd.data_ptr(), n, 1e-3, 0.9, 0.999,
+               1e-8, 1e-2, step, 1.0, L.stream_ptr())
+        pn, mn, vn = O.adamw_step(pn, gr.double().numpy(), mn, vn, step, 1e-3)
+    np.testing.assert_allclose(pd.cpu().numpy(), pn, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_bn_bwd_and_se(dtype):
+    """BN train fwd + SE block tail + backward vs torch autograd."""
+    L = _L()
+    g = torch.Generator().manual_seed(7)
+    B, C, H, W = 3, 64, 4, 6
+    HW = H * W
+    Cr = C // 16
+    z2 = torch.randn(B, C, H, W, generator=g).to(dtype).float()
+    idn = torch.randn(B, C, H, W, generator=g).to(dtype).float()
+    gamma = torch.rand(C, generator=g) + 0.5
+    beta = torch.randn(C, generator=g) * 0.1
+    w1 = torch.randn(Cr, C, generator=g) * 0.3
+    w2 = torch.randn(C, Cr, generator=g) * 0.3
+    dy = torch.randn(B, C, H, W, generator=g).to(dtype).float()
+    # reference
+    zr = z2.clone().requires_grad_(True)
+    ir = idn.clone().requires_grad_(True)
+    pr = [t.clone().requires_grad_(True) for t in (gamma, beta, w1, w2)]
+    u = F.batch_norm(zr, None, None, pr[0], pr[1], training=True, eps=1e-5)
+    pooled = u.mean(dim=(2, 3))
+    sref = torch.sigmoid(torch.relu(pooled @ pr[2].t()) @ pr[3].t())
+    y = torch.relu(u * sref[:, :, None, None] + ir)
+    y.backward(dy)
+    # HIP
+    dt = L.dtype_code(dtype)
+    st = L.stream_ptr()
+    zd, idd, dyd = to_nhwc(z2, None, dtype), to_nhwc(idn, None, dtype), to_nhwc(dy, None, dtype)
+    M = B * HW
+    rows = L.lib().crnn_bn_rows(M)
+    ps, pq = torch.empty(rows, C, device=DEV), torch.empty(rows, C, device=DEV)
+    L.call("crnn_channel_stats", dt, zd.data_ptr(), M, C, ps.data_ptr(), pq.data_ptr(), rows, st)
+    gd, bd = gamma.to(DEV), beta.to(DEV)
+    rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+    mean, inv, sc, sh = [torch.empty(C, device=DEV) for _ in range(4)]
+    L.call("crnn_bn_finalize", ps.data_ptr(), pq.data_ptr(), rows, (M + rows - 1) // rows, C, M, gd.data_ptr(),
+           bd.data_ptr(), rm.data_ptr(),
+           rv.data_ptr(), 0.1, 1e-5, 1, mean.data_ptr(), inv.data_ptr(), sc.data_ptr(), sh.data_ptr(), st)
+    pooled_d = torch.empty(B, C, device=DEV)
+    hid = torch.empty(B, Cr, device=DEV)
+    sd = torch.empty(B, C, device=DEV)
+    L.call("crnn_se_pool", dt, zd.data_ptr(), sc.data_ptr(), sh.data_ptr(), pooled_d.data_ptr(), B, HW, C, st)
+    w1d, w2d = w1.to(DEV), w2.to(DEV)
+    L.call("crnn_se_mlp_fwd", pooled_d.data_ptr(), w1d.data_ptr(), w2d.data_ptr(), hid.data_ptr(), sd.data_ptr(), B,
+           C, Cr, st)
+    yd = torch.empty(B, H, W, C, dtype=dtype, device=DEV)
+    L.call("crnn_se_residual_fwd", dt, zd.data_ptr(), sc.data_ptr(), sh.data_ptr(), sd.data_ptr(), idd.data_ptr(),
+           None, None, yd.data_ptr(), B, HW, C, st)
+    tol = 1e-5 if dtype == torch.float32 else 2e-2
+    assert relerr(yd.float().permute(0, 3, 1, 2).cpu(), y.detach()) < tol
+    # backward
+    ds = torch.empty(B, C, device=DEV)
+    L.call("crnn_se_bwd_reduce", dt, dyd.data_ptr(), yd.data_ptr(), zd.data_ptr(), sc.data_ptr(), sh.data_ptr(),
+           ds.data_ptr(), B, HW, C, st)
+    dsig, dpool = torch.empty(B, C, device=DEV), torch.empty(B, C, device=DEV)
+    dhid = torch.empty(B, Cr, device=DEV)
+    dw1, dw2 = torch.empty(Cr, C, device=DEV), torch.empty(C, Cr, device=DEV)
+    L.call("crnn_se_mlp_bwd", ds.data_ptr(), pooled_d.data_ptr(), hid.data_ptr(), sd.data_ptr(), w1d.data_ptr(),
+           w2d.data_ptr(), dsig.data_ptr(), dhid.data_ptr(), dpool.data_ptr(), dw1.data_ptr(), dw2.data_ptr(), B, C,
+           Cr, HW, st)
+    gtol = 1e-4 if dtype == torch.float32 else 5e-2
+    assert relerr(dw1.cpu(), pr[2].grad) < gtol
+    assert relerr(dw2.cpu(), pr[3].grad) < gtol
+    from crnn_hip._lib import BnBwdDesc
+    desc = BnBwdDesc(dyd.data_ptr(), zd.data_ptr(), mean.data_ptr(), inv.data_ptr(), sc.data_ptr(), sh.data_ptr(),
+                     yd.data_ptr(), sd.data_ptr(), dpool.data_ptr(), 3, M, C, HW)
+    pg, pgx = torch.empty(rows, C, device=DEV), torch.empty(rows, C, device=DEV)
+    L.call("crnn_bn_bwd_reduce", dt, desc, pg.data_ptr(), pgx.data_ptr(), rows, st)
+    dgam, dbet, mg, mgx = [torch.empty(C, device=DEV) for _ in range(4)]
+    L.call("crnn_bn_bwd_finalize", pg.data_ptr(), pgx.data_ptr(), rows, C, M, dgam.data_ptr(), dbet.data_ptr(),
+           mg.data_ptr(), mgx.data_ptr(), 0, st)
+    dz = torch.empty(B, H, W, C, dtype=dtype, device=DEV)
+    L.call("crnn_bn_bwd_apply", dt, desc, mg.data_ptr(), mgx.data_ptr(), dz.data_ptr(), st)
+    assert relerr(dgam.cpu(), pr[0].grad) < gtol
+    assert relerr(dbet.cpu(), pr[1].grad) < gtol
+    assert relerr(dz.float().permute(0, 3, 1, 2).cpu(), zr.grad) < gtol
+    # running stats: unbiased variance
+    assert relerr(rv.cpu(), 0.9 + 0.1 * z2.var(dim=(0, 2, 3), unbiased=True)) < 1e-5
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_maxpool_relu_bn(dtype):
+    L = _L()
+    g = torch.Generator().manual_seed(8)
+    B, C, H, W = 2, 16, 6, 8
+    z = torch.randn(B, C, H, W, generator=g).to(dtype).float()
+    sc = torch.rand(C, generator=g) + 0.5
+    sh = torch.randn(C, generator=g) * 0.2
+    zr = z.clone().requires_grad_(True)
+    y = F.max_pool2d(torch.relu(zr * sc[None, :, None, None] + sh[None, :, None, None]), 2, 2)
+    dy = torch.randn(y.shape, generator=g).to(dtype).float()
+    y.backward(dy)
+    dt = L.dtype_code(dtype)
+    st = L.stream_ptr()
+    zd = to_nhwc(z, None, dtype)
+    yd = torch.empty(B, H // 2, W // 2, C, dtype=dtype, device=DEV)
+    scd, shd = sc.to(DEV), sh.to(DEV)
+    L.call("crnn_bn_relu_maxpool", dt, zd.data_ptr(), scd.data_ptr(), shd.data_ptr(), yd.data_ptr(), B, H, W, C, st)
+    tol = 1e-6 if dtype == torch.float32 else 1e-2
+    assert relerr(yd.float().permute(0, 3, 1, 2).cpu(), y.detach()) < tol
+    dfull = torch.empty(B, H, W, C, dtype=dtype, device=DEV)
+    L.call("crnn_maxpool_bwd", dt, zd.data_ptr(), scd.data_ptr(), shd.data_ptr(), to_nhwc(dy, None, dtype).data_ptr(),
+           dfull.data_ptr(), B, H, W, C, st)
+    # d/dz = dfull * relu'(.) * sc
+    pre = z * sc[None, :, None, None] + sh[None, :, None, None]
+    dz = dfull.float().permute(0, 3, 1, 2).cpu() * (pre > 0).float() * sc[None, :, None, None]
+    assert relerr(dz, zr.grad) < tol
