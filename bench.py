@@ -1,0 +1,199 @@
+"""Benchmark: CRNN training step (SE-ResNet31 -> 2x512 BiLSTM -> CTC head, fwd + CTC bwd +
+AdamW) in bf16 at B=256 per GPU on 32x256 synthetic crops — BASELINE.json configs[2]
+(1 GPU) / configs[3] (data parallel, RCCL all-reduce of gradients).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
+    torchrun --nproc-per-node N bench.py --gpus N ...      (one process per GPU)
+
+Rank 0 prints ONE JSON line (metric/value/...); value = lines/s over all ranks.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+for sub in ("rcnn-ocr_amd", "oracle"):
+    p = os.path.join(REPO, sub)
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "text-lines/sec (train step incl. CTC bwd) at B=256, 32×256 crops; 1/2/4/8 MI355X"
+PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (spec, MI355X_MICROARCH.md)
+PEAK_HBM_GBS = 8000.0       # HBM3E spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--height", type=int, default=32)
+    ap.add_argument("--width", type=int, default=256)
+    ap.add_argument("--hidden", type=int, default=512)
+    ap.add_argument("--layers", type=int, default=2)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample", type=int, default=32, help="batch of the CPU baseline sample")
+    ap.add_argument("--cpu-steps", type=int, default=6)
+    return ap.parse_args()
+
+
+def cpu_baseline(args, threads):
+    """oracle (CPU fp32 restatement, 'port') train step on a bounded sample."""
+    import crnn_oracle as O
+    from crnn_hip.recipe import recipe_state_dict, synthetic_batch
+    torch.set_num_threads(threads)
+    C = 194
+    T = args.width // 8
+    sd = recipe_state_dict(O.param_shapes(args.hidden, C, args.layers), 0)
+    p = {k: (v.clone().requires_grad_(True) if v.is_floating_point() and "running" not in k else v)
+         for k, v in sd.items()}
+    params = [v for v in p.values() if getattr(v, "requires_grad", False)]
+    opt = torch.optim.AdamW(params, lr=1e-4)
+    x, _, tg, tl = synthetic_batch(args.cpu_sample, args.height, args.width, T, C, seed=99)
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        logits = O.head(O.encode(x, p, O.Ctx(train=True), args.layers), p)
+        O.ctc_loss(logits, tg, tl).backward()
+        opt.step()
+
+    step()  # warm-up
+    t0 = time.perf_counter()
+    for _ in range(args.cpu_steps):
+        step()
+    dt = time.perf_counter() - t0
+    return {"value": round(args.cpu_sample * args.cpu_steps / dt, 3), "unit": "text-lines/s",
+            "cores": threads, "kind": "port",
+            "sample": f"oracle/crnn_oracle.py fp32 torch-CPU train step (fwd + numpy CTC + bwd + AdamW), "
+                      f"B={args.cpu_sample} x {args.cpu_steps} steps (+1 warm-up) at {args.height}x{args.width}, "
+                      f"hidden {args.hidden}; {dt:.1f} s"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    import crnn_oracle as O
+    from crnn_hip.optim import FusedAdamW
+    from crnn_hip.recipe import recipe_state_dict, synthetic_batch
+    from model.model import RCNN
+
+    C = 194
+    T = args.width // 8
+    dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    model = RCNN(num_classes=C, hidden_size=args.hidden, blank_id=None, num_rnn_layers=args.layers,
+                 compute_dtype=dtype)
+    model.load_state_dict(recipe_state_dict(O.param_shapes(args.hidden, C, args.layers), 0), strict=False)
+    model = model.to(dev).train()
+    x, _, tg, tl = synthetic_batch(args.batch, args.height, args.width, T, C, seed=1234 + rank)
+    x = x.to(dev)
+    tg = tg.to(dev, torch.int32)
+    tl = tl.to(dev, torch.int32)
+    eng = model._engine_for(x)
+    model.flatten_parameters_()
+    if world > 1:
+        dist.broadcast(model._flat_param, 0)
+        model.mark_params_changed()
+    grads, _ = model._grad_views()
+    opt = FusedAdamW(model, lr=1e-4, weight_decay=1e-2)
+    inv_world = 1.0 / world
+
+    def step():
+        eng.forward(x, train=True, save_for_backward=True)
+        loss, dl = eng.ctc(eng.logits_padded(), tg, tl)
+        eng.backward(dl, grads, accumulate=False)
+        if world > 1:
+            dist.all_reduce(model._flat_grad)
+        opt.step(grad_scale=inv_world)
+        return loss
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    eng.enable_timing(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+        torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    timing = eng.conv_timing()
+    eng.enable_timing(False)
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    lines = args.batch * world * args.steps
+    value = lines / elapsed
+    final_loss = float(loss.item())
+
+    if rank == 0:
+        conv_launches = sum(v[0] for v in timing.values())
+        conv_ms = sum(v[1] for v in timing.values())
+        conv_flop = sum(v[2] for v in timing.values())
+        achieved = conv_flop / (conv_ms * 1e-3) / 1e12 if conv_ms > 0 else 0.0
+        per_kind = {k: {"launches_per_step": v[0] // args.steps, "ms_per_step": round(v[1] / args.steps, 3),
+                        "tflops": round(v[2] / (v[1] * 1e-3) / 1e12, 1) if v[1] > 0 else None}
+                    for k, v in timing.items()}
+        out = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "text-lines/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16" if dtype == torch.bfloat16 else "fp32",
+            "data": "synthetic (seeded 32xW uint8 crops with white padding, random labels; recipe-init weights)",
+            "config": {"workload": "train step: SE-ResNet31 + 2x512 BiLSTM + CTC head, fwd + CTC bwd + AdamW "
+                                   "(BASELINE configs[2]/[3])",
+                       "global_batch": args.batch * world, "per_gpu_batch": args.batch,
+                       "crop": f"{args.height}x{args.width}", "seq_len": T, "hidden": args.hidden,
+                       "rnn_layers": args.layers, "num_classes": C,
+                       "parallelism": f"dp{world}" if world > 1 else "single"},
+            "roofline": {"bound": "mfma", "kernel": "implicit-GEMM conv (fwd+dgrad+wgrad, all 28 convs)",
+                         "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                         "algorithmic_flop_per_step": conv_flop / args.steps,
+                         "launches_per_step": conv_launches // args.steps,
+                         "kernel_ms_per_step": round(conv_ms / args.steps, 3),
+                         "timing": "HIP events around every conv launch on the launch stream, timed region"},
+            "kernels": per_kind,
+            "final_loss": round(final_loss, 4),
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            try:
+                threads = min(16, os.cpu_count() or 1)
+                out["cpu_baseline"] = cpu_baseline(args, threads)
+            except Exception as e:  # report, never fake
+                out["cpu_baseline"] = {"value": None, "error": repr(e)}
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -199,6 +199,38 @@ class CRNNEngine:
         hb[: self.C].copy_(self.p["ctc_head.bias"])
         self.packed_version = ver
 
+    # ------------------------------------------------------------------ instrumentation
+    def enable_timing(self, on: bool = True):
+        """record HIP events around every implicit-GEMM conv launch (fwd / dgrad / wgrad)
+        on the launch stream; conv_time_ms() sums them after a synchronize."""
+        self.timers = [] if on else None
+
+    def _conv_call(self, kind, flops, name, *args):
+        if getattr(self, "timers", None) is None:
+            call(name, *args)
+            return
+        a = torch.cuda.Event(enable_timing=True)
+        b = torch.cuda.Event(enable_timing=True)
+        a.record()
+        call(name, *args)
+        b.record()
+        self.timers.append((kind, flops, a, b))
+
+    def conv_timing(self):
+        """{kind: (launches, total_ms, total_flop)} since enable_timing(); clears the list."""
+        out = {}
+        for kind, flops, a, b in self.timers or []:
+            n, ms, fl = out.get(kind, (0, 0.0, 0.0))
+            out[kind] = (n + 1, ms + a.elapsed_time(b), fl + flops)
+        if self.timers is not None:
+            self.timers.clear()
+        return out
+
+    @staticmethod
+    def conv_flops(cs: "ConvSpec", b, h, w):
+        ho, wo = cs.out_hw(h, w)
+        return 2.0 * b * ho * wo * cs.co * cs.ci_real * cs.kh * cs.kw
+
     def _pbuf(self, name, shape, dtype, zero=False):
         t = self.packed.get(name)
         if t is None:
@@ -236,11 +268,13 @@ class CRNNEngine:
             rows = L.lib().crnn_conv_stat_rows(d)
             psum = self.ws.get("stat.sum", (self._stat_cap,), torch.float32)[: rows * cs.co].view(rows, cs.co)
             psq = self.ws.get("stat.sq", (self._stat_cap,), torch.float32)[: rows * cs.co].view(rows, cs.co)
-            call("crnn_conv_fwd", self.dt, d, ptr(x), ptr(self.packed[cs.name]), ptr(z), ptr(psum), ptr(psq), s)
+            self._conv_call("fwd", self.conv_flops(cs, b, h, w), "crnn_conv_fwd", self.dt, d, ptr(x),
+                            ptr(self.packed[cs.name]), ptr(z), ptr(psum), ptr(psq), s)
             rpp = L.lib().crnn_conv_stat_rows_per_partial(d)
             stats = self._bn_finalize(cs.bn, psum, psq, rows, b * ho * wo, True, tag, rpp)
         else:
-            call("crnn_conv_fwd", self.dt, d, ptr(x), ptr(self.packed[cs.name]), ptr(z), None, None, s)
+            self._conv_call("fwd", self.conv_flops(cs, b, h, w), "crnn_conv_fwd", self.dt, d, ptr(x),
+                            ptr(self.packed[cs.name]), ptr(z), None, None, s)
             stats = self._bn_finalize(cs.bn, None, None, 0, b * ho * wo, False, tag)
         return (z,) + stats + (ho, wo)
 
@@ -418,8 +452,8 @@ class CRNNEngine:
         if need > wsb.numel() * 4:
             raise RuntimeError("wgrad workspace too small")
         beta = 1.0 if self.accumulate else 0.0
-        call("crnn_conv_wgrad", self.dt, d, ptr(dz), ptr(x), ptr(self.g[cs.name]), ptr(wsb), wsb.numel() * 4,
-             beta, L.stream_ptr())
+        self._conv_call("wgrad", self.conv_flops(cs, b, h, w), "crnn_conv_wgrad", self.dt, d, ptr(dz), ptr(x),
+                        ptr(self.g[cs.name]), ptr(wsb), wsb.numel() * 4, beta, L.stream_ptr())
 
     def _wgrad_capacity(self, B, H, W):
         lib = L.lib()
@@ -520,14 +554,14 @@ class CRNNEngine:
                      out=dz, accumulate_params=accumulate)
         self._wgrad(self.co1, dz, co["a0"], B, co["h2"], co["w2"])
         da = bufC[: B * co["h2"] * co["w2"] * 512]
-        call("crnn_conv_dgrad", dt, self.co1.desc(B, co["h2"], co["w2"]), ptr(dz), ptr(self.packed[self.co1.name]),
+        self._conv_call("dgrad", self.conv_flops(self.co1, B, co["h2"], co["w2"]), "crnn_conv_dgrad", dt, self.co1.desc(B, co["h2"], co["w2"]), ptr(dz), ptr(self.packed[self.co1.name]),
              ptr(da), None, None, 0, s)
         dz0 = bufA[: B * co["h2"] * co["w2"] * 512]
         self._bn_bwd(1, da, co["z0"], (co["m0"], co["i0"], co["sc0"], co["sh0"]), self.co0.bn,
                      B * co["h2"] * co["w2"], 512, out=dz0, accumulate_params=accumulate)
         self._wgrad(self.co0, dz0, co["x"], B, co["h"], co["w"])
         dy = bufB[: B * co["h"] * co["w"] * 512]
-        call("crnn_conv_dgrad", dt, self.co0.desc(B, co["h"], co["w"]), ptr(dz0), ptr(self.packed[self.co0.name]),
+        self._conv_call("dgrad", self.conv_flops(self.co0, B, co["h"], co["w"]), "crnn_conv_dgrad", dt, self.co0.desc(B, co["h"], co["w"]), ptr(dz0), ptr(self.packed[self.co0.name]),
              ptr(dy), None, None, 0, s)
         # ---- residual blocks, reverse
         bufs = [bufA, bufB, bufC]
@@ -562,7 +596,7 @@ class CRNNEngine:
                          y=sb["y"], se=sb["s"], dpool=dpool, out=dz2, accumulate_params=accumulate)
             self._wgrad(blk.conv2, dz2, sb["a1"], B, ho, wo)
             da1 = bufs[o2][: Mo * P]
-            call("crnn_conv_dgrad", dt, blk.conv2.desc(B, ho, wo), ptr(dz2), ptr(self.packed[blk.conv2.name]),
+            self._conv_call("dgrad", self.conv_flops(blk.conv2, B, ho, wo), "crnn_conv_dgrad", dt, blk.conv2.desc(B, ho, wo), ptr(dz2), ptr(self.packed[blk.conv2.name]),
                  ptr(da1), None, None, 0, s)
             dz1 = bufs[o1][: Mo * P]
             self._bn_bwd(1, da1, sb["z1"], (sb["m1"], sb["i1"], sb["sc1"], sb["sh1"]), blk.conv1.bn, Mo, P,
@@ -571,18 +605,18 @@ class CRNNEngine:
             Ci = blk.conv1.ci
             dxb = bufs[o2][: B * h * w * Ci]
             if blk.ds is None:
-                call("crnn_conv_dgrad", dt, blk.conv1.desc(B, h, w), ptr(dz1), ptr(self.packed[blk.conv1.name]),
+                self._conv_call("dgrad", self.conv_flops(blk.conv1, B, h, w), "crnn_conv_dgrad", dt, blk.conv1.desc(B, h, w), ptr(dz1), ptr(self.packed[blk.conv1.name]),
                      ptr(dxb), ptr(dyb), ptr(sb["y"]), 0, s)
                 cur = o2
             else:
-                call("crnn_conv_dgrad", dt, blk.conv1.desc(B, h, w), ptr(dz1), ptr(self.packed[blk.conv1.name]),
+                self._conv_call("dgrad", self.conv_flops(blk.conv1, B, h, w), "crnn_conv_dgrad", dt, blk.conv1.desc(B, h, w), ptr(dz1), ptr(self.packed[blk.conv1.name]),
                      ptr(dxb), None, None, 0, s)
                 dsv = sb["ds"]
                 dzd = bufs[o1][: Mo * P]
                 self._bn_bwd(2, dyb, dsv["zd"], (dsv["m"], dsv["i"], dsv["sc"], dsv["sh"]), blk.ds.bn, Mo, P,
                              y=sb["y"], out=dzd, accumulate_params=accumulate)
                 self._wgrad(blk.ds, dzd, sb["x"], B, h, w)
-                call("crnn_conv_dgrad", dt, blk.ds.desc(B, h, w), ptr(dzd), ptr(self.packed[blk.ds.name]),
+                self._conv_call("dgrad", self.conv_flops(blk.ds, B, h, w), "crnn_conv_dgrad", dt, blk.ds.desc(B, h, w), ptr(dzd), ptr(self.packed[blk.ds.name]),
                      ptr(dxb), None, None, 1, s)
                 cur = o2
         # ---- stem
@@ -599,7 +633,7 @@ class CRNNEngine:
                      out=dz1, accumulate_params=accumulate)
         self._wgrad(self.stem1, dz1, st["a0"], B, h1, w1)
         da0 = bufs[o1][: B * h1 * w1 * 64]
-        call("crnn_conv_dgrad", dt, self.stem1.desc(B, h1, w1), ptr(dz1), ptr(self.packed[self.stem1.name]),
+        self._conv_call("dgrad", self.conv_flops(self.stem1, B, h1, w1), "crnn_conv_dgrad", dt, self.stem1.desc(B, h1, w1), ptr(dz1), ptr(self.packed[self.stem1.name]),
              ptr(da0), None, None, 0, s)
         dz0 = bufs[cur][: B * h1 * w1 * 64]
         self._bn_bwd(1, da0, st["z0"], (st["m0"], st["i0"], st["sc0"], st["sh0"]), self.stem0.bn, B * h1 * w1, 64,
