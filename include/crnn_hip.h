@@ -89,7 +89,9 @@ void crnn_conv_wgrad_plan(const crnn_conv_desc* d, int* bm, int* bn, int* splits
 int crnn_bn_finalize(const float* psum, const float* psq, int rows, long rows_per_partial, int C, long count,
                      const float* gamma, const float* beta,
                      float* running_mean, float* running_var, float momentum, float eps, int train,
-                     float* mean, float* invstd, float* scale, float* shift, void* stream);
+                     float* mean, float* invstd, float* scale, float* shift, float* ws, void* stream);
+/* bytes of `ws` crnn_bn_finalize / crnn_bn_bwd_finalize need for C channels */
+size_t crnn_bn_finalize_workspace(int C);
 /* per-channel (sum, M2) partials of an NHWC tensor [M][C] (for tensors not produced by a conv);
  * partial r covers ceil(M/rows) rows. */
 int crnn_channel_stats(int dtype, const void* x, long M, int C, float* psum, float* psq, int rows, void* stream);
@@ -123,7 +125,7 @@ typedef struct {
 int crnn_bn_bwd_reduce(int dtype, const crnn_bn_bwd_desc* d, float* pg, float* pgx, int rows, void* stream);
 /* -> dgamma, dbeta (written, or added if accumulate), mean_g = sum(g)/count, mean_gx = sum(g xhat)/count */
 int crnn_bn_bwd_finalize(const float* pg, const float* pgx, int rows, int C, long count, float* dgamma, float* dbeta,
-                         float* mean_g, float* mean_gx, int accumulate, void* stream);
+                         float* mean_g, float* mean_gx, int accumulate, float* ws, void* stream);
 /* dz = scale * (g - mean_g - xhat*mean_gx) */
 int crnn_bn_bwd_apply(int dtype, const crnn_bn_bwd_desc* d, const float* mean_g, const float* mean_gx, void* dz, void* stream);
 int crnn_bn_rows(long M); /* partial rows used by the reduce kernels for M */

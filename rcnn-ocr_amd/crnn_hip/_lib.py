@@ -49,13 +49,14 @@ _SIGS = {
     "crnn_conv_dgrad": ([i32, C.POINTER(ConvDesc), vp, vp, vp, vp, vp, i32, vp], i32),
     "crnn_conv_wgrad": ([i32, C.POINTER(ConvDesc), vp, vp, vp, vp, sz, f32, vp], i32),
     "crnn_conv_wgrad_workspace": ([C.POINTER(ConvDesc)], sz),
-    "crnn_bn_finalize": ([vp, vp, i32, i64, i32, i64, vp, vp, vp, vp, f32, f32, i32, vp, vp, vp, vp, vp], i32),
+    "crnn_bn_finalize": ([vp, vp, i32, i64, i32, i64, vp, vp, vp, vp, f32, f32, i32, vp, vp, vp, vp, vp, vp], i32),
+    "crnn_bn_finalize_workspace": ([i32], sz),
     "crnn_channel_stats": ([i32, vp, i64, i32, vp, vp, i32, vp], i32),
     "crnn_bn_act": ([i32, vp, vp, vp, vp, i64, i32, i32, vp], i32),
     "crnn_bn_relu_maxpool": ([i32, vp, vp, vp, vp, i32, i32, i32, i32, vp], i32),
     "crnn_maxpool_bwd": ([i32, vp, vp, vp, vp, vp, i32, i32, i32, i32, vp], i32),
     "crnn_bn_bwd_reduce": ([i32, C.POINTER(BnBwdDesc), vp, vp, i32, vp], i32),
-    "crnn_bn_bwd_finalize": ([vp, vp, i32, i32, i64, vp, vp, vp, vp, i32, vp], i32),
+    "crnn_bn_bwd_finalize": ([vp, vp, i32, i32, i64, vp, vp, vp, vp, i32, vp, vp], i32),
     "crnn_bn_bwd_apply": ([i32, C.POINTER(BnBwdDesc), vp, vp, vp, vp], i32),
     "crnn_bn_rows": ([i64], i32),
     "crnn_se_pool": ([i32, vp, vp, vp, vp, i32, i32, i32, vp], i32),

@@ -251,12 +251,15 @@ class CRNNEngine:
         call("crnn_bn_finalize", ptr(psum) if train else None, ptr(psq) if train else None, rows, rpp, C, count,
              ptr(self.p[prefix + ".weight"]), ptr(self.p[prefix + ".bias"]),
              ptr(rm), ptr(rv), BN_MOMENTUM if self.update_running else 0.0, BN_EPS, 1 if train else 0,
-             ptr(mean), ptr(inv), ptr(sc), ptr(sh), L.stream_ptr())
+             ptr(mean), ptr(inv), ptr(sc), ptr(sh), ptr(self._fin_ws()), L.stream_ptr())
         if train and self.update_running:
             nbt = self.buf.get(prefix + ".num_batches_tracked")
             if nbt is not None:
                 nbt.add_(1)
         return mean, inv, sc, sh
+
+    def _fin_ws(self):
+        return self.ws.get("bn.fin_ws", (L.lib().crnn_bn_finalize_workspace(512) // 4,), torch.float32)
 
     def _conv_bn(self, cs: ConvSpec, x, b, h, w, train, tag):
         """z = conv(x); BN statistics (train) or running stats (eval) -> (z, mean, inv, scale, shift, ho, wo)."""
@@ -441,7 +444,7 @@ class CRNNEngine:
         mg = ws.get("bnb.mg", (512,), torch.float32)
         mgx = ws.get("bnb.mgx", (512,), torch.float32)
         call("crnn_bn_bwd_finalize", ptr(pg), ptr(pgx), rows, C, M, ptr(self.g[prefix + ".weight"]),
-             ptr(self.g[prefix + ".bias"]), ptr(mg), ptr(mgx), 1 if accumulate_params else 0, s)
+             ptr(self.g[prefix + ".bias"]), ptr(mg), ptr(mgx), 1 if accumulate_params else 0, ptr(self._fin_ws()), s)
         call("crnn_bn_bwd_apply", self.dt, d, ptr(mg), ptr(mgx), ptr(out), s)
         return out
 

@@ -107,9 +107,9 @@ __global__ __launch_bounds__(NT) void chan_stats_kernel(const T* __restrict__ x,
 
 // upstream gradient g of a BN output, by mode (see crnn_hip.h CRNN_BNG_*)
 template <typename T>
-__device__ __forceinline__ void bn_g(const crnn_bn_bwd_desc& d, long m, int c8, const float* zz, float* g) {
+__device__ __forceinline__ void bn_g(const crnn_bn_bwd_desc& d, unsigned m, int c8, const float* zz, float* g) {
   float dy[8];
-  unpack8<T>(ld8<T>((const T*)d.dy + m * d.C + c8), dy);
+  unpack8<T>(ld8<T>((const T*)d.dy + (size_t)m * d.C + c8), dy);
   if (d.mode == CRNN_BNG_PLAIN) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) g[i] = dy[i];
@@ -118,14 +118,14 @@ __device__ __forceinline__ void bn_g(const crnn_bn_bwd_desc& d, long m, int c8, 
     for (int i = 0; i < 8; ++i) g[i] = (zz[i] * d.scale[c8 + i] + d.shift[c8 + i]) > 0.f ? dy[i] : 0.f;
   } else {
     float y[8];
-    unpack8<T>(ld8<T>((const T*)d.y + m * d.C + c8), y);
+    unpack8<T>(ld8<T>((const T*)d.y + (size_t)m * d.C + c8), y);
     if (d.mode == CRNN_BNG_RESID) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) g[i] = y[i] > 0.f ? dy[i] : 0.f;
     } else {
-      long b = m / d.HW;
-      const float* s = d.s + b * d.C + c8;
-      const float* dp = d.dpool + b * d.C + c8;
+      const unsigned b = m / (unsigned)d.HW;
+      const float* s = d.s + (size_t)b * d.C + c8;
+      const float* dp = d.dpool + (size_t)b * d.C + c8;
 #pragma unroll
       for (int i = 0; i < 8; ++i) g[i] = (y[i] > 0.f ? dy[i] * s[i] : 0.f) + dp[i];
     }
@@ -137,7 +137,7 @@ template <typename T> struct BnBwdF {
   __device__ __forceinline__ void operator()(long m, int c8, float* s, float* q) const {
     float z[8], g[8];
     unpack8<T>(ld8<T>((const T*)d.z + m * d.C + c8), z);
-    bn_g<T>(d, m, c8, z, g);
+    bn_g<T>(d, (unsigned)m, c8, z, g);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       float xh = (z[i] - d.mean[c8 + i]) * d.invstd[c8 + i];
@@ -146,6 +146,13 @@ template <typename T> struct BnBwdF {
     }
   }
 };
+
+int cg_shift(int C) {
+  if (C % 8) return -1;
+  int g = C / 8, s = 0;
+  while ((1 << s) < g) ++s;
+  return (1 << s) == g ? s : -1;
+}
 
 int rows_for(long M) {
   long r = (M + 63) / 64;
@@ -163,27 +170,77 @@ template <class F> int chan_reduce(F f, long M, int C, float* p0, float* p1, int
   return (int)hipGetLastError();
 }
 
-// ------------------------------------------------------------ finalize (double)
-// partial r covers rows [r*rpp, r*rpp + rpp) of `count`; psum = sum, psq = M2 about the
-// partial's own mean. Chan: M2 = sum M2_r + sum n_r (mean_r - mean)^2.
-__global__ void bn_finalize_kernel(const float* psum, const float* psq, int rows, long rpp, int C, long count,
+// ------------------------------------------------------------ finalize
+// Two stages, both parallel over channels:
+//  (1) chunk_kernel: grid (C/64, P): block y folds partial rows [y*chunk, ...) of 64 channels
+//      (4 row lanes per channel) into one chunk partial. Chan mode: rows hold (sum, M2 about the
+//      row's own mean) covering rpp data rows each; the chunk result is (sum, M2 about the chunk
+//      mean), computed two-pass from the L2-resident partials. Plain mode: two independent sums.
+//  (2) per-channel combine of the P chunk partials in double.
+constexpr int FIN_P = 64;
+
+__device__ __forceinline__ long span_rows(long r0, long r1, long rpp, long count) {
+  long a = r0 * rpp, b = r1 * rpp;
+  if (b > count) b = count;
+  return b > a ? b - a : 0;
+}
+
+__global__ __launch_bounds__(256) void chunk_kernel(const float* __restrict__ p0, const float* __restrict__ p1,
+                                                    int rows, long rpp, int C, long count, int chunk, int chan,
+                                                    float* __restrict__ o0, float* __restrict__ o1) {
+  __shared__ float red[2][4][64];
+  const int lc = threadIdx.x & 63, ln = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lc;
+  const int r0 = blockIdx.y * chunk, r1 = min(rows, r0 + chunk);
+  float s = 0.f, q = 0.f;
+  if (c < C)
+    for (int r = r0 + ln; r < r1; r += 4) {
+      s += p0[(size_t)r * C + c];
+      if (!chan) q += p1[(size_t)r * C + c];
+    }
+  red[0][ln][lc] = s;
+  red[1][ln][lc] = q;
+  __syncthreads();
+  const float S = red[0][0][lc] + red[0][1][lc] + red[0][2][lc] + red[0][3][lc];
+  if (chan) {
+    const long n = span_rows(r0, r1, rpp, count);
+    const float mu = n > 0 ? S / (float)n : 0.f;
+    q = 0.f;
+    if (c < C)
+      for (int r = r0 + ln; r < r1; r += 4) {
+        long nr = span_rows(r, r + 1, rpp, count);
+        if (nr == 0) continue;
+        float d = p0[(size_t)r * C + c] / (float)nr - mu;
+        q += p1[(size_t)r * C + c] + (float)nr * d * d;
+      }
+    __syncthreads();
+    red[1][ln][lc] = q;
+    __syncthreads();
+  }
+  if (ln == 0 && c < C) {
+    o0[(size_t)blockIdx.y * C + c] = S;
+    o1[(size_t)blockIdx.y * C + c] = red[1][0][lc] + red[1][1][lc] + red[1][2][lc] + red[1][3][lc];
+  }
+}
+
+__global__ void bn_finalize_kernel(const float* cs, const float* cq, int P, long crows, int C, long count,
                                    const float* gamma, const float* beta, float* rmean, float* rvar,
                                    float momentum, float eps, int train, float* mean_o, float* inv_o,
                                    float* scale_o, float* shift_o) {
+  // cs/cq: [P][C] chunk (sum, M2); chunk p spans `crows` data rows (last one clipped)
   int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
   double mean, var;
   if (train) {
     double s = 0.0;
-    for (int r = 0; r < rows; ++r) s += psum[(size_t)r * C + c];
+    for (int p = 0; p < P; ++p) s += cs[(size_t)p * C + c];
     mean = s / (double)count;
     double m2 = 0.0;
-    for (int r = 0; r < rows; ++r) {
-      long nr = count - (long)r * rpp;
-      nr = nr < 0 ? 0 : (nr > rpp ? rpp : nr);
-      if (nr == 0) continue;
-      double mr = (double)psum[(size_t)r * C + c] / (double)nr - mean;
-      m2 += (double)psq[(size_t)r * C + c] + (double)nr * mr * mr;
+    for (int p = 0; p < P; ++p) {
+      long n = span_rows(p, p + 1, crows, count);
+      if (n == 0) continue;
+      double d = (double)cs[(size_t)p * C + c] / (double)n - mean;
+      m2 += (double)cq[(size_t)p * C + c] + (double)n * d * d;
     }
     var = m2 / (double)count;
     if (var < 0.0) var = 0.0;
@@ -204,14 +261,14 @@ __global__ void bn_finalize_kernel(const float* psum, const float* psq, int rows
   shift_o[c] = (float)((double)beta[c] - mean * sc);
 }
 
-__global__ void bn_bwd_finalize_kernel(const float* pg, const float* pgx, int rows, int C, long count,
+__global__ void bn_bwd_finalize_kernel(const float* cg, const float* cgx, int P, int C, long count,
                                        float* dgamma, float* dbeta, float* mean_g, float* mean_gx, int acc) {
   int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
   double s = 0.0, q = 0.0;
-  for (int r = 0; r < rows; ++r) {
-    s += pg[(size_t)r * C + c];
-    q += pgx[(size_t)r * C + c];
+  for (int p = 0; p < P; ++p) {
+    s += cg[(size_t)p * C + c];
+    q += cgx[(size_t)p * C + c];
   }
   if (dgamma) dgamma[c] = (float)(acc ? dgamma[c] + q : q);
   if (dbeta) dbeta[c] = (float)(acc ? dbeta[c] + s : s);
@@ -219,31 +276,47 @@ __global__ void bn_bwd_finalize_kernel(const float* pg, const float* pgx, int ro
   mean_gx[c] = (float)(q / (double)count);
 }
 
+int launch_chunks(const float* p0, const float* p1, int rows, long rpp, int C, long count, int chan, float* ws,
+                  int* P_out, long* crows_out, hipStream_t st) {
+  int P = rows < FIN_P ? rows : FIN_P;
+  if (P < 1) P = 1;
+  int chunk = (rows + P - 1) / P;
+  P = (rows + chunk - 1) / chunk;
+  hipLaunchKernelGGL(chunk_kernel, dim3((C + 63) / 64, P), dim3(256), 0, st, p0, p1, rows, rpp, C, count, chunk, chan,
+                     ws, ws + (size_t)FIN_P * C);
+  *P_out = P;
+  *crows_out = (long)chunk * rpp;
+  return (int)hipGetLastError();
+}
+
 // ------------------------------------------------------------ elementwise
+// one lane = 8 channels of one row; C/8 is a power of two (cg_shift = log2(C/8))
 template <typename T>
 __global__ void bn_act_kernel(const T* __restrict__ z, const float* __restrict__ sc, const float* __restrict__ sh,
-                              T* __restrict__ y, long nvec, int C, int relu) {
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < nvec; i += (long)gridDim.x * blockDim.x) {
-    int c8 = (int)((i * 8) % C);
+                              T* __restrict__ y, unsigned nvec, int cg_shift, int relu) {
+  const unsigned cgm = (1u << cg_shift) - 1u;
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += gridDim.x * blockDim.x) {
+    const int c8 = (int)(i & cgm) * 8;
     float v[8];
-    unpack8<T>(ld8<T>(z + i * 8), v);
+    unpack8<T>(ld8<T>(z + (size_t)i * 8), v);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       v[k] = v[k] * sc[c8 + k] + sh[c8 + k];
       if (relu) v[k] = fmaxf(v[k], 0.f);
     }
-    st8<T>(y + i * 8, pack8<T>(v));
+    st8<T>(y + (size_t)i * 8, pack8<T>(v));
   }
 }
 
 template <typename T>
 __global__ void bn_apply_bwd_kernel(crnn_bn_bwd_desc d, const float* __restrict__ mg, const float* __restrict__ mgx,
-                                    T* __restrict__ dz, long nvec) {
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < nvec; i += (long)gridDim.x * blockDim.x) {
-    long m = (i * 8) / d.C;
-    int c8 = (int)(i * 8 - m * d.C);
+                                    T* __restrict__ dz, unsigned nvec, int cg_shift) {
+  const unsigned cgm = (1u << cg_shift) - 1u;
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += gridDim.x * blockDim.x) {
+    const unsigned m = i >> cg_shift;
+    const int c8 = (int)(i & cgm) * 8;
     float z[8], g[8], o[8];
-    unpack8<T>(ld8<T>((const T*)d.z + i * 8), z);
+    unpack8<T>(ld8<T>((const T*)d.z + (size_t)i * 8), z);
     bn_g<T>(d, m, c8, z, g);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -251,7 +324,7 @@ __global__ void bn_apply_bwd_kernel(crnn_bn_bwd_desc d, const float* __restrict_
       float xh = (z[k] - d.mean[c]) * d.invstd[c];
       o[k] = d.scale[c] * (g[k] - mg[c] - xh * mgx[c]);
     }
-    st8<T>(dz + i * 8, pack8<T>(o));
+    st8<T>(dz + (size_t)i * 8, pack8<T>(o));
   }
 }
 
@@ -459,22 +532,24 @@ template <typename T>
 __global__ void se_residual_kernel(const T* __restrict__ z, const float* __restrict__ sc, const float* __restrict__ sh,
                                    const float* __restrict__ s, const T* __restrict__ idn,
                                    const float* __restrict__ isc, const float* __restrict__ ish, T* __restrict__ y,
-                                   long nvec, int HW, int C) {
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < nvec; i += (long)gridDim.x * blockDim.x) {
-    long m = (i * 8) / C;
-    int c8 = (int)(i * 8 - m * C);
-    long b = m / HW;
+                                   unsigned nvec, unsigned HW, int C, int cg_shift) {
+  const unsigned cgm = (1u << cg_shift) - 1u;
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += gridDim.x * blockDim.x) {
+    const unsigned m = i >> cg_shift;
+    const int c8 = (int)(i & cgm) * 8;
+    const unsigned b = m / HW;
     float v[8], d[8];
-    unpack8<T>(ld8<T>(z + i * 8), v);
-    unpack8<T>(ld8<T>(idn + i * 8), d);
+    unpack8<T>(ld8<T>(z + (size_t)i * 8), v);
+    unpack8<T>(ld8<T>(idn + (size_t)i * 8), d);
+    const float* sb = s + (size_t)b * C + c8;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       int c = c8 + k;
-      float u = (v[k] * sc[c] + sh[c]) * s[b * C + c];
+      float u = (v[k] * sc[c] + sh[c]) * sb[k];
       float id = isc ? d[k] * isc[c] + ish[c] : d[k];
       v[k] = fmaxf(u + id, 0.f);
     }
-    st8<T>(y + i * 8, pack8<T>(v));
+    st8<T>(y + (size_t)i * 8, pack8<T>(v));
   }
 }
 
@@ -594,11 +669,21 @@ int crnn_channel_stats(int dtype, const void* x, long M, int C, float* psum, flo
   return (int)hipGetLastError();
 }
 
+size_t crnn_bn_finalize_workspace(int C) { return (size_t)2 * FIN_P * C * sizeof(float); }
+
 int crnn_bn_finalize(const float* psum, const float* psq, int rows, long rows_per_partial, int C, long count,
                      const float* gamma, const float* beta, float* running_mean, float* running_var, float momentum,
-                     float eps, int train, float* mean, float* invstd, float* scale, float* shift, void* stream) {
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 127) / 128), dim3(128), 0, (hipStream_t)stream, psum, psq, rows,
-                     rows_per_partial, C,
+                     float eps, int train, float* mean, float* invstd, float* scale, float* shift, float* ws,
+                     void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  int P = 0;
+  long crows = 0;
+  if (train) {
+    int rc = launch_chunks(psum, psq, rows, rows_per_partial, C, count, 1, ws, &P, &crows, st);
+    if (rc) return rc;
+  }
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 127) / 128), dim3(128), 0, st, ws, ws + (size_t)FIN_P * C, P,
+                     crows, C,
                      count, gamma, beta, running_mean, running_var, momentum, eps, train, mean, invstd, scale, shift);
   return (int)hipGetLastError();
 }
@@ -606,8 +691,10 @@ int crnn_bn_finalize(const float* psum, const float* psq, int rows, long rows_pe
 int crnn_bn_act(int dtype, const void* z, const float* scale, const float* shift, void* y, long M, int C, int relu,
                 void* stream) {
   long nvec = M * C / 8;
-  DISPATCH(dtype, hipLaunchKernelGGL(bn_act_kernel<T>, dim3(grid_for(nvec)), dim3(256), 0, (hipStream_t)stream,
-                                     (const T*)z, scale, shift, (T*)y, nvec, C, relu));
+  int sh = cg_shift(C);
+  if (sh < 0 || nvec >= (1L << 32)) return crnn_set_error(hipErrorInvalidValue, "bn_act: C/8 must be a power of two");
+  DISPATCH(dtype, hipLaunchKernelGGL(bn_act_kernel<T>, dim3(grid_for(nvec, 256, 16384)), dim3(256), 0,
+                                     (hipStream_t)stream, (const T*)z, scale, shift, (T*)y, (unsigned)nvec, sh, relu));
   return (int)hipGetLastError();
 }
 
@@ -634,8 +721,13 @@ int crnn_bn_bwd_reduce(int dtype, const crnn_bn_bwd_desc* d, float* pg, float* p
 }
 
 int crnn_bn_bwd_finalize(const float* pg, const float* pgx, int rows, int C, long count, float* dgamma, float* dbeta,
-                         float* mean_g, float* mean_gx, int accumulate, void* stream) {
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 127) / 128), dim3(128), 0, (hipStream_t)stream, pg, pgx, rows, C,
+                         float* mean_g, float* mean_gx, int accumulate, float* ws, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  int P = 0;
+  long crows = 0;
+  int rc = launch_chunks(pg, pgx, rows, 1, C, (long)rows, 0, ws, &P, &crows, st);
+  if (rc) return rc;
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 127) / 128), dim3(128), 0, st, ws, ws + (size_t)FIN_P * C, P, C,
                      count, dgamma, dbeta, mean_g, mean_gx, accumulate);
   return (int)hipGetLastError();
 }
@@ -643,8 +735,10 @@ int crnn_bn_bwd_finalize(const float* pg, const float* pgx, int rows, int C, lon
 int crnn_bn_bwd_apply(int dtype, const crnn_bn_bwd_desc* d, const float* mean_g, const float* mean_gx, void* dz,
                       void* stream) {
   long nvec = d->M * d->C / 8;
-  DISPATCH(dtype, hipLaunchKernelGGL(bn_apply_bwd_kernel<T>, dim3(grid_for(nvec)), dim3(256), 0, (hipStream_t)stream,
-                                     *d, mean_g, mean_gx, (T*)dz, nvec));
+  int sh = cg_shift(d->C);
+  if (sh < 0 || nvec >= (1L << 32)) return crnn_set_error(hipErrorInvalidValue, "bn_bwd_apply: C/8 must be a power of two");
+  DISPATCH(dtype, hipLaunchKernelGGL(bn_apply_bwd_kernel<T>, dim3(grid_for(nvec, 256, 16384)), dim3(256), 0,
+                                     (hipStream_t)stream, *d, mean_g, mean_gx, (T*)dz, (unsigned)nvec, sh));
   return (int)hipGetLastError();
 }
 
@@ -668,8 +762,11 @@ int crnn_se_residual_fwd(int dtype, const void* z2, const float* scale, const fl
                          const void* idn, const float* iscale, const float* ishift, void* y, int B, int HW, int C,
                          void* stream) {
   long nvec = (long)B * HW * C / 8;
-  DISPATCH(dtype, hipLaunchKernelGGL(se_residual_kernel<T>, dim3(grid_for(nvec)), dim3(256), 0, (hipStream_t)stream,
-                                     (const T*)z2, scale, shift, s, (const T*)idn, iscale, ishift, (T*)y, nvec, HW, C));
+  int sh = cg_shift(C);
+  if (sh < 0 || nvec >= (1L << 32)) return crnn_set_error(hipErrorInvalidValue, "se_residual: C/8 must be a power of two");
+  DISPATCH(dtype, hipLaunchKernelGGL(se_residual_kernel<T>, dim3(grid_for(nvec, 256, 16384)), dim3(256), 0,
+                                     (hipStream_t)stream, (const T*)z2, scale, shift, s, (const T*)idn, iscale, ishift,
+                                     (T*)y, (unsigned)nvec, (unsigned)HW, C, sh));
   return (int)hipGetLastError();
 }
 

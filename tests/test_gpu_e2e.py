@@ -96,8 +96,21 @@ def _hip_train_grads(z, hidden, sd):
     return model, logits, loss
 
 
+def _oracle_grads(sd, z, dt):
+    x = pixels_to_images(z["pixels"])
+    tg, tl = torch.from_numpy(z["targets"]), torch.from_numpy(z["target_lengths"])
+    p = {k: (v.to(dt).clone().requires_grad_(True) if v.is_floating_point() and "running" not in k
+             else (v.to(dt) if v.is_floating_point() else v)) for k, v in sd.items()}
+    lg = O.head(O.encode(x.to(dt), p, O.Ctx(train=True)), p)
+    O.ctc_loss(lg, tg, tl).backward()
+    return {k: v.grad.double() for k, v in p.items() if getattr(v, "grad", None) is not None}
+
+
 def test_train_step_fp32_grads_match_reference():
-    """well-conditioned golden case: every parameter gradient within 2e-4 of the reference."""
+    """Well-conditioned golden case. (a) vs the reference's own output (tests/golden): loss,
+    logits and dlogits tight; parameter gradients within 5e-3 — the reference's CPU fp32
+    (mkldnn) gradients themselves sit up to 2e-3 from an fp64 evaluation on this case.
+    (b) vs the fp64 oracle: EVERY parameter gradient of the HIP fp32 path within 1e-4."""
     z = load("train_b4_32x128_h256.npz")
     sd, hidden = case_params(z, with_running=False)
     model, logits, loss = _hip_train_grads(z, hidden, sd)
@@ -114,9 +127,13 @@ def test_train_step_fp32_grads_match_reference():
         idx = z["gidx::" + name]
         ref = z["gval::" + name].astype(np.float64)
         serr = np.linalg.norm(g[idx] - ref) / max(np.linalg.norm(ref), 1e-12)
-        if nerr > 1e-4 or serr > 2e-4:
+        if nerr > 1e-3 or serr > 5e-3:
             bad.append((name, nerr, serr))
     assert not bad, bad
+    g64 = _oracle_grads(sd, z, torch.float64)
+    worst = max((float((params[k].grad.double().cpu() - r).norm() / (r.norm() + 1e-30)), k) for k, r in g64.items())
+    print("max per-parameter grad error vs fp64:", worst)
+    assert worst[0] < 1e-4, worst
     bufs = dict(model.named_buffers())
     for k in z.keys():
         if k.startswith("bnrun::"):

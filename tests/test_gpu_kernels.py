@@ -314,9 +314,10 @@ def test_bn_bwd_and_se(dtype):
     gd, bd = gamma.to(DEV), beta.to(DEV)
     rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
     mean, inv, sc, sh = [torch.empty(C, device=DEV) for _ in range(4)]
+    fws = torch.empty(L.lib().crnn_bn_finalize_workspace(C) // 4, device=DEV)
     L.call("crnn_bn_finalize", ps.data_ptr(), pq.data_ptr(), rows, (M + rows - 1) // rows, C, M, gd.data_ptr(),
            bd.data_ptr(), rm.data_ptr(),
-           rv.data_ptr(), 0.1, 1e-5, 1, mean.data_ptr(), inv.data_ptr(), sc.data_ptr(), sh.data_ptr(), st)
+           rv.data_ptr(), 0.1, 1e-5, 1, mean.data_ptr(), inv.data_ptr(), sc.data_ptr(), sh.data_ptr(), fws.data_ptr(), st)
     pooled_d = torch.empty(B, C, device=DEV)
     hid = torch.empty(B, Cr, device=DEV)
     sd = torch.empty(B, C, device=DEV)
@@ -349,7 +350,7 @@ def test_bn_bwd_and_se(dtype):
     L.call("crnn_bn_bwd_reduce", dt, desc, pg.data_ptr(), pgx.data_ptr(), rows, st)
     dgam, dbet, mg, mgx = [torch.empty(C, device=DEV) for _ in range(4)]
     L.call("crnn_bn_bwd_finalize", pg.data_ptr(), pgx.data_ptr(), rows, C, M, dgam.data_ptr(), dbet.data_ptr(),
-           mg.data_ptr(), mgx.data_ptr(), 0, st)
+           mg.data_ptr(), mgx.data_ptr(), 0, fws.data_ptr(), st)
     dz = torch.empty(B, H, W, C, dtype=dtype, device=DEV)
     L.call("crnn_bn_bwd_apply", dt, desc, mg.data_ptr(), mgx.data_ptr(), dz.data_ptr(), st)
     assert relerr(dgam.cpu(), pr[0].grad) < gtol
