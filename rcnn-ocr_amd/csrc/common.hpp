@@ -120,4 +120,29 @@ __device__ __forceinline__ int xcd_remap(int b, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + b / nx;
 }
 
+// Division by a runtime-invariant divisor via a precomputed magic number:
+// n / d = (umulhi(n, mul) + n) >> shift, exact for 0 <= n < 2^31 (Granlund-Montgomery).
+struct FastDiv {
+  uint32_t d, mul, shift;
+  FastDiv() = default;
+  __host__ FastDiv(uint32_t div) : d(div) {
+    uint32_t s = 0;
+    while (s < 32 && (1ull << s) < div) ++s;
+    uint64_t one = 1;
+    uint64_t m = ((one << 32) * ((one << s) - div)) / div + 1;
+    mul = (uint32_t)m;
+    shift = s;
+  }
+  __device__ __forceinline__ uint32_t div(uint32_t n) const {
+    uint32_t t = __umulhi(n, mul);
+    return (t + n) >> shift;
+  }
+  // q = n / d, r = n - q*d
+  __device__ __forceinline__ uint32_t divmod(uint32_t n, uint32_t& r) const {
+    uint32_t q = div(n);
+    r = n - q * d;
+    return q;
+  }
+};
+
 #define CRNN_CHECK_LAUNCH() return (int)hipGetLastError()

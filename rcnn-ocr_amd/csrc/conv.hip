@@ -19,10 +19,22 @@ namespace {
 
 struct Geo {
   int B, Hi, Wi, Ci, Ho, Wo, Co, KH, KW, sh, sw, ph, pw;
+  // magic divisors for the im2col decodes (no hardware integer division on the GPU)
+  FastDiv dCi, dCo, dKW, dWo, dHoWo, dWi, dHiWi, dsh, dsw;
 };
 
 inline Geo geo(const crnn_conv_desc* d) {
-  return Geo{d->B, d->Hi, d->Wi, d->Ci, d->Ho, d->Wo, d->Co, d->KH, d->KW, d->sh, d->sw, d->ph, d->pw};
+  Geo g{d->B, d->Hi, d->Wi, d->Ci, d->Ho, d->Wo, d->Co, d->KH, d->KW, d->sh, d->sw, d->ph, d->pw};
+  g.dCi = FastDiv(d->Ci);
+  g.dCo = FastDiv(d->Co);
+  g.dKW = FastDiv(d->KW);
+  g.dWo = FastDiv(d->Wo);
+  g.dHoWo = FastDiv(d->Ho * d->Wo);
+  g.dWi = FastDiv(d->Wi);
+  g.dHiWi = FastDiv(d->Hi * d->Wi);
+  g.dsh = FastDiv(d->sh);
+  g.dsw = FastDiv(d->sw);
+  return g;
 }
 
 // ---- fwd A: im2col rows of x (NHWC [B][Hi][Wi][Ci]), K-contiguous
@@ -35,10 +47,9 @@ template <typename T> struct FwdA {
   __device__ __forceinline__ Ctx row_ctx(int m) const {
     Ctx c;
     c.ok = m < M;
-    int mm = c.ok ? m : 0;
-    int hw = g.Ho * g.Wo;
-    int b = mm / hw, r = mm - b * hw;
-    int ho = r / g.Wo, wo = r - ho * g.Wo;
+    uint32_t r, wo;
+    uint32_t b = g.dHoWo.divmod(c.ok ? m : 0, r);
+    uint32_t ho = g.dWo.divmod(r, wo);
     c.hb = ho * g.sh - g.ph;
     c.wb = wo * g.sw - g.pw;
     c.base = x + (size_t)b * g.Hi * g.Wi * g.Ci;
@@ -46,11 +57,12 @@ template <typename T> struct FwdA {
   }
   __device__ __forceinline__ typename VT<T>::v8 load(const Ctx& c, int k) const {
     if (!c.ok || k >= K) return zero8<T>();
-    int tap = k / g.Ci, ci = k - tap * g.Ci;
-    int kh = tap / g.KW, kw = tap - kh * g.KW;
-    int hi = c.hb + kh, wi = c.wb + kw;
+    uint32_t ci, kw;
+    uint32_t tap = g.dCi.divmod(k, ci);
+    uint32_t kh = g.dKW.divmod(tap, kw);
+    int hi = c.hb + (int)kh, wi = c.wb + (int)kw;
     if ((unsigned)hi >= (unsigned)g.Hi || (unsigned)wi >= (unsigned)g.Wi) return zero8<T>();
-    return ld8<T>(c.base + ((size_t)hi * g.Wi + wi) * g.Ci + ci);
+    return ld8<T>(c.base + (uint32_t)((hi * g.Wi + wi) * g.Ci + (int)ci));
   }
 };
 
@@ -64,10 +76,9 @@ template <typename T> struct DgradA {
   __device__ __forceinline__ Ctx row_ctx(int m) const {
     Ctx c;
     c.ok = m < M;
-    int mm = c.ok ? m : 0;
-    int hw = g.Hi * g.Wi;
-    int b = mm / hw, r = mm - b * hw;
-    int hi = r / g.Wi, wi = r - hi * g.Wi;
+    uint32_t r, wi;
+    uint32_t b = g.dHiWi.divmod(c.ok ? m : 0, r);
+    uint32_t hi = g.dWi.divmod(r, wi);
     c.hp = hi + g.ph;
     c.wp = wi + g.pw;
     c.base = dy + (size_t)b * g.Ho * g.Wo * g.Co;
@@ -75,13 +86,15 @@ template <typename T> struct DgradA {
   }
   __device__ __forceinline__ typename VT<T>::v8 load(const Ctx& c, int k) const {
     if (!c.ok || k >= K) return zero8<T>();
-    int tap = k / g.Co, co = k - tap * g.Co;
-    int kh = tap / g.KW, kw = tap - kh * g.KW;
-    int th = c.hp - kh, tw = c.wp - kw;
+    uint32_t co, kw;
+    uint32_t tap = g.dCo.divmod(k, co);
+    uint32_t kh = g.dKW.divmod(tap, kw);
+    int th = c.hp - (int)kh, tw = c.wp - (int)kw;
     if (th < 0 || tw < 0) return zero8<T>();
-    int ho = th / g.sh, wo = tw / g.sw;
-    if (ho * g.sh != th || wo * g.sw != tw || ho >= g.Ho || wo >= g.Wo) return zero8<T>();
-    return ld8<T>(c.base + ((size_t)ho * g.Wo + wo) * g.Co + co);
+    uint32_t rh, rw;
+    int ho = (int)g.dsh.divmod(th, rh), wo = (int)g.dsw.divmod(tw, rw);
+    if (rh | rw || ho >= g.Ho || wo >= g.Wo) return zero8<T>();
+    return ld8<T>(c.base + (uint32_t)((ho * g.Wo + wo) * g.Co + (int)co));
   }
 };
 
@@ -95,8 +108,9 @@ template <typename T> struct DgradB {
   __device__ __forceinline__ Ctx row_ctx(int r8) const { return Ctx{r8, r8 < g.Ci}; }
   __device__ __forceinline__ typename VT<T>::v8 load(const Ctx& c, int k) const {
     if (!c.ok || k >= K) return zero8<T>();
-    int tap = k / g.Co, co = k - tap * g.Co;
-    return ld8<T>(w + ((size_t)co * g.KH * g.KW + tap) * g.Ci + c.ci);
+    uint32_t co;
+    uint32_t tap = g.dCo.divmod(k, co);
+    return ld8<T>(w + (uint32_t)(((int)co * g.KH * g.KW + (int)tap) * g.Ci + c.ci));
   }
 };
 
@@ -123,21 +137,22 @@ template <typename T> struct WgradB {
   __device__ __forceinline__ Ctx row_ctx(int r8) const {
     Ctx c;
     c.ok = r8 < Kp;
-    int rr = c.ok ? r8 : 0;
-    int tap = rr / g.Ci;
-    c.ci = rr - tap * g.Ci;
-    c.kh = tap / g.KW;
-    c.kw = tap - c.kh * g.KW;
+    uint32_t ci, kw;
+    uint32_t tap = g.dCi.divmod(c.ok ? r8 : 0, ci);
+    uint32_t kh = g.dKW.divmod(tap, kw);
+    c.ci = ci;
+    c.kh = kh;
+    c.kw = kw;
     return c;
   }
   __device__ __forceinline__ typename VT<T>::v8 load(const Ctx& c, int m) const {
     if (!c.ok || m >= M) return zero8<T>();
-    int hw = g.Ho * g.Wo;
-    int b = m / hw, r = m - b * hw;
-    int ho = r / g.Wo, wo = r - ho * g.Wo;
-    int hi = ho * g.sh - g.ph + c.kh, wi = wo * g.sw - g.pw + c.kw;
+    uint32_t r, wo;
+    uint32_t b = g.dHoWo.divmod(m, r);
+    uint32_t ho = g.dWo.divmod(r, wo);
+    int hi = (int)ho * g.sh - g.ph + c.kh, wi = (int)wo * g.sw - g.pw + c.kw;
     if ((unsigned)hi >= (unsigned)g.Hi || (unsigned)wi >= (unsigned)g.Wi) return zero8<T>();
-    return ld8<T>(x + (((size_t)b * g.Hi + hi) * g.Wi + wi) * g.Ci + c.ci);
+    return ld8<T>(x + (size_t)b * g.Hi * g.Wi * g.Ci + (uint32_t)((hi * g.Wi + wi) * g.Ci + c.ci));
   }
 };
 
@@ -230,6 +245,7 @@ template <typename T> int conv_dgrad_t(const crnn_conv_desc* d, const void* dy, 
   DgradB<T> lb{(const T*)w, g, K};
   DgradEpi<T> ep{(T*)dx, (const T*)dres, (const T*)yres, M, N, accumulate};
   if (N >= 128 && (long)M * N >= 128L * 128 * 256) return launch<T, 128, 128>(la, lb, ep, M, N, K, 1, st);
+  if (N <= 64 && (long)M * N >= 128L * 64 * 256) return launch<T, 128, 64>(la, lb, ep, M, N, K, 1, st);
   return launch<T, 64, 64>(la, lb, ep, M, N, K, 1, st);
 }
 
