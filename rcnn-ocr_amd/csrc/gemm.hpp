@@ -27,15 +27,15 @@
 
 namespace gemm {
 
-constexpr int BK = 32;
+constexpr int BK = 32;  // K per MFMA sub-step; a pipeline stage holds KS = 32 or 64
 constexpr int NT = 256;
 
-template <typename T> constexpr int kpitch() { return BK + (int)(16 / sizeof(T)); }
+template <typename T, int KS = BK> constexpr int kpitch() { return KS + (int)(16 / sizeof(T)); }
 // row-contiguous pitch: 32*odd bytes for bf16 (conflict-free ds_read_b64_tr_b16
 // over 8 k-rows), (R+4) floats for f32 (conflict-free strided ds_read_b32)
 template <typename T, int R> constexpr int rpitch() { return sizeof(T) == 2 ? R + 16 : R + 4; }
-template <typename T, int R, bool RowVec> constexpr int tile_elems() {
-  return RowVec ? BK * rpitch<T, R>() : R * kpitch<T>();
+template <typename T, int R, bool RowVec, int KS = BK> constexpr int tile_elems() {
+  return RowVec ? KS * rpitch<T, R>() : R * kpitch<T, KS>();
 }
 
 // k index held by element j of a lane in 16-lane group g.
@@ -47,9 +47,9 @@ template <bool PERM> __device__ __forceinline__ int kmap(int g, int j) {
   else return 8 * g + j;
 }
 
-template <typename T, int R, class L> struct Stager {
+template <typename T, int R, int KS, class L> struct Stager {
   static constexpr bool RV = L::kRowVec;
-  static constexpr int ITEMS = R * BK / 8;
+  static constexpr int ITEMS = R * KS / 8;
   static constexpr int PT = ITEMS >= NT ? ITEMS / NT : 1;
   static constexpr bool PARTIAL = ITEMS < NT;  // small tiles: only the first ITEMS threads stage
   static_assert(ITEMS < NT || ITEMS % NT == 0, "tile/thread mismatch");
@@ -70,9 +70,9 @@ template <typename T, int R, class L> struct Stager {
         lds_off[j] = k * rpitch<T, R>() + r8;
         kofs[j] = k;
       } else {
-        int r = i / (BK / 8), kg = i % (BK / 8);
+        int r = i / (KS / 8), kg = i % (KS / 8);
         ctx[j] = l.row_ctx(row0 + r);
-        lds_off[j] = r * kpitch<T>() + kg * 8;
+        lds_off[j] = r * kpitch<T, KS>() + kg * 8;
         kofs[j] = kg * 8;
       }
     }
@@ -90,12 +90,13 @@ template <typename T, int R, class L> struct Stager {
 };
 
 // Fragment of 16 MFMA rows [rb, rb+16) x 32 k for this lane.
-template <typename T, int R, bool RV, bool PERM>
-__device__ __forceinline__ typename VT<T>::v8 frag(const T* tile, int rb, int lane) {
+// kk: which 32-deep MFMA sub-step of the KS-deep stage
+template <typename T, int R, bool RV, bool PERM, int KS>
+__device__ __forceinline__ typename VT<T>::v8 frag(const T* tile, int rb, int kk, int lane) {
   typename VT<T>::v8 v;
   const int g = lane >> 4, c = lane & 15;
   if constexpr (!RV) {
-    const T* p = tile + (rb + c) * kpitch<T>();
+    const T* p = tile + (rb + c) * kpitch<T, KS>() + kk * BK;
     if constexpr (!PERM) {
       v = *reinterpret_cast<const typename VT<T>::v8*>(p + 8 * g);
     } else {
@@ -109,15 +110,15 @@ __device__ __forceinline__ typename VT<T>::v8 frag(const T* tile, int rb, int la
     if constexpr (sizeof(T) == 2) {
       const int q = c >> 2, p = c & 3;
       typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
-      const T* a0 = tile + (4 * g + q) * rpitch<T, R>() + rb + 4 * p;
-      const T* a1 = tile + (16 + 4 * g + q) * rpitch<T, R>() + rb + 4 * p;
+      const T* a0 = tile + (kk * BK + 4 * g + q) * rpitch<T, R>() + rb + 4 * p;
+      const T* a1 = tile + (kk * BK + 16 + 4 * g + q) * rpitch<T, R>() + rb + 4 * p;
       s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0));
       s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a1));
       s16x4 tmp[2] = {lo, hi};
       v = *reinterpret_cast<const bf16x8*>(tmp);
     } else {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = tile[kmap<true>(g, j) * rpitch<T, R>() + rb + c];
+      for (int j = 0; j < 8; ++j) v[j] = tile[(kk * BK + kmap<true>(g, j)) * rpitch<T, R>() + rb + c];
     }
   }
   return v;
@@ -133,13 +134,13 @@ __device__ __forceinline__ void mma(f32x4& acc, const typename VT<T>::v8& a, con
   }
 }
 
-template <typename T, int BM, int BN, class LA, class LB, class EPI>
+template <typename T, int BM, int BN, int KS, class LA, class LB, class EPI>
 __global__ __launch_bounds__(256) void gemm_kernel(LA la, LB lb, EPI epi, int M, int N, int K,
                                                    int klen, int tiles_m, int tiles_n, int nsplit) {
   constexpr bool PERM = LA::kRowVec || LB::kRowVec;
   constexpr int WM = BM / 2, WN = BN / 2, MI = WM / 16, NI = WN / 16;
-  constexpr int AE = tile_elems<T, BM, LA::kRowVec>();
-  constexpr int BE = tile_elems<T, BN, LB::kRowVec>();
+  constexpr int AE = tile_elems<T, BM, LA::kRowVec, KS>();
+  constexpr int BE = tile_elems<T, BN, LB::kRowVec, KS>();
   __shared__ __attribute__((aligned(16))) T smem[2 * (AE + BE)];
 
   const int nwg = tiles_m * tiles_n * nsplit;
@@ -150,13 +151,13 @@ __global__ __launch_bounds__(256) void gemm_kernel(LA la, LB lb, EPI epi, int M,
   const int m0 = m_tile * BM, n0 = n_tile * BN;
   const int kbeg = kz * klen;
   const int kend = min(K, kbeg + klen);
-  const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+  const int nk = kend > kbeg ? (kend - kbeg + KS - 1) / KS : 0;
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
 
-  Stager<T, BM, LA> sa;
-  Stager<T, BN, LB> sb;
+  Stager<T, BM, KS, LA> sa;
+  Stager<T, BN, KS, LB> sb;
   sa.init(la, m0, tid);
   sb.init(lb, n0, tid);
 
@@ -184,18 +185,21 @@ __global__ __launch_bounds__(256) void gemm_kernel(LA la, LB lb, EPI epi, int M,
     const T* Ac = (kt & 1) ? As1 : As0;
     const T* Bc = (kt & 1) ? Bs1 : Bs0;
     if (more) {
-      sa.load(la, kbeg + (kt + 1) * BK);
-      sb.load(lb, kbeg + (kt + 1) * BK);
+      sa.load(la, kbeg + (kt + 1) * KS);
+      sb.load(lb, kbeg + (kt + 1) * KS);
     }
-    typename VT<T>::v8 af[MI], bfr[NI];
 #pragma unroll
-    for (int i = 0; i < MI; ++i) af[i] = frag<T, BM, LA::kRowVec, PERM>(Ac, wm * WM + i * 16, lane);
+    for (int kk = 0; kk < KS / BK; ++kk) {
+      typename VT<T>::v8 af[MI], bfr[NI];
 #pragma unroll
-    for (int j = 0; j < NI; ++j) bfr[j] = frag<T, BN, LB::kRowVec, PERM>(Bc, wn * WN + j * 16, lane);
+      for (int i = 0; i < MI; ++i) af[i] = frag<T, BM, LA::kRowVec, PERM, KS>(Ac, wm * WM + i * 16, kk, lane);
 #pragma unroll
-    for (int i = 0; i < MI; ++i)
+      for (int j = 0; j < NI; ++j) bfr[j] = frag<T, BN, LB::kRowVec, PERM, KS>(Bc, wn * WN + j * 16, kk, lane);
 #pragma unroll
-      for (int j = 0; j < NI; ++j) mma<T>(acc[i][j], bfr[j], af[i]);
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j) mma<T>(acc[i][j], bfr[j], af[i]);
+    }
     if (more) {
       sa.store((kt & 1) ? As0 : As1);
       sb.store((kt & 1) ? Bs0 : Bs1);
@@ -244,27 +248,36 @@ __global__ __launch_bounds__(256) void gemm_kernel(LA la, LB lb, EPI epi, int M,
   }
 }
 
-template <typename T, int BM, int BN, class LA, class LB, class EPI>
-inline int launch(const LA& la, const LB& lb, const EPI& epi, int M, int N, int K, int nsplit,
-                  hipStream_t st) {
-  if (M <= 0 || N <= 0) return 0;
-  const int tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN;
+// K splits are whole multiples of 64 so that both stage depths tile them exactly
+constexpr int KSPLIT_Q = 64;
+
+inline int split_len(int K, int nsplit) {
   if (nsplit < 1) nsplit = 1;
-  int klen = ((K + nsplit - 1) / nsplit + BK - 1) / BK * BK;
-  if (klen < BK) klen = BK;
-  nsplit = K > 0 ? (K + klen - 1) / klen : 1;
-  const int nwg = tm * tn * nsplit;
-  hipLaunchKernelGGL((gemm_kernel<T, BM, BN, LA, LB, EPI>), dim3(nwg), dim3(NT), 0, st, la, lb, epi,
-                     M, N, K, klen, tm, tn, nsplit);
-  return (int)hipGetLastError();
+  int klen = ((K + nsplit - 1) / nsplit + KSPLIT_Q - 1) / KSPLIT_Q * KSPLIT_Q;
+  return klen < KSPLIT_Q ? KSPLIT_Q : klen;
 }
 
 // number of K splits the launcher will actually use
 inline int eff_splits(int K, int nsplit) {
-  if (nsplit < 1) nsplit = 1;
-  int klen = ((K + nsplit - 1) / nsplit + BK - 1) / BK * BK;
-  if (klen < BK) klen = BK;
+  int klen = split_len(K, nsplit);
   return K > 0 ? (K + klen - 1) / klen : 1;
+}
+
+// default pipeline stage depth: 64 for bf16 (one barrier per two MFMA K-steps), 32 for the
+// f32 parity mode (its exact-f32 MFMA is 16x slower; LDS stays small)
+template <typename T> constexpr int kstage() { return sizeof(T) == 2 ? 64 : 32; }
+
+template <typename T, int BM, int BN, int KS = kstage<T>(), class LA, class LB, class EPI>
+inline int launch(const LA& la, const LB& lb, const EPI& epi, int M, int N, int K, int nsplit,
+                  hipStream_t st) {
+  if (M <= 0 || N <= 0) return 0;
+  const int tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN;
+  const int klen = split_len(K, nsplit);
+  nsplit = K > 0 ? (K + klen - 1) / klen : 1;
+  const int nwg = tm * tn * nsplit;
+  hipLaunchKernelGGL((gemm_kernel<T, BM, BN, KS, LA, LB, EPI>), dim3(nwg), dim3(NT), 0, st, la, lb, epi,
+                     M, N, K, klen, tm, tn, nsplit);
+  return (int)hipGetLastError();
 }
 
 // ---------------------------------------------------------------- simple loaders
