@@ -120,6 +120,37 @@ __device__ __forceinline__ int xcd_remap(int b, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + b / nx;
 }
 
+// ---- range-checked buffer loads (CDNA raw buffer addressing)
+// A lane whose byte offset is >= the descriptor's num_records reads zeros in hardware,
+// so masked / out-of-bounds gathers need no exec-mask branches.
+constexpr uint32_t OOB = 0x80000000u;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t mk_rsrc(const void* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+
+template <typename T>
+__device__ __forceinline__ typename VT<T>::v8 bld8(__amdgpu_buffer_rsrc_t r, uint32_t byteoff) {
+  if constexpr (sizeof(T) == 2) {
+    u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, byteoff, 0, 0);
+    return __builtin_bit_cast(bf16x8, v);
+  } else {
+    u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(r, byteoff, 0, 0);
+    u32x4 b = __builtin_amdgcn_raw_buffer_load_b128(r, byteoff + 16u, 0, 0);
+    f32x4 fa = __builtin_bit_cast(f32x4, a), fb = __builtin_bit_cast(f32x4, b);
+    f32x8 o;
+    o[0] = fa[0]; o[1] = fa[1]; o[2] = fa[2]; o[3] = fa[3];
+    o[4] = fb[0]; o[5] = fb[1]; o[6] = fb[2]; o[7] = fb[3];
+    return o;
+  }
+}
+
+// element offset -> byte offset, or OOB when !ok
+template <typename T> __device__ __forceinline__ uint32_t boff(uint32_t elem, bool ok) {
+  return ok ? elem * (uint32_t)sizeof(T) : OOB;
+}
+
 // Division by a runtime-invariant divisor via a precomputed magic number:
 // n / d = (umulhi(n, mul) + n) >> shift, exact for 0 <= n < 2^31 (Granlund-Montgomery).
 struct FastDiv {

@@ -37,64 +37,113 @@ inline Geo geo(const crnn_conv_desc* d) {
   return g;
 }
 
-// ---- fwd A: im2col rows of x (NHWC [B][Hi][Wi][Ci]), K-contiguous
-template <typename T> struct FwdA {
+// Per-stage K decode shared by the loaders whose K = (tap, channel) with channel-minor order.
+// When the channel count C is a multiple of the stage depth (every conv except the 8-channel
+// stem input), a stage never straddles a tap: tap / channel base are wave-uniform scalars.
+struct TapPrep {
+  int tap;   // kh*KW + kw (>= KH*KW means past K: masked)
+  int kh, kw;
+  int c0;    // channel of k0
+};
+
+__device__ __forceinline__ TapPrep tap_prep(const FastDiv& dC, const FastDiv& dKW, int k0) {
+  TapPrep p;
+  uint32_t c, kw;
+  uint32_t tap = dC.divmod((uint32_t)k0, c);
+  uint32_t kh = dKW.divmod(tap, kw);
+  p.tap = (int)tap;
+  p.kh = (int)kh;
+  p.kw = (int)kw;
+  p.c0 = (int)c;
+  return p;
+}
+
+// ---- fwd A: im2col rows of x (NHWC [B][Hi][Wi][Ci]), K-contiguous, K = (kh, kw, ci)
+// UT: the stage never straddles a tap (Ci % stage depth == 0)
+template <typename T, bool UT> struct FwdA {
   static constexpr bool kRowVec = false;
   const T* x;
   Geo g;
   int M, K;
-  struct Ctx { const T* base; int hb, wb; bool ok; };
+  uint32_t bytes;
+  struct Ctx { int off; uint32_t mask; int hb, wb; };  // off = element offset of (b, hb, wb, 0)
+  typedef TapPrep Prep;
   __device__ __forceinline__ Ctx row_ctx(int m) const {
     Ctx c;
-    c.ok = m < M;
     uint32_t r, wo;
-    uint32_t b = g.dHoWo.divmod(c.ok ? m : 0, r);
+    uint32_t b = g.dHoWo.divmod(m < M ? m : 0, r);
     uint32_t ho = g.dWo.divmod(r, wo);
-    c.hb = ho * g.sh - g.ph;
-    c.wb = wo * g.sw - g.pw;
-    c.base = x + (size_t)b * g.Hi * g.Wi * g.Ci;
+    c.hb = (int)ho * g.sh - g.ph;
+    c.wb = (int)wo * g.sw - g.pw;
+    c.off = (((int)b * g.Hi + c.hb) * g.Wi + c.wb) * g.Ci;
+    c.mask = 0;
+    if (m < M)
+      for (int kh = 0; kh < g.KH; ++kh)
+        for (int kw = 0; kw < g.KW; ++kw)
+          if ((unsigned)(c.hb + kh) < (unsigned)g.Hi && (unsigned)(c.wb + kw) < (unsigned)g.Wi)
+            c.mask |= 1u << (kh * g.KW + kw);
     return c;
   }
-  __device__ __forceinline__ typename VT<T>::v8 load(const Ctx& c, int k) const {
-    if (!c.ok || k >= K) return zero8<T>();
-    uint32_t ci, kw;
-    uint32_t tap = g.dCi.divmod(k, ci);
-    uint32_t kh = g.dKW.divmod(tap, kw);
-    int hi = c.hb + (int)kh, wi = c.wb + (int)kw;
-    if ((unsigned)hi >= (unsigned)g.Hi || (unsigned)wi >= (unsigned)g.Wi) return zero8<T>();
-    return ld8<T>(c.base + (uint32_t)((hi * g.Wi + wi) * g.Ci + (int)ci));
+  __device__ __forceinline__ Prep prep(int k0) const {
+    if constexpr (UT) return tap_prep(g.dCi, g.dKW, k0);
+    TapPrep p;
+    p.tap = k0;
+    return p;
+  }
+  __device__ __forceinline__ typename VT<T>::v8 load(const Ctx& c, const Prep& p, int kofs) const {
+    auto rs = mk_rsrc(x, bytes);
+    if constexpr (UT) {
+      const bool ok = (c.mask >> p.tap) & 1u;
+      const int off = c.off + (p.kh * g.Wi + p.kw) * g.Ci + p.c0 + kofs;
+      return bld8<T>(rs, boff<T>((uint32_t)off, ok));
+    } else {
+      const int k = p.tap + kofs;
+      uint32_t ci, kw;
+      uint32_t tap = g.dCi.divmod((uint32_t)k, ci);
+      uint32_t kh = g.dKW.divmod(tap, kw);
+      const bool ok = k < K && ((c.mask >> tap) & 1u);
+      const int off = c.off + ((int)kh * g.Wi + (int)kw) * g.Ci + (int)ci;
+      return bld8<T>(rs, boff<T>((uint32_t)off, ok));
+    }
   }
 };
 
-// ---- dgrad A: gather of dy for input pixel rows, K = (kh,kw,co) contiguous in co
+// ---- dgrad A: for input pixel rows (b, hi, wi), K = (kh, kw, co): dy at
+// ((hi+ph-kh)/sh, (wi+pw-kw)/sw). Strides are 1 or 2 (lsh/lsw = log2), so for a valid tap
+// (in range, divisible) the output row is (hp>>lsh) - (kh>>lsh): linear in a per-row base
+// plus a per-stage scalar.
 template <typename T> struct DgradA {
   static constexpr bool kRowVec = false;
   const T* dy;
   Geo g;
-  int M, K;
-  struct Ctx { const T* base; int hp, wp; bool ok; };
+  int M, K, lsh, lsw;
+  uint32_t bytes;
+  struct Ctx { int off; uint32_t mask; };
+  typedef TapPrep Prep;
   __device__ __forceinline__ Ctx row_ctx(int m) const {
     Ctx c;
-    c.ok = m < M;
     uint32_t r, wi;
-    uint32_t b = g.dHiWi.divmod(c.ok ? m : 0, r);
+    uint32_t b = g.dHiWi.divmod(m < M ? m : 0, r);
     uint32_t hi = g.dWi.divmod(r, wi);
-    c.hp = hi + g.ph;
-    c.wp = wi + g.pw;
-    c.base = dy + (size_t)b * g.Ho * g.Wo * g.Co;
+    const int hp = (int)hi + g.ph, wp = (int)wi + g.pw;
+    c.off = (((int)b * g.Ho + (hp >> lsh)) * g.Wo + (wp >> lsw)) * g.Co;
+    c.mask = 0;
+    if (m < M)
+      for (int kh = 0; kh < g.KH; ++kh)
+        for (int kw = 0; kw < g.KW; ++kw) {
+          const int th = hp - kh, tw = wp - kw;
+          if (th < 0 || tw < 0) continue;
+          if ((th & ((1 << lsh) - 1)) || (tw & ((1 << lsw) - 1))) continue;
+          if ((th >> lsh) >= g.Ho || (tw >> lsw) >= g.Wo) continue;
+          c.mask |= 1u << (kh * g.KW + kw);
+        }
     return c;
   }
-  __device__ __forceinline__ typename VT<T>::v8 load(const Ctx& c, int k) const {
-    if (!c.ok || k >= K) return zero8<T>();
-    uint32_t co, kw;
-    uint32_t tap = g.dCo.divmod(k, co);
-    uint32_t kh = g.dKW.divmod(tap, kw);
-    int th = c.hp - (int)kh, tw = c.wp - (int)kw;
-    if (th < 0 || tw < 0) return zero8<T>();
-    uint32_t rh, rw;
-    int ho = (int)g.dsh.divmod(th, rh), wo = (int)g.dsw.divmod(tw, rw);
-    if (rh | rw || ho >= g.Ho || wo >= g.Wo) return zero8<T>();
-    return ld8<T>(c.base + (uint32_t)((ho * g.Wo + wo) * g.Co + (int)co));
+  __device__ __forceinline__ Prep prep(int k0) const { return tap_prep(g.dCo, g.dKW, k0); }
+  __device__ __forceinline__ typename VT<T>::v8 load(const Ctx& c, const Prep& p, int kofs) const {
+    const bool ok = (c.mask >> p.tap) & 1u;
+    const int off = c.off - ((p.kh >> lsh) * g.Wo + (p.kw >> lsw)) * g.Co + p.c0 + kofs;
+    return bld8<T>(mk_rsrc(dy, bytes), boff<T>((uint32_t)off, ok));
   }
 };
 
@@ -104,13 +153,15 @@ template <typename T> struct DgradB {
   const T* w;  // [Co][KH][KW][Ci]
   Geo g;
   int K;       // KH*KW*Co
+  uint32_t bytes;
   struct Ctx { int ci; bool ok; };
+  typedef TapPrep Prep;
   __device__ __forceinline__ Ctx row_ctx(int r8) const { return Ctx{r8, r8 < g.Ci}; }
-  __device__ __forceinline__ typename VT<T>::v8 load(const Ctx& c, int k) const {
-    if (!c.ok || k >= K) return zero8<T>();
-    uint32_t co;
-    uint32_t tap = g.dCo.divmod(k, co);
-    return ld8<T>(w + (uint32_t)(((int)co * g.KH * g.KW + (int)tap) * g.Ci + c.ci));
+  __device__ __forceinline__ Prep prep(int k0) const { return tap_prep(g.dCo, g.dKW, k0); }
+  __device__ __forceinline__ typename VT<T>::v8 load(const Ctx& c, const Prep& p, int kofs) const {
+    const bool ok = c.ok && p.tap < g.KH * g.KW;
+    const int off = ((p.c0 + kofs) * g.KH * g.KW + p.tap) * g.Ci + c.ci;
+    return bld8<T>(mk_rsrc(w, bytes), boff<T>((uint32_t)off, ok));
   }
 };
 
@@ -119,11 +170,14 @@ template <typename T> struct WgradA {
   static constexpr bool kRowVec = true;
   const T* dy;
   int Co, M;
-  struct Ctx { const T* base; bool ok; };
-  __device__ __forceinline__ Ctx row_ctx(int r8) const { return Ctx{dy + r8, r8 < Co}; }
-  __device__ __forceinline__ typename VT<T>::v8 load(const Ctx& c, int k) const {
-    if (!c.ok || k >= M) return zero8<T>();
-    return ld8<T>(c.base + (size_t)k * Co);
+  uint32_t bytes;
+  struct Ctx { int co; bool ok; };
+  typedef int Prep;
+  __device__ __forceinline__ Ctx row_ctx(int r8) const { return Ctx{r8, r8 < Co}; }
+  __device__ __forceinline__ Prep prep(int k0) const { return k0; }
+  __device__ __forceinline__ typename VT<T>::v8 load(const Ctx& c, Prep k0, int kofs) const {
+    const int m = k0 + kofs;
+    return bld8<T>(mk_rsrc(dy, bytes), boff<T>((uint32_t)(m * Co + c.co), c.ok && m < M));
   }
 };
 
@@ -133,26 +187,30 @@ template <typename T> struct WgradB {
   const T* x;
   Geo g;
   int Kp, M;  // Kp = KH*KW*Ci
+  uint32_t bytes;
   struct Ctx { int kh, kw, ci; bool ok; };
+  typedef int Prep;
   __device__ __forceinline__ Ctx row_ctx(int r8) const {
     Ctx c;
     c.ok = r8 < Kp;
     uint32_t ci, kw;
     uint32_t tap = g.dCi.divmod(c.ok ? r8 : 0, ci);
     uint32_t kh = g.dKW.divmod(tap, kw);
-    c.ci = ci;
-    c.kh = kh;
-    c.kw = kw;
+    c.ci = (int)ci;
+    c.kh = (int)kh - g.ph;
+    c.kw = (int)kw - g.pw;
     return c;
   }
-  __device__ __forceinline__ typename VT<T>::v8 load(const Ctx& c, int m) const {
-    if (!c.ok || m >= M) return zero8<T>();
+  __device__ __forceinline__ Prep prep(int k0) const { return k0; }
+  __device__ __forceinline__ typename VT<T>::v8 load(const Ctx& c, Prep k0, int kofs) const {
+    const int m = k0 + kofs;
     uint32_t r, wo;
-    uint32_t b = g.dHoWo.divmod(m, r);
+    uint32_t b = g.dHoWo.divmod((uint32_t)m, r);
     uint32_t ho = g.dWo.divmod(r, wo);
-    int hi = (int)ho * g.sh - g.ph + c.kh, wi = (int)wo * g.sw - g.pw + c.kw;
-    if ((unsigned)hi >= (unsigned)g.Hi || (unsigned)wi >= (unsigned)g.Wi) return zero8<T>();
-    return ld8<T>(x + (size_t)b * g.Hi * g.Wi * g.Ci + (uint32_t)((hi * g.Wi + wi) * g.Ci + c.ci));
+    const int hi = (int)ho * g.sh + c.kh, wi = (int)wo * g.sw + c.kw;
+    const bool ok = c.ok && m < M && (unsigned)hi < (unsigned)g.Hi && (unsigned)wi < (unsigned)g.Wi;
+    const int off = (((int)b * g.Hi + hi) * g.Wi + wi) * g.Ci + c.ci;
+    return bld8<T>(mk_rsrc(x, bytes), boff<T>((uint32_t)off, ok));
   }
 };
 
@@ -223,11 +281,13 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ ws, int S, float* 
   }
 }
 
-template <typename T> int conv_fwd_t(const crnn_conv_desc* d, const void* x, const void* w, void* y,
-                                     float* psum, float* psq, hipStream_t st) {
-  Geo g = geo(d);
+inline uint32_t nbytes(long elems, size_t es) { return (uint32_t)((size_t)elems * es); }
+
+template <typename T, bool UT>
+int conv_fwd_tt(const Geo& g, const crnn_conv_desc* d, const void* x, const void* w, void* y, float* psum,
+                float* psq, hipStream_t st) {
   int M = g.B * g.Ho * g.Wo, N = g.Co, K = g.KH * g.KW * g.Ci;
-  FwdA<T> la{(const T*)x, g, M, K};
+  FwdA<T, UT> la{(const T*)x, g, M, K, nbytes((long)g.B * g.Hi * g.Wi * g.Ci, sizeof(T))};
   RowMajorK<T> lb{(const T*)w, K, N, K};
   FwdEpi<T> ep{(T*)y, psum, psq, M, N};
   int bm, bn;
@@ -237,12 +297,24 @@ template <typename T> int conv_fwd_t(const crnn_conv_desc* d, const void* x, con
   return launch<T, 64, 64>(la, lb, ep, M, N, K, 1, st);
 }
 
+template <typename T> int conv_fwd_t(const crnn_conv_desc* d, const void* x, const void* w, void* y,
+                                     float* psum, float* psq, hipStream_t st) {
+  Geo g = geo(d);
+  if (g.Ci % kstage<T>() == 0) return conv_fwd_tt<T, true>(g, d, x, w, y, psum, psq, st);
+  return conv_fwd_tt<T, false>(g, d, x, w, y, psum, psq, st);
+}
+
+inline int ilog2s(int s) { return s == 1 ? 0 : (s == 2 ? 1 : -1); }
+
 template <typename T> int conv_dgrad_t(const crnn_conv_desc* d, const void* dy, const void* w, void* dx,
                                        const void* dres, const void* yres, int accumulate, hipStream_t st) {
   Geo g = geo(d);
   int M = g.B * g.Hi * g.Wi, N = g.Ci, K = g.KH * g.KW * g.Co;
-  DgradA<T> la{(const T*)dy, g, M, K};
-  DgradB<T> lb{(const T*)w, g, K};
+  int lsh = ilog2s(g.sh), lsw = ilog2s(g.sw);
+  if (lsh < 0 || lsw < 0 || g.Co % kstage<T>())
+    return crnn_set_error(hipErrorInvalidValue, "conv_dgrad: strides must be 1 or 2, Co a multiple of the stage depth");
+  DgradA<T> la{(const T*)dy, g, M, K, lsh, lsw, nbytes((long)g.B * g.Ho * g.Wo * g.Co, sizeof(T))};
+  DgradB<T> lb{(const T*)w, g, K, nbytes((long)g.Co * g.KH * g.KW * g.Ci, sizeof(T))};
   DgradEpi<T> ep{(T*)dx, (const T*)dres, (const T*)yres, M, N, accumulate};
   if (N >= 128 && (long)M * N >= 128L * 128 * 256) return launch<T, 128, 128>(la, lb, ep, M, N, K, 1, st);
   if (N <= 64 && (long)M * N >= 128L * 64 * 256) return launch<T, 128, 64>(la, lb, ep, M, N, K, 1, st);
@@ -257,8 +329,8 @@ template <typename T> int conv_wgrad_t(const crnn_conv_desc* d, const void* dy, 
   crnn_conv_wgrad_plan(d, &bm, &bn, &splits);
   size_t need = (size_t)splits * g.Co * Kp * sizeof(float);
   if (ws_bytes < need) return crnn_set_error(hipErrorInvalidValue, "conv_wgrad: workspace too small");
-  WgradA<T> la{(const T*)dy, g.Co, Mp};
-  WgradB<T> lb{(const T*)x, g, Kp, Mp};
+  WgradA<T> la{(const T*)dy, g.Co, Mp, nbytes((long)Mp * g.Co, sizeof(T))};
+  WgradB<T> lb{(const T*)x, g, Kp, Mp, nbytes((long)g.B * g.Hi * g.Wi * g.Ci, sizeof(T))};
   SlabEpi ep{ws, g.Co, Kp};
   int rc;
   if (bm == 128) rc = launch<T, 128, 128>(la, lb, ep, g.Co, Kp, Mp, splits, st);

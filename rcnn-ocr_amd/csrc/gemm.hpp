@@ -4,8 +4,11 @@
 //
 // A and B are produced by *loaders* that fetch 8 elements at a time from global
 // memory in whichever direction is contiguous there:
-//   kRowVec = false : load(ctx(row), k) -> elements (row, k..k+7)   ("K-contiguous")
-//   kRowVec = true  : load(ctx(row8), k) -> elements (row8..row8+7, k) ("row-contiguous")
+//   kRowVec = false : elements (row, k..k+7)    ("K-contiguous")
+//   kRowVec = true  : elements (row8..row8+7, k) ("row-contiguous")
+// Loader interface: Ctx row_ctx(row) once per thread and staged row (row offsets, masks);
+// Prep prep(k0) once per pipeline stage (wave-uniform: lands in SALU); and
+// v8 load(ctx, prep, kofs) for k = k0 + kofs — a range-checked buffer load.
 // and stage them to LDS in that same orientation. Fragments for the MFMA are
 // then read K-contiguous (ds_read_b64/b128) or transposed (gfx950
 // ds_read_b64_tr_b16), so implicit-GEMM conv fwd (im2col rows), conv dgrad
@@ -79,8 +82,9 @@ template <typename T, int R, int KS, class L> struct Stager {
   }
   __device__ __forceinline__ void load(const L& l, int k0) {
     if (!act) return;
+    const auto pr = l.prep(k0);
 #pragma unroll
-    for (int j = 0; j < PT; ++j) reg[j] = l.load(ctx[j], k0 + kofs[j]);
+    for (int j = 0; j < PT; ++j) reg[j] = l.load(ctx[j], pr, kofs[j]);
   }
   __device__ __forceinline__ void store(T* tile) {
     if (!act) return;
@@ -281,30 +285,35 @@ inline int launch(const LA& la, const LB& lb, const EPI& epi, int M, int N, int 
 }
 
 // ---------------------------------------------------------------- simple loaders
-// Row-major matrix, K-contiguous: element (row, k) at p[row*ld + k]. rows, K bounds.
+// Row-major matrix, K-contiguous: element (row, k) at p[row*ld + k]; rows, K bounds.
 template <typename T> struct RowMajorK {
   static constexpr bool kRowVec = false;
   const T* p;
   int ld, rows, K;
-  struct Ctx { const T* base; bool ok; };
-  __device__ __forceinline__ Ctx row_ctx(int r) const { return Ctx{p + (size_t)r * ld, r < rows}; }
-  __device__ __forceinline__ typename VT<T>::v8 load(const Ctx& c, int k) const {
-    if (!c.ok || k >= K) return zero8<T>();
-    return ld8<T>(c.base + k);
+  struct Ctx { uint32_t off; bool ok; };
+  typedef int Prep;
+  __device__ __forceinline__ Ctx row_ctx(int r) const { return Ctx{(uint32_t)r * (uint32_t)ld, r < rows}; }
+  __device__ __forceinline__ Prep prep(int k0) const { return k0; }
+  __device__ __forceinline__ typename VT<T>::v8 load(const Ctx& c, Prep k0, int kofs) const {
+    const int k = k0 + kofs;
+    return bld8<T>(mk_rsrc(p, bytes()), boff<T>(c.off + k, c.ok && k < K));
   }
+  __device__ __forceinline__ uint32_t bytes() const { return (uint32_t)((size_t)(rows > 0 ? rows : 1) * ld * sizeof(T)); }
 };
 
-// Row-contiguous view: element (row, k) at p[k*ld + row] (8 rows per vector).
-// rows must be a multiple of 8.
+// Row-contiguous view: element (row, k) at p[k*ld + row] (8 rows per vector); rows % 8 == 0.
 template <typename T> struct ColMajorK {
   static constexpr bool kRowVec = true;
   const T* p;
   int ld, rows, K;
-  struct Ctx { const T* base; bool ok; };
-  __device__ __forceinline__ Ctx row_ctx(int r8) const { return Ctx{p + r8, r8 < rows}; }
-  __device__ __forceinline__ typename VT<T>::v8 load(const Ctx& c, int k) const {
-    if (!c.ok || k >= K) return zero8<T>();
-    return ld8<T>(c.base + (size_t)k * ld);
+  struct Ctx { uint32_t off; bool ok; };
+  typedef int Prep;
+  __device__ __forceinline__ Ctx row_ctx(int r8) const { return Ctx{(uint32_t)r8, r8 < rows}; }
+  __device__ __forceinline__ Prep prep(int k0) const { return k0; }
+  __device__ __forceinline__ typename VT<T>::v8 load(const Ctx& c, Prep k0, int kofs) const {
+    const int k = k0 + kofs;
+    return bld8<T>(mk_rsrc(p, (uint32_t)((size_t)K * ld * sizeof(T))),
+                   boff<T>((uint32_t)k * (uint32_t)ld + c.off, c.ok && k < K));
   }
 };
 

@@ -144,13 +144,16 @@ template <typename T> struct HPrevB {
   const T* hseq;
   int B, Tn, H, d;
   struct Ctx { int j; bool ok; };
+  typedef int Prep;
   __device__ __forceinline__ Ctx row_ctx(int r8) const { return Ctx{r8, r8 < H}; }
-  __device__ __forceinline__ typename VT<T>::v8 load(const Ctx& c, int k) const {
-    if (!c.ok || k >= Tn * B) return zero8<T>();
-    int t = k / B, b = k - t * B;
-    int tp = d == 0 ? t - 1 : t + 1;
-    if (tp < 0 || tp >= Tn) return zero8<T>();
-    return ld8<T>(hseq + ((size_t)b * Tn + tp) * 2 * H + d * H + c.j);
+  __device__ __forceinline__ Prep prep(int k0) const { return k0; }
+  __device__ __forceinline__ typename VT<T>::v8 load(const Ctx& c, Prep k0, int kofs) const {
+    const int k = k0 + kofs;
+    const int t = k / B, b = k - t * B;
+    const int tp = d == 0 ? t - 1 : t + 1;
+    const bool ok = c.ok && k < Tn * B && tp >= 0 && tp < Tn;
+    const uint32_t off = (uint32_t)(((b * Tn + tp) * 2 * H) + d * H + c.j);
+    return bld8<T>(mk_rsrc(hseq, (uint32_t)((size_t)B * Tn * 2 * H * sizeof(T))), boff<T>(off, ok));
   }
 };
 // B (dW_ih): x rows i, k = t*B + b : x[b][t][i]
@@ -159,11 +162,15 @@ template <typename T> struct XB {
   const T* x;
   int B, Tn, In;
   struct Ctx { int i; bool ok; };
+  typedef int Prep;
   __device__ __forceinline__ Ctx row_ctx(int r8) const { return Ctx{r8, r8 < In}; }
-  __device__ __forceinline__ typename VT<T>::v8 load(const Ctx& c, int k) const {
-    if (!c.ok || k >= Tn * B) return zero8<T>();
-    int t = k / B, b = k - t * B;
-    return ld8<T>(x + ((size_t)b * Tn + t) * In + c.i);
+  __device__ __forceinline__ Prep prep(int k0) const { return k0; }
+  __device__ __forceinline__ typename VT<T>::v8 load(const Ctx& c, Prep k0, int kofs) const {
+    const int k = k0 + kofs;
+    const int t = k / B, b = k - t * B;
+    const bool ok = c.ok && k < Tn * B;
+    return bld8<T>(mk_rsrc(x, (uint32_t)((size_t)B * Tn * In * sizeof(T))),
+                   boff<T>((uint32_t)((b * Tn + t) * In + c.i), ok));
   }
 };
 
@@ -235,6 +242,7 @@ template <typename T> struct DgatesA {
   const T* dg;
   int B, Tn, H;
   struct Ctx { int b, t; bool ok; };
+  typedef int Prep;
   __device__ __forceinline__ Ctx row_ctx(int m) const {
     Ctx c;
     c.ok = m < B * Tn;
@@ -243,11 +251,13 @@ template <typename T> struct DgatesA {
     c.t = mm - c.b * Tn;
     return c;
   }
-  __device__ __forceinline__ typename VT<T>::v8 load(const Ctx& c, int k) const {
-    const int H4 = 4 * H;
-    if (!c.ok || k >= 2 * H4) return zero8<T>();
-    int d = k >= H4 ? 1 : 0, gp = k - d * H4;
-    return ld8<T>(dg + ((size_t)(d * Tn + c.t) * B + c.b) * H4 + gp);
+  __device__ __forceinline__ Prep prep(int k0) const { return k0; }
+  __device__ __forceinline__ typename VT<T>::v8 load(const Ctx& c, Prep k0, int kofs) const {
+    const int H4 = 4 * H, k = k0 + kofs;
+    const bool ok = c.ok && k < 2 * H4;
+    const int d = k >= H4 ? 1 : 0, gp = k - d * H4;
+    return bld8<T>(mk_rsrc(dg, (uint32_t)((size_t)2 * Tn * B * H4 * sizeof(T))),
+                   boff<T>((uint32_t)(((d * Tn + c.t) * B + c.b) * H4 + gp), ok));
   }
 };
 
