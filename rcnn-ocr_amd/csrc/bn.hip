@@ -223,27 +223,41 @@ __global__ __launch_bounds__(256) void chunk_kernel(const float* __restrict__ p0
   }
 }
 
-__global__ void bn_finalize_kernel(const float* cs, const float* cq, int P, long crows, int C, long count,
-                                   const float* gamma, const float* beta, float* rmean, float* rvar,
-                                   float momentum, float eps, int train, float* mean_o, float* inv_o,
-                                   float* scale_o, float* shift_o) {
-  // cs/cq: [P][C] chunk (sum, M2); chunk p spans `crows` data rows (last one clipped)
-  int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double mean, var;
+// block = 64 channels x 4 lanes; each lane folds a quarter of the P chunk partials
+// (independent loads in flight), combined through LDS in double.
+__global__ __launch_bounds__(256) void bn_finalize_kernel(const float* cs, const float* cq, int P, long crows, int C,
+                                                          long count, const float* gamma, const float* beta,
+                                                          float* rmean, float* rvar, float momentum, float eps,
+                                                          int train, float* mean_o, float* inv_o, float* scale_o,
+                                                          float* shift_o) {
+  __shared__ double red[4][64];
+  const int lc = threadIdx.x & 63, ln = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lc;
+  const bool okc = c < C;
+  double mean = 0.0, var = 1.0;
   if (train) {
     double s = 0.0;
-    for (int p = 0; p < P; ++p) s += cs[(size_t)p * C + c];
-    mean = s / (double)count;
+    if (okc)
+      for (int p = ln; p < P; p += 4) s += cs[(size_t)p * C + c];
+    red[ln][lc] = s;
+    __syncthreads();
+    mean = (red[0][lc] + red[1][lc] + red[2][lc] + red[3][lc]) / (double)count;
+    __syncthreads();
     double m2 = 0.0;
-    for (int p = 0; p < P; ++p) {
-      long n = span_rows(p, p + 1, crows, count);
-      if (n == 0) continue;
-      double d = (double)cs[(size_t)p * C + c] / (double)n - mean;
-      m2 += (double)cq[(size_t)p * C + c] + (double)n * d * d;
-    }
-    var = m2 / (double)count;
+    if (okc)
+      for (int p = ln; p < P; p += 4) {
+        long n = span_rows(p, p + 1, crows, count);
+        if (n == 0) continue;
+        double d = (double)cs[(size_t)p * C + c] / (double)n - mean;
+        m2 += (double)cq[(size_t)p * C + c] + (double)n * d * d;
+      }
+    red[ln][lc] = m2;
+    __syncthreads();
+    var = (red[0][lc] + red[1][lc] + red[2][lc] + red[3][lc]) / (double)count;
     if (var < 0.0) var = 0.0;
+  }
+  if (ln != 0 || !okc) return;
+  if (train) {
     if (rmean) {
       double unb = count > 1 ? var * (double)count / (double)(count - 1) : var;
       rmean[c] = (float)((1.0 - momentum) * rmean[c] + momentum * mean);
@@ -261,15 +275,24 @@ __global__ void bn_finalize_kernel(const float* cs, const float* cq, int P, long
   shift_o[c] = (float)((double)beta[c] - mean * sc);
 }
 
-__global__ void bn_bwd_finalize_kernel(const float* cg, const float* cgx, int P, int C, long count,
-                                       float* dgamma, float* dbeta, float* mean_g, float* mean_gx, int acc) {
-  int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* cg, const float* cgx, int P, int C,
+                                                              long count, float* dgamma, float* dbeta, float* mean_g,
+                                                              float* mean_gx, int acc) {
+  __shared__ double red[2][4][64];
+  const int lc = threadIdx.x & 63, ln = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lc;
   double s = 0.0, q = 0.0;
-  for (int p = 0; p < P; ++p) {
-    s += cg[(size_t)p * C + c];
-    q += cgx[(size_t)p * C + c];
-  }
+  if (c < C)
+    for (int p = ln; p < P; p += 4) {
+      s += cg[(size_t)p * C + c];
+      q += cgx[(size_t)p * C + c];
+    }
+  red[0][ln][lc] = s;
+  red[1][ln][lc] = q;
+  __syncthreads();
+  if (ln != 0 || c >= C) return;
+  s = red[0][0][lc] + red[0][1][lc] + red[0][2][lc] + red[0][3][lc];
+  q = red[1][0][lc] + red[1][1][lc] + red[1][2][lc] + red[1][3][lc];
   if (dgamma) dgamma[c] = (float)(acc ? dgamma[c] + q : q);
   if (dbeta) dbeta[c] = (float)(acc ? dbeta[c] + s : s);
   mean_g[c] = (float)(s / (double)count);
@@ -513,19 +536,26 @@ __global__ void se_mlp_bwd_kernel(const float* __restrict__ ds, const float* __r
 }
 
 // dw2[c][r] = sum_b dsig[b][c] hid[b][r] ; dw1[r][c] = sum_b dhid[b][r] pooled[b][c]
-__global__ void se_wgrad_kernel(const float* __restrict__ dsig, const float* __restrict__ hid,
-                                const float* __restrict__ dhid, const float* __restrict__ pooled,
-                                float* __restrict__ dw1, float* __restrict__ dw2, int B, int C, int Cr) {
-  int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= C * Cr) return;
-  int c = i % C, r = i / C;
+// block = 64 channels x 4 batch lanes for one r; batch split over the lanes, LDS combine.
+__global__ __launch_bounds__(256) void se_wgrad_kernel(const float* __restrict__ dsig, const float* __restrict__ hid,
+                                                       const float* __restrict__ dhid,
+                                                       const float* __restrict__ pooled, float* __restrict__ dw1,
+                                                       float* __restrict__ dw2, int B, int C, int Cr) {
+  __shared__ float red[2][4][64];
+  const int lc = threadIdx.x & 63, ln = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lc, r = blockIdx.y;
   float a2 = 0.f, a1 = 0.f;
-  for (int b = 0; b < B; ++b) {
-    a2 += dsig[(size_t)b * C + c] * hid[(size_t)b * Cr + r];
-    a1 += dhid[(size_t)b * Cr + r] * pooled[(size_t)b * C + c];
-  }
-  dw2[(size_t)c * Cr + r] = a2;
-  dw1[(size_t)r * C + c] = a1;
+  if (c < C)
+    for (int b = ln; b < B; b += 4) {
+      a2 += dsig[(size_t)b * C + c] * hid[(size_t)b * Cr + r];
+      a1 += dhid[(size_t)b * Cr + r] * pooled[(size_t)b * C + c];
+    }
+  red[0][ln][lc] = a2;
+  red[1][ln][lc] = a1;
+  __syncthreads();
+  if (ln != 0 || c >= C) return;
+  dw2[(size_t)c * Cr + r] = red[0][0][lc] + red[0][1][lc] + red[0][2][lc] + red[0][3][lc];
+  dw1[(size_t)r * C + c] = red[1][0][lc] + red[1][1][lc] + red[1][2][lc] + red[1][3][lc];
 }
 
 template <typename T>
@@ -682,7 +712,7 @@ int crnn_bn_finalize(const float* psum, const float* psq, int rows, long rows_pe
     int rc = launch_chunks(psum, psq, rows, rows_per_partial, C, count, 1, ws, &P, &crows, st);
     if (rc) return rc;
   }
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 127) / 128), dim3(128), 0, st, ws, ws + (size_t)FIN_P * C, P,
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, st, ws, ws + (size_t)FIN_P * C, P,
                      crows, C,
                      count, gamma, beta, running_mean, running_var, momentum, eps, train, mean, invstd, scale, shift);
   return (int)hipGetLastError();
@@ -727,7 +757,7 @@ int crnn_bn_bwd_finalize(const float* pg, const float* pgx, int rows, int C, lon
   long crows = 0;
   int rc = launch_chunks(pg, pgx, rows, 1, C, (long)rows, 0, ws, &P, &crows, st);
   if (rc) return rc;
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 127) / 128), dim3(128), 0, st, ws, ws + (size_t)FIN_P * C, P, C,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, st, ws, ws + (size_t)FIN_P * C, P, C,
                      count, dgamma, dbeta, mean_g, mean_gx, accumulate);
   return (int)hipGetLastError();
 }
@@ -786,9 +816,8 @@ int crnn_se_mlp_bwd(const float* ds, const float* pooled, const float* hid, cons
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(se_mlp_bwd_kernel, dim3(B), dim3(256), (C + Cr) * sizeof(float), st, ds, hid, s, w1, w2, dsig,
                      dhid, dpool, C, Cr, 1.f / (float)HW);
-  int n = C * Cr;
-  hipLaunchKernelGGL(se_wgrad_kernel, dim3((n + 255) / 256), dim3(256), 0, st, dsig, hid, dhid, pooled, dw1, dw2, B, C,
-                     Cr);
+  hipLaunchKernelGGL(se_wgrad_kernel, dim3((C + 63) / 64, Cr), dim3(256), 0, st, dsig, hid, dhid, pooled, dw1, dw2, B,
+                     C, Cr);
   return (int)hipGetLastError();
 }
 

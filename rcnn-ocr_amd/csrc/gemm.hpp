@@ -33,7 +33,20 @@ namespace gemm {
 constexpr int BK = 32;  // K per MFMA sub-step; a pipeline stage holds KS = 32 or 64
 constexpr int NT = 256;
 
-template <typename T, int KS = BK> constexpr int kpitch() { return KS + (int)(16 / sizeof(T)); }
+// K-contiguous tiles: bf16 rows are unpadded (KS elements) with the 16-byte chunks XOR-swizzled
+// per row (swz below) so every ds_read_b128 lane group hits 16 distinct 16-B bank slots;
+// f32 rows (parity mode) are padded by 16 B instead.
+template <typename T, int KS = BK> constexpr int kpitch() { return sizeof(T) == 2 ? KS : KS + (int)(16 / sizeof(T)); }
+
+// physical 16-byte chunk of logical chunk c in row r (bf16 K-contiguous tiles)
+template <typename T, int KS> __device__ __forceinline__ int swz(int r, int c) {
+  if constexpr (sizeof(T) != 2) return c;
+  else if constexpr (KS == 64) return c ^ ((r >> 1) & 7);
+  else {
+    const int q = (r >> 2) & 3;
+    return c ^ (q == 1 ? 3 : (q == 3 ? 1 : q));  // h = {0,3,2,1}
+  }
+}
 // row-contiguous pitch: 32*odd bytes for bf16 (conflict-free ds_read_b64_tr_b16
 // over 8 k-rows), (R+4) floats for f32 (conflict-free strided ds_read_b32)
 template <typename T, int R> constexpr int rpitch() { return sizeof(T) == 2 ? R + 16 : R + 4; }
@@ -75,7 +88,7 @@ template <typename T, int R, int KS, class L> struct Stager {
       } else {
         int r = i / (KS / 8), kg = i % (KS / 8);
         ctx[j] = l.row_ctx(row0 + r);
-        lds_off[j] = r * kpitch<T, KS>() + kg * 8;
+        lds_off[j] = r * kpitch<T, KS>() + swz<T, KS>(r, kg) * 8;
         kofs[j] = kg * 8;
       }
     }
@@ -100,12 +113,15 @@ __device__ __forceinline__ typename VT<T>::v8 frag(const T* tile, int rb, int kk
   typename VT<T>::v8 v;
   const int g = lane >> 4, c = lane & 15;
   if constexpr (!RV) {
-    const T* p = tile + (rb + c) * kpitch<T, KS>() + kk * BK;
+    const int row = rb + c;
+    const T* p = tile + row * kpitch<T, KS>();
     if constexpr (!PERM) {
-      v = *reinterpret_cast<const typename VT<T>::v8*>(p + 8 * g);
+      v = *reinterpret_cast<const typename VT<T>::v8*>(p + swz<T, KS>(row, kk * 4 + g) * 8);
     } else {
-      typename VT<T>::v4 lo = *reinterpret_cast<const typename VT<T>::v4*>(p + 4 * g);
-      typename VT<T>::v4 hi = *reinterpret_cast<const typename VT<T>::v4*>(p + 16 + 4 * g);
+      // k = 4g..4g+3 and 16+4g..: halves of chunks kk*4 + g/2 and kk*4 + 2 + g/2
+      const int h = (g & 1) * 4;
+      typename VT<T>::v4 lo = *reinterpret_cast<const typename VT<T>::v4*>(p + swz<T, KS>(row, kk * 4 + (g >> 1)) * 8 + h);
+      typename VT<T>::v4 hi = *reinterpret_cast<const typename VT<T>::v4*>(p + swz<T, KS>(row, kk * 4 + 2 + (g >> 1)) * 8 + h);
       v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
       v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
     }
