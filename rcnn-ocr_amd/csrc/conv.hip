@@ -165,6 +165,107 @@ template <typename T> struct DgradB {
   }
 };
 
+// ---- strided dgrad by parity class (sub-pixel decomposition)
+// Input pixels with (hi % sh, wi % sw) == (pc_h, pc_w) only receive gradient from taps with
+// kh = (pc_h + ph) mod sh (same for w); for those taps ho = i + dh, wo = j + dw, linear in the
+// class coordinates (hi = sh*i + pc_h). Each class is a dense GEMM over its own taps only.
+struct TapTable {
+  int n;
+  int dh[4], dw[4], id[4];  // per class tap: ho offset, wo offset, kh*KW + kw
+};
+
+template <typename T> struct DgradClsA {
+  static constexpr bool kRowVec = false;
+  const T* dy;
+  Geo g;
+  TapTable tt;
+  int Hc, Wc, M, K;  // K = n * Co
+  FastDiv dWc, dHcWc;
+  uint32_t bytes;
+  struct Ctx { int off; uint32_t mask; };
+  typedef TapPrep Prep;
+  __device__ __forceinline__ Ctx row_ctx(int m) const {
+    Ctx c;
+    uint32_t r, j;
+    uint32_t b = dHcWc.divmod(m < M ? m : 0, r);
+    uint32_t i = dWc.divmod(r, j);
+    c.off = (((int)b * g.Ho + (int)i) * g.Wo + (int)j) * g.Co;
+    c.mask = 0;
+    if (m < M)
+      for (int t = 0; t < tt.n; ++t)
+        if ((unsigned)((int)i + tt.dh[t]) < (unsigned)g.Ho && (unsigned)((int)j + tt.dw[t]) < (unsigned)g.Wo)
+          c.mask |= 1u << t;
+    return c;
+  }
+  __device__ __forceinline__ Prep prep(int k0) const {
+    TapPrep p;
+    uint32_t co;
+    p.tap = (int)g.dCo.divmod((uint32_t)k0, co);
+    p.c0 = (int)co;
+    const int t = p.tap < tt.n ? p.tap : 0;
+    p.kh = tt.dh[t];
+    p.kw = tt.dw[t];
+    return p;
+  }
+  __device__ __forceinline__ typename VT<T>::v8 load(const Ctx& c, const Prep& p, int kofs) const {
+    const bool ok = (c.mask >> p.tap) & 1u;
+    const int off = c.off + (p.kh * g.Wo + p.kw) * g.Co + p.c0 + kofs;
+    return bld8<T>(mk_rsrc(dy, bytes), boff<T>((uint32_t)off, ok));
+  }
+};
+
+template <typename T> struct DgradClsB {
+  static constexpr bool kRowVec = true;
+  const T* w;  // [Co][KH][KW][Ci]
+  Geo g;
+  TapTable tt;
+  int K;
+  uint32_t bytes;
+  struct Ctx { int ci; bool ok; };
+  typedef TapPrep Prep;
+  __device__ __forceinline__ Ctx row_ctx(int r8) const { return Ctx{r8, r8 < g.Ci}; }
+  __device__ __forceinline__ Prep prep(int k0) const {
+    TapPrep p;
+    uint32_t co;
+    p.tap = (int)g.dCo.divmod((uint32_t)k0, co);
+    p.c0 = (int)co;
+    p.kh = tt.id[p.tap < tt.n ? p.tap : 0];
+    return p;
+  }
+  __device__ __forceinline__ typename VT<T>::v8 load(const Ctx& c, const Prep& p, int kofs) const {
+    const bool ok = c.ok && p.tap < tt.n;
+    const int off = ((p.c0 + kofs) * g.KH * g.KW + p.kh) * g.Ci + c.ci;
+    return bld8<T>(mk_rsrc(w, bytes), boff<T>((uint32_t)off, ok));
+  }
+};
+
+// dx at class pixel (b, sh*i + pc_h, sw*j + pc_w) (+= if accumulate) (+ residual)
+template <typename T> struct DgradClsEpi {
+  static constexpr bool kStats = false;
+  T* dx;
+  const T* dres;
+  const T* yres;
+  Geo g;
+  int M, N, accumulate, pch, pcw;
+  FastDiv dWc, dHcWc;
+  __device__ __forceinline__ void store(int m, int n, f32x4 v, int) const {
+    if (m >= M || n >= N) return;
+    uint32_t r, j;
+    uint32_t b = dHcWc.divmod(m, r);
+    uint32_t i = dWc.divmod(r, j);
+    const int hi = (int)i * g.sh + pch, wi = (int)j * g.sw + pcw;
+    size_t o = ((size_t)((int)b * g.Hi + hi) * g.Wi + wi) * N + n;
+    if (accumulate) v += ld4f<T>(dx + o);
+    if (dres) {
+      f32x4 d = ld4f<T>(dres + o), yy = ld4f<T>(yres + o);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] += yy[q] > 0.f ? d[q] : 0.f;
+    }
+    st4<T>(dx + o, v);
+  }
+  __device__ __forceinline__ void stats(int, int, f32x4, f32x4) const {}
+};
+
 // ---- wgrad A: dy rows = co, k = output pixel m (row-contiguous: dy[m][co..co+7])
 template <typename T> struct WgradA {
   static constexpr bool kRowVec = true;
@@ -306,9 +407,45 @@ template <typename T> int conv_fwd_t(const crnn_conv_desc* d, const void* x, con
 
 inline int ilog2s(int s) { return s == 1 ? 0 : (s == 2 ? 1 : -1); }
 
+template <typename T>
+int conv_dgrad_strided(const Geo& g, const void* dy, const void* w, void* dx, const void* dres, const void* yres,
+                       int accumulate, hipStream_t st) {
+  const uint32_t dyb = nbytes((long)g.B * g.Ho * g.Wo * g.Co, sizeof(T));
+  const uint32_t wb = nbytes((long)g.Co * g.KH * g.KW * g.Ci, sizeof(T));
+  for (int pch = 0; pch < g.sh; ++pch)
+    for (int pcw = 0; pcw < g.sw; ++pcw) {
+      TapTable tt{};
+      for (int kh = 0; kh < g.KH; ++kh) {
+        if (((pch + g.ph - kh) % g.sh + g.sh) % g.sh) continue;
+        for (int kw = 0; kw < g.KW; ++kw) {
+          if (((pcw + g.pw - kw) % g.sw + g.sw) % g.sw) continue;
+          if (tt.n >= 4) return crnn_set_error(hipErrorInvalidValue, "conv_dgrad: > 4 taps per parity class");
+          tt.dh[tt.n] = (pch + g.ph - kh) / g.sh;
+          tt.dw[tt.n] = (pcw + g.pw - kw) / g.sw;
+          tt.id[tt.n] = kh * g.KW + kw;
+          ++tt.n;
+        }
+      }
+      const int Hc = (g.Hi - pch + g.sh - 1) / g.sh, Wc = (g.Wi - pcw + g.sw - 1) / g.sw;
+      if (Hc <= 0 || Wc <= 0) continue;
+      const int M = g.B * Hc * Wc, N = g.Ci, K = tt.n * g.Co;
+      FastDiv dWc(Wc), dHcWc(Hc * Wc);
+      DgradClsA<T> la{(const T*)dy, g, tt, Hc, Wc, M, K, dWc, dHcWc, dyb};
+      DgradClsB<T> lb{(const T*)w, g, tt, K, wb};
+      DgradClsEpi<T> ep{(T*)dx, (const T*)dres, (const T*)yres, g, M, N, accumulate, pch, pcw, dWc, dHcWc};
+      int rc;
+      if (N >= 128 && (long)M * N >= 128L * 128 * 256) rc = launch<T, 128, 128>(la, lb, ep, M, N, K, 1, st);
+      else rc = launch<T, 64, 64>(la, lb, ep, M, N, K, 1, st);
+      if (rc) return rc;
+    }
+  return 0;
+}
+
 template <typename T> int conv_dgrad_t(const crnn_conv_desc* d, const void* dy, const void* w, void* dx,
                                        const void* dres, const void* yres, int accumulate, hipStream_t st) {
   Geo g = geo(d);
+  if ((g.sh > 1 || g.sw > 1) && g.Co % kstage<T>() == 0)
+    return conv_dgrad_strided<T>(g, dy, w, dx, dres, yres, accumulate, st);
   int M = g.B * g.Hi * g.Wi, N = g.Ci, K = g.KH * g.KW * g.Co;
   int lsh = ilog2s(g.sh), lsw = ilog2s(g.sw);
   if (lsh < 0 || lsw < 0 || g.Co % kstage<T>())
