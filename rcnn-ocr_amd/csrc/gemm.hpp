@@ -26,9 +26,39 @@
 // store 8/16 B per lane and LSTM gate quadruples (i,f,g,o interleaved) land in
 // one lane.
 #pragma once
+#include <type_traits>
+#include <utility>
 #include "common.hpp"
 
 namespace gemm {
+
+// optional batch hook: loaders / epilogues with set_batch(int) are re-targeted per batch entry
+template <class X, class = void> struct has_set_batch : std::false_type {};
+template <class X>
+struct has_set_batch<X, std::void_t<decltype(std::declval<X&>().set_batch(0))>> : std::true_type {};
+
+// two parameter sets (e.g. the two LSTM directions) of one loader type, selected per batch
+template <class L> struct Pair {
+  static constexpr bool kRowVec = L::kRowVec;
+  using Ctx = typename L::Ctx;
+  using Prep = decltype(std::declval<const L&>().prep(0));
+  L a, b;
+  __device__ __forceinline__ void set_batch(int bz) {
+    if (bz) a = b;
+  }
+  __device__ __forceinline__ Ctx row_ctx(int r) const { return a.row_ctx(r); }
+  __device__ __forceinline__ Prep prep(int k0) const { return a.prep(k0); }
+  __device__ __forceinline__ auto load(const Ctx& c, const Prep& p, int kofs) const { return a.load(c, p, kofs); }
+};
+template <class E> struct EpiPair {
+  static constexpr bool kStats = E::kStats;
+  E a, b;
+  __device__ __forceinline__ void set_batch(int bz) {
+    if (bz) a = b;
+  }
+  __device__ __forceinline__ void store(int m, int n, f32x4 v, int kz) const { a.store(m, n, v, kz); }
+  __device__ __forceinline__ void stats(int r, int n, f32x4 s, f32x4 q) const { a.stats(r, n, s, q); }
+};
 
 constexpr int BK = 32;  // K per MFMA sub-step; a pipeline stage holds KS = 32 or 64
 constexpr int NT = 256;
@@ -156,18 +186,22 @@ __device__ __forceinline__ void mma(f32x4& acc, const typename VT<T>::v8& a, con
 
 template <typename T, int BM, int BN, int KS, class LA, class LB, class EPI>
 __global__ __launch_bounds__(256) void gemm_kernel(LA la, LB lb, EPI epi, int M, int N, int K,
-                                                   int klen, int tiles_m, int tiles_n, int nsplit) {
+                                                   int klen, int tiles_m, int tiles_n, int nsplit, int nbatch) {
   constexpr bool PERM = LA::kRowVec || LB::kRowVec;
   constexpr int WM = BM / 2, WN = BN / 2, MI = WM / 16, NI = WN / 16;
   constexpr int AE = tile_elems<T, BM, LA::kRowVec, KS>();
   constexpr int BE = tile_elems<T, BN, LB::kRowVec, KS>();
   __shared__ __attribute__((aligned(16))) T smem[2 * (AE + BE)];
 
-  const int nwg = tiles_m * tiles_n * nsplit;
+  const int nwg = tiles_m * tiles_n * nsplit * nbatch;
   const int wg = xcd_remap(blockIdx.x, nwg);
   const int n_tile = wg % tiles_n;
   const int m_tile = (wg / tiles_n) % tiles_m;
-  const int kz = wg / (tiles_n * tiles_m);
+  const int kz = (wg / (tiles_n * tiles_m)) % nsplit;
+  const int bz = wg / (tiles_n * tiles_m * nsplit);
+  if constexpr (has_set_batch<LA>::value) la.set_batch(bz);
+  if constexpr (has_set_batch<LB>::value) lb.set_batch(bz);
+  if constexpr (has_set_batch<EPI>::value) epi.set_batch(bz);
   const int m0 = m_tile * BM, n0 = n_tile * BN;
   const int kbeg = kz * klen;
   const int kend = min(K, kbeg + klen);
@@ -289,14 +323,14 @@ template <typename T> constexpr int kstage() { return sizeof(T) == 2 ? 64 : 32; 
 
 template <typename T, int BM, int BN, int KS = kstage<T>(), class LA, class LB, class EPI>
 inline int launch(const LA& la, const LB& lb, const EPI& epi, int M, int N, int K, int nsplit,
-                  hipStream_t st) {
+                  hipStream_t st, int nbatch = 1) {
   if (M <= 0 || N <= 0) return 0;
   const int tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN;
   const int klen = split_len(K, nsplit);
   nsplit = K > 0 ? (K + klen - 1) / klen : 1;
-  const int nwg = tm * tn * nsplit;
+  const int nwg = tm * tn * nsplit * nbatch;
   hipLaunchKernelGGL((gemm_kernel<T, BM, BN, KS, LA, LB, EPI>), dim3(nwg), dim3(NT), 0, st, la, lb, epi,
-                     M, N, K, klen, tm, tn, nsplit);
+                     M, N, K, klen, tm, tn, nsplit, nbatch);
   return (int)hipGetLastError();
 }
 

@@ -41,23 +41,26 @@ template <typename T> struct StepFwdEpi {
   __device__ __forceinline__ void stats(int, int, f32x4, f32x4) const {}
 };
 
+// both directions in one launch (batch index = direction)
 template <typename T>
 int step_fwd_t(const void* xg, const void* whh, void* hseq, void* gsv, float* csv, int B, int Tn, int H, int s,
                hipStream_t st) {
+  Pair<RowMajorK<T>> la, lb;
+  EpiPair<StepFwdEpi<T>> ep;
   for (int d = 0; d < 2; ++d) {
     int t = d == 0 ? s : Tn - 1 - s;
     int tp = d == 0 ? t - 1 : t + 1;
     int first = s == 0;
     // A: h_{t-1} rows b, k = j  (all-zero rows at the first step)
-    RowMajorK<T> la{(const T*)hseq + (size_t)(first ? 0 : tp) * 2 * H + d * H, Tn * 2 * H, first ? 0 : B, H};
-    RowMajorK<T> lb{(const T*)whh + (size_t)d * 4 * H * H, H, 4 * H, H};
-    StepFwdEpi<T> ep{(const T*)xg, (T*)hseq, (T*)gsv, csv, B, Tn, H, d, t, tp, first};
-    int rc;
-    if ((long)B * 4 * H >= 64L * 64 * 256) rc = launch<T, 64, 64>(la, lb, ep, B, 4 * H, H, 1, st);
-    else rc = launch<T, 32, 32>(la, lb, ep, B, 4 * H, H, 1, st);
-    if (rc) return rc;
+    RowMajorK<T> a{(const T*)hseq + (size_t)(first ? 0 : tp) * 2 * H + d * H, Tn * 2 * H, first ? 0 : B, H};
+    RowMajorK<T> b{(const T*)whh + (size_t)d * 4 * H * H, H, 4 * H, H};
+    StepFwdEpi<T> e{(const T*)xg, (T*)hseq, (T*)gsv, csv, B, Tn, H, d, t, tp, first};
+    (d ? la.b : la.a) = a;
+    (d ? lb.b : lb.a) = b;
+    (d ? ep.b : ep.a) = e;
   }
-  return 0;
+  if ((long)B * 4 * H >= 64L * 64 * 256) return launch<T, 64, 64>(la, lb, ep, B, 4 * H, H, 1, st, 2);
+  return launch<T, 32, 32>(la, lb, ep, B, 4 * H, H, 1, st, 2);
 }
 
 // ---------------------------------------------------------------- backward step
@@ -122,18 +125,21 @@ int step_bwd_t(const void* dhseq, const void* whh, const void* gsv, const float*
                        (T*)dgates, dc, B, Tn, H);
     return (int)hipGetLastError();
   }
+  Pair<RowMajorK<T>> la;
+  Pair<ColMajorK<T>> lb;
+  EpiPair<StepBwdEpi<T>> ep;
   for (int d = 0; d < 2; ++d) {
     int t = d == 0 ? Tn - 1 - s : s;  // time processed now
     int tn = d == 0 ? t + 1 : t - 1;  // time processed at step s-1
-    RowMajorK<T> la{(const T*)dgates + (size_t)(d * Tn + tn) * B * 4 * H, 4 * H, B, 4 * H};
-    ColMajorK<T> lb{(const T*)whh + (size_t)d * 4 * H * H, H, H, 4 * H};
-    StepBwdEpi<T> ep{(const T*)dhseq, (const T*)gsv, csv, (T*)dgates, dc, B, Tn, H, d, t};
-    int rc;
-    if ((long)B * H >= 64L * 64 * 256) rc = launch<T, 64, 64>(la, lb, ep, B, H, 4 * H, 1, st);
-    else rc = launch<T, 32, 32>(la, lb, ep, B, H, 4 * H, 1, st);
-    if (rc) return rc;
+    RowMajorK<T> a{(const T*)dgates + (size_t)(d * Tn + tn) * B * 4 * H, 4 * H, B, 4 * H};
+    ColMajorK<T> b{(const T*)whh + (size_t)d * 4 * H * H, H, H, 4 * H};
+    StepBwdEpi<T> e{(const T*)dhseq, (const T*)gsv, csv, (T*)dgates, dc, B, Tn, H, d, t};
+    (d ? la.b : la.a) = a;
+    (d ? lb.b : lb.a) = b;
+    (d ? ep.b : ep.a) = e;
   }
-  return 0;
+  if ((long)B * H >= 64L * 64 * 256) return launch<T, 64, 64>(la, lb, ep, B, H, 4 * H, 1, st, 2);
+  return launch<T, 32, 32>(la, lb, ep, B, H, 4 * H, 1, st, 2);
 }
 
 // ---------------------------------------------------------------- weight grads
@@ -143,13 +149,15 @@ template <typename T> struct HPrevB {
   static constexpr bool kRowVec = true;
   const T* hseq;
   int B, Tn, H, d;
+  FastDiv dB;
   struct Ctx { int j; bool ok; };
   typedef int Prep;
   __device__ __forceinline__ Ctx row_ctx(int r8) const { return Ctx{r8, r8 < H}; }
   __device__ __forceinline__ Prep prep(int k0) const { return k0; }
   __device__ __forceinline__ typename VT<T>::v8 load(const Ctx& c, Prep k0, int kofs) const {
     const int k = k0 + kofs;
-    const int t = k / B, b = k - t * B;
+    uint32_t bu;
+    const int t = (int)dB.divmod((uint32_t)k, bu), b = (int)bu;
     const int tp = d == 0 ? t - 1 : t + 1;
     const bool ok = c.ok && k < Tn * B && tp >= 0 && tp < Tn;
     const uint32_t off = (uint32_t)(((b * Tn + tp) * 2 * H) + d * H + c.j);
@@ -161,13 +169,15 @@ template <typename T> struct XB {
   static constexpr bool kRowVec = true;
   const T* x;
   int B, Tn, In;
+  FastDiv dB;
   struct Ctx { int i; bool ok; };
   typedef int Prep;
   __device__ __forceinline__ Ctx row_ctx(int r8) const { return Ctx{r8, r8 < In}; }
   __device__ __forceinline__ Prep prep(int k0) const { return k0; }
   __device__ __forceinline__ typename VT<T>::v8 load(const Ctx& c, Prep k0, int kofs) const {
     const int k = k0 + kofs;
-    const int t = k / B, b = k - t * B;
+    uint32_t bu;
+    const int t = (int)dB.divmod((uint32_t)k, bu), b = (int)bu;
     const bool ok = c.ok && k < Tn * B;
     return bld8<T>(mk_rsrc(x, (uint32_t)((size_t)B * Tn * In * sizeof(T))),
                    boff<T>((uint32_t)((b * Tn + t) * In + c.i), ok));
@@ -298,9 +308,9 @@ int crnn_lstm_dwhh(int dtype, const void* dgates, const void* hseq, float* dwhh,
     size_t off = (size_t)d * T * B * 4 * H;
     float* out = dwhh + (size_t)d * 4 * H * H;
     int rc = dtype == CRNN_BF16
-                 ? gate_wgrad<bf16>((const bf16*)dgates + off, HPrevB<bf16>{(const bf16*)hseq, B, T, H, d}, out, B, T,
+                 ? gate_wgrad<bf16>((const bf16*)dgates + off, HPrevB<bf16>{(const bf16*)hseq, B, T, H, d, FastDiv(B)}, out, B, T,
                                     H, H, accumulate, st)
-                 : gate_wgrad<float>((const float*)dgates + off, HPrevB<float>{(const float*)hseq, B, T, H, d}, out, B,
+                 : gate_wgrad<float>((const float*)dgates + off, HPrevB<float>{(const float*)hseq, B, T, H, d, FastDiv(B)}, out, B,
                                      T, H, H, accumulate, st);
     if (rc) return rc;
   }
@@ -315,9 +325,9 @@ int crnn_lstm_dwih(int dtype, const void* dgates, const void* x, float* dwih, in
     size_t off = (size_t)d * T * B * 4 * H;
     float* out = dwih + (size_t)d * 4 * H * In;
     int rc = dtype == CRNN_BF16
-                 ? gate_wgrad<bf16>((const bf16*)dgates + off, XB<bf16>{(const bf16*)x, B, T, In}, out, B, T, H, In,
+                 ? gate_wgrad<bf16>((const bf16*)dgates + off, XB<bf16>{(const bf16*)x, B, T, In, FastDiv(B)}, out, B, T, H, In,
                                     accumulate, st)
-                 : gate_wgrad<float>((const float*)dgates + off, XB<float>{(const float*)x, B, T, In}, out, B, T, H,
+                 : gate_wgrad<float>((const float*)dgates + off, XB<float>{(const float*)x, B, T, In, FastDiv(B)}, out, B, T, H,
                                      In, accumulate, st);
     if (rc) return rc;
   }
