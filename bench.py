@@ -78,13 +78,8 @@ def cpu_baseline(args, threads):
 
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    from crnn_hip import dist as D
+    world, rank, local = D.init_from_env()
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -107,7 +102,7 @@ def main():
     eng = model._engine_for(x)
     model.flatten_parameters_()
     if world > 1:
-        dist.broadcast(model._flat_param, 0)
+        D.broadcast_params(model._flat_param)
         model.mark_params_changed()
     grads, _ = model._grad_views()
     opt = FusedAdamW(model, lr=1e-4, weight_decay=1e-2)
@@ -118,7 +113,7 @@ def main():
         loss, dl = eng.ctc(eng.logits_padded(), tg, tl)
         eng.backward(dl, grads, accumulate=False)
         if world > 1:
-            dist.all_reduce(model._flat_grad)
+            D.allreduce_grads(model._flat_grad)
         opt.step(grad_scale=inv_world)
         return loss
 

@@ -18,7 +18,7 @@ Parameters are a dict keyed by the reference's state_dict names
 from __future__ import annotations
 
 import math
-from typing import Dict, List, Tuple
+from typing import Dict, List, Optional, Tuple
 
 import numpy as np
 import torch
@@ -35,19 +35,40 @@ STAGES = [("layer1", 1, 2, 128, 256), ("layer2", 2, 1, 256, 256),
 
 
 class Ctx:
-    """train flag + BN running-stat updates + recorded intermediates."""
+    """train flag + BN running-stat updates + recorded intermediates.
 
-    def __init__(self, train: bool, record: bool = False):
+    `force` (test use): ReLU masks / 2x2 max-pool window indices, by decision-site name, that
+    replace the oracle's own decisions. An fp64 evaluation that takes an fp32 path's decisions
+    is that path's exact reference: fp32 ties (|pre-activation| within rounding of 0) no longer
+    decide which side of a ReLU kink the two evaluations land on."""
+
+    def __init__(self, train: bool, record: bool = False, force: Optional[Dict[str, torch.Tensor]] = None):
         self.train = train
         self.record = record
         self.acts: Dict[str, torch.Tensor] = {}
         self.running: Dict[str, torch.Tensor] = {}
+        self.force = force or {}
 
     def rec(self, name, t):
         if self.record:
             if t.requires_grad:
                 t.retain_grad()
             self.acts[name] = t
+
+
+def relu(ctx: Ctx, site: str, u):
+    m = ctx.force.get(site)
+    return torch.relu(u) if m is None else u * m.to(u.dtype)
+
+
+def maxpool2(ctx: Ctx, site: str, x):
+    """F.max_pool2d(x, 2, 2); forced: window element t = 2*dh + dw per output."""
+    idx = ctx.force.get(site)
+    if idx is None:
+        return F.max_pool2d(x, 2, 2)
+    B, C, H, W = x.shape
+    win = x.reshape(B, C, H // 2, 2, W // 2, 2).permute(0, 1, 2, 4, 3, 5).reshape(B, C, H // 2, W // 2, 4)
+    return win.gather(-1, idx.long()[..., None]).squeeze(-1)
 
 
 def batchnorm(x, p, prefix, ctx: Ctx):
@@ -69,10 +90,11 @@ def batchnorm(x, p, prefix, ctx: Ctx):
     return (x - mean.view(1, -1, 1, 1)) * (inv * w).view(1, -1, 1, 1) + b.view(1, -1, 1, 1)
 
 
-def se_layer(x, p, prefix):
+def se_layer(x, p, prefix, ctx: Optional[Ctx] = None):
     """SELayer.forward, model/seresnet31.py:16-20 (reduction 16, no biases)."""
     y = x.mean(dim=(2, 3))
-    y = torch.relu(y @ p[prefix + ".fc.0.weight"].t())
+    y = y @ p[prefix + ".fc.0.weight"].t()
+    y = relu(ctx, prefix, y) if ctx is not None else torch.relu(y)
     y = torch.sigmoid(y @ p[prefix + ".fc.2.weight"].t())
     return x * y[:, :, None, None]
 
@@ -80,25 +102,25 @@ def se_layer(x, p, prefix):
 def se_block(x, p, prefix, stride, has_ds, ctx):
     """SEBasicBlock.forward, model/seresnet31.py:55-67 (dropblock = Identity at p=0)."""
     out = F.conv2d(x, p[prefix + ".conv1.weight"], stride=stride, padding=1)
-    out = torch.relu(batchnorm(out, p, prefix + ".bn1", ctx))
+    out = relu(ctx, prefix + ".bn1", batchnorm(out, p, prefix + ".bn1", ctx))
     out = F.conv2d(out, p[prefix + ".conv2.weight"], stride=1, padding=1)
     out = batchnorm(out, p, prefix + ".bn2", ctx)
-    out = se_layer(out, p, prefix + ".se")
+    out = se_layer(out, p, prefix + ".se", ctx)
     if has_ds:
         idn = F.conv2d(x, p[prefix + ".downsample.0.weight"], stride=stride)
         idn = batchnorm(idn, p, prefix + ".downsample.1", ctx)
     else:
         idn = x
-    return torch.relu(out + idn)
+    return relu(ctx, prefix + ".out", out + idn)
 
 
 def backbone(x, p, ctx):
     """SEResNet31.forward, model/seresnet31.py:180-187."""
     x = F.conv2d(x, p["cnn.conv0.0.weight"], padding=1)
-    x = torch.relu(batchnorm(x, p, "cnn.conv0.1", ctx))
+    x = relu(ctx, "cnn.conv0.1", batchnorm(x, p, "cnn.conv0.1", ctx))
     x = F.conv2d(x, p["cnn.conv0.3.weight"], padding=1)
-    x = torch.relu(batchnorm(x, p, "cnn.conv0.4", ctx))
-    x = F.max_pool2d(x, 2, 2)
+    x = relu(ctx, "cnn.conv0.4", batchnorm(x, p, "cnn.conv0.4", ctx))
+    x = maxpool2(ctx, "stem.pool", x)
     ctx.rec("stem", x)
     for name, blocks, stride, inp, planes in STAGES:
         for i in range(blocks):
@@ -109,9 +131,9 @@ def backbone(x, p, ctx):
         ctx.rec(name, x)
     # conv_out, model/seresnet31.py:129-136
     x = F.conv2d(x, p["cnn.conv_out.0.weight"], stride=(2, 1), padding=(0, 1))
-    x = torch.relu(batchnorm(x, p, "cnn.conv_out.1", ctx))
+    x = relu(ctx, "cnn.conv_out.1", batchnorm(x, p, "cnn.conv_out.1", ctx))
     x = F.conv2d(x, p["cnn.conv_out.3.weight"], stride=1, padding=0)
-    x = torch.relu(batchnorm(x, p, "cnn.conv_out.4", ctx))
+    x = relu(ctx, "cnn.conv_out.4", batchnorm(x, p, "cnn.conv_out.4", ctx))
     ctx.rec("cnn_out", x)
     return x
 

@@ -1,0 +1,60 @@
+"""Data parallelism for the CRNN step: one process per GPU, RCCL over xGMI.
+
+The path shards by sample: every rank runs the full train step on its own
+batch shard; BatchNorm uses per-rank batch statistics (the reference's plain BatchNorm2d,
+no SyncBN). The only exchange is a sum all-reduce of the flat fp32 gradient buffer,
+issued in buckets so several collectives are in flight at once; the optimizer then scales
+by 1/world. Parameters are broadcast from rank 0 once at start.
+"""
+from __future__ import annotations
+
+import os
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+
+BUCKET_BYTES = 32 << 20
+
+
+def env_world():
+    return (int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def init_from_env(backend: Optional[str] = None):
+    """init_process_group from torchrun's env (MASTER_ADDR/PORT, RANK, WORLD_SIZE);
+    backend 'nccl' (= RCCL on ROCm) for HIP devices, 'gloo' for CPU tests."""
+    world, rank, local = env_world()
+    if world <= 1 or dist.is_initialized():
+        return world, rank, local
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    if backend is None:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    if backend == "nccl":
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        dist.init_process_group(backend)
+    return world, rank, local
+
+
+def buckets(n: int, elem_bytes: int = 4, bucket_bytes: int = BUCKET_BYTES) -> List[slice]:
+    per = max(1, bucket_bytes // elem_bytes)
+    return [slice(i, min(n, i + per)) for i in range(0, n, per)]
+
+
+def broadcast_params(flat: torch.Tensor, src: int = 0):
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        dist.broadcast(flat, src)
+
+
+def allreduce_grads(flat_grad: torch.Tensor, bucket_bytes: int = BUCKET_BYTES):
+    """sum all-reduce of a flat gradient buffer in reverse-order buckets (the head / LSTM
+    gradients live at the end of the buffer and are final first), all in flight together."""
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return
+    works = [dist.all_reduce(flat_grad[s], async_op=True)
+             for s in reversed(buckets(flat_grad.numel(), flat_grad.element_size(), bucket_bytes))]
+    for w in works:
+        w.wait()

@@ -132,21 +132,6 @@ __device__ __forceinline__ void bn_g(const crnn_bn_bwd_desc& d, unsigned m, int 
   }
 }
 
-template <typename T> struct BnBwdF {
-  crnn_bn_bwd_desc d;
-  __device__ __forceinline__ void operator()(long m, int c8, float* s, float* q) const {
-    float z[8], g[8];
-    unpack8<T>(ld8<T>((const T*)d.z + m * d.C + c8), z);
-    bn_g<T>(d, (unsigned)m, c8, z, g);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      float xh = (z[i] - d.mean[c8 + i]) * d.invstd[c8 + i];
-      s[i] += g[i];
-      q[i] += g[i] * xh;
-    }
-  }
-};
-
 int cg_shift(int C) {
   if (C % 8) return -1;
   int g = C / 8, s = 0;
@@ -312,45 +297,6 @@ int launch_chunks(const float* p0, const float* p1, int rows, long rpp, int C, l
   return (int)hipGetLastError();
 }
 
-// ------------------------------------------------------------ elementwise
-// one lane = 8 channels of one row; C/8 is a power of two (cg_shift = log2(C/8))
-template <typename T>
-__global__ void bn_act_kernel(const T* __restrict__ z, const float* __restrict__ sc, const float* __restrict__ sh,
-                              T* __restrict__ y, unsigned nvec, int cg_shift, int relu) {
-  const unsigned cgm = (1u << cg_shift) - 1u;
-  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += gridDim.x * blockDim.x) {
-    const int c8 = (int)(i & cgm) * 8;
-    float v[8];
-    unpack8<T>(ld8<T>(z + (size_t)i * 8), v);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      v[k] = v[k] * sc[c8 + k] + sh[c8 + k];
-      if (relu) v[k] = fmaxf(v[k], 0.f);
-    }
-    st8<T>(y + (size_t)i * 8, pack8<T>(v));
-  }
-}
-
-template <typename T>
-__global__ void bn_apply_bwd_kernel(crnn_bn_bwd_desc d, const float* __restrict__ mg, const float* __restrict__ mgx,
-                                    T* __restrict__ dz, unsigned nvec, int cg_shift) {
-  const unsigned cgm = (1u << cg_shift) - 1u;
-  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += gridDim.x * blockDim.x) {
-    const unsigned m = i >> cg_shift;
-    const int c8 = (int)(i & cgm) * 8;
-    float z[8], g[8], o[8];
-    unpack8<T>(ld8<T>((const T*)d.z + (size_t)i * 8), z);
-    bn_g<T>(d, m, c8, z, g);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      int c = c8 + k;
-      float xh = (z[k] - d.mean[c]) * d.invstd[c];
-      o[k] = d.scale[c] * (g[k] - mg[c] - xh * mgx[c]);
-    }
-    st8<T>(dz + (size_t)i * 8, pack8<T>(o));
-  }
-}
-
 // maxpool 2x2/2 over relu(z*sc+sh); NHWC, one lane = 8 channels of one output pixel
 template <typename T>
 __global__ void bn_relu_maxpool_kernel(const T* __restrict__ z, const float* __restrict__ sc, const float* __restrict__ sh,
@@ -421,61 +367,6 @@ __global__ void maxpool_bwd_kernel(const T* __restrict__ z, const float* __restr
 }
 
 // ------------------------------------------------------------ SE
-// per-sample spatial reduction: out[b][c] = scale_out * sum_hw f(b, hw, c8)
-template <class F>
-__global__ __launch_bounds__(NT) void sample_reduce_kernel(F f, int HW, int C, float* __restrict__ out, float mul) {
-  extern __shared__ float red[];
-  const int cg = C / 8, rl = NT / cg;
-  const int tid = threadIdx.x, c8 = (tid % cg) * 8, r = tid / cg;
-  const int b = blockIdx.x;
-  float a[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) a[i] = 0.f;
-  if (r < rl)
-    for (int hw = r; hw < HW; hw += rl) f(b, hw, c8, a);
-  if (r < rl) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) red[r * C + c8 + i] = a[i];
-  }
-  __syncthreads();
-  for (int c = tid; c < C; c += NT) {
-    float s = 0.f;
-    for (int q = 0; q < rl; ++q) s += red[q * C + c];
-    out[(size_t)b * C + c] = s * mul;
-  }
-}
-
-template <typename T> struct SePoolF {
-  const T* z;
-  const float* sc;
-  const float* sh;
-  int HW, C;
-  __device__ __forceinline__ void operator()(int b, int hw, int c8, float* a) const {
-    float v[8];
-    unpack8<T>(ld8<T>(z + ((size_t)b * HW + hw) * C + c8), v);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) a[i] += v[i] * sc[c8 + i] + sh[c8 + i];
-  }
-};
-
-template <typename T> struct SeBwdF {
-  const T* dy;
-  const T* y;
-  const T* z;
-  const float* sc;
-  const float* sh;
-  int HW, C;
-  __device__ __forceinline__ void operator()(int b, int hw, int c8, float* a) const {
-    size_t o = ((size_t)b * HW + hw) * C + c8;
-    float d[8], yy[8], v[8];
-    unpack8<T>(ld8<T>(dy + o), d);
-    unpack8<T>(ld8<T>(y + o), yy);
-    unpack8<T>(ld8<T>(z + o), v);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) a[i] += yy[i] > 0.f ? d[i] * (v[i] * sc[c8 + i] + sh[c8 + i]) : 0.f;
-  }
-};
-
 __global__ void se_mlp_fwd_kernel(const float* __restrict__ pooled, const float* __restrict__ w1,
                                   const float* __restrict__ w2, float* __restrict__ hid, float* __restrict__ s,
                                   int C, int Cr) {
@@ -556,31 +447,6 @@ __global__ __launch_bounds__(256) void se_wgrad_kernel(const float* __restrict__
   if (ln != 0 || c >= C) return;
   dw2[(size_t)c * Cr + r] = red[0][0][lc] + red[0][1][lc] + red[0][2][lc] + red[0][3][lc];
   dw1[(size_t)r * C + c] = red[1][0][lc] + red[1][1][lc] + red[1][2][lc] + red[1][3][lc];
-}
-
-template <typename T>
-__global__ void se_residual_kernel(const T* __restrict__ z, const float* __restrict__ sc, const float* __restrict__ sh,
-                                   const float* __restrict__ s, const T* __restrict__ idn,
-                                   const float* __restrict__ isc, const float* __restrict__ ish, T* __restrict__ y,
-                                   unsigned nvec, unsigned HW, int C, int cg_shift) {
-  const unsigned cgm = (1u << cg_shift) - 1u;
-  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += gridDim.x * blockDim.x) {
-    const unsigned m = i >> cg_shift;
-    const int c8 = (int)(i & cgm) * 8;
-    const unsigned b = m / HW;
-    float v[8], d[8];
-    unpack8<T>(ld8<T>(z + (size_t)i * 8), v);
-    unpack8<T>(ld8<T>(idn + (size_t)i * 8), d);
-    const float* sb = s + (size_t)b * C + c8;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      int c = c8 + k;
-      float u = (v[k] * sc[c] + sh[c]) * sb[k];
-      float id = isc ? d[k] * isc[c] + ish[c] : d[k];
-      v[k] = fmaxf(u + id, 0.f);
-    }
-    st8<T>(y + (size_t)i * 8, pack8<T>(v));
-  }
 }
 
 // ------------------------------------------------------------ height collapse
@@ -674,6 +540,266 @@ __global__ void pack_rows_kernel(const float* __restrict__ src, T* __restrict__ 
   }
 }
 
+// ------------------------------------------------------------ row-streaming elementwise kernels
+// Thread = (8-channel group c8, row lane r): the group is fixed for the thread's lifetime so
+// per-channel coefficients live in registers; a block streams a contiguous chunk of rows
+// (per-sample SE values are re-fetched only when the row crosses into the next sample).
+struct RowMap {
+  int cg, rl, c8, r;
+};
+__device__ __forceinline__ RowMap rowmap(int C) {
+  RowMap q;
+  q.cg = C >> 3;
+  q.rl = NT / q.cg;
+  q.c8 = (threadIdx.x % q.cg) * 8;
+  q.r = threadIdx.x / q.cg;
+  return q;
+}
+
+__device__ __forceinline__ void ld8f(const float* p, float* o) {
+  f32x4 a = *reinterpret_cast<const f32x4*>(p), b = *reinterpret_cast<const f32x4*>(p + 4);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    o[i] = a[i];
+    o[4 + i] = b[i];
+  }
+}
+
+// upstream gradient g by mode, with per-thread cached channel / sample constants
+template <typename T, int MODE>
+__device__ __forceinline__ void bng(const crnn_bn_bwd_desc& d, size_t o, const float* z, const float* sc,
+                                    const float* sh, const float* s8, const float* dp8, float* g) {
+  float dy[8];
+  unpack8<T>(ld8<T>((const T*)d.dy + o), dy);
+  if constexpr (MODE == CRNN_BNG_PLAIN) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) g[i] = dy[i];
+  } else if constexpr (MODE == CRNN_BNG_RELU) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) g[i] = (z[i] * sc[i] + sh[i]) > 0.f ? dy[i] : 0.f;
+  } else {
+    float y[8];
+    unpack8<T>(ld8<T>((const T*)d.y + o), y);
+    if constexpr (MODE == CRNN_BNG_RESID) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) g[i] = y[i] > 0.f ? dy[i] : 0.f;
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) g[i] = (y[i] > 0.f ? dy[i] * s8[i] : 0.f) + dp8[i];
+    }
+  }
+}
+
+template <typename T, int MODE>
+__global__ __launch_bounds__(NT) void bnb_reduce_kernel(crnn_bn_bwd_desc d, FastDiv dHW, long rpb,
+                                                        float* __restrict__ p0, float* __restrict__ p1) {
+  extern __shared__ float red[];  // [2][rl][C]
+  const int C = d.C;
+  const RowMap q = rowmap(C);
+  float mean[8], inv[8], sc[8], sh[8], s8[8], dp8[8], a0[8], a1[8];
+  ld8f(d.mean + q.c8, mean);
+  ld8f(d.invstd + q.c8, inv);
+  if (MODE == CRNN_BNG_RELU) {
+    ld8f(d.scale + q.c8, sc);
+    ld8f(d.shift + q.c8, sh);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) a0[i] = a1[i] = 0.f;
+  const long m0 = blockIdx.x * rpb, m1 = min(d.M, m0 + rpb);
+  uint32_t cb = 0xffffffffu;
+  for (long m = m0 + q.r; m < m1; m += q.rl) {
+    const size_t o = (size_t)m * C + q.c8;
+    if constexpr (MODE == CRNN_BNG_SE) {
+      const uint32_t bb = dHW.div((uint32_t)m);
+      if (bb != cb) {
+        cb = bb;
+        ld8f(d.s + (size_t)bb * C + q.c8, s8);
+        ld8f(d.dpool + (size_t)bb * C + q.c8, dp8);
+      }
+    }
+    float z[8], g[8];
+    unpack8<T>(ld8<T>((const T*)d.z + o), z);
+    bng<T, MODE>(d, o, z, sc, sh, s8, dp8, g);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      a0[i] += g[i];
+      a1[i] += g[i] * ((z[i] - mean[i]) * inv[i]);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    red[q.r * C + q.c8 + i] = a0[i];
+    red[(q.rl + q.r) * C + q.c8 + i] = a1[i];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += NT) {
+    float s0 = 0.f, s1 = 0.f;
+    for (int k = 0; k < q.rl; ++k) {
+      s0 += red[k * C + c];
+      s1 += red[(q.rl + k) * C + c];
+    }
+    p0[(size_t)blockIdx.x * C + c] = s0;
+    p1[(size_t)blockIdx.x * C + c] = s1;
+  }
+}
+
+// dz = A g - Bx xhat - Cg with A = scale, Bx = scale*mgx, Cg = scale*mg, xhat = (z - mean)*invstd.
+// (Folding xhat into z-coefficients would cancel catastrophically on channels with |mean| >> std.)
+template <typename T, int MODE>
+__global__ __launch_bounds__(NT) void bnb_apply_kernel(crnn_bn_bwd_desc d, FastDiv dHW, const float* __restrict__ mg,
+                                                       const float* __restrict__ mgx, T* __restrict__ dz, long rpb) {
+  const int C = d.C;
+  const RowMap q = rowmap(C);
+  float A[8], Bx[8], Cg[8], mean[8], inv[8], sc[8], sh[8], s8[8], dp8[8];
+  {
+    float g1[8], g2[8];
+    ld8f(d.mean + q.c8, mean);
+    ld8f(d.invstd + q.c8, inv);
+    ld8f(d.scale + q.c8, A);
+    ld8f(mg + q.c8, g1);
+    ld8f(mgx + q.c8, g2);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      Bx[i] = A[i] * g2[i];
+      Cg[i] = A[i] * g1[i];
+    }
+  }
+  if (MODE == CRNN_BNG_RELU) {
+    ld8f(d.scale + q.c8, sc);
+    ld8f(d.shift + q.c8, sh);
+  }
+  const long m0 = blockIdx.x * rpb, m1 = min(d.M, m0 + rpb);
+  uint32_t cb = 0xffffffffu;
+  for (long m = m0 + q.r; m < m1; m += q.rl) {
+    const size_t o = (size_t)m * C + q.c8;
+    if constexpr (MODE == CRNN_BNG_SE) {
+      const uint32_t bb = dHW.div((uint32_t)m);
+      if (bb != cb) {
+        cb = bb;
+        ld8f(d.s + (size_t)bb * C + q.c8, s8);
+        ld8f(d.dpool + (size_t)bb * C + q.c8, dp8);
+      }
+    }
+    float z[8], g[8], out[8];
+    unpack8<T>(ld8<T>((const T*)d.z + o), z);
+    bng<T, MODE>(d, o, z, sc, sh, s8, dp8, g);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) out[i] = A[i] * g[i] - Bx[i] * ((z[i] - mean[i]) * inv[i]) - Cg[i];
+    st8<T>(dz + o, pack8<T>(out));
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(NT) void se_residual2_kernel(const T* __restrict__ z, const float* __restrict__ scp,
+                                                          const float* __restrict__ shp, const float* __restrict__ s,
+                                                          const T* __restrict__ idn, const float* __restrict__ iscp,
+                                                          const float* __restrict__ ishp, T* __restrict__ y, long M,
+                                                          int C, FastDiv dHW, long rpb) {
+  const RowMap q = rowmap(C);
+  float sc[8], sh[8], isc[8], ish[8], s8[8];
+  ld8f(scp + q.c8, sc);
+  ld8f(shp + q.c8, sh);
+  if (iscp) {
+    ld8f(iscp + q.c8, isc);
+    ld8f(ishp + q.c8, ish);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      isc[i] = 1.f;
+      ish[i] = 0.f;
+    }
+  }
+  const long m0 = blockIdx.x * rpb, m1 = min(M, m0 + rpb);
+  uint32_t cb = 0xffffffffu;
+  for (long m = m0 + q.r; m < m1; m += q.rl) {
+    const uint32_t bb = dHW.div((uint32_t)m);
+    if (bb != cb) {
+      cb = bb;
+      ld8f(s + (size_t)bb * C + q.c8, s8);
+    }
+    const size_t o = (size_t)m * C + q.c8;
+    float v[8], dd[8];
+    unpack8<T>(ld8<T>(z + o), v);
+    unpack8<T>(ld8<T>(idn + o), dd);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = fmaxf((v[i] * sc[i] + sh[i]) * s8[i] + dd[i] * isc[i] + ish[i], 0.f);
+    st8<T>(y + o, pack8<T>(v));
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(NT) void bn_act2_kernel(const T* __restrict__ z, const float* __restrict__ scp,
+                                                     const float* __restrict__ shp, T* __restrict__ y, long M, int C,
+                                                     int relu, long rpb) {
+  const RowMap q = rowmap(C);
+  float sc[8], sh[8];
+  ld8f(scp + q.c8, sc);
+  ld8f(shp + q.c8, sh);
+  const long m0 = blockIdx.x * rpb, m1 = min(M, m0 + rpb);
+  for (long m = m0 + q.r; m < m1; m += q.rl) {
+    const size_t o = (size_t)m * C + q.c8;
+    float v[8];
+    unpack8<T>(ld8<T>(z + o), v);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      v[i] = v[i] * sc[i] + sh[i];
+      if (relu) v[i] = fmaxf(v[i], 0.f);
+    }
+    st8<T>(y + o, pack8<T>(v));
+  }
+}
+
+// per-sample spatial reductions with hoisted channel constants; block per sample
+template <typename T, int KIND>  // KIND 0: SE pool (mean of z*sc+sh); 1: SE bwd (sum dy*(y>0)*(z*sc+sh))
+__global__ __launch_bounds__(NT) void se_reduce_kernel(const T* __restrict__ z, const float* __restrict__ scp,
+                                                       const float* __restrict__ shp, const T* __restrict__ dy,
+                                                       const T* __restrict__ y, int HW, int C,
+                                                       float* __restrict__ out, float mul) {
+  extern __shared__ float red[];
+  const RowMap q = rowmap(C);
+  const int b = blockIdx.x;
+  float sc[8], sh[8], a[8];
+  ld8f(scp + q.c8, sc);
+  ld8f(shp + q.c8, sh);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) a[i] = 0.f;
+  for (int hw = q.r; hw < HW; hw += q.rl) {
+    const size_t o = ((size_t)b * HW + hw) * C + q.c8;
+    float v[8];
+    unpack8<T>(ld8<T>(z + o), v);
+    if constexpr (KIND == 0) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) a[i] += v[i] * sc[i] + sh[i];
+    } else {
+      float dd[8], yy[8];
+      unpack8<T>(ld8<T>(dy + o), dd);
+      unpack8<T>(ld8<T>(y + o), yy);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) a[i] += yy[i] > 0.f ? dd[i] * (v[i] * sc[i] + sh[i]) : 0.f;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) red[q.r * C + q.c8 + i] = a[i];
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += NT) {
+    float s = 0.f;
+    for (int k = 0; k < q.rl; ++k) s += red[k * C + c];
+    out[(size_t)b * C + c] = s * mul;
+  }
+}
+
+inline bool rowmap_ok(int C) { return C % 8 == 0 && C / 8 <= NT && NT % (C / 8) == 0; }
+
+// blocks for a row-streaming launch: enough to fill the chip, each a contiguous row chunk
+inline void stream_grid(long M, int C, int* blocks, long* rpb) {
+  const int rl = NT / (C / 8);
+  long nb = (M + rl * 8 - 1) / (rl * 8);  // >= 8 rows per thread
+  if (nb > 4096) nb = 4096;
+  if (nb < 1) nb = 1;
+  *rpb = (M + nb - 1) / nb;
+  *blocks = (int)((M + *rpb - 1) / *rpb);
+}
+
 #define DISPATCH(dtype, ...)            \
   if ((dtype) == CRNN_BF16) {           \
     using T = bf16;                     \
@@ -682,6 +808,53 @@ __global__ void pack_rows_kernel(const float* __restrict__ src, T* __restrict__ 
     using T = float;                    \
     __VA_ARGS__;                        \
   }
+
+}  // namespace
+
+namespace {
+template <typename T>
+int bnb_reduce_launch(const crnn_bn_bwd_desc* d, float* pg, float* pgx, int rows, hipStream_t st) {
+  const long rpb = (d->M + rows - 1) / rows;
+  const int rl = NT / (d->C / 8);
+  const size_t sm = (size_t)2 * rl * d->C * sizeof(float);
+  const FastDiv dHW(d->HW > 0 ? d->HW : 1);
+  switch (d->mode) {
+    case CRNN_BNG_PLAIN:
+      hipLaunchKernelGGL((bnb_reduce_kernel<T, CRNN_BNG_PLAIN>), dim3(rows), dim3(NT), sm, st, *d, dHW, rpb, pg, pgx);
+      break;
+    case CRNN_BNG_RELU:
+      hipLaunchKernelGGL((bnb_reduce_kernel<T, CRNN_BNG_RELU>), dim3(rows), dim3(NT), sm, st, *d, dHW, rpb, pg, pgx);
+      break;
+    case CRNN_BNG_RESID:
+      hipLaunchKernelGGL((bnb_reduce_kernel<T, CRNN_BNG_RESID>), dim3(rows), dim3(NT), sm, st, *d, dHW, rpb, pg, pgx);
+      break;
+    default:
+      hipLaunchKernelGGL((bnb_reduce_kernel<T, CRNN_BNG_SE>), dim3(rows), dim3(NT), sm, st, *d, dHW, rpb, pg, pgx);
+  }
+  return (int)hipGetLastError();
+}
+
+template <typename T>
+int bnb_apply_launch(const crnn_bn_bwd_desc* d, const float* mg, const float* mgx, void* dz, hipStream_t st) {
+  int nb;
+  long rpb;
+  stream_grid(d->M, d->C, &nb, &rpb);
+  const FastDiv dHW(d->HW > 0 ? d->HW : 1);
+  switch (d->mode) {
+    case CRNN_BNG_PLAIN:
+      hipLaunchKernelGGL((bnb_apply_kernel<T, CRNN_BNG_PLAIN>), dim3(nb), dim3(NT), 0, st, *d, dHW, mg, mgx, (T*)dz, rpb);
+      break;
+    case CRNN_BNG_RELU:
+      hipLaunchKernelGGL((bnb_apply_kernel<T, CRNN_BNG_RELU>), dim3(nb), dim3(NT), 0, st, *d, dHW, mg, mgx, (T*)dz, rpb);
+      break;
+    case CRNN_BNG_RESID:
+      hipLaunchKernelGGL((bnb_apply_kernel<T, CRNN_BNG_RESID>), dim3(nb), dim3(NT), 0, st, *d, dHW, mg, mgx, (T*)dz, rpb);
+      break;
+    default:
+      hipLaunchKernelGGL((bnb_apply_kernel<T, CRNN_BNG_SE>), dim3(nb), dim3(NT), 0, st, *d, dHW, mg, mgx, (T*)dz, rpb);
+  }
+  return (int)hipGetLastError();
+}
 
 }  // namespace
 
@@ -720,11 +893,12 @@ int crnn_bn_finalize(const float* psum, const float* psq, int rows, long rows_pe
 
 int crnn_bn_act(int dtype, const void* z, const float* scale, const float* shift, void* y, long M, int C, int relu,
                 void* stream) {
-  long nvec = M * C / 8;
-  int sh = cg_shift(C);
-  if (sh < 0 || nvec >= (1L << 32)) return crnn_set_error(hipErrorInvalidValue, "bn_act: C/8 must be a power of two");
-  DISPATCH(dtype, hipLaunchKernelGGL(bn_act_kernel<T>, dim3(grid_for(nvec, 256, 16384)), dim3(256), 0,
-                                     (hipStream_t)stream, (const T*)z, scale, shift, (T*)y, (unsigned)nvec, sh, relu));
+  if (!rowmap_ok(C)) return crnn_set_error(hipErrorInvalidValue, "bn_act: C/8 must divide 256");
+  int nb;
+  long rpb;
+  stream_grid(M, C, &nb, &rpb);
+  DISPATCH(dtype, hipLaunchKernelGGL(bn_act2_kernel<T>, dim3(nb), dim3(NT), 0, (hipStream_t)stream, (const T*)z, scale,
+                                     shift, (T*)y, M, C, relu, rpb));
   return (int)hipGetLastError();
 }
 
@@ -746,8 +920,9 @@ int crnn_maxpool_bwd(int dtype, const void* z, const float* scale, const float* 
 }
 
 int crnn_bn_bwd_reduce(int dtype, const crnn_bn_bwd_desc* d, float* pg, float* pgx, int rows, void* stream) {
+  if (!rowmap_ok(d->C)) return crnn_set_error(hipErrorInvalidValue, "bn_bwd_reduce: C/8 must divide 256");
   hipStream_t st = (hipStream_t)stream;
-  DISPATCH(dtype, return chan_reduce(BnBwdF<T>{*d}, d->M, d->C, pg, pgx, rows, st));
+  return dtype == CRNN_BF16 ? bnb_reduce_launch<bf16>(d, pg, pgx, rows, st) : bnb_reduce_launch<float>(d, pg, pgx, rows, st);
 }
 
 int crnn_bn_bwd_finalize(const float* pg, const float* pgx, int rows, int C, long count, float* dgamma, float* dbeta,
@@ -764,20 +939,19 @@ int crnn_bn_bwd_finalize(const float* pg, const float* pgx, int rows, int C, lon
 
 int crnn_bn_bwd_apply(int dtype, const crnn_bn_bwd_desc* d, const float* mean_g, const float* mean_gx, void* dz,
                       void* stream) {
-  long nvec = d->M * d->C / 8;
-  int sh = cg_shift(d->C);
-  if (sh < 0 || nvec >= (1L << 32)) return crnn_set_error(hipErrorInvalidValue, "bn_bwd_apply: C/8 must be a power of two");
-  DISPATCH(dtype, hipLaunchKernelGGL(bn_apply_bwd_kernel<T>, dim3(grid_for(nvec, 256, 16384)), dim3(256), 0,
-                                     (hipStream_t)stream, *d, mean_g, mean_gx, (T*)dz, (unsigned)nvec, sh));
-  return (int)hipGetLastError();
+  if (!rowmap_ok(d->C)) return crnn_set_error(hipErrorInvalidValue, "bn_bwd_apply: C/8 must divide 256");
+  hipStream_t st = (hipStream_t)stream;
+  return dtype == CRNN_BF16 ? bnb_apply_launch<bf16>(d, mean_g, mean_gx, dz, st)
+                            : bnb_apply_launch<float>(d, mean_g, mean_gx, dz, st);
 }
 
 int crnn_se_pool(int dtype, const void* z2, const float* scale, const float* shift, float* pooled, int B, int HW, int C,
                  void* stream) {
   if (C % 8 || NT % (C / 8)) return crnn_set_error(hipErrorInvalidValue, "se_pool: bad C");
   size_t sm = (size_t)(NT / (C / 8)) * C * sizeof(float);
-  DISPATCH(dtype, hipLaunchKernelGGL(sample_reduce_kernel<SePoolF<T>>, dim3(B), dim3(NT), sm, (hipStream_t)stream,
-                                     SePoolF<T>{(const T*)z2, scale, shift, HW, C}, HW, C, pooled, 1.f / (float)HW));
+  DISPATCH(dtype, hipLaunchKernelGGL((se_reduce_kernel<T, 0>), dim3(B), dim3(NT), sm, (hipStream_t)stream,
+                                     (const T*)z2, scale, shift, (const T*)nullptr, (const T*)nullptr, HW, C, pooled,
+                                     1.f / (float)HW));
   return (int)hipGetLastError();
 }
 
@@ -791,12 +965,13 @@ int crnn_se_mlp_fwd(const float* pooled, const float* w1, const float* w2, float
 int crnn_se_residual_fwd(int dtype, const void* z2, const float* scale, const float* shift, const float* s,
                          const void* idn, const float* iscale, const float* ishift, void* y, int B, int HW, int C,
                          void* stream) {
-  long nvec = (long)B * HW * C / 8;
-  int sh = cg_shift(C);
-  if (sh < 0 || nvec >= (1L << 32)) return crnn_set_error(hipErrorInvalidValue, "se_residual: C/8 must be a power of two");
-  DISPATCH(dtype, hipLaunchKernelGGL(se_residual_kernel<T>, dim3(grid_for(nvec, 256, 16384)), dim3(256), 0,
-                                     (hipStream_t)stream, (const T*)z2, scale, shift, s, (const T*)idn, iscale, ishift,
-                                     (T*)y, (unsigned)nvec, (unsigned)HW, C, sh));
+  if (!rowmap_ok(C)) return crnn_set_error(hipErrorInvalidValue, "se_residual: C/8 must divide 256");
+  const long M = (long)B * HW;
+  int nb;
+  long rpb;
+  stream_grid(M, C, &nb, &rpb);
+  DISPATCH(dtype, hipLaunchKernelGGL(se_residual2_kernel<T>, dim3(nb), dim3(NT), 0, (hipStream_t)stream, (const T*)z2,
+                                     scale, shift, s, (const T*)idn, iscale, ishift, (T*)y, M, C, FastDiv(HW), rpb));
   return (int)hipGetLastError();
 }
 
@@ -804,9 +979,8 @@ int crnn_se_bwd_reduce(int dtype, const void* dy, const void* y, const void* z2,
                        const float* shift, float* ds, int B, int HW, int C, void* stream) {
   if (C % 8 || NT % (C / 8)) return crnn_set_error(hipErrorInvalidValue, "se_bwd_reduce: bad C");
   size_t sm = (size_t)(NT / (C / 8)) * C * sizeof(float);
-  DISPATCH(dtype, hipLaunchKernelGGL(sample_reduce_kernel<SeBwdF<T>>, dim3(B), dim3(NT), sm, (hipStream_t)stream,
-                                     SeBwdF<T>{(const T*)dy, (const T*)y, (const T*)z2, scale, shift, HW, C}, HW, C,
-                                     ds, 1.f));
+  DISPATCH(dtype, hipLaunchKernelGGL((se_reduce_kernel<T, 1>), dim3(B), dim3(NT), sm, (hipStream_t)stream,
+                                     (const T*)z2, scale, shift, (const T*)dy, (const T*)y, HW, C, ds, 1.f));
   return (int)hipGetLastError();
 }
 

@@ -1,0 +1,86 @@
+"""world_size-2 gloo tests of the data-parallel glue (crnn_hip/dist.py) on CPU.
+
+The HIP compute path has no CPU fallback, so these exercise what DP adds on top of it:
+the bucketed gradient all-reduce and the parameter broadcast, and check the DP identity on
+the oracle's train step: averaging per-rank gradients of a BN-free sub-network equals the
+single-process gradient of the concatenated batch."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    for sub in ("../rcnn-ocr_amd", "../oracle"):
+        sys.path.insert(0, os.path.join(here, sub))
+    from crnn_hip import dist as D
+    D.init_from_env("gloo")
+    try:
+        # bucketed all-reduce: tiny buckets force many collectives in flight
+        g = torch.arange(1000, dtype=torch.float32) * (rank + 1)
+        D.allreduce_grads(g, bucket_bytes=4 * 37)
+        ok_sum = torch.allclose(g, torch.arange(1000, dtype=torch.float32) * 3)
+        # broadcast from rank 0
+        p = torch.full((17,), float(rank + 5))
+        D.broadcast_params(p)
+        ok_bc = bool((p == 5).all())
+        # DP identity on the oracle's BiLSTM + head (no BN): mean of rank grads == full-batch grad
+        import crnn_oracle as O
+        from crnn_hip.recipe import recipe_state_dict
+        torch.manual_seed(0)
+        shapes = [(k, s) for k, s in O.param_shapes(16, 10, 1, enc_dim=24) if k.startswith(("enc_rnn", "ctc_head"))]
+        sd = recipe_state_dict(shapes, 7)
+        gen = torch.Generator().manual_seed(3)
+        x = torch.randn(4, 6, 24, generator=gen)
+        tg = torch.randint(1, 10, (4, 3), generator=gen)
+        tl = torch.tensor([3, 2, 1, 3])
+
+        def grads(xs, ts, ls):
+            p = {k: v.clone().requires_grad_(True) for k, v in sd.items()}
+            lg = O.head(O.bilstm(xs, p, "enc_rnn.0"), p)
+            # sum-reduction makes the per-sample decomposition exact
+            O.ctc_loss(lg, ts, ls, reduction="sum").backward()
+            return torch.cat([p[k].grad.reshape(-1) for k, _ in shapes])
+
+        full = grads(x, tg, tl)
+        part = grads(x[2 * rank:2 * rank + 2], tg[2 * rank:2 * rank + 2], tl[2 * rank:2 * rank + 2])
+        D.allreduce_grads(part)
+        ok_dp = torch.allclose(part, full, rtol=1e-4, atol=1e-5)
+        q.put((rank, ok_sum, ok_bc, ok_dp))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_allreduce_broadcast_and_dp_identity():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=240) for _ in ps]
+    for p in ps:
+        p.join(timeout=60)
+    assert all(r[1] and r[2] and r[3] for r in res), res
+
+
+def test_buckets_cover_buffer():
+    from crnn_hip.dist import buckets
+    bs = buckets(1003, 4, 40)
+    assert bs[0] == slice(0, 10) and bs[-1].stop == 1003
+    assert sum(s.stop - s.start for s in bs) == 1003

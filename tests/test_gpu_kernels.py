@@ -387,3 +387,73 @@ def test_maxpool_relu_bn(dtype):
     pre = z * sc[None, :, None, None] + sh[None, :, None, None]
     dz = dfull.float().permute(0, 3, 1, 2).cpu() * (pre > 0).float() * sc[None, :, None, None]
     assert relerr(dz, zr.grad) < tol
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2, 3])
+def test_bn_bwd_modes_ill_conditioned_channels(mode):
+    """BN backward in every upstream-gradient mode, fp32, M = 4096 rows x 512 channels, with
+    channels whose |mean| >> std (as in trained / deep layers) — vs torch fp64 autograd."""
+    L = _L()
+    from crnn_hip._lib import BnBwdDesc
+    g = torch.Generator().manual_seed(11)
+    B, H, W, C = 4, 8, 132, 512   # HW not a power of two (per-sample index by division)
+    HW, M = H * W, B * H * W
+    mu = torch.randn(C, generator=g) * 3
+    mu[:64] = 50.0 + torch.rand(64, generator=g) * 50   # |mean| >> std channels
+    sd = torch.rand(C, generator=g) + 0.5
+    sd[:64] = 1e-2
+    z = (torch.randn(B, H, W, C, generator=g, dtype=torch.float64) * sd + mu).float()
+    gamma = (torch.rand(C, generator=g) + 0.5)
+    beta = torch.randn(C, generator=g) * 0.1
+    dy = torch.randn(B, H, W, C, generator=g)
+    s = torch.rand(B, C, generator=g)
+    dpool = torch.randn(B, C, generator=g) * 0.01
+    # forward stats in fp64 (what crnn_bn_finalize produces)
+    z64 = z.double()
+    mean = z64.mean(dim=(0, 1, 2))
+    var = z64.var(dim=(0, 1, 2), unbiased=False)
+    inv = 1 / torch.sqrt(var + 1e-5)
+    sc = gamma.double() * inv
+    sh = beta.double() - mean * sc
+    u = z64 * sc + sh
+    # the kernel's ReLU mask is the fp32 z*sc+sh of the forward; keep dy off the |u| ~ 0 boundary
+    dy = torch.where(u.abs() < 1e-2, torch.zeros_like(dy), dy)
+    y = torch.relu(u * s.double()[:, None, None, :] + torch.randn(B, H, W, C, generator=g, dtype=torch.float64))
+    # reference grad wrt z in fp64 by the BN-backward formula with g by mode
+    dy64 = dy.double()
+    if mode == 0:
+        gg = dy64
+    elif mode == 1:
+        gg = dy64 * (u > 0)
+    elif mode == 2:
+        gg = dy64 * (y > 0)
+    else:
+        gg = dy64 * (y > 0) * s.double()[:, None, None, :] + dpool.double()[:, None, None, :]
+    xh = (z64 - mean) * inv
+    mg = gg.mean(dim=(0, 1, 2))
+    mgx = (gg * xh).mean(dim=(0, 1, 2))
+    dz_ref = sc * (gg - mg - xh * mgx)
+    # HIP
+    dev = lambda t: t.float().contiguous().to(DEV)
+    zd, dyd, yd = dev(z), dev(dy), dev(y)
+    meand, invd, scd, shd = dev(mean), dev(inv), dev(sc), dev(sh)
+    sdv, dpd = dev(s), dev(dpool)
+    desc = BnBwdDesc(dyd.data_ptr(), zd.data_ptr(), meand.data_ptr(), invd.data_ptr(), scd.data_ptr(), shd.data_ptr(),
+                     yd.data_ptr(), sdv.data_ptr(), dpd.data_ptr(), mode, M, C, HW)
+    rows = L.lib().crnn_bn_rows(M)
+    pg, pgx = torch.empty(rows, C, device=DEV), torch.empty(rows, C, device=DEV)
+    st = L.stream_ptr()
+    L.call("crnn_bn_bwd_reduce", L.F32, desc, pg.data_ptr(), pgx.data_ptr(), rows, st)
+    fws = torch.empty(L.lib().crnn_bn_finalize_workspace(C) // 4, device=DEV)
+    dgam, dbet, mgd, mgxd = [torch.empty(C, device=DEV) for _ in range(4)]
+    L.call("crnn_bn_bwd_finalize", pg.data_ptr(), pgx.data_ptr(), rows, C, M, dgam.data_ptr(), dbet.data_ptr(),
+           mgd.data_ptr(), mgxd.data_ptr(), 0, fws.data_ptr(), st)
+    dz = torch.empty(B, H, W, C, device=DEV)
+    L.call("crnn_bn_bwd_apply", L.F32, desc, mgd.data_ptr(), mgxd.data_ptr(), dz.data_ptr(), st)
+    torch.cuda.synchronize()
+    assert relerr(dbet.cpu(), gg.sum(dim=(0, 1, 2))) < 1e-5
+    assert relerr(dgam.cpu(), (gg * xh).sum(dim=(0, 1, 2))) < 1e-4
+    err = relerr(dz.cpu(), dz_ref)
+    err_bad = relerr(dz.cpu()[..., :64], dz_ref[..., :64])
+    print("mode", mode, "dz rel err", err, "ill-conditioned channels", err_bad)
+    assert err < 1e-4 and err_bad < 1e-3

@@ -101,3 +101,22 @@ def test_oracle_bilstm_stack():
     np.testing.assert_allclose(y.detach().numpy(), z["y"], rtol=1e-4, atol=1e-5)
     (y * torch.from_numpy(z["proj"])).sum().backward()
     np.testing.assert_allclose(x.grad.numpy(), z["dx"], rtol=1e-3, atol=1e-5)
+
+
+def test_forced_decisions_reproduce_own_decisions():
+    """crnn_oracle.relu / maxpool2 with forced decisions equal to the oracle's own give the
+    unforced result (the forced fp64 reference used by the GPU train-step tests)."""
+    import torch.nn.functional as F
+    g = torch.Generator().manual_seed(5)
+    u = torch.randn(2, 8, 6, 10, generator=g, dtype=torch.float64)
+    own = O.Ctx(train=True)
+    forced = O.Ctx(train=True, force={"r": u > 0})
+    assert torch.equal(O.relu(own, "r", u), O.relu(forced, "r", u))
+    x = torch.relu(u)
+    ref, idx = F.max_pool2d(x, 2, 2, return_indices=True)
+    # flat index h*W + w -> window element t = 2*dh + dw
+    W = x.shape[-1]
+    t = 2 * ((idx // W) % 2) + (idx % W) % 2
+    got = O.maxpool2(O.Ctx(train=True, force={"stem.pool": t}), "stem.pool", x)
+    assert torch.equal(got, ref)
+    assert torch.equal(O.maxpool2(own, "stem.pool", x), ref)

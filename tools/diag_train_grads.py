@@ -53,7 +53,7 @@ def main(case="b4_32x128_h256"):
     print("median hip32", np.median([w[0] for w in worst]), "median cpu32", np.median([w[1] for w in worst]))
 
 
-if __name__ == "__main__" and (len(sys.argv) == 1 or sys.argv[1] not in ("stages", "bwd")):
+if __name__ == "__main__" and (len(sys.argv) == 1 or sys.argv[1] not in ("stages", "bwd", "local")):
     main(*sys.argv[1:])
 
 
@@ -144,3 +144,27 @@ def bwd_stages(case="b4_32x128_h256"):
 
 if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "bwd":
     bwd_stages(*sys.argv[2:])
+
+
+def block_local(case="b4_32x128_h256"):
+    """per-block decision-consistent local errors (tests/blockcheck.py)."""
+    from blockcheck import block_errors
+    z = load(f"train_{case}.npz")
+    sd, hidden = case_params(z, with_running=False)
+    x = pixels_to_images(z["pixels"])
+    tg, tl = torch.from_numpy(z["targets"]), torch.from_numpy(z["target_lengths"])
+    from model.model import RCNN
+    from crnn_hip.ctc import ctc_loss
+    m = RCNN(num_classes=194, hidden_size=hidden, blank_id=None, compute_dtype=torch.float32)
+    m.load_state_dict(sd, strict=False)
+    m = m.cuda().train()
+    m._engine_for(x.cuda()).debug = True
+    ctc_loss(m(x.cuda()), tg, tl).backward()
+    torch.cuda.synchronize()
+    params = dict(m.named_parameters())
+    for bi, e in block_errors(m._engine, params, {k: v.grad for k, v in params.items()}):
+        print(f"block {bi:2d} " + " ".join(f"{k}={v:.1e}" for k, v in e.items()))
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "local":
+    block_local(*sys.argv[2:])
