@@ -71,15 +71,17 @@ typedef struct {
  * partial's own mean, each partial covering crnn_conv_stat_rows_per_partial(d) rows;
  * consumed by crnn_bn_finalize. */
 int crnn_conv_fwd(int dtype, const crnn_conv_desc* d, const void* x, const void* w, void* y, float* psum, float* psq, void* stream);
-int crnn_conv_stat_rows(const crnn_conv_desc* d);
-int crnn_conv_stat_rows_per_partial(const crnn_conv_desc* d);
+int crnn_conv_stat_rows(int dtype, const crnn_conv_desc* d);
+int crnn_conv_stat_rows_per_partial(int dtype, const crnn_conv_desc* d);
 /* dx[B][Hi][Wi][Ci] = dgrad(dy) (+= dx if accumulate) (+ dres*(yres>0) if dres != NULL). */
 int crnn_conv_dgrad(int dtype, const crnn_conv_desc* d, const void* dy, const void* w, void* dx, const void* dres, const void* yres, int accumulate, void* stream);
 /* dw_oihw (fp32, reference layout) = beta*dw + wgrad(dy, x); ws = split-K slabs. */
 int crnn_conv_wgrad(int dtype, const crnn_conv_desc* d, const void* dy, const void* x, float* dw_oihw, float* ws, size_t ws_bytes, float beta, void* stream);
-size_t crnn_conv_wgrad_workspace(const crnn_conv_desc* d);
-void crnn_conv_fwd_tile(const crnn_conv_desc* d, int* bm, int* bn);
-void crnn_conv_wgrad_plan(const crnn_conv_desc* d, int* bm, int* bn, int* splits);
+size_t crnn_conv_wgrad_workspace(int dtype, const crnn_conv_desc* d);
+/* fwd tile (BM x BN) the library picks for (dtype, d): bf16 GEMM-sized convs run the 256-row
+ * deep-pipelined kernel, fp32 (parity mode) and small ones the 128/64 kernels */
+void crnn_conv_fwd_tile(int dtype, const crnn_conv_desc* d, int* bm, int* bn);
+void crnn_conv_wgrad_plan(int dtype, const crnn_conv_desc* d, int* bm, int* bn, int* splits);
 
 /* ------------------------------------------------------------------ batchnorm */
 /* Combine (sum, M2) partials (Chan, in double) -> per-channel affine (scale = gamma*invstd,

@@ -13,7 +13,8 @@ import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.dirname(HERE)
-LIB_PATH = os.path.join(HERE, "libcrnn_hip.so")
+# CRNN_HIP_LIB: an alternative build of the same library (tuning A/B runs)
+LIB_PATH = os.environ.get("CRNN_HIP_LIB", os.path.join(HERE, "libcrnn_hip.so"))
 CSRC = os.path.join(PKG, "csrc")
 
 F32, BF16 = 0, 1
@@ -44,11 +45,11 @@ _SIGS = {
     "crnn_pack_conv_weight": ([i32, vp, vp, i32, i32, i32, i32, i32, vp], i32),
     "crnn_pack_rows": ([i32, vp, vp, vp, i32, i32, i32, vp], i32),
     "crnn_conv_fwd": ([i32, C.POINTER(ConvDesc), vp, vp, vp, vp, vp, vp], i32),
-    "crnn_conv_stat_rows": ([C.POINTER(ConvDesc)], i32),
-    "crnn_conv_stat_rows_per_partial": ([C.POINTER(ConvDesc)], i32),
+    "crnn_conv_stat_rows": ([i32, C.POINTER(ConvDesc)], i32),
+    "crnn_conv_stat_rows_per_partial": ([i32, C.POINTER(ConvDesc)], i32),
     "crnn_conv_dgrad": ([i32, C.POINTER(ConvDesc), vp, vp, vp, vp, vp, i32, vp], i32),
     "crnn_conv_wgrad": ([i32, C.POINTER(ConvDesc), vp, vp, vp, vp, sz, f32, vp], i32),
-    "crnn_conv_wgrad_workspace": ([C.POINTER(ConvDesc)], sz),
+    "crnn_conv_wgrad_workspace": ([i32, C.POINTER(ConvDesc)], sz),
     "crnn_bn_finalize": ([vp, vp, i32, i64, i32, i64, vp, vp, vp, vp, f32, f32, i32, vp, vp, vp, vp, vp, vp], i32),
     "crnn_bn_finalize_workspace": ([i32], sz),
     "crnn_channel_stats": ([i32, vp, i64, i32, vp, vp, i32, vp], i32),

@@ -268,12 +268,12 @@ class CRNNEngine:
         z = self.ws.get(tag + ".z", (b, ho, wo, cs.co), self.dtype)
         s = L.stream_ptr()
         if train:
-            rows = L.lib().crnn_conv_stat_rows(d)
+            rows = L.lib().crnn_conv_stat_rows(self.dt, d)
             psum = self.ws.get("stat.sum", (self._stat_cap,), torch.float32)[: rows * cs.co].view(rows, cs.co)
             psq = self.ws.get("stat.sq", (self._stat_cap,), torch.float32)[: rows * cs.co].view(rows, cs.co)
             self._conv_call("fwd", self.conv_flops(cs, b, h, w), "crnn_conv_fwd", self.dt, d, ptr(x),
                             ptr(self.packed[cs.name]), ptr(z), ptr(psum), ptr(psq), s)
-            rpp = L.lib().crnn_conv_stat_rows_per_partial(d)
+            rpp = L.lib().crnn_conv_stat_rows_per_partial(self.dt, d)
             stats = self._bn_finalize(cs.bn, psum, psq, rows, b * ho * wo, True, tag, rpp)
         else:
             self._conv_call("fwd", self.conv_flops(cs, b, h, w), "crnn_conv_fwd", self.dt, d, ptr(x),
@@ -288,7 +288,7 @@ class CRNNEngine:
         def upd(cs, h, w):
             nonlocal cap
             d = cs.desc(B, h, w)
-            cap = max(cap, lib.crnn_conv_stat_rows(d) * cs.co)
+            cap = max(cap, lib.crnn_conv_stat_rows(self.dt, d) * cs.co)
             return d.Ho, d.Wo
 
         h, w = upd(self.stem0, H, W)
@@ -450,7 +450,7 @@ class CRNNEngine:
 
     def _wgrad(self, cs: ConvSpec, dz, x, b, h, w):
         d = cs.desc(b, h, w)
-        need = L.lib().crnn_conv_wgrad_workspace(d)
+        need = L.lib().crnn_conv_wgrad_workspace(self.dt, d)
         wsb = self.ws.get("wgrad.ws", (self._wg_cap,), torch.float32)
         if need > wsb.numel() * 4:
             raise RuntimeError("wgrad workspace too small")
@@ -465,7 +465,7 @@ class CRNNEngine:
         def upd(cs, h, w):
             nonlocal cap
             d = cs.desc(B, h, w)
-            cap = max(cap, lib.crnn_conv_wgrad_workspace(d) // 4)
+            cap = max(cap, lib.crnn_conv_wgrad_workspace(self.dt, d) // 4)
             return d.Ho, d.Wo
 
         h, w = upd(self.stem0, H, W)

@@ -11,9 +11,19 @@
 // fwd also emits per-column (channel) partial sum / sum-of-squares of the fp32
 // accumulators for training-mode BatchNorm (two rows per 128-row M tile).
 #include "gemm.hpp"
+#include "gemm256.hpp"
 #include "crnn_internal.hpp"
 
 using namespace gemm;
+
+// target grid of the deep split-K wgrad (tuning knob; slab bytes grow with the split count)
+#ifndef CRNN_WGRAD_BLOCKS
+#define CRNN_WGRAD_BLOCKS 256
+#endif
+// smallest Co that takes the deep-pipelined fwd kernel (tuning knob)
+#ifndef CRNN_DEEP_MIN_CO
+#define CRNN_DEEP_MIN_CO 128
+#endif
 
 namespace {
 
@@ -90,12 +100,16 @@ template <typename T, bool UT> struct FwdA {
     p.tap = k0;
     return p;
   }
+  __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc() const { return mk_rsrc(x, bytes); }
+  // byte offset of elements (row, k0+kofs .. +7), or OOB (reads zeros) — UT only
+  __device__ __forceinline__ uint32_t offs(const Ctx& c, const Prep& p, int kofs) const {
+    const bool ok = (c.mask >> p.tap) & 1u;
+    return boff<T>((uint32_t)(c.off + (p.kh * g.Wi + p.kw) * g.Ci + p.c0 + kofs), ok);
+  }
   __device__ __forceinline__ typename VT<T>::v8 load(const Ctx& c, const Prep& p, int kofs) const {
     auto rs = mk_rsrc(x, bytes);
     if constexpr (UT) {
-      const bool ok = (c.mask >> p.tap) & 1u;
-      const int off = c.off + (p.kh * g.Wi + p.kw) * g.Ci + p.c0 + kofs;
-      return bld8<T>(rs, boff<T>((uint32_t)off, ok));
+      return bld8<T>(rs, offs(c, p, kofs));
     } else {
       const int k = p.tap + kofs;
       uint32_t ci, kw;
@@ -140,10 +154,13 @@ template <typename T> struct DgradA {
     return c;
   }
   __device__ __forceinline__ Prep prep(int k0) const { return tap_prep(g.dCo, g.dKW, k0); }
-  __device__ __forceinline__ typename VT<T>::v8 load(const Ctx& c, const Prep& p, int kofs) const {
+  __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc() const { return mk_rsrc(dy, bytes); }
+  __device__ __forceinline__ uint32_t offs(const Ctx& c, const Prep& p, int kofs) const {
     const bool ok = (c.mask >> p.tap) & 1u;
-    const int off = c.off - ((p.kh >> lsh) * g.Wo + (p.kw >> lsw)) * g.Co + p.c0 + kofs;
-    return bld8<T>(mk_rsrc(dy, bytes), boff<T>((uint32_t)off, ok));
+    return boff<T>((uint32_t)(c.off - ((p.kh >> lsh) * g.Wo + (p.kw >> lsw)) * g.Co + p.c0 + kofs), ok);
+  }
+  __device__ __forceinline__ typename VT<T>::v8 load(const Ctx& c, const Prep& p, int kofs) const {
+    return bld8<T>(rsrc(), offs(c, p, kofs));
   }
 };
 
@@ -158,10 +175,13 @@ template <typename T> struct DgradB {
   typedef TapPrep Prep;
   __device__ __forceinline__ Ctx row_ctx(int r8) const { return Ctx{r8, r8 < g.Ci}; }
   __device__ __forceinline__ Prep prep(int k0) const { return tap_prep(g.dCo, g.dKW, k0); }
-  __device__ __forceinline__ typename VT<T>::v8 load(const Ctx& c, const Prep& p, int kofs) const {
+  __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc() const { return mk_rsrc(w, bytes); }
+  __device__ __forceinline__ uint32_t offs(const Ctx& c, const Prep& p, int kofs) const {
     const bool ok = c.ok && p.tap < g.KH * g.KW;
-    const int off = ((p.c0 + kofs) * g.KH * g.KW + p.tap) * g.Ci + c.ci;
-    return bld8<T>(mk_rsrc(w, bytes), boff<T>((uint32_t)off, ok));
+    return boff<T>((uint32_t)(((p.c0 + kofs) * g.KH * g.KW + p.tap) * g.Ci + c.ci), ok);
+  }
+  __device__ __forceinline__ typename VT<T>::v8 load(const Ctx& c, const Prep& p, int kofs) const {
+    return bld8<T>(rsrc(), offs(c, p, kofs));
   }
 };
 
@@ -207,10 +227,13 @@ template <typename T> struct DgradClsA {
     p.kw = tt.dw[t];
     return p;
   }
-  __device__ __forceinline__ typename VT<T>::v8 load(const Ctx& c, const Prep& p, int kofs) const {
+  __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc() const { return mk_rsrc(dy, bytes); }
+  __device__ __forceinline__ uint32_t offs(const Ctx& c, const Prep& p, int kofs) const {
     const bool ok = (c.mask >> p.tap) & 1u;
-    const int off = c.off + (p.kh * g.Wo + p.kw) * g.Co + p.c0 + kofs;
-    return bld8<T>(mk_rsrc(dy, bytes), boff<T>((uint32_t)off, ok));
+    return boff<T>((uint32_t)(c.off + (p.kh * g.Wo + p.kw) * g.Co + p.c0 + kofs), ok);
+  }
+  __device__ __forceinline__ typename VT<T>::v8 load(const Ctx& c, const Prep& p, int kofs) const {
+    return bld8<T>(rsrc(), offs(c, p, kofs));
   }
 };
 
@@ -232,10 +255,13 @@ template <typename T> struct DgradClsB {
     p.kh = tt.id[p.tap < tt.n ? p.tap : 0];
     return p;
   }
-  __device__ __forceinline__ typename VT<T>::v8 load(const Ctx& c, const Prep& p, int kofs) const {
+  __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc() const { return mk_rsrc(w, bytes); }
+  __device__ __forceinline__ uint32_t offs(const Ctx& c, const Prep& p, int kofs) const {
     const bool ok = c.ok && p.tap < tt.n;
-    const int off = ((p.c0 + kofs) * g.KH * g.KW + p.kh) * g.Ci + c.ci;
-    return bld8<T>(mk_rsrc(w, bytes), boff<T>((uint32_t)off, ok));
+    return boff<T>((uint32_t)(((p.c0 + kofs) * g.KH * g.KW + p.kh) * g.Ci + c.ci), ok);
+  }
+  __device__ __forceinline__ typename VT<T>::v8 load(const Ctx& c, const Prep& p, int kofs) const {
+    return bld8<T>(rsrc(), offs(c, p, kofs));
   }
 };
 
@@ -276,9 +302,13 @@ template <typename T> struct WgradA {
   typedef int Prep;
   __device__ __forceinline__ Ctx row_ctx(int r8) const { return Ctx{r8, r8 < Co}; }
   __device__ __forceinline__ Prep prep(int k0) const { return k0; }
-  __device__ __forceinline__ typename VT<T>::v8 load(const Ctx& c, Prep k0, int kofs) const {
+  __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc() const { return mk_rsrc(dy, bytes); }
+  __device__ __forceinline__ uint32_t offs(const Ctx& c, Prep k0, int kofs) const {
     const int m = k0 + kofs;
-    return bld8<T>(mk_rsrc(dy, bytes), boff<T>((uint32_t)(m * Co + c.co), c.ok && m < M));
+    return boff<T>((uint32_t)(m * Co + c.co), c.ok && m < M);
+  }
+  __device__ __forceinline__ typename VT<T>::v8 load(const Ctx& c, Prep k0, int kofs) const {
+    return bld8<T>(rsrc(), offs(c, k0, kofs));
   }
 };
 
@@ -303,15 +333,18 @@ template <typename T> struct WgradB {
     return c;
   }
   __device__ __forceinline__ Prep prep(int k0) const { return k0; }
-  __device__ __forceinline__ typename VT<T>::v8 load(const Ctx& c, Prep k0, int kofs) const {
+  __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc() const { return mk_rsrc(x, bytes); }
+  __device__ __forceinline__ uint32_t offs(const Ctx& c, Prep k0, int kofs) const {
     const int m = k0 + kofs;
     uint32_t r, wo;
     uint32_t b = g.dHoWo.divmod((uint32_t)m, r);
     uint32_t ho = g.dWo.divmod(r, wo);
     const int hi = (int)ho * g.sh + c.kh, wi = (int)wo * g.sw + c.kw;
     const bool ok = c.ok && m < M && (unsigned)hi < (unsigned)g.Hi && (unsigned)wi < (unsigned)g.Wi;
-    const int off = (((int)b * g.Hi + hi) * g.Wi + wi) * g.Ci + c.ci;
-    return bld8<T>(mk_rsrc(x, bytes), boff<T>((uint32_t)off, ok));
+    return boff<T>((uint32_t)((((int)b * g.Hi + hi) * g.Wi + wi) * g.Ci + c.ci), ok);
+  }
+  __device__ __forceinline__ typename VT<T>::v8 load(const Ctx& c, Prep k0, int kofs) const {
+    return bld8<T>(rsrc(), offs(c, k0, kofs));
   }
 };
 
@@ -392,7 +425,11 @@ int conv_fwd_tt(const Geo& g, const crnn_conv_desc* d, const void* x, const void
   RowMajorK<T> lb{(const T*)w, K, N, K};
   FwdEpi<T> ep{(T*)y, psum, psq, M, N};
   int bm, bn;
-  crnn_conv_fwd_tile(d, &bm, &bn);
+  crnn_conv_fwd_tile(sizeof(T) == 2 ? CRNN_BF16 : CRNN_F32, d, &bm, &bn);
+  if constexpr (sizeof(T) == 2 && UT) {
+    if (bm == 256 && bn == 256) return launch256<256, 256>(la, lb, ep, M, N, K, st);
+    if (bm == 256 && bn == 128) return launch256<256, 128>(la, lb, ep, M, N, K, st);
+  }
   if (bm == 128 && bn == 128) return launch<T, 128, 128>(la, lb, ep, M, N, K, 1, st);
   if (bm == 128 && bn == 64) return launch<T, 128, 64>(la, lb, ep, M, N, K, 1, st);
   return launch<T, 64, 64>(la, lb, ep, M, N, K, 1, st);
@@ -406,6 +443,15 @@ template <typename T> int conv_fwd_t(const crnn_conv_desc* d, const void* x, con
 }
 
 inline int ilog2s(int s) { return s == 1 ? 0 : (s == 2 ? 1 : -1); }
+
+// BN of the deep dgrad kernel for an (M = input pixels, N = Ci) GEMM, or 0 for the 128/64 kernels
+// min_tiles: the grid must hold at least this many 256-row tiles (1 block per CU)
+template <typename T> int deep_dgrad_bn(long M, int N, int Co, long min_tiles) {
+  if (sizeof(T) != 2 || Co % 64 || N % 128) return 0;
+  if (N % 256 == 0 && M * N >= 256L * 256 * min_tiles) return 256;
+  if (M * N >= 256L * 128 * min_tiles) return 128;
+  return 0;
+}
 
 template <typename T>
 int conv_dgrad_strided(const Geo& g, const void* dy, const void* w, void* dx, const void* dres, const void* yres,
@@ -433,8 +479,14 @@ int conv_dgrad_strided(const Geo& g, const void* dy, const void* w, void* dx, co
       DgradClsA<T> la{(const T*)dy, g, tt, Hc, Wc, M, K, dWc, dHcWc, dyb};
       DgradClsB<T> lb{(const T*)w, g, tt, K, wb};
       DgradClsEpi<T> ep{(T*)dx, (const T*)dres, (const T*)yres, g, M, N, accumulate, pch, pcw, dWc, dHcWc};
-      int rc;
-      if (N >= 128 && (long)M * N >= 128L * 128 * 256) rc = launch<T, 128, 128>(la, lb, ep, M, N, K, 1, st);
+      int rc = 0;
+      const int deep = deep_dgrad_bn<T>(M, N, g.Co, 256);
+      if constexpr (sizeof(T) == 2) {
+        if (deep == 256) rc = launch256<256, 256>(la, lb, ep, M, N, K, st);
+        else if (deep == 128) rc = launch256<256, 128>(la, lb, ep, M, N, K, st);
+      }
+      if (deep) {
+      } else if (N >= 128 && (long)M * N >= 128L * 128 * 256) rc = launch<T, 128, 128>(la, lb, ep, M, N, K, 1, st);
       else rc = launch<T, 64, 64>(la, lb, ep, M, N, K, 1, st);
       if (rc) return rc;
     }
@@ -453,6 +505,11 @@ template <typename T> int conv_dgrad_t(const crnn_conv_desc* d, const void* dy, 
   DgradA<T> la{(const T*)dy, g, M, K, lsh, lsw, nbytes((long)g.B * g.Ho * g.Wo * g.Co, sizeof(T))};
   DgradB<T> lb{(const T*)w, g, K, nbytes((long)g.Co * g.KH * g.KW * g.Ci, sizeof(T))};
   DgradEpi<T> ep{(T*)dx, (const T*)dres, (const T*)yres, M, N, accumulate};
+  if constexpr (sizeof(T) == 2) {
+    const int deep = deep_dgrad_bn<T>(M, N, g.Co, 128);
+    if (deep == 256) return launch256<256, 256>(la, lb, ep, M, N, K, st);
+    if (deep == 128) return launch256<256, 128>(la, lb, ep, M, N, K, st);
+  }
   if (N >= 128 && (long)M * N >= 128L * 128 * 256) return launch<T, 128, 128>(la, lb, ep, M, N, K, 1, st);
   if (N <= 64 && (long)M * N >= 128L * 64 * 256) return launch<T, 128, 64>(la, lb, ep, M, N, K, 1, st);
   return launch<T, 64, 64>(la, lb, ep, M, N, K, 1, st);
@@ -463,14 +520,19 @@ template <typename T> int conv_wgrad_t(const crnn_conv_desc* d, const void* dy, 
   Geo g = geo(d);
   int Mp = g.B * g.Ho * g.Wo, Kp = g.KH * g.KW * g.Ci;
   int bm, bn, splits;
-  crnn_conv_wgrad_plan(d, &bm, &bn, &splits);
+  crnn_conv_wgrad_plan(sizeof(T) == 2 ? CRNN_BF16 : CRNN_F32, d, &bm, &bn, &splits);
   size_t need = (size_t)splits * g.Co * Kp * sizeof(float);
   if (ws_bytes < need) return crnn_set_error(hipErrorInvalidValue, "conv_wgrad: workspace too small");
   WgradA<T> la{(const T*)dy, g.Co, Mp, nbytes((long)Mp * g.Co, sizeof(T))};
   WgradB<T> lb{(const T*)x, g, Kp, Mp, nbytes((long)g.B * g.Hi * g.Wi * g.Ci, sizeof(T))};
   SlabEpi ep{ws, g.Co, Kp};
-  int rc;
-  if (bm == 128) rc = launch<T, 128, 128>(la, lb, ep, g.Co, Kp, Mp, splits, st);
+  int rc = 0;
+  if constexpr (sizeof(T) == 2) {
+    if (bm == 256 && bn == 256) rc = launch256<256, 256>(la, lb, ep, g.Co, Kp, Mp, st, splits);
+    else if (bm == 256 && bn == 128) rc = launch256<256, 128>(la, lb, ep, g.Co, Kp, Mp, st, splits);
+  }
+  if (bm == 256) {
+  } else if (bm == 128) rc = launch<T, 128, 128>(la, lb, ep, g.Co, Kp, Mp, splits, st);
   else rc = launch<T, 64, 64>(la, lb, ep, g.Co, Kp, Mp, splits, st);
   if (rc) return rc;
   int ci_real = d->Ci_real > 0 ? d->Ci_real : g.Ci;
@@ -486,29 +548,46 @@ template <typename T> int conv_wgrad_t(const crnn_conv_desc* d, const void* dy, 
 
 extern "C" {
 
-void crnn_conv_fwd_tile(const crnn_conv_desc* d, int* bm, int* bn) {
+void crnn_conv_fwd_tile(int dtype, const crnn_conv_desc* d, int* bm, int* bn) {
   long M = (long)d->B * d->Ho * d->Wo;
-  if (d->Co <= 64) { *bm = 128; *bn = 64; }
+  // the 256-row kernel: bf16, whole 64-deep K-tiles inside one tap, >= ~1 block per CU
+  const bool deep = dtype == CRNN_BF16 && d->Ci % 64 == 0 && d->Co % 128 == 0 && d->Co >= CRNN_DEEP_MIN_CO;
+  if (deep && d->Co >= 256 && M * d->Co >= 256L * 256 * 128) { *bm = 256; *bn = 256; }
+  else if (deep && M * d->Co >= 256L * 128 * 128) { *bm = 256; *bn = 128; }
+  else if (d->Co <= 64) { *bm = 128; *bn = 64; }
   else if (M * d->Co >= 128L * 128 * 192) { *bm = 128; *bn = 128; }
   else { *bm = 64; *bn = 64; }
 }
 
-int crnn_conv_stat_rows_per_partial(const crnn_conv_desc* d) {
+int crnn_conv_stat_rows_per_partial(int dtype, const crnn_conv_desc* d) {
   int bm, bn;
-  crnn_conv_fwd_tile(d, &bm, &bn);
+  crnn_conv_fwd_tile(dtype, d, &bm, &bn);
   return bm / 2;
 }
 
-int crnn_conv_stat_rows(const crnn_conv_desc* d) {
+int crnn_conv_stat_rows(int dtype, const crnn_conv_desc* d) {
   int bm, bn;
-  crnn_conv_fwd_tile(d, &bm, &bn);
+  crnn_conv_fwd_tile(dtype, d, &bm, &bn);
   long M = (long)d->B * d->Ho * d->Wo;
   return (int)(((M + bm - 1) / bm) * 2);
 }
 
-void crnn_conv_wgrad_plan(const crnn_conv_desc* d, int* bm, int* bn, int* splits) {
+void crnn_conv_wgrad_plan(int dtype, const crnn_conv_desc* d, int* bm, int* bn, int* splits) {
   long Mp = (long)d->B * d->Ho * d->Wo;
   int Kp = d->KH * d->KW * d->Ci;
+  if (dtype == CRNN_BF16 && d->Co % 256 == 0 && Kp % 128 == 0 && Mp >= 256L * 64) {
+    // deep kernel: 1 block per CU, ~2 blocks per CU over the split-K grid, >= 8 K-tiles per split
+    *bm = 256;
+    *bn = Kp % 256 == 0 ? 256 : 128;
+    long tiles = (long)(d->Co / 256) * (Kp / *bn);
+    long want = CRNN_WGRAD_BLOCKS / tiles;      // whole rounds of 1-block-per-CU waves
+    long maxs = (Mp + 512 - 1) / 512;
+    if (want > maxs) want = maxs;
+    if (want < 1) want = 1;
+    if (want > 256) want = 256;
+    *splits = eff_splits((int)Mp, (int)want);
+    return;
+  }
   int b = (d->Co >= 128 && Kp >= 128) ? 128 : 64;
   *bm = b; *bn = b;
   long tiles = ((d->Co + b - 1) / b) * (long)((Kp + b - 1) / b);
@@ -520,9 +599,9 @@ void crnn_conv_wgrad_plan(const crnn_conv_desc* d, int* bm, int* bn, int* splits
   *splits = eff_splits((int)Mp, (int)want);
 }
 
-size_t crnn_conv_wgrad_workspace(const crnn_conv_desc* d) {
+size_t crnn_conv_wgrad_workspace(int dtype, const crnn_conv_desc* d) {
   int bm, bn, s;
-  crnn_conv_wgrad_plan(d, &bm, &bn, &s);
+  crnn_conv_wgrad_plan(dtype, d, &bm, &bn, &s);
   return (size_t)s * d->Co * d->KH * d->KW * d->Ci * sizeof(float);
 }
 

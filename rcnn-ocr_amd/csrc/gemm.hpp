@@ -344,9 +344,13 @@ template <typename T> struct RowMajorK {
   typedef int Prep;
   __device__ __forceinline__ Ctx row_ctx(int r) const { return Ctx{(uint32_t)r * (uint32_t)ld, r < rows}; }
   __device__ __forceinline__ Prep prep(int k0) const { return k0; }
-  __device__ __forceinline__ typename VT<T>::v8 load(const Ctx& c, Prep k0, int kofs) const {
+  __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc() const { return mk_rsrc(p, bytes()); }
+  __device__ __forceinline__ uint32_t offs(const Ctx& c, Prep k0, int kofs) const {
     const int k = k0 + kofs;
-    return bld8<T>(mk_rsrc(p, bytes()), boff<T>(c.off + k, c.ok && k < K));
+    return boff<T>(c.off + k, c.ok && k < K);
+  }
+  __device__ __forceinline__ typename VT<T>::v8 load(const Ctx& c, Prep k0, int kofs) const {
+    return bld8<T>(rsrc(), offs(c, k0, kofs));
   }
   __device__ __forceinline__ uint32_t bytes() const { return (uint32_t)((size_t)(rows > 0 ? rows : 1) * ld * sizeof(T)); }
 };

@@ -1,0 +1,343 @@
+// Deep-pipelined bf16 MFMA GEMM: BM x BN = 256 x {256,128} tiles, 512 threads (8 waves as
+// 2(M) x 4(N)), K-tile 64, operands staged global -> LDS by LDS-DMA (buffer_load ... lds).
+//
+//   C[m][n] = sum_k A(m,k) * B(n,k)       (gemm.hpp loaders with offs()/rsrc(); either operand
+//                                          K-contiguous or row-contiguous, split-K optional)
+//
+// Why this shape (cdna_hip_programming.md §5): a 128^2 tile with a barrier per K-step stalls on the
+// vmcnt(0) that __syncthreads() emits while the next stage is in flight. Here the LDS-DMA
+// prefetch stays in flight ACROSS raw s_barriers and is retired by a counted vmcnt once per
+// K-tile, with 1 block per CU doing 64 MFMAs per wave per K-tile.
+//
+// Schedule of K-tile t (LDS buffer b = t & 1), four phases, one C quadrant (mh, nh) each:
+//   P1 (0,0): read A[mh=0], B[nh=0] fragments     issue A-half1 of tile t+1 -> buffer b^1
+//   P2 (0,1): read B[nh=1]                         issue A-half0 of tile t+2 -> buffer b
+//   P3 (1,1): read A[mh=1]                         issue B-half0 of tile t+2 -> buffer b
+//   P4 (1,0): (registers only)                     issue B-half1 of tile t+2 -> buffer b; vmcnt(VM)
+// each phase: ds_reads, DMA issue, s_barrier, lgkmcnt(0), 16 MFMA, s_barrier. A half-tile slot is
+// re-filled only after the phase that read it into registers has passed its second barrier (WAR),
+// and tile t+1 is complete once P4 of tile t retires everything but tile t+2's last three
+// half-tiles (RAW: read one phase after the wait).
+//
+// LDS image: rows of 64 bf16 (128 B), 16-B chunks XOR-swizzled by (row>>1)&7 (gemm::swz) — the
+// DMA destination is lane-linear (1 KiB = 8 rows per wave-instruction), so the swizzle is applied
+// on the SOURCE side: the lane that fills physical chunk c of row r loads logical chunk c^swz(r).
+// A half h holds the quadrant row blocks {r : (r / QM) % 2 == h} (same for B with QN).
+#pragma once
+#include "gemm.hpp"
+
+namespace gemm {
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds_seg, uint32_t voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_t*)lds_seg, 16, voff, 0, 0, 0);
+}
+
+// Row-contiguous fragments are read with ds_read_b64_tr_b16 as inline asm (Op256::trd): the
+// builtin makes hipcc drain every in-flight LDS-DMA (s_waitcnt vmcnt(0)) before it, which would
+// de-pipeline the kernel; the asm read is not tracked by hipcc, so the kernel's own lgkmcnt(0)
+// after each phase barrier retires it.
+
+// after the explicit lgkmcnt(0): keep the scheduler from hoisting MFMAs that consume asm reads
+__device__ __forceinline__ void lds_wait_all() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+__device__ __forceinline__ void raw_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// per-wave, per-column partial statistics (sum, sum of squared deviations from the partial
+// mean) over this wave's WM accumulator rows — the BN two-pass-in-registers epilogue
+template <int MI, int NI, class EPI>
+__device__ __forceinline__ void wave_col_stats(const f32x4 (&acc)[MI][NI], const EPI& epi, int M, int rbase,
+                                               int prow, int ncol0, int lane) {
+  constexpr int WM = MI * 16;
+  const int mr = lane & 15, nq = 4 * (lane >> 4);
+  const int nval = min(WM, max(0, M - rbase));
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    f32x4 s = {0.f, 0.f, 0.f, 0.f}, q = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < MI; ++i) s += acc[i][j];
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) s[r] += __shfl_xor(s[r], o, 64);
+    const float inv_n = nval > 0 ? 1.f / (float)nval : 0.f;
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const bool ok = rbase + i * 16 + mr < M;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float dv = acc[i][j][r] - s[r] * inv_n;
+        q[r] += ok ? dv * dv : 0.f;
+      }
+    }
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) q[r] += __shfl_xor(q[r], o, 64);
+    if (mr == 0) epi.stats(prow, ncol0 + j * 16 + nq, s, q);
+  }
+}
+
+// One operand of the deep kernel: R rows (BM or BN), quadrant extent Q, staged by LDS-DMA.
+//  K-contiguous (L::kRowVec false): image [R][64] (row pitch 128 B), chunk swizzle (row>>1)&7;
+//    half h = rows {r : (r/Q) % 2 == h}, each wave-instruction fills 8 consecutive rows.
+//  row-contiguous (L::kRowVec true): image [half][64 k][R/2 rows] (k-row pitch R bytes), 16-B chunk
+//    swizzle fsw(k) on 32-B slots, read with ds_read_b64_tr_b16 from k-rows 8g+q (lo) and
+//    8g+4+q (hi): a lane then holds k = 8g..8g+7 — the same k map as a K-contiguous ds_read_b128,
+//    so mixed operands need no permuted (bank-conflicting) 8-byte reads. fsw keeps the 32 lanes
+//    of each read pass on distinct banks for both R (checked by enumeration).
+template <class L, int R, int Q> struct Op256 {
+  static constexpr bool RV = L::kRowVec;
+  static constexpr int I = R / 128;        // DMA wave-instructions per wave per half-tile
+  static constexpr int TB = R * 64 * 2;    // tile bytes
+  static constexpr int HB = TB / 2;
+  typename L::Ctx ctx[2][I];
+  int kofs[2][I], seg[2][I];
+  uint32_t plo, phi;                       // RV: per-lane read offsets (half 0, kk 0, fragment 0)
+
+  static __device__ __forceinline__ int fsw(int k) {
+    return R == 256 ? 2 * ((k + 4 * (k >> 3)) & 7) : 2 * (((k >> 1) + 2 * (k >> 3)) & 3);
+  }
+
+  // base: first tile row of the block; blk: this wave's row block (wr or wc) of extent 2Q
+  __device__ __forceinline__ void init(const L& l, int base, int wid, int lane, int blk) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i = 0; i < I; ++i) {
+        const int g = wid * I + i;
+        if constexpr (!RV) {
+          constexpr int per = Q / 8;
+          const int r0 = (g / per) * 2 * Q + h * Q + (g % per) * 8;
+          const int r = r0 + (lane >> 3);
+          ctx[h][i] = l.row_ctx(base + r);
+          kofs[h][i] = ((lane & 7) ^ ((r >> 1) & 7)) * 8;
+          seg[h][i] = r0 * 128;
+        } else {
+          constexpr int CPR = R / 16, KPI = 64 / CPR;  // chunks per k-row, k-rows per instruction
+          const int kr = g * KPI + lane / CPR;
+          const int j = ((lane % CPR) ^ fsw(kr)) * 8;  // half-local row of this lane's 8 rows
+          ctx[h][i] = l.row_ctx(base + (j / Q) * 2 * Q + h * Q + j % Q);
+          kofs[h][i] = kr;
+          seg[h][i] = h * HB + g * 1024;
+        }
+      }
+    if constexpr (RV) {
+      // fragment f of the wave's quadrant rows: half-local column blk*Q + 16f + 4p -> chunk
+      // c0 + 2f with c0 = blk*Q/8 + (p>>1); c0 and 2f occupy disjoint bits, so chunk ^ fsw =
+      // (c0 ^ fsw) ^ 2f and a fragment's offset is the lane offset XOR 32f.
+      const int g = lane >> 4, c = lane & 15, q = c >> 2, p = c & 3;
+      const int c0 = blk * (Q / 8) + (p >> 1);
+      const int klo = 8 * g + q, khi = klo + 4;
+      plo = (uint32_t)(klo * R + ((c0 ^ fsw(klo)) << 4) + (p & 1) * 8);
+      phi = (uint32_t)(khi * R + ((c0 ^ fsw(khi)) << 4) + (p & 1) * 8);
+    }
+  }
+  __device__ __forceinline__ void issue(const L& l, __amdgpu_buffer_rsrc_t rs, char* tile, int h,
+                                        const typename L::Prep& p) const {
+#pragma unroll
+    for (int i = 0; i < I; ++i) dma16(rs, tile + seg[h][i], l.offs(ctx[h][i], p, kofs[h][i]));
+  }
+
+  template <int OFF> static __device__ __forceinline__ s16x4 trd(uint32_t a) {
+    s16x4 v;
+    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(v) : "v"(a), "i"(OFF));
+    return v;
+  }
+  static __device__ __forceinline__ bf16x8 cat(s16x4 lo, s16x4 hi) {
+    s16x4 t[2] = {lo, hi};
+    return *reinterpret_cast<const bf16x8*>(t);
+  }
+  // N fragments (rows rb0 + H*Q + 16f) x both 32-deep k sub-steps, from the operand tile at `tile`
+  // (LDS address `lds` of the same tile for the row-contiguous asm reads)
+  template <int H, int N>
+  __device__ __forceinline__ void load(bf16x8 (&fr)[N][2], const char* tile, uint32_t lds, int rb0, int lane) const {
+    if constexpr (!RV) {
+#pragma unroll
+      for (int f = 0; f < N; ++f)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+          fr[f][kk] = gemm::frag<bf16, R, false, false, 64>(reinterpret_cast<const bf16*>(tile), rb0 + H * Q + f * 16, kk, lane);
+    } else {
+      const uint32_t bl = lds + plo, bh = lds + phi;
+#pragma unroll
+      for (int f = 0; f < N; ++f) {
+        const uint32_t al = bl ^ (uint32_t)(32 * f), ah = bh ^ (uint32_t)(32 * f);
+        fr[f][0] = cat(trd<H * HB>(al), trd<H * HB>(ah));
+        fr[f][1] = cat(trd<H * HB + 32 * R>(al), trd<H * HB + 32 * R>(ah));
+      }
+    }
+  }
+};
+
+__device__ __forceinline__ uint32_t lds_addr(const char* p) {
+  return (uint32_t)(size_t)((const __attribute__((address_space(3))) char*)p);
+}
+
+template <int BM, int BN, class LA, class LB, class EPI>
+__global__ __launch_bounds__(512) void gemm256_kernel(LA la, LB lb, EPI epi, int M, int N, int K, int klen,
+                                                      int tiles_m, int tiles_n, int nsplit) {
+  using T = bf16;
+  static_assert(BM == 256 && (BN == 256 || BN == 128), "tile");
+  constexpr int KS = 64;
+  constexpr int WM = BM / 2, WN = BN / 4;        // per-wave output block
+  constexpr int MI = WM / 16, NI = WN / 16;      // 16x16 fragments per wave
+  constexpr int MQ = MI / 2, NQ = NI / 2;        // fragments per quadrant
+  constexpr int QM = WM / 2, QN = WN / 2;        // quadrant extent
+  using OA = Op256<LA, BM, QM>;
+  using OB = Op256<LB, BN, QN>;
+  constexpr int STAGE = OA::TB + OB::TB;
+  constexpr int VM = OA::I + 2 * OB::I;          // DMA instructions of tile t+2 issued before the P4 wait
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+
+  const int nwg = tiles_m * tiles_n * nsplit;
+  const int wg = xcd_remap(blockIdx.x, nwg);
+  const int n_tile = wg % tiles_n, m_tile = (wg / tiles_n) % tiles_m, kz = wg / (tiles_n * tiles_m);
+  const int m0 = m_tile * BM, n0 = n_tile * BN;
+  const int kbeg = kz * klen, kend = min(K, kbeg + klen);
+  const int nk = kend > kbeg ? (kend - kbeg + KS - 1) / KS : 0;
+
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wid >> 2, wc = wid & 3;
+
+  OA oa;
+  OB ob;
+  oa.init(la, m0, wid, lane, wr);
+  ob.init(lb, n0, wid, lane, wc);
+  const __amdgpu_buffer_rsrc_t ra = la.rsrc(), rb = lb.rsrc();
+  char* const sA0 = smem;
+  char* const sB0 = smem + OA::TB;
+
+  f32x4 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // ---- prologue: tile 0 whole, tile 1 except its A-half1 (issued in P1 of tile 0)
+  typename LA::Prep pa2 = la.prep(kbeg);
+  typename LB::Prep pb2 = lb.prep(kbeg);
+  if (nk > 0) {
+    oa.issue(la, ra, sA0, 0, pa2);
+    ob.issue(lb, rb, sB0, 0, pb2);
+    ob.issue(lb, rb, sB0, 1, pb2);
+    oa.issue(la, ra, sA0, 1, pa2);
+  }
+  typename LA::Prep pa1 = pa2;  // prep of tile t+1 (for its A-half1)
+  if (nk > 1) {
+    pa1 = la.prep(kbeg + KS);
+    const typename LB::Prep pb1 = lb.prep(kbeg + KS);
+    oa.issue(la, ra, sA0 + STAGE, 0, pa1);
+    ob.issue(lb, rb, sB0 + STAGE, 0, pb1);
+    ob.issue(lb, rb, sB0 + STAGE, 1, pb1);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(VM) : "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  raw_barrier();
+
+  bf16x8 af[MQ][2], bfr[NI][2];
+  for (int t = 0; t < nk; ++t) {
+    const int b = t & 1;
+    const char* As = smem + b * STAGE;
+    const char* Bs = As + OA::TB;
+    const uint32_t lA = lds_addr(As), lB = lds_addr(Bs);
+    const bool n1 = t + 1 < nk, n2 = t + 2 < nk;
+    if (n2) {
+      pa2 = la.prep(kbeg + (t + 2) * KS);
+      pb2 = lb.prep(kbeg + (t + 2) * KS);
+    }
+    // ---- P1: quadrant (0,0)
+    oa.template load<0, MQ>(af, As, lA, wr * WM, lane);
+    ob.template load<0, NQ>(*reinterpret_cast<bf16x8(*)[NQ][2]>(&bfr[0]), Bs, lB, wc * WN, lane);
+    if (n1) oa.issue(la, ra, sA0 + (b ^ 1) * STAGE, 1, pa1);
+    raw_barrier();
+    lds_wait_all();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < MQ; ++i)
+#pragma unroll
+        for (int j = 0; j < NQ; ++j) mma<T>(acc[i][j], bfr[j][kk], af[i][kk]);
+    __builtin_amdgcn_s_setprio(0);
+    raw_barrier();
+    // ---- P2: quadrant (0,1)
+    ob.template load<1, NQ>(*reinterpret_cast<bf16x8(*)[NQ][2]>(&bfr[NQ]), Bs, lB, wc * WN, lane);
+    if (n2) oa.issue(la, ra, sA0 + b * STAGE, 0, pa2);
+    raw_barrier();
+    lds_wait_all();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < MQ; ++i)
+#pragma unroll
+        for (int j = NQ; j < NI; ++j) mma<T>(acc[i][j], bfr[j][kk], af[i][kk]);
+    __builtin_amdgcn_s_setprio(0);
+    raw_barrier();
+    // ---- P3: quadrant (1,1)
+    oa.template load<1, MQ>(af, As, lA, wr * WM, lane);
+    if (n2) ob.issue(lb, rb, sB0 + b * STAGE, 0, pb2);
+    raw_barrier();
+    lds_wait_all();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < MQ; ++i)
+#pragma unroll
+        for (int j = NQ; j < NI; ++j) mma<T>(acc[MQ + i][j], bfr[j][kk], af[i][kk]);
+    __builtin_amdgcn_s_setprio(0);
+    raw_barrier();
+    // ---- P4: quadrant (1,0)
+    if (n2) {
+      ob.issue(lb, rb, sB0 + b * STAGE, 1, pb2);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(VM) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    pa1 = pa2;
+    raw_barrier();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < MQ; ++i)
+#pragma unroll
+        for (int j = 0; j < NQ; ++j) mma<T>(acc[MQ + i][j], bfr[j][kk], af[i][kk]);
+    __builtin_amdgcn_s_setprio(0);
+    raw_barrier();
+  }
+
+  const int mr = lane & 15, nq = 4 * (lane >> 4);
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) epi.store(m0 + wr * WM + i * 16 + mr, n0 + wc * WN + j * 16 + nq, acc[i][j], kz);
+  if constexpr (EPI::kStats) wave_col_stats<MI, NI>(acc, epi, M, m0 + wr * WM, m_tile * 2 + wr, n0 + wc * WN, lane);
+}
+
+// nsplit: split-K factor (K ranges of split_len(K, nsplit), multiples of 64)
+template <int BM, int BN, class LA, class LB, class EPI>
+inline int launch256(const LA& la, const LB& lb, const EPI& epi, int M, int N, int K, hipStream_t st,
+                     int nsplit = 1) {
+  if (M <= 0 || N <= 0) return 0;
+  const int tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN;
+  const int klen = split_len(K, nsplit);
+  nsplit = K > 0 ? (K + klen - 1) / klen : 1;
+  hipLaunchKernelGGL((gemm256_kernel<BM, BN, LA, LB, EPI>), dim3(tm * tn * nsplit), dim3(512), 0, st, la, lb, epi,
+                     M, N, K, klen, tm, tn, nsplit);
+  return (int)hipGetLastError();
+}
+
+}  // namespace gemm

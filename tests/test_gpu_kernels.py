@@ -51,8 +51,20 @@ CONVS = [
 ]
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("cfg", CONVS)
+# bf16 shapes large enough for the 256-row deep-pipelined kernels (fwd: crnn_conv_fwd_tile; dgrad
+# incl. stride-2 parity classes with zero-tap classes; wgrad split-K: crnn_conv_wgrad_plan):
+# 256x256 and 256x128 tiles, Ci = 64 (9 K-tiles), stride 2, a ragged last M tile
+CONVS_DEEP = [
+    (64, 256, 16, 64, 256, (3, 3), (1, 1), (1, 1)),
+    (32, 64, 32, 128, 128, (3, 3), (1, 1), (1, 1)),
+    (256, 256, 8, 64, 512, (3, 3), (2, 2), (1, 1)),
+    (52, 256, 16, 63, 256, (3, 3), (1, 1), (1, 1)),
+    (128, 128, 16, 64, 256, (1, 1), (2, 2), (0, 0)),
+]
+
+
+@pytest.mark.parametrize("dtype,cfg", [(dt, c) for c in CONVS for dt in (torch.float32, torch.bfloat16)]
+                         + [(torch.bfloat16, c) for c in CONVS_DEEP])
 def test_conv_fwd_dgrad_wgrad(cfg, dtype):
     L = _L()
     B, Ci, H, W, Co, k, s, p = cfg
@@ -78,7 +90,7 @@ def test_conv_fwd_dgrad_wgrad(cfg, dtype):
     st = L.stream_ptr()
     L.call("crnn_pack_conv_weight", dt, w.to(DEV).data_ptr(), wd.data_ptr(), Co, Ci, k[0], k[1], Cip, st)
     yd = torch.empty(B, Ho, Wo, Co, dtype=dtype, device=DEV)
-    rows = L.lib().crnn_conv_stat_rows(d)
+    rows = L.lib().crnn_conv_stat_rows(dt, d)
     ps = torch.empty(rows, Co, device=DEV)
     pq = torch.empty(rows, Co, device=DEV)
     L.call("crnn_conv_fwd", dt, d, xd.data_ptr(), wd.data_ptr(), yd.data_ptr(), ps.data_ptr(), pq.data_ptr(), st)
@@ -89,6 +101,15 @@ def test_conv_fwd_dgrad_wgrad(cfg, dtype):
     ssum = ps.sum(0).cpu().double()
     ref_sum = y_ref.sum(dim=(0, 2, 3)).double()
     assert float((ssum - ref_sum).abs().max()) < 1e-3 * float(y_ref.abs().sum() / Co + 1)
+    # (sum, M2) partials of rows_per_partial rows each -> population variance (Chan combine)
+    rpp = L.lib().crnn_conv_stat_rows_per_partial(dt, d)
+    Mrows = B * Ho * Wo
+    n = torch.tensor([min(rpp, max(0, Mrows - i * rpp)) for i in range(rows)], dtype=torch.float64)[:, None]
+    ps64, pq64 = ps.cpu().double(), pq.cpu().double()
+    mean = ps64.sum(0) / Mrows
+    pm = torch.where(n > 0, ps64 / n.clamp(min=1), mean)
+    var = (pq64.sum(0) + (n * (pm - mean) ** 2).sum(0)) / Mrows
+    assert relerr(var, y_ref.double().var(dim=(0, 2, 3), unbiased=False)) < (1e-5 if dtype == torch.float32 else 1e-2)
     # dgrad
     dyd = to_nhwc(dy, None, dtype)
     if Ci % 8 == 0:
@@ -97,7 +118,7 @@ def test_conv_fwd_dgrad_wgrad(cfg, dtype):
         dx = dxd.float().permute(0, 3, 1, 2).cpu()
         assert relerr(dx, xr.grad) < tol
     # wgrad
-    need = L.lib().crnn_conv_wgrad_workspace(d)
+    need = L.lib().crnn_conv_wgrad_workspace(dt, d)
     ws = torch.empty(need // 4 + 1, device=DEV)
     dw = torch.full((Co, Ci, k[0], k[1]), 7.0, device=DEV)
     L.call("crnn_conv_wgrad", dt, d, dyd.data_ptr(), xd.data_ptr(), dw.data_ptr(), ws.data_ptr(), need, 0.0, st)

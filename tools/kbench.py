@@ -54,10 +54,10 @@ def main():
         y = torch.empty(a.batch, d.Ho, d.Wo, cs.co, device=dev, dtype=T)
         dy = torch.randn_like(y)
         dx = torch.empty_like(x)
-        rows = L.lib().crnn_conv_stat_rows(d)
+        rows = L.lib().crnn_conv_stat_rows(L.BF16, d)
         ps = torch.empty(rows, cs.co, device=dev)
         pq = torch.empty(rows, cs.co, device=dev)
-        need = L.lib().crnn_conv_wgrad_workspace(d)
+        need = L.lib().crnn_conv_wgrad_workspace(L.BF16, d)
         ws = torch.empty(need // 4 + 1, device=dev)
         dw = torch.empty(cs.co, cs.ci_real, cs.kh, cs.kw, device=dev)
         flop = 2.0 * a.batch * d.Ho * d.Wo * cs.co * cs.ci_real * cs.kh * cs.kw
