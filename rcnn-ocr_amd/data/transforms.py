@@ -84,3 +84,16 @@ def ctc_targets(texts: Sequence[str], stoi: Dict[str, int], max_len: int) -> Tup
         if r:
             out[i, :len(r)] = torch.tensor(r)
     return out, torch.tensor([len(r) for r in ids], dtype=torch.long)
+
+
+def decode_tokens(ids, itos, pad_id, eos_id, blank_id=None) -> str:
+    """data/transforms.py:196-206: stop at EOS, skip PAD / BLANK, join the rest."""
+    out = []
+    for t in ids:
+        t = int(t)
+        if t == eos_id:
+            break
+        if t == pad_id or (blank_id is not None and t == blank_id):
+            continue
+        out.append(itos[t])
+    return "".join(out)

@@ -1,0 +1,91 @@
+"""OCRInference — the reference's inference.py:12-195 API on the MI355X CTC path.
+
+Same constructor arguments, checkpoint formats and predict() contract (single image -> str,
+list -> list, optional (text, confidence)). The head is CTC, so decoding is the
+greedy CTC collapse (repeats merged, blank = id 0 = <PAD> dropped) done by the HIP greedy
+kernel; confidence = mean max-softmax over the emitted frames. Images go through
+data.transforms.get_val_transform (aspect-preserving resize onto a white canvas, (x-0.5)/0.5).
+"""
+from __future__ import annotations
+
+import os
+from typing import List, Union
+
+import numpy as np
+import torch
+
+from crnn_hip.ctc import ctc_greedy_decode
+from data.transforms import get_val_transform, load_charset
+from model.model import RCNN
+
+
+class OCRInference:
+    def __init__(self, model_path: str, charset_path: str, device: str = "auto", img_h: int = 64,
+                 img_w: int = 256, compute_dtype: torch.dtype = torch.bfloat16):
+        self.model_path, self.charset_path = model_path, charset_path
+        self.img_h, self.img_w = img_h, img_w
+        if device == "auto":
+            device = "cuda" if torch.cuda.is_available() else "cpu"
+        self.device = torch.device(device)
+        self.itos, self.stoi = load_charset(charset_path)
+        self.pad_id = self.stoi["<PAD>"]
+        self.sos_id = self.stoi["<SOS>"]
+        self.eos_id = self.stoi["<EOS>"]
+        self.blank_id = self.stoi.get("<BLANK>", None)
+        self.compute_dtype = compute_dtype
+        self.transform = get_val_transform(img_h, img_w)
+        self.model = self._load_model()
+
+    def _load_model(self) -> RCNN:
+        ckpt = torch.load(self.model_path, map_location="cpu", weights_only=True)
+        if isinstance(ckpt, dict) and "config" in ckpt:
+            hidden = ckpt["config"].get("hidden_size", 256)
+            state = ckpt["model_state"]
+        elif isinstance(ckpt, dict) and "model_state_dict" in ckpt:
+            hidden = ckpt.get("hidden_size", 256)
+            state = ckpt["model_state_dict"]
+        else:
+            hidden, state = 256, ckpt
+        model = RCNN(num_classes=len(self.itos), hidden_size=hidden, sos_id=self.sos_id, eos_id=self.eos_id,
+                     pad_id=self.pad_id, blank_id=self.blank_id, compute_dtype=self.compute_dtype)
+        state = {k: v for k, v in state.items() if not k.startswith("attn.")}
+        model.load_state_dict(state, strict=any(k.startswith("ctc_head.") for k in state))
+        return model.to(self.device).eval()
+
+    def _preprocess_image(self, image) -> torch.Tensor:
+        from PIL import Image
+        if isinstance(image, str):
+            if not os.path.exists(image):
+                raise FileNotFoundError(f"Image file not found: {image}")
+            img = np.asarray(Image.open(image).convert("RGB"))
+        elif isinstance(image, Image.Image):
+            img = np.asarray(image.convert("RGB"))
+        elif isinstance(image, np.ndarray):
+            img = image
+        else:
+            raise ValueError(f"Unsupported image type: {type(image)}")
+        return self.transform(image=img)["image"]
+
+    @torch.no_grad()
+    def predict(self, images: Union[np.ndarray, str, "Image.Image", List], max_length: int = 25, batch_size: int = 32,
+                return_confidence: bool = False):
+        single = not isinstance(images, list)
+        items = [images] if single else images
+        results = []
+        for i in range(0, len(items), batch_size):
+            batch = torch.stack([self._preprocess_image(im) for im in items[i:i + batch_size]]).to(self.device)
+            logits = self.model(batch, is_train=False, batch_max_length=max_length)   # [B, T, C]
+            seqs = ctc_greedy_decode(logits)
+            if return_confidence:
+                probs = torch.softmax(logits.float(), dim=-1).max(dim=-1)
+                best, arg = probs.values.cpu(), probs.indices.cpu()
+            for j, seq in enumerate(seqs):
+                text = "".join(self.itos[t] for t in seq[:max_length])
+                if return_confidence:
+                    a = arg[j]
+                    keep = (a != 0) & torch.cat([torch.ones(1, dtype=torch.bool), a[1:] != a[:-1]])
+                    conf = float(best[j][keep].mean()) if bool(keep.any()) else 0.0
+                    results.append((text, conf))
+                else:
+                    results.append(text)
+        return results[0] if single else results
