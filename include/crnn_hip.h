@@ -57,6 +57,26 @@ int crnn_pack_conv_weight(int dtype, const float* w, void* out, int Co, int Ci, 
  * Used for LSTM gate interleave (row 4*j+gate <- gate*H+j) and padded heads. */
 int crnn_pack_rows(int dtype, const float* src, void* out, const int* perm, int rows_out, int rows_src, int cols, void* stream);
 
+/* Batched packing: every job of a DEVICE-resident table in one launch (the per-step re-pack of
+ * all weights after an optimizer step). kind CRNN_PACK_CONV: src OIHW -> dst OHWI(Cip),
+ * (a,b,c,d,e) = (Co,Ci,KH,KW,Cip); CRNN_PACK_ROWS: crnn_pack_rows with (a,b,c) = (rows_out,
+ * rows_src, cols); CRNN_PACK_ROWS_SUM: the same with src2 added (LSTM b_ih + b_hh). out_f32
+ * selects an fp32 destination instead of dtype. start = first element of the job in the
+ * concatenation (jobs in order, start[0] = 0); total = all elements. */
+#define CRNN_PACK_CONV 0
+#define CRNN_PACK_ROWS 1
+#define CRNN_PACK_ROWS_SUM 2
+typedef struct {
+  int kind, out_f32;
+  int a, b, c, d, e, pad_;
+  long start;
+  const float* src;
+  const float* src2;
+  const int* perm;
+  void* dst;
+} crnn_pack_job;
+int crnn_pack_batch(int dtype, const crnn_pack_job* jobs, int njobs, long total, void* stream);
+
 /* ------------------------------------------------------------------ conv */
 typedef struct {
   int B, Hi, Wi, Ci; /* Ci: stored (padded) input channels */
@@ -145,7 +165,8 @@ int crnn_se_bwd_reduce(int dtype, const void* dy, const void* y, const void* z2,
                        float* ds, int B, int HW, int C, void* stream);
 /* SE MLP backward: dsig, dhid (work [B][C] and [B][Cr]), dpool = W1^T dhid / HW; dw1/dw2 (fp32, written) */
 int crnn_se_mlp_bwd(const float* ds, const float* pooled, const float* hid, const float* s, const float* w1, const float* w2,
-                    float* dsig, float* dhid, float* dpool, float* dw1, float* dw2, int B, int C, int Cr, int HW, void* stream);
+                    float* dsig, float* dhid, float* dpool, float* dw1, float* dw2, int B, int C, int Cr, int HW, int accumulate,
+                    void* stream);
 
 /* ------------------------------------------------------------------ height collapse */
 /* seq[b][w][c] = mean_h relu(z*scale+shift), z [B][Hh][W][C] */
@@ -179,11 +200,14 @@ int crnn_lstm_step_fwd(int dtype, const void* xg, const void* whh, void* hseq, v
 int crnn_lstm_step_bwd(int dtype, const void* dhseq, const void* whh, const void* gsv, const float* csv, void* dgates,
                        float* dc, int B, int T, int H, int step, void* stream);
 /* dW_hh (reference row order, fp32 [2][4H][H]) (+)= sum_t dgates_t^T h_{t-1} */
-int crnn_lstm_dwhh(int dtype, const void* dgates, const void* hseq, float* dwhh, int B, int T, int H, int accumulate, void* stream);
+int crnn_lstm_dwhh(int dtype, const void* dgates, const void* hseq, float* dwhh_fwd, float* dwhh_rev, int B, int T, int H, int accumulate, void* stream);
 /* dW_ih (reference row order, fp32 [2][4H][In]) (+)= sum dgates^T x ; x [B][T][In] */
-int crnn_lstm_dwih(int dtype, const void* dgates, const void* x, float* dwih, int B, int T, int H, int In, int accumulate, void* stream);
+int crnn_lstm_dwih(int dtype, const void* dgates, const void* x, float* dwih_fwd, float* dwih_rev, int B, int T, int H, int In, int accumulate, void* stream);
 /* db (reference order, fp32 [2][4H]) (+)= sum_{t,b} dgates */
-int crnn_lstm_dbias(int dtype, const void* dgates, float* db, int B, int T, int H, int accumulate, void* stream);
+/* bias gradient of each direction into both b_ih and b_hh (they receive the same gradient; b2_* may be NULL);
+ * ws: crnn_lstm_dbias_workspace(H) bytes; deterministic (no atomics) */
+int crnn_lstm_dbias(int dtype, const void* dgates, float* b_fwd, float* b2_fwd, float* b_rev, float* b2_rev, float* ws, int B, int T, int H, int accumulate, void* stream);
+size_t crnn_lstm_dbias_workspace(int H);
 /* dx [B][T][In] (dtype) = sum_dir dgates . W_ih'  (wih packed [2][4H][In]) */
 int crnn_lstm_dx(int dtype, const void* dgates, const void* wih, void* dx, int B, int T, int H, int In, void* stream);
 

@@ -37,7 +37,16 @@ class BnBwdDesc(C.Structure):
                 ("C", C.c_int), ("HW", C.c_int)]
 
 
+class PackJob(C.Structure):  # crnn_pack_job
+    _fields_ = [("kind", C.c_int), ("out_f32", C.c_int), ("a", C.c_int), ("b", C.c_int), ("c", C.c_int),
+                ("d", C.c_int), ("e", C.c_int), ("pad_", C.c_int), ("start", C.c_long), ("src", vp),
+                ("src2", vp), ("perm", vp), ("dst", vp)]
+
+
+PACK_CONV, PACK_ROWS, PACK_ROWS_SUM = 0, 1, 2
+
 _SIGS = {
+    "crnn_pack_batch": ([i32, vp, i32, i64, vp], i32),
     "crnn_version": ([], i32),
     "crnn_last_error_string": ([], C.c_char_p),
     "crnn_nchw_to_nhwc": ([i32, vp, vp, i32, i32, i32, i32, i32, vp], i32),
@@ -64,7 +73,7 @@ _SIGS = {
     "crnn_se_mlp_fwd": ([vp, vp, vp, vp, vp, i32, i32, i32, vp], i32),
     "crnn_se_residual_fwd": ([i32, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, vp], i32),
     "crnn_se_bwd_reduce": ([i32, vp, vp, vp, vp, vp, vp, i32, i32, i32, vp], i32),
-    "crnn_se_mlp_bwd": ([vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, vp], i32),
+    "crnn_se_mlp_bwd": ([vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, vp], i32),
     "crnn_hpool_fwd": ([i32, vp, vp, vp, vp, i32, i32, i32, i32, vp], i32),
     "crnn_hpool_bwd": ([i32, vp, vp, i32, i32, i32, i32, vp], i32),
     "crnn_gemm_nt": ([i32, vp, i32, vp, i32, vp, i32, vp, i32, i32, i32, i32, i32, vp], i32),
@@ -73,9 +82,10 @@ _SIGS = {
     "crnn_colsum": ([i32, vp, i32, i64, i32, vp, i32, i32, vp], i32),
     "crnn_lstm_step_fwd": ([i32, vp, vp, vp, vp, vp, i32, i32, i32, i32, vp], i32),
     "crnn_lstm_step_bwd": ([i32, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, vp], i32),
-    "crnn_lstm_dwhh": ([i32, vp, vp, vp, i32, i32, i32, i32, vp], i32),
-    "crnn_lstm_dwih": ([i32, vp, vp, vp, i32, i32, i32, i32, i32, vp], i32),
-    "crnn_lstm_dbias": ([i32, vp, vp, i32, i32, i32, i32, vp], i32),
+    "crnn_lstm_dwhh": ([i32, vp, vp, vp, vp, i32, i32, i32, i32, vp], i32),
+    "crnn_lstm_dwih": ([i32, vp, vp, vp, vp, i32, i32, i32, i32, i32, vp], i32),
+    "crnn_lstm_dbias": ([i32, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, vp], i32),
+    "crnn_lstm_dbias_workspace": ([i32], sz),
     "crnn_lstm_dx": ([i32, vp, vp, vp, i32, i32, i32, i32, vp], i32),
     "crnn_ctc_loss": ([vp, i32, i32, i32, i32, vp, i32, vp, vp, vp, i32, vp], i32),
     "crnn_ctc_reduce_mean": ([vp, vp, i32, vp, vp], i32),

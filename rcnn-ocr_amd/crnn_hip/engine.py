@@ -139,6 +139,7 @@ class CRNNEngine:
         self.packed: Dict[str, torch.Tensor] = {}
         self.perm = torch.tensor(gate_perm(hidden), dtype=torch.int32, device=self.device)
         self.packed_version = None
+        self._pack_jobs = None
         self.version = 0
         # in-place edits of the parameters (torch optimizers, load_state_dict) bump the
         # flat buffer's version counter; kernel-side updates call mark_params_changed()
@@ -163,20 +164,30 @@ class CRNNEngine:
         yield self.co1
 
     def pack(self):
-        """fp32 reference-layout parameters -> compute-dtype kernel layouts."""
+        """fp32 reference-layout parameters -> compute-dtype kernel layouts: every weight in one
+        crnn_pack_batch launch (job table built once; all pointers are persistent views)."""
         ver = (self.version, self.version_source() if self.version_source is not None else 0)
         if self.packed_version == ver:
             return
-        s = L.stream_ptr()
-        dt, T = self.dt, self.dtype
+        if self._pack_jobs is None:
+            self._build_pack_jobs()
+        jobs, n, total = self._pack_jobs
+        call("crnn_pack_batch", self.dt, ptr(jobs), n, total, L.stream_ptr())
+        self.packed_version = ver
+
+    def _build_pack_jobs(self):
+        T, H = self.dtype, self.H
+        jobs = []
+
+        def job(kind, src, dst, a, b, c, d=0, e=0, out_f32=False, perm=None, src2=None):
+            jobs.append(L.PackJob(kind, 1 if out_f32 else 0, a, b, c, d, e, 0, 0, ptr(src), ptr(src2), ptr(perm),
+                                  ptr(dst)))
+            return dst.numel()
+
+        sizes = []
         for cs in self.convs():
-            w = self.p[cs.name]
-            out = self.packed.get(cs.name)
-            if out is None:
-                out = torch.empty((cs.co, cs.kh, cs.kw, cs.ci), dtype=T, device=self.device)
-                self.packed[cs.name] = out
-            call("crnn_pack_conv_weight", dt, ptr(w), ptr(out), cs.co, cs.ci_real, cs.kh, cs.kw, cs.ci, s)
-        H = self.H
+            out = self._pbuf(cs.name, (cs.co, cs.kh, cs.kw, cs.ci), T)
+            sizes.append(job(L.PACK_CONV, self.p[cs.name], out, cs.co, cs.ci_real, cs.kh, cs.kw, cs.ci))
         for l in range(self.nl):
             pre = f"enc_rnn.{l}"
             ind = self.enc_dim if l == 0 else H
@@ -185,19 +196,25 @@ class CRNNEngine:
             bias = self._pbuf(pre + ".bias", (2, 4 * H), torch.float32)
             for d, sfx in enumerate(["", "_reverse"]):
                 r = pre + ".rnn."
-                call("crnn_pack_rows", dt, ptr(self.p[r + "weight_ih_l0" + sfx]), ptr(wih[d]), ptr(self.perm),
-                     4 * H, 4 * H, ind, s)
-                call("crnn_pack_rows", dt, ptr(self.p[r + "weight_hh_l0" + sfx]), ptr(whh[d]), ptr(self.perm),
-                     4 * H, 4 * H, H, s)
-                bsum = self.p[r + "bias_ih_l0" + sfx] + self.p[r + "bias_hh_l0" + sfx]
-                call("crnn_pack_rows", L.F32, ptr(bsum), ptr(bias[d]), ptr(self.perm), 4 * H, 4 * H, 1, s)
+                sizes.append(job(L.PACK_ROWS, self.p[r + "weight_ih_l0" + sfx], wih[d], 4 * H, 4 * H, ind,
+                                 perm=self.perm))
+                sizes.append(job(L.PACK_ROWS, self.p[r + "weight_hh_l0" + sfx], whh[d], 4 * H, 4 * H, H,
+                                 perm=self.perm))
+                sizes.append(job(L.PACK_ROWS_SUM, self.p[r + "bias_ih_l0" + sfx], bias[d], 4 * H, 4 * H, 1,
+                                 out_f32=True, perm=self.perm, src2=self.p[r + "bias_hh_l0" + sfx]))
             lw = self._pbuf(pre + ".lin", (H, 2 * H), T)
-            call("crnn_cast_f32", dt, ptr(self.p[pre + ".linear.weight"]), ptr(lw), H * 2 * H, s)
+            sizes.append(job(L.PACK_ROWS, self.p[pre + ".linear.weight"], lw, H, H, 2 * H))
         hw = self._pbuf("head.w", (self.Cpad, H), T)
-        call("crnn_pack_rows", dt, ptr(self.p["ctc_head.weight"]), ptr(hw), None, self.Cpad, self.C, H, s)
-        hb = self._pbuf("head.b", (self.Cpad,), torch.float32, zero=True)
-        hb[: self.C].copy_(self.p["ctc_head.bias"])
-        self.packed_version = ver
+        sizes.append(job(L.PACK_ROWS, self.p["ctc_head.weight"], hw, self.Cpad, self.C, H))
+        hb = self._pbuf("head.b", (self.Cpad,), torch.float32)
+        sizes.append(job(L.PACK_ROWS, self.p["ctc_head.bias"], hb, self.Cpad, self.C, 1, out_f32=True))
+        start = 0
+        for jb, n in zip(jobs, sizes):
+            jb.start = start
+            start += n
+        arr = (L.PackJob * len(jobs))(*jobs)
+        raw = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(self.device)
+        self._pack_jobs = (raw, len(jobs), start)
 
     # ------------------------------------------------------------------ instrumentation
     def enable_timing(self, on: bool = True):
@@ -255,7 +272,7 @@ class CRNNEngine:
         if train and self.update_running:
             nbt = self.buf.get(prefix + ".num_batches_tracked")
             if nbt is not None:
-                nbt.add_(1)
+                self._nbt.append(nbt)
         return mean, inv, sc, sh
 
     def _fin_ws(self):
@@ -318,6 +335,7 @@ class CRNNEngine:
         ws, dt, T = self.ws, self.dt, self.dtype
         s = L.stream_ptr()
         self._stat_cap = self._stat_capacity(B, H, W) if train else 0
+        self._nbt = []
         sv = {}
 
         x0 = ws.get("in", (B, H, W, 8), T)
@@ -376,6 +394,8 @@ class CRNNEngine:
         call("crnn_hpool_fwd", dt, ptr(zc1), ptr(cs1), ptr(ch1), ptr(seq), B, h3, w3, 512, s)
         sv["co"] = dict(x=x, h=h, w=w, z0=zc0, m0=cm0, i0=ci0, sc0=cs0, sh0=ch0, a0=ac0, h2=h2, w2=w2, z1=zc1,
                         m1=cm1, i1=ci1, sc1=cs1, sh1=ch1, h3=h3, w3=w3)
+        if self._nbt:
+            torch._foreach_add_(self._nbt, 1)   # BN num_batches_tracked, one launch
         # BiLSTM stack (model/model.py:195-198)
         Hd = self.H
         xin = seq
@@ -522,18 +542,16 @@ class CRNNEngine:
             for stp in range(Tn):
                 call("crnn_lstm_step_bwd", dt, ptr(dh), ptr(whh), ptr(r["gates"]), ptr(r["c"]), ptr(dg), ptr(dc),
                      B, Tn, Hd, stp, s)
-            dwhh = ws.get("rnn.dwhh", (2, 4 * Hd, Hd), torch.float32)
-            call("crnn_lstm_dwhh", dt, ptr(dg), ptr(r["hseq"]), ptr(dwhh), B, Tn, Hd, 0, s)
-            dwih = ws.get(f"rnn.dwih{ind}", (2, 4 * Hd, ind), torch.float32)
-            call("crnn_lstm_dwih", dt, ptr(dg), ptr(r["x"]), ptr(dwih), B, Tn, Hd, ind, 0, s)
-            db = ws.get("rnn.db", (2, 4 * Hd), torch.float32)
-            call("crnn_lstm_dbias", dt, ptr(dg), ptr(db), B, Tn, Hd, 0, s)
-            for d, sfx in enumerate(["", "_reverse"]):
-                rr = pre + ".rnn."
-                self._store_grad(rr + "weight_hh_l0" + sfx, dwhh[d], accumulate)
-                self._store_grad(rr + "weight_ih_l0" + sfx, dwih[d], accumulate)
-                self._store_grad(rr + "bias_ih_l0" + sfx, db[d], accumulate)
-                self._store_grad(rr + "bias_hh_l0" + sfx, db[d], accumulate)
+            rr = pre + ".rnn."
+            gq = lambda n: ptr(self._gview(rr + n))
+            # gradients straight into the parameters' .grad views (reference row order)
+            call("crnn_lstm_dwhh", dt, ptr(dg), ptr(r["hseq"]), gq("weight_hh_l0"), gq("weight_hh_l0_reverse"),
+                 B, Tn, Hd, acc, s)
+            call("crnn_lstm_dwih", dt, ptr(dg), ptr(r["x"]), gq("weight_ih_l0"), gq("weight_ih_l0_reverse"),
+                 B, Tn, Hd, ind, acc, s)
+            dbws = ws.get("rnn.dbws", (L.lib().crnn_lstm_dbias_workspace(Hd) // 4,), torch.float32)
+            call("crnn_lstm_dbias", dt, ptr(dg), gq("bias_ih_l0"), gq("bias_hh_l0"), gq("bias_ih_l0_reverse"),
+                 gq("bias_hh_l0_reverse"), ptr(dbws), B, Tn, Hd, acc, s)
             nxt = ws.get(f"rnn.dx_l{l}", (B, Tn, ind), T)
             call("crnn_lstm_dx", dt, ptr(dg), ptr(self.packed[pre + ".wih"]), ptr(nxt), B, Tn, Hd, ind, s)
             dx = nxt
@@ -587,13 +605,10 @@ class CRNNEngine:
             dsig = ws.get(f"se.dsig{P}", (B, P), torch.float32)
             dhid = ws.get(f"se.dhid{P}", (B, Cr), torch.float32)
             dpool = ws.get(f"se.dpool{P}", (B, P), torch.float32)
-            dw1 = ws.get(f"se.dw1{P}", (Cr, P), torch.float32)
-            dw2 = ws.get(f"se.dw2{P}", (P, Cr), torch.float32)
             call("crnn_se_mlp_bwd", ptr(ds), ptr(sb["pooled"]), ptr(sb["hid"]), ptr(sb["s"]),
                  ptr(self.p[blk.prefix + ".se.fc.0.weight"]), ptr(self.p[blk.prefix + ".se.fc.2.weight"]),
-                 ptr(dsig), ptr(dhid), ptr(dpool), ptr(dw1), ptr(dw2), B, P, Cr, HW, s)
-            self._store_grad(blk.prefix + ".se.fc.0.weight", dw1, accumulate)
-            self._store_grad(blk.prefix + ".se.fc.2.weight", dw2, accumulate)
+                 ptr(dsig), ptr(dhid), ptr(dpool), ptr(self._gview(blk.prefix + ".se.fc.0.weight")),
+                 ptr(self._gview(blk.prefix + ".se.fc.2.weight")), B, P, Cr, HW, acc, s)
             dz2 = bufs[o1][: Mo * P]
             self._bn_bwd(3, dyb, sb["z2"], (sb["m2"], sb["i2"], sb["sc2"], sb["sh2"]), blk.conv2.bn, Mo, P, HW=HW,
                          y=sb["y"], se=sb["s"], dpool=dpool, out=dz2, accumulate_params=accumulate)
@@ -647,6 +662,13 @@ class CRNNEngine:
         st = sv["stem"]
         B = sv["B"]
         return B * st["h1"] * st["w1"] * 128
+
+    def _gview(self, name):
+        """the .grad tensor a kernel writes into directly (contiguous fp32 on the device)."""
+        g = self.g[name]
+        if g.dtype != torch.float32 or not g.is_contiguous() or g.device != self.device:
+            raise ValueError(f"gradient buffer for {name} must be a contiguous fp32 tensor on {self.device}")
+        return g
 
     def _store_grad(self, name, src, accumulate):
         g = self.g[name]

@@ -41,7 +41,12 @@ class FusedAdamW(torch.optim.Optimizer):
         m.mark_params_changed()
         return loss
 
-    def zero_grad(self, set_to_none: bool = False):
-        # gradients live in the flat buffer and are overwritten by the next backward
-        if self.model._flat_grad is not None and not set_to_none:
+    def zero_grad(self, set_to_none: bool = True):
+        """torch semantics. set_to_none: .grad becomes None and the next backward re-attaches the
+        flat-buffer views and OVERWRITES them (no memset); otherwise the flat buffer is zeroed and
+        the next backward accumulates into it."""
+        if set_to_none:
+            for p in self.model.parameters():
+                p.grad = None
+        elif self.model._flat_grad is not None:
             self.model._flat_grad.zero_()

@@ -431,7 +431,7 @@ __global__ void se_mlp_bwd_kernel(const float* __restrict__ ds, const float* __r
 __global__ __launch_bounds__(256) void se_wgrad_kernel(const float* __restrict__ dsig, const float* __restrict__ hid,
                                                        const float* __restrict__ dhid,
                                                        const float* __restrict__ pooled, float* __restrict__ dw1,
-                                                       float* __restrict__ dw2, int B, int C, int Cr) {
+                                                       float* __restrict__ dw2, int B, int C, int Cr, int accumulate) {
   __shared__ float red[2][4][64];
   const int lc = threadIdx.x & 63, ln = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lc, r = blockIdx.y;
@@ -445,8 +445,12 @@ __global__ __launch_bounds__(256) void se_wgrad_kernel(const float* __restrict__
   red[1][ln][lc] = a1;
   __syncthreads();
   if (ln != 0 || c >= C) return;
-  dw2[(size_t)c * Cr + r] = red[0][0][lc] + red[0][1][lc] + red[0][2][lc] + red[0][3][lc];
-  dw1[(size_t)r * C + c] = red[1][0][lc] + red[1][1][lc] + red[1][2][lc] + red[1][3][lc];
+  const float v2 = red[0][0][lc] + red[0][1][lc] + red[0][2][lc] + red[0][3][lc];
+  const float v1 = red[1][0][lc] + red[1][1][lc] + red[1][2][lc] + red[1][3][lc];
+  float* p2 = dw2 + (size_t)c * Cr + r;
+  float* p1 = dw1 + (size_t)r * C + c;
+  *p2 = accumulate ? *p2 + v2 : v2;
+  *p1 = accumulate ? *p1 + v1 : v1;
 }
 
 // ------------------------------------------------------------ height collapse
@@ -537,6 +541,52 @@ __global__ void pack_rows_kernel(const float* __restrict__ src, T* __restrict__ 
     int sr = perm ? perm[r] : r;
     float v = (r < rows_src && sr >= 0) ? src[(size_t)sr * cols + c] : 0.f;
     o[i] = fromf<T>(v);
+  }
+}
+
+// all pack jobs in one launch: block b owns elements [b*chunk, (b+1)*chunk) of the concatenation
+// and walks the (start-sorted) job table from the job holding its first element
+template <typename T>
+__global__ __launch_bounds__(256) void pack_batch_kernel(const crnn_pack_job* __restrict__ jobs, int njobs, long total,
+                                                         long chunk) {
+  const long e0 = blockIdx.x * chunk, e1 = min(total, e0 + chunk);
+  if (e0 >= e1) return;
+  int lo = 0, hi = njobs - 1;
+  while (lo < hi) {  // last job with start <= e0
+    const int mid = (lo + hi + 1) >> 1;
+    if (jobs[mid].start <= e0) lo = mid;
+    else hi = mid - 1;
+  }
+  for (int j = lo; j < njobs; ++j) {
+    const crnn_pack_job jb = jobs[j];
+    const long jend = j + 1 < njobs ? jobs[j + 1].start : total;
+    const long a0 = max(e0, jb.start), a1 = min(e1, jend);
+    if (a0 >= a1) {
+      if (jb.start >= e1) break;
+      continue;
+    }
+    for (long g = a0 + threadIdx.x; g < a1; g += blockDim.x) {
+      const long i = g - jb.start;
+      float v;
+      if (jb.kind == CRNN_PACK_CONV) {
+        const int Ci = jb.b, KH = jb.c, KW = jb.d, Cip = jb.e;
+        const int ci = (int)(i % Cip);
+        long t = i / Cip;
+        const int kw = (int)(t % KW);
+        t /= KW;
+        const int kh = (int)(t % KH), co = (int)(t / KH);
+        v = ci < Ci ? jb.src[(((size_t)co * Ci + ci) * KH + kh) * KW + kw] : 0.f;
+      } else {
+        const int cols = jb.c;
+        const int r = (int)(i / cols), c = (int)(i - (long)r * cols);
+        const int sr = jb.perm ? jb.perm[r] : r;
+        const bool ok = r < jb.b && sr >= 0;
+        v = ok ? jb.src[(size_t)sr * cols + c] : 0.f;
+        if (jb.kind == CRNN_PACK_ROWS_SUM && ok) v += jb.src2[(size_t)sr * cols + c];
+      }
+      if (jb.out_f32) ((float*)jb.dst)[i] = v;
+      else ((T*)jb.dst)[i] = fromf<T>(v);
+    }
   }
 }
 
@@ -986,12 +1036,12 @@ int crnn_se_bwd_reduce(int dtype, const void* dy, const void* y, const void* z2,
 
 int crnn_se_mlp_bwd(const float* ds, const float* pooled, const float* hid, const float* s, const float* w1,
                     const float* w2, float* dsig, float* dhid, float* dpool, float* dw1, float* dw2, int B, int C,
-                    int Cr, int HW, void* stream) {
+                    int Cr, int HW, int accumulate, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(se_mlp_bwd_kernel, dim3(B), dim3(256), (C + Cr) * sizeof(float), st, ds, hid, s, w1, w2, dsig,
                      dhid, dpool, C, Cr, 1.f / (float)HW);
   hipLaunchKernelGGL(se_wgrad_kernel, dim3((C + 63) / 64, Cr), dim3(256), 0, st, dsig, hid, dhid, pooled, dw1, dw2, B,
-                     C, Cr);
+                     C, Cr, accumulate);
   return (int)hipGetLastError();
 }
 
@@ -1027,6 +1077,16 @@ int crnn_pack_conv_weight(int dtype, const float* w, void* out, int Co, int Ci, 
   long n = (long)Co * KH * KW * Cip;
   DISPATCH(dtype, hipLaunchKernelGGL(pack_conv_kernel<T>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, w,
                                      (T*)out, Co, Ci, KH, KW, Cip));
+  return (int)hipGetLastError();
+}
+
+int crnn_pack_batch(int dtype, const crnn_pack_job* jobs, int njobs, long total, void* stream) {
+  if (njobs <= 0 || total <= 0) return 0;
+  long blocks = (total + 4095) / 4096;
+  if (blocks > 8192) blocks = 8192;
+  const long chunk = (total + blocks - 1) / blocks;
+  DISPATCH(dtype, hipLaunchKernelGGL(pack_batch_kernel<T>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
+                                     jobs, njobs, total, chunk));
   return (int)hipGetLastError();
 }
 

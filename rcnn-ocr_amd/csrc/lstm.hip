@@ -226,9 +226,11 @@ int gate_wgrad(const T* dgates_d, const LB& lb, float* out, int B, int Tn, int H
   return launch<T, 64, 64>(la, lb, ep, 4 * H, N, K, splits, st);
 }
 
-// db[d][q*H+j] = sum_k dgates[d][k][4j+q]
+// db[d][q*H+j] = sum_k dgates[d][k][4j+q], two deterministic stages:
+// partials ws[chunk][d][gp] over row chunks, then a fixed-order sum scattered to reference rows
+constexpr int DB_CHUNKS = 64;
 template <typename T>
-__global__ void dbias_kernel(const T* __restrict__ dg, float* __restrict__ db, int K, int H, long rpc) {
+__global__ void dbias_part_kernel(const T* __restrict__ dg, float* __restrict__ ws, int K, int H, long rpc) {
   __shared__ float red[4][64];
   const int c = threadIdx.x & 63, r = threadIdx.x >> 6;
   const int H4 = 4 * H, d = blockIdx.z;
@@ -240,10 +242,23 @@ __global__ void dbias_kernel(const T* __restrict__ dg, float* __restrict__ db, i
     for (long k = k0 + r; k < k1; k += 4) s += tof(p[k * H4 + gp]);
   red[r][c] = s;
   __syncthreads();
-  if (r == 0 && gp < H4) {
-    int row = (gp & 3) * H + (gp >> 2);
-    atomicAdd(db + (size_t)d * H4 + row, red[0][c] + red[1][c] + red[2][c] + red[3][c]);
-  }
+  if (r == 0 && gp < H4)
+    ws[((size_t)blockIdx.y * 2 + d) * H4 + gp] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+}
+
+__global__ void dbias_fin_kernel(const float* __restrict__ ws, int chunks, int H, float* bf, float* b2f, float* br,
+                                 float* b2r, int accumulate) {
+  const int H4 = 4 * H;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 2 * H4) return;
+  const int d = i / H4, gp = i - d * H4;
+  float s = 0.f;
+  for (int c = 0; c < chunks; ++c) s += ws[((size_t)c * 2 + d) * H4 + gp];
+  const int row = (gp & 3) * H + (gp >> 2);
+  float* o1 = d ? br : bf;
+  float* o2 = d ? b2r : b2f;
+  o1[row] = accumulate ? o1[row] + s : s;
+  if (o2) o2[row] = accumulate ? o2[row] + s : s;
 }
 
 // dx: A rows m = b*T + t, k = (d, g') -> dgates[(d*T + t)*B + b][g']
@@ -301,12 +316,12 @@ int crnn_lstm_step_bwd(int dtype, const void* dhseq, const void* whh, const void
                             : step_bwd_t<float>(dhseq, whh, gsv, csv, dgates, dc, B, T, H, step, st);
 }
 
-int crnn_lstm_dwhh(int dtype, const void* dgates, const void* hseq, float* dwhh, int B, int T, int H, int accumulate,
-                   void* stream) {
+int crnn_lstm_dwhh(int dtype, const void* dgates, const void* hseq, float* dwhh_f, float* dwhh_r, int B, int T, int H,
+                   int accumulate, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   for (int d = 0; d < 2; ++d) {
     size_t off = (size_t)d * T * B * 4 * H;
-    float* out = dwhh + (size_t)d * 4 * H * H;
+    float* out = d ? dwhh_r : dwhh_f;
     int rc = dtype == CRNN_BF16
                  ? gate_wgrad<bf16>((const bf16*)dgates + off, HPrevB<bf16>{(const bf16*)hseq, B, T, H, d, FastDiv(B)}, out, B, T,
                                     H, H, accumulate, st)
@@ -317,13 +332,13 @@ int crnn_lstm_dwhh(int dtype, const void* dgates, const void* hseq, float* dwhh,
   return 0;
 }
 
-int crnn_lstm_dwih(int dtype, const void* dgates, const void* x, float* dwih, int B, int T, int H, int In,
-                   int accumulate, void* stream) {
+int crnn_lstm_dwih(int dtype, const void* dgates, const void* x, float* dwih_f, float* dwih_r, int B, int T, int H,
+                   int In, int accumulate, void* stream) {
   if (In % 8) return crnn_set_error(hipErrorInvalidValue, "lstm: In must be a multiple of 8");
   hipStream_t st = (hipStream_t)stream;
   for (int d = 0; d < 2; ++d) {
     size_t off = (size_t)d * T * B * 4 * H;
-    float* out = dwih + (size_t)d * 4 * H * In;
+    float* out = d ? dwih_r : dwih_f;
     int rc = dtype == CRNN_BF16
                  ? gate_wgrad<bf16>((const bf16*)dgates + off, XB<bf16>{(const bf16*)x, B, T, In, FastDiv(B)}, out, B, T, H, In,
                                     accumulate, st)
@@ -334,21 +349,21 @@ int crnn_lstm_dwih(int dtype, const void* dgates, const void* x, float* dwih, in
   return 0;
 }
 
-int crnn_lstm_dbias(int dtype, const void* dgates, float* db, int B, int T, int H, int accumulate, void* stream) {
+size_t crnn_lstm_dbias_workspace(int H) { return (size_t)DB_CHUNKS * 2 * 4 * H * sizeof(float); }
+
+int crnn_lstm_dbias(int dtype, const void* dgates, float* b_f, float* b2_f, float* b_r, float* b2_r, float* ws, int B,
+                    int T, int H, int accumulate, void* stream) {
   hipStream_t st = (hipStream_t)stream;
-  if (!accumulate) {
-    hipError_t e = hipMemsetAsync(db, 0, (size_t)8 * H * sizeof(float), st);
-    if (e != hipSuccess) return (int)e;
-  }
-  int K = T * B;
-  long chunks = (K + 255) / 256;
-  if (chunks > 128) chunks = 128;
-  long rpc = (K + chunks - 1) / chunks;
+  const int K = T * B;
+  const long rpc = (K + DB_CHUNKS - 1) / DB_CHUNKS;
+  const int chunks = (int)((K + rpc - 1) / rpc);
   dim3 grid((4 * H + 63) / 64, (unsigned)chunks, 2);
   if (dtype == CRNN_BF16)
-    hipLaunchKernelGGL(dbias_kernel<bf16>, grid, dim3(256), 0, st, (const bf16*)dgates, db, K, H, rpc);
+    hipLaunchKernelGGL(dbias_part_kernel<bf16>, grid, dim3(256), 0, st, (const bf16*)dgates, ws, K, H, rpc);
   else
-    hipLaunchKernelGGL(dbias_kernel<float>, grid, dim3(256), 0, st, (const float*)dgates, db, K, H, rpc);
+    hipLaunchKernelGGL(dbias_part_kernel<float>, grid, dim3(256), 0, st, (const float*)dgates, ws, K, H, rpc);
+  hipLaunchKernelGGL(dbias_fin_kernel, dim3((8 * H + 255) / 256), dim3(256), 0, st, ws, chunks, H, b_f, b2_f, b_r, b2_r,
+                     accumulate);
   return (int)hipGetLastError();
 }
 

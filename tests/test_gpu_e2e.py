@@ -239,6 +239,35 @@ def test_train_step_fp32_ill_conditioned_case_vs_fp64():
     _assert_vs_forced_fp64(model, sd, z)
 
 
+def test_zero_grad_then_backward_overwrites_not_accumulates():
+    """FusedAdamW.zero_grad(set_to_none=True) + backward twice == one backward (no leftover
+    accumulation); zero_grad(set_to_none=False) zeroes, and a second backward then doubles."""
+    from crnn_hip.ctc import ctc_loss
+    from crnn_hip.optim import FusedAdamW
+    z = load("train_b4_32x128_h256.npz")
+    sd, hidden = case_params(z, with_running=False)
+    model = build_model(sd, hidden, torch.float32).train()
+    x = pixels_to_images(z["pixels"]).to(DEV)
+    tg, tl = torch.from_numpy(z["targets"]), torch.from_numpy(z["target_lengths"])
+    opt = FusedAdamW(model)
+
+    def grads():
+        ctc_loss(model(x), tg, tl).backward()
+        return {k: p.grad.detach().clone() for k, p in model.named_parameters()}
+
+    opt.zero_grad()
+    g1 = grads()
+    opt.zero_grad()
+    g2 = grads()
+    for k in g1:
+        assert torch.allclose(g1[k], g2[k], rtol=1e-5, atol=1e-8), k
+    opt.zero_grad(set_to_none=False)
+    grads()
+    g3 = grads()
+    for k in g1:
+        assert torch.allclose(g3[k], 2 * g1[k], rtol=1e-4, atol=1e-7), k
+
+
 def test_train_step_bf16_runs_and_descends():
     from crnn_hip.ctc import ctc_loss
     from crnn_hip.optim import FusedAdamW

@@ -218,9 +218,13 @@ def test_bilstm_fwd_bwd(BTHI, dtype):
     dwhh = torch.empty(2, 4 * H, H, device=DEV)
     dwih = torch.empty(2, 4 * H, In, device=DEV)
     db = torch.empty(2, 4 * H, device=DEV)
-    L.call("crnn_lstm_dwhh", dt, dg.data_ptr(), hseq.data_ptr(), dwhh.data_ptr(), B, T, H, 0, st)
-    L.call("crnn_lstm_dwih", dt, dg.data_ptr(), xd.data_ptr(), dwih.data_ptr(), B, T, H, In, 0, st)
-    L.call("crnn_lstm_dbias", dt, dg.data_ptr(), db.data_ptr(), B, T, H, 0, st)
+    L.call("crnn_lstm_dwhh", dt, dg.data_ptr(), hseq.data_ptr(), dwhh[0].data_ptr(), dwhh[1].data_ptr(), B, T, H, 0, st)
+    L.call("crnn_lstm_dwih", dt, dg.data_ptr(), xd.data_ptr(), dwih[0].data_ptr(), dwih[1].data_ptr(), B, T, H, In, 0, st)
+    db2 = torch.full((2, 4 * H), 3.0, device=DEV)
+    dbws = torch.empty(L.lib().crnn_lstm_dbias_workspace(H) // 4, device=DEV)
+    L.call("crnn_lstm_dbias", dt, dg.data_ptr(), db[0].data_ptr(), db2[0].data_ptr(), db[1].data_ptr(), None,
+           dbws.data_ptr(), B, T, H, 0, st)
+    assert torch.equal(db2[0], db[0]) and bool((db2[1] == 3.0).all())   # second target optional
     dx = torch.empty(B, T, In, dtype=dtype, device=DEV)
     L.call("crnn_lstm_dx", dt, dg.data_ptr(), wih.data_ptr(), dx.data_ptr(), B, T, H, In, st)
     gtol = 1e-4 if dtype == torch.float32 else 5e-2
@@ -360,7 +364,7 @@ def test_bn_bwd_and_se(dtype):
     dw1, dw2 = torch.empty(Cr, C, device=DEV), torch.empty(C, Cr, device=DEV)
     L.call("crnn_se_mlp_bwd", ds.data_ptr(), pooled_d.data_ptr(), hid.data_ptr(), sd.data_ptr(), w1d.data_ptr(),
            w2d.data_ptr(), dsig.data_ptr(), dhid.data_ptr(), dpool.data_ptr(), dw1.data_ptr(), dw2.data_ptr(), B, C,
-           Cr, HW, st)
+           Cr, HW, 0, st)
     gtol = 1e-4 if dtype == torch.float32 else 5e-2
     assert relerr(dw1.cpu(), pr[2].grad) < gtol
     assert relerr(dw2.cpu(), pr[3].grad) < gtol
