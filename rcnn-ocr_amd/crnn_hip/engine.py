@@ -276,7 +276,11 @@ class CRNNEngine:
         return mean, inv, sc, sh
 
     def _fin_ws(self):
-        return self.ws.get("bn.fin_ws", (L.lib().crnn_bn_finalize_workspace(512) // 4,), torch.float32)
+        t = self.ws.bufs.get("bn.fin_ws")
+        if t is None:   # zeroed once: the finalize kernels keep their ticket counters re-armed
+            n = (L.lib().crnn_bn_finalize_workspace(512) + 3) // 4
+            t = self.ws.bufs["bn.fin_ws"] = torch.zeros(n, dtype=torch.float32, device=self.device)
+        return t
 
     def _conv_bn(self, cs: ConvSpec, x, b, h, w, train, tag):
         """z = conv(x); BN statistics (train) or running stats (eval) -> (z, mean, inv, scale, shift, ho, wo)."""

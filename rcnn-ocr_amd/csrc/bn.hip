@@ -156,13 +156,17 @@ template <class F> int chan_reduce(F f, long M, int C, float* p0, float* p1, int
 }
 
 // ------------------------------------------------------------ finalize
-// Two stages, both parallel over channels:
-//  (1) chunk_kernel: grid (C/64, P): block y folds partial rows [y*chunk, ...) of 64 channels
-//      (4 row lanes per channel) into one chunk partial. Chan mode: rows hold (sum, M2 about the
-//      row's own mean) covering rpp data rows each; the chunk result is (sum, M2 about the chunk
-//      mean), computed two-pass from the L2-resident partials. Plain mode: two independent sums.
-//  (2) per-channel combine of the P chunk partials in double.
-constexpr int FIN_P = 64;
+// Two launches (a cross-block ticket costs more than the launch boundary: up to 256 same-address
+// atomics serialize):
+//  (1) fin_chunk_kernel, grid (C/64, P): block y folds partial rows [y*chunk, ...) of 64 channels
+//      (4 row lanes per channel, 8 loads in flight per lane) into one chunk partial. Chan mode
+//      (forward): rows hold (sum, M2 about the row's own mean) covering rpp data rows, the chunk
+//      result is (sum, M2 about the chunk mean), two-pass over the L2-resident rows; plain mode
+//      (backward): two independent sums. P adapts so a block folds ~16 rows.
+//  (2) fin_combine_kernel, grid C/16: 16 lanes per channel fold the P (<= 256) chunk partials
+//      in double — one batch of 16 loads per lane, full chunks share one reciprocal.
+constexpr int FIN_P = 256;   // max chunk partials
+constexpr int FIN_CNT = 64;  // reserved head of the workspace (floats)
 
 __device__ __forceinline__ long span_rows(long r0, long r1, long rpp, long count) {
   long a = r0 * rpp, b = r1 * rpp;
@@ -170,33 +174,94 @@ __device__ __forceinline__ long span_rows(long r0, long r1, long rpp, long count
   return b > a ? b - a : 0;
 }
 
-__global__ __launch_bounds__(256) void chunk_kernel(const float* __restrict__ p0, const float* __restrict__ p1,
-                                                    int rows, long rpp, int C, long count, int chunk, int chan,
-                                                    float* __restrict__ o0, float* __restrict__ o1) {
+struct FinFwd {  // forward: batch statistics -> running stats, mean/invstd, affine scale/shift
+  const float* gamma;
+  const float* beta;
+  float* rmean;
+  float* rvar;
+  float momentum, eps;
+  float* mean_o;
+  float* inv_o;
+  float* scale_o;
+  float* shift_o;
+};
+struct FinBwd {  // backward: sum(g), sum(g xhat) -> dbeta, dgamma, their means
+  float* dgamma;
+  float* dbeta;
+  float* mean_g;
+  float* mean_gx;
+  int acc;
+};
+
+__device__ __forceinline__ void write_affine(const FinFwd& a, int c, double mean, double var, bool train, long count) {
+  if (train) {
+    if (a.rmean) {
+      double unb = count > 1 ? var * (double)count / (double)(count - 1) : var;
+      a.rmean[c] = (float)((1.0 - a.momentum) * a.rmean[c] + a.momentum * mean);
+      a.rvar[c] = (float)((1.0 - a.momentum) * a.rvar[c] + a.momentum * unb);
+    }
+  } else {
+    mean = a.rmean[c];
+    var = a.rvar[c];
+  }
+  double inv = 1.0 / sqrt(var + (double)a.eps);
+  double sc = (double)a.gamma[c] * inv;
+  if (a.mean_o) a.mean_o[c] = (float)mean;
+  if (a.inv_o) a.inv_o[c] = (float)inv;
+  a.scale_o[c] = (float)sc;
+  a.shift_o[c] = (float)((double)a.beta[c] - mean * sc);
+}
+
+template <bool CHAN>
+__global__ __launch_bounds__(256) void fin_chunk_kernel(const float* __restrict__ p0, const float* __restrict__ p1,
+                                                        int rows, long rpp, int C, long count, int chunk,
+                                                        float* __restrict__ o0, float* __restrict__ o1) {
   __shared__ float red[2][4][64];
   const int lc = threadIdx.x & 63, ln = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lc;
   const int r0 = blockIdx.y * chunk, r1 = min(rows, r0 + chunk);
   float s = 0.f, q = 0.f;
   if (c < C)
-    for (int r = r0 + ln; r < r1; r += 4) {
-      s += p0[(size_t)r * C + c];
-      if (!chan) q += p1[(size_t)r * C + c];
+    for (int rb = r0 + ln; rb < r1; rb += 32) {  // 8 independent loads in flight per lane
+      float a[8], b[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int r = rb + 4 * u;
+        a[u] = r < r1 ? p0[(size_t)r * C + c] : 0.f;
+        b[u] = (!CHAN && r < r1) ? p1[(size_t)r * C + c] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        s += a[u];
+        q += b[u];
+      }
     }
   red[0][ln][lc] = s;
   red[1][ln][lc] = q;
   __syncthreads();
   const float S = red[0][0][lc] + red[0][1][lc] + red[0][2][lc] + red[0][3][lc];
-  if (chan) {
+  if (CHAN) {
     const long n = span_rows(r0, r1, rpp, count);
     const float mu = n > 0 ? S / (float)n : 0.f;
+    const float rr = 1.f / (float)rpp;
     q = 0.f;
     if (c < C)
-      for (int r = r0 + ln; r < r1; r += 4) {
-        long nr = span_rows(r, r + 1, rpp, count);
-        if (nr == 0) continue;
-        float d = p0[(size_t)r * C + c] / (float)nr - mu;
-        q += p1[(size_t)r * C + c] + (float)nr * d * d;
+      for (int rb = r0 + ln; rb < r1; rb += 32) {
+        float a[8], b[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int r = rb + 4 * u;
+          a[u] = r < r1 ? p0[(size_t)r * C + c] : 0.f;
+          b[u] = r < r1 ? p1[(size_t)r * C + c] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int r = rb + 4 * u;
+          const long nr = r < r1 ? span_rows(r, r + 1, rpp, count) : 0;
+          if (nr == 0) continue;
+          const float d = a[u] * (nr == rpp ? rr : 1.f / (float)nr) - mu;
+          q += b[u] + (float)nr * d * d;
+        }
       }
     __syncthreads();
     red[1][ln][lc] = q;
@@ -208,92 +273,86 @@ __global__ __launch_bounds__(256) void chunk_kernel(const float* __restrict__ p0
   }
 }
 
-// block = 64 channels x 4 lanes; each lane folds a quarter of the P chunk partials
-// (independent loads in flight), combined through LDS in double.
-__global__ __launch_bounds__(256) void bn_finalize_kernel(const float* cs, const float* cq, int P, long crows, int C,
-                                                          long count, const float* gamma, const float* beta,
-                                                          float* rmean, float* rvar, float momentum, float eps,
-                                                          int train, float* mean_o, float* inv_o, float* scale_o,
-                                                          float* shift_o) {
-  __shared__ double red[4][64];
-  const int lc = threadIdx.x & 63, ln = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + lc;
+template <bool CHAN, class A>
+__global__ __launch_bounds__(256) void fin_combine_kernel(const float* __restrict__ o0, const float* __restrict__ o1,
+                                                          int P, long crows, int C, long count, A args) {
+  __shared__ double dred[2][16][16];
+  const int lc = threadIdx.x & 15, ln = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + lc;
   const bool okc = c < C;
-  double mean = 0.0, var = 1.0;
-  if (train) {
-    double s = 0.0;
-    if (okc)
-      for (int p = ln; p < P; p += 4) s += cs[(size_t)p * C + c];
-    red[ln][lc] = s;
-    __syncthreads();
-    mean = (red[0][lc] + red[1][lc] + red[2][lc] + red[3][lc]) / (double)count;
-    __syncthreads();
-    double m2 = 0.0;
-    if (okc)
-      for (int p = ln; p < P; p += 4) {
-        long n = span_rows(p, p + 1, crows, count);
-        if (n == 0) continue;
-        double d = (double)cs[(size_t)p * C + c] / (double)n - mean;
-        m2 += (double)cq[(size_t)p * C + c] + (double)n * d * d;
-      }
-    red[ln][lc] = m2;
-    __syncthreads();
-    var = (red[0][lc] + red[1][lc] + red[2][lc] + red[3][lc]) / (double)count;
-    if (var < 0.0) var = 0.0;
+  float v[16], w[16];
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {  // P <= 256: one batch
+    const int p = ln + 16 * u;
+    v[u] = (okc && p < P) ? o0[(size_t)p * C + c] : 0.f;
+    w[u] = (okc && p < P) ? o1[(size_t)p * C + c] : 0.f;
   }
-  if (ln != 0 || !okc) return;
-  if (train) {
-    if (rmean) {
-      double unb = count > 1 ? var * (double)count / (double)(count - 1) : var;
-      rmean[c] = (float)((1.0 - momentum) * rmean[c] + momentum * mean);
-      rvar[c] = (float)((1.0 - momentum) * rvar[c] + momentum * unb);
-    }
-  } else {
-    mean = rmean[c];
-    var = rvar[c];
-  }
-  double inv = 1.0 / sqrt(var + (double)eps);
-  double sc = (double)gamma[c] * inv;
-  if (mean_o) mean_o[c] = (float)mean;
-  if (inv_o) inv_o[c] = (float)inv;
-  scale_o[c] = (float)sc;
-  shift_o[c] = (float)((double)beta[c] - mean * sc);
-}
-
-__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* cg, const float* cgx, int P, int C,
-                                                              long count, float* dgamma, float* dbeta, float* mean_g,
-                                                              float* mean_gx, int acc) {
-  __shared__ double red[2][4][64];
-  const int lc = threadIdx.x & 63, ln = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + lc;
   double s = 0.0, q = 0.0;
-  if (c < C)
-    for (int p = ln; p < P; p += 4) {
-      s += cg[(size_t)p * C + c];
-      q += cgx[(size_t)p * C + c];
-    }
-  red[0][ln][lc] = s;
-  red[1][ln][lc] = q;
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    s += v[u];
+    if (!CHAN) q += w[u];
+  }
+  dred[0][ln][lc] = s;
+  dred[1][ln][lc] = q;
   __syncthreads();
-  if (ln != 0 || c >= C) return;
-  s = red[0][0][lc] + red[0][1][lc] + red[0][2][lc] + red[0][3][lc];
-  q = red[1][0][lc] + red[1][1][lc] + red[1][2][lc] + red[1][3][lc];
-  if (dgamma) dgamma[c] = (float)(acc ? dgamma[c] + q : q);
-  if (dbeta) dbeta[c] = (float)(acc ? dbeta[c] + s : s);
-  mean_g[c] = (float)(s / (double)count);
-  mean_gx[c] = (float)(q / (double)count);
+  s = 0.0;
+  q = 0.0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    s += dred[0][k][lc];
+    q += dred[1][k][lc];
+  }
+  if constexpr (CHAN) {
+    const double mean = s / (double)count;
+    const double rfull = 1.0 / (double)crows;
+    double m2 = 0.0;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int p = ln + 16 * u;
+      const long n = p < P ? span_rows(p, p + 1, crows, count) : 0;
+      if (n == 0) continue;
+      const double d = (double)v[u] * (n == crows ? rfull : 1.0 / (double)n) - mean;
+      m2 += (double)w[u] + (double)n * d * d;
+    }
+    __syncthreads();
+    dred[1][ln][lc] = m2;
+    __syncthreads();
+    if (ln != 0 || !okc) return;
+    m2 = 0.0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) m2 += dred[1][k][lc];
+    double var = m2 / (double)count;
+    if (var < 0.0) var = 0.0;
+    write_affine(args, c, mean, var, true, count);
+  } else {
+    if (ln != 0 || !okc) return;
+    if (args.dgamma) args.dgamma[c] = (float)(args.acc ? args.dgamma[c] + q : q);
+    if (args.dbeta) args.dbeta[c] = (float)(args.acc ? args.dbeta[c] + s : s);
+    args.mean_g[c] = (float)(s / (double)count);
+    args.mean_gx[c] = (float)(q / (double)count);
+  }
 }
 
-int launch_chunks(const float* p0, const float* p1, int rows, long rpp, int C, long count, int chan, float* ws,
-                  int* P_out, long* crows_out, hipStream_t st) {
-  int P = rows < FIN_P ? rows : FIN_P;
+// eval mode: running statistics only
+__global__ void bn_eval_affine_kernel(int C, FinFwd a) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < C) write_affine(a, c, 0.0, 1.0, false, 0);
+}
+
+template <bool CHAN, class A>
+int launch_fin(const float* p0, const float* p1, int rows, long rpp, int C, long count, float* ws, const A& args,
+               hipStream_t st) {
+  int P = rows / 16;  // ~16 partial rows per stage-1 block (4 per lane)
+  if (P > FIN_P) P = FIN_P;
   if (P < 1) P = 1;
-  int chunk = (rows + P - 1) / P;
+  const int chunk = (rows + P - 1) / P;
   P = (rows + chunk - 1) / chunk;
-  hipLaunchKernelGGL(chunk_kernel, dim3((C + 63) / 64, P), dim3(256), 0, st, p0, p1, rows, rpp, C, count, chunk, chan,
-                     ws, ws + (size_t)FIN_P * C);
-  *P_out = P;
-  *crows_out = (long)chunk * rpp;
+  float* part = ws + FIN_CNT;
+  hipLaunchKernelGGL((fin_chunk_kernel<CHAN>), dim3((C + 63) / 64, P), dim3(256), 0, st, p0, p1, rows, rpp, C, count,
+                     chunk, part, part + (size_t)FIN_P * C);
+  hipLaunchKernelGGL((fin_combine_kernel<CHAN, A>), dim3((C + 15) / 16), dim3(256), 0, st, part,
+                     part + (size_t)FIN_P * C, P, (long)chunk * rpp, C, count, args);
   return (int)hipGetLastError();
 }
 
@@ -922,23 +981,21 @@ int crnn_channel_stats(int dtype, const void* x, long M, int C, float* psum, flo
   return (int)hipGetLastError();
 }
 
-size_t crnn_bn_finalize_workspace(int C) { return (size_t)2 * FIN_P * C * sizeof(float); }
+size_t crnn_bn_finalize_workspace(int C) {
+  return (size_t)FIN_CNT * sizeof(unsigned) + (size_t)2 * FIN_P * C * sizeof(float);
+}
 
 int crnn_bn_finalize(const float* psum, const float* psq, int rows, long rows_per_partial, int C, long count,
                      const float* gamma, const float* beta, float* running_mean, float* running_var, float momentum,
                      float eps, int train, float* mean, float* invstd, float* scale, float* shift, float* ws,
                      void* stream) {
   hipStream_t st = (hipStream_t)stream;
-  int P = 0;
-  long crows = 0;
-  if (train) {
-    int rc = launch_chunks(psum, psq, rows, rows_per_partial, C, count, 1, ws, &P, &crows, st);
-    if (rc) return rc;
+  FinFwd a{gamma, beta, running_mean, running_var, momentum, eps, mean, invstd, scale, shift};
+  if (!train) {
+    hipLaunchKernelGGL(bn_eval_affine_kernel, dim3((C + 255) / 256), dim3(256), 0, st, C, a);
+    return (int)hipGetLastError();
   }
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, st, ws, ws + (size_t)FIN_P * C, P,
-                     crows, C,
-                     count, gamma, beta, running_mean, running_var, momentum, eps, train, mean, invstd, scale, shift);
-  return (int)hipGetLastError();
+  return launch_fin<true>(psum, psq, rows, rows_per_partial, C, count, ws, a, st);
 }
 
 int crnn_bn_act(int dtype, const void* z, const float* scale, const float* shift, void* y, long M, int C, int relu,
@@ -977,14 +1034,8 @@ int crnn_bn_bwd_reduce(int dtype, const crnn_bn_bwd_desc* d, float* pg, float* p
 
 int crnn_bn_bwd_finalize(const float* pg, const float* pgx, int rows, int C, long count, float* dgamma, float* dbeta,
                          float* mean_g, float* mean_gx, int accumulate, float* ws, void* stream) {
-  hipStream_t st = (hipStream_t)stream;
-  int P = 0;
-  long crows = 0;
-  int rc = launch_chunks(pg, pgx, rows, 1, C, (long)rows, 0, ws, &P, &crows, st);
-  if (rc) return rc;
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, st, ws, ws + (size_t)FIN_P * C, P, C,
-                     count, dgamma, dbeta, mean_g, mean_gx, accumulate);
-  return (int)hipGetLastError();
+  FinBwd a{dgamma, dbeta, mean_g, mean_gx, accumulate};
+  return launch_fin<false>(pg, pgx, rows, 1, C, count, ws, a, (hipStream_t)stream);
 }
 
 int crnn_bn_bwd_apply(int dtype, const crnn_bn_bwd_desc* d, const float* mean_g, const float* mean_gx, void* dz,

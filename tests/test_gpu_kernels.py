@@ -339,7 +339,7 @@ def test_bn_bwd_and_se(dtype):
     gd, bd = gamma.to(DEV), beta.to(DEV)
     rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
     mean, inv, sc, sh = [torch.empty(C, device=DEV) for _ in range(4)]
-    fws = torch.empty(L.lib().crnn_bn_finalize_workspace(C) // 4, device=DEV)
+    fws = torch.zeros(L.lib().crnn_bn_finalize_workspace(C) // 4, device=DEV)
     L.call("crnn_bn_finalize", ps.data_ptr(), pq.data_ptr(), rows, (M + rows - 1) // rows, C, M, gd.data_ptr(),
            bd.data_ptr(), rm.data_ptr(),
            rv.data_ptr(), 0.1, 1e-5, 1, mean.data_ptr(), inv.data_ptr(), sc.data_ptr(), sh.data_ptr(), fws.data_ptr(), st)
@@ -469,7 +469,7 @@ def test_bn_bwd_modes_ill_conditioned_channels(mode):
     pg, pgx = torch.empty(rows, C, device=DEV), torch.empty(rows, C, device=DEV)
     st = L.stream_ptr()
     L.call("crnn_bn_bwd_reduce", L.F32, desc, pg.data_ptr(), pgx.data_ptr(), rows, st)
-    fws = torch.empty(L.lib().crnn_bn_finalize_workspace(C) // 4, device=DEV)
+    fws = torch.zeros(L.lib().crnn_bn_finalize_workspace(C) // 4, device=DEV)
     dgam, dbet, mgd, mgxd = [torch.empty(C, device=DEV) for _ in range(4)]
     L.call("crnn_bn_bwd_finalize", pg.data_ptr(), pgx.data_ptr(), rows, C, M, dgam.data_ptr(), dbet.data_ptr(),
            mgd.data_ptr(), mgxd.data_ptr(), 0, fws.data_ptr(), st)
@@ -482,3 +482,65 @@ def test_bn_bwd_modes_ill_conditioned_channels(mode):
     err_bad = relerr(dz.cpu()[..., :64], dz_ref[..., :64])
     print("mode", mode, "dz rel err", err, "ill-conditioned channels", err_bad)
     assert err < 1e-4 and err_bad < 1e-3
+
+
+@pytest.mark.parametrize("rows,rpp,C", [(5000, 64, 64), (300, 128, 512), (1, 7, 24)])
+def test_bn_finalize_ticketed_combine(rows, rpp, C):
+    """crnn_bn_finalize / crnn_bn_bwd_finalize: one launch whose last block per channel block
+    combines up to 64 chunk partials (Chan, double). Twice on ONE workspace (ticket counters
+    re-armed by the kernel), vs fp64; a ragged last partial (count not a multiple of rpp)."""
+    L = _L()
+    g = torch.Generator().manual_seed(4)
+    count = rows * rpp - (rpp // 3)
+    x = (torch.randn(count, C, generator=g, dtype=torch.float64) * 0.01 + torch.randn(C, generator=g) * 50)
+    # partials: (sum, M2 about the partial's own mean) per rpp rows
+    ps, pq = torch.zeros(rows, C, dtype=torch.float64), torch.zeros(rows, C, dtype=torch.float64)
+    for r in range(rows):
+        blk = x[r * rpp: min(count, (r + 1) * rpp)]
+        if len(blk):
+            ps[r] = blk.sum(0)
+            pq[r] = ((blk - blk.mean(0)) ** 2).sum(0)
+    gamma, beta = torch.rand(C, generator=g) + 0.5, torch.randn(C, generator=g)
+    fws = torch.zeros(L.lib().crnn_bn_finalize_workspace(C) // 4, device=DEV)
+    st = L.stream_ptr()
+    dev = lambda t: t.float().contiguous().to(DEV)
+    psd, pqd, gd, bd = dev(ps), dev(pq), dev(gamma), dev(beta)
+    for it in range(2):
+        rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+        mean, inv, sc, sh = [torch.empty(C, device=DEV) for _ in range(4)]
+        L.call("crnn_bn_finalize", psd.data_ptr(), pqd.data_ptr(), rows, rpp, C, count, gd.data_ptr(), bd.data_ptr(),
+               rm.data_ptr(), rv.data_ptr(), 0.1, 1e-5, 1, mean.data_ptr(), inv.data_ptr(), sc.data_ptr(),
+               sh.data_ptr(), fws.data_ptr(), st)
+        torch.cuda.synchronize()
+        m64, v64 = x.mean(0), x.var(0, unbiased=False)
+        assert relerr(mean.cpu(), m64) < 1e-6, it
+        assert relerr(inv.cpu(), 1 / torch.sqrt(v64 + 1e-5)) < 1e-4, it
+        assert relerr(rv.cpu(), 0.9 + 0.1 * x.var(0, unbiased=True)) < 1e-4, it
+    # backward sums on the same workspace
+    pg, pgx = torch.randn(rows, C, generator=g), torch.randn(rows, C, generator=g)
+    pgd, pgxd = dev(pg), dev(pgx)   # keep device copies referenced for the calls
+    dgam, dbet, mg, mgx = [torch.empty(C, device=DEV) for _ in range(4)]
+    for it in range(2):
+        L.call("crnn_bn_bwd_finalize", pgd.data_ptr(), pgxd.data_ptr(), rows, C, count, dgam.data_ptr(),
+               dbet.data_ptr(), mg.data_ptr(), mgx.data_ptr(), 0, fws.data_ptr(), st)
+        torch.cuda.synchronize()
+        assert relerr(dbet.cpu(), pg.double().sum(0)) < 1e-6 and relerr(dgam.cpu(), pgx.double().sum(0)) < 1e-6
+        assert relerr(mg.cpu(), pg.double().sum(0) / count) < 1e-6
+
+
+def test_bn_finalize_shared_workspace_mixed_channels():
+    """one workspace (sized for the largest C) shared by finalize calls of different C in any
+    order — the engine's usage (ticket counters must not overlap any call's partials)."""
+    L = _L()
+    g = torch.Generator().manual_seed(6)
+    fws = torch.zeros(L.lib().crnn_bn_finalize_workspace(512) // 4, device=DEV)
+    st = L.stream_ptr()
+    for C, rows in [(512, 300), (64, 900), (512, 200), (128, 700), (64, 50)]:
+        pg, pgx = torch.randn(rows, C, generator=g), torch.randn(rows, C, generator=g)
+        pgd, pgxd = pg.to(DEV), pgx.to(DEV)
+        dgam, dbet, mg, mgx = [torch.empty(C, device=DEV) for _ in range(4)]
+        L.call("crnn_bn_bwd_finalize", pgd.data_ptr(), pgxd.data_ptr(), rows, C, rows, dgam.data_ptr(),
+               dbet.data_ptr(), mg.data_ptr(), mgx.data_ptr(), 0, fws.data_ptr(), st)
+        torch.cuda.synchronize()
+        assert relerr(dbet.cpu(), pg.double().sum(0)) < 1e-6, (C, rows)
+        assert relerr(dgam.cpu(), pgx.double().sum(0)) < 1e-6, (C, rows)
