@@ -66,6 +66,7 @@ int crnn_pack_rows(int dtype, const float* src, void* out, const int* perm, int 
 #define CRNN_PACK_CONV 0
 #define CRNN_PACK_ROWS 1
 #define CRNN_PACK_ROWS_SUM 2
+#define CRNN_PACK_TRANSPOSE 3 /* dst[c][r] = src[perm[r]][c], (a,b,c) = (rows, rows_src, cols) */
 typedef struct {
   int kind, out_f32;
   int a, b, c, d, e, pad_;
@@ -198,8 +199,11 @@ int crnn_lstm_step_fwd(int dtype, const void* xg, const void* whh, void* hseq, v
 /* BPTT. dgates [2][T][B][4H] (dtype, pre-activation gate grads), dc [2][B][H] fp32 running cell grad.
  * step 0 initialises (dh_rec = 0, dc = 0); step s>0 runs dh_rec = dgates(step s-1) . W_hh with the
  * cell backward of step s fused into the GEMM epilogue. */
-int crnn_lstm_step_bwd(int dtype, const void* dhseq, const void* whh, const void* gsv, const float* csv, void* dgates,
-                       float* dc, int B, int T, int H, int step, void* stream);
+int crnn_lstm_step_bwd(int dtype, const void* dhseq, const void* whh, const void* whh_t, const void* gsv,
+                       const float* csv, void* dgates, float* dc, float* ws, int B, int T, int H, int step, void* stream);
+/* whh_t [2][H][4H] = packed W_hh transposed (bf16; CRNN_PACK_TRANSPOSE) and ws
+ * (crnn_lstm_bptt_workspace bytes) enable the split-K one-shot step; NULL -> the staged kernel. */
+size_t crnn_lstm_bptt_workspace(int B, int H);
 /* dW_hh (reference row order, fp32 [2][4H][H]) (+)= sum_t dgates_t^T h_{t-1} */
 int crnn_lstm_dwhh(int dtype, const void* dgates, const void* hseq, float* dwhh_fwd, float* dwhh_rev, int B, int T, int H, int accumulate, void* stream);
 /* dW_ih (reference row order, fp32 [2][4H][In]) (+)= sum dgates^T x ; x [B][T][In] */

@@ -43,7 +43,7 @@ class PackJob(C.Structure):  # crnn_pack_job
                 ("src2", vp), ("perm", vp), ("dst", vp)]
 
 
-PACK_CONV, PACK_ROWS, PACK_ROWS_SUM = 0, 1, 2
+PACK_CONV, PACK_ROWS, PACK_ROWS_SUM, PACK_TRANSPOSE = 0, 1, 2, 3
 
 _SIGS = {
     "crnn_pack_batch": ([i32, vp, i32, i64, vp], i32),
@@ -81,7 +81,8 @@ _SIGS = {
     "crnn_gemm_tn": ([i32, vp, i32, vp, i32, vp, i32, i32, i32, i32, i32, vp], i32),
     "crnn_colsum": ([i32, vp, i32, i64, i32, vp, i32, i32, vp], i32),
     "crnn_lstm_step_fwd": ([i32, vp, vp, vp, vp, vp, i32, i32, i32, i32, vp], i32),
-    "crnn_lstm_step_bwd": ([i32, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, vp], i32),
+    "crnn_lstm_step_bwd": ([i32, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, vp], i32),
+    "crnn_lstm_bptt_workspace": ([i32, i32], sz),
     "crnn_lstm_dwhh": ([i32, vp, vp, vp, vp, i32, i32, i32, i32, vp], i32),
     "crnn_lstm_dwih": ([i32, vp, vp, vp, vp, i32, i32, i32, i32, i32, vp], i32),
     "crnn_lstm_dbias": ([i32, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, vp], i32),

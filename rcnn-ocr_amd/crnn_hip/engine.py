@@ -193,12 +193,15 @@ class CRNNEngine:
             ind = self.enc_dim if l == 0 else H
             wih = self._pbuf(pre + ".wih", (2, 4 * H, ind), T)
             whh = self._pbuf(pre + ".whh", (2, 4 * H, H), T)
+            whh_t = self._pbuf(pre + ".whh_t", (2, H, 4 * H), T)   # BPTT B operand, K-contiguous
             bias = self._pbuf(pre + ".bias", (2, 4 * H), torch.float32)
             for d, sfx in enumerate(["", "_reverse"]):
                 r = pre + ".rnn."
                 sizes.append(job(L.PACK_ROWS, self.p[r + "weight_ih_l0" + sfx], wih[d], 4 * H, 4 * H, ind,
                                  perm=self.perm))
                 sizes.append(job(L.PACK_ROWS, self.p[r + "weight_hh_l0" + sfx], whh[d], 4 * H, 4 * H, H,
+                                 perm=self.perm))
+                sizes.append(job(L.PACK_TRANSPOSE, self.p[r + "weight_hh_l0" + sfx], whh_t[d], 4 * H, 4 * H, H,
                                  perm=self.perm))
                 sizes.append(job(L.PACK_ROWS_SUM, self.p[r + "bias_ih_l0" + sfx], bias[d], 4 * H, 4 * H, 1,
                                  out_f32=True, perm=self.perm, src2=self.p[r + "bias_hh_l0" + sfx]))
@@ -542,10 +545,11 @@ class CRNNEngine:
             call("crnn_colsum", dt, ptr(dx), Hd, M, Hd, ptr(grads[pre + ".linear.bias"]), acc, 0, s)
             dg = ws.get("rnn.dgates", (2, Tn, B, 4 * Hd), T)
             dc = ws.get("rnn.dc", (2, B, Hd), torch.float32)
-            whh = self.packed[pre + ".whh"]
+            whh, whh_t = self.packed[pre + ".whh"], self.packed[pre + ".whh_t"]
+            bws = ws.get("rnn.bptt_ws", (L.lib().crnn_lstm_bptt_workspace(B, Hd) // 4,), torch.float32)
             for stp in range(Tn):
-                call("crnn_lstm_step_bwd", dt, ptr(dh), ptr(whh), ptr(r["gates"]), ptr(r["c"]), ptr(dg), ptr(dc),
-                     B, Tn, Hd, stp, s)
+                call("crnn_lstm_step_bwd", dt, ptr(dh), ptr(whh), ptr(whh_t), ptr(r["gates"]), ptr(r["c"]), ptr(dg),
+                     ptr(dc), ptr(bws), B, Tn, Hd, stp, s)
             rr = pre + ".rnn."
             gq = lambda n: ptr(self._gview(rr + n))
             # gradients straight into the parameters' .grad views (reference row order)

@@ -635,6 +635,11 @@ __global__ __launch_bounds__(256) void pack_batch_kernel(const crnn_pack_job* __
         t /= KW;
         const int kh = (int)(t % KH), co = (int)(t / KH);
         v = ci < Ci ? jb.src[(((size_t)co * Ci + ci) * KH + kh) * KW + kw] : 0.f;
+      } else if (jb.kind == CRNN_PACK_TRANSPOSE) {
+        const int rows = jb.a;
+        const int c = (int)(i / rows), r = (int)(i - (long)c * rows);
+        const int sr = jb.perm ? jb.perm[r] : r;
+        v = (r < jb.b && sr >= 0) ? jb.src[(size_t)sr * jb.c + c] : 0.f;
       } else {
         const int cols = jb.c;
         const int r = (int)(i / cols), c = (int)(i - (long)r * cols);

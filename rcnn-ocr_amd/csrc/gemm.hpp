@@ -49,6 +49,8 @@ template <class L> struct Pair {
   __device__ __forceinline__ Ctx row_ctx(int r) const { return a.row_ctx(r); }
   __device__ __forceinline__ Prep prep(int k0) const { return a.prep(k0); }
   __device__ __forceinline__ auto load(const Ctx& c, const Prep& p, int kofs) const { return a.load(c, p, kofs); }
+  __device__ __forceinline__ auto rsrc() const { return a.rsrc(); }
+  __device__ __forceinline__ auto offs(const Ctx& c, const Prep& p, int kofs) const { return a.offs(c, p, kofs); }
 };
 template <class E> struct EpiPair {
   static constexpr bool kStats = E::kStats;

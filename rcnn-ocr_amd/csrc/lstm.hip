@@ -11,6 +11,7 @@
 // BPTT mirrors it: step s's GEMM dgates_{s-1} . W_hh' produces dh_rec and its
 // epilogue runs the cell backward of step s (again one lane per (b, 4 units)).
 #include "gemm.hpp"
+#include "gemm_oneshot.hpp"
 #include "crnn_internal.hpp"
 
 using namespace gemm;
@@ -58,6 +59,9 @@ int step_fwd_t(const void* xg, const void* whh, void* hseq, void* gsv, float* cs
     (d ? la.b : la.a) = a;
     (d ? lb.b : lb.a) = b;
     (d ? ep.b : ep.a) = e;
+  }
+  if constexpr (sizeof(T) == 2) {
+    if (H <= 512 && H % 16 == 0) return launch_oneshot<512>(la, lb, ep, B, 4 * H, H, 1, st, 2);  // one K burst
   }
   if ((long)B * 4 * H >= 64L * 64 * 256) return launch<T, 64, 64>(la, lb, ep, B, 4 * H, H, 1, st, 2);
   return launch<T, 32, 32>(la, lb, ep, B, 4 * H, H, 1, st, 2);
@@ -114,6 +118,57 @@ __global__ void bptt_init_kernel(const T* dhseq, const T* gsv, const float* csv,
     int t = d == 0 ? Tn - 1 : 0;
     cell_bwd<T>(dhseq, gsv, csv, dgates, dc, B, Tn, H, d, t, b, u, 0.f);
   }
+}
+
+// ---- bf16 BPTT step as split-K one-shot GEMM (dh_rec partials) + sum-and-cell-backward pass
+constexpr int BPTT_KC = 512;
+inline int bptt_splits(int H) { return (4 * H + BPTT_KC - 1) / BPTT_KC; }
+
+struct BpttSlabEpi {
+  static constexpr bool kStats = false;
+  float* ws;  // [nsplit][2][B][H]
+  int B, H, d;
+  __device__ __forceinline__ void set_batch(int bz) { d = bz; }
+  __device__ __forceinline__ void store(int b, int n, f32x4 v, int kz) const {
+    if (b < B && n < H) *reinterpret_cast<f32x4*>(ws + (((size_t)kz * 2 + d) * B + b) * H + n) = v;
+  }
+  __device__ __forceinline__ void stats(int, int, f32x4, f32x4) const {}
+};
+
+template <typename T>
+__global__ void bptt_cell_kernel(const float* __restrict__ ws, int nsplit, const T* dhseq, const T* gsv,
+                                 const float* csv, T* dgates, float* dc, int B, int Tn, int H, int s) {
+  const long n = 2L * B * H;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int u = (int)(i % H);
+    const long q = i / H;
+    const int b = (int)(q % B), d = (int)(q / B);
+    float dh = 0.f;
+    for (int z = 0; z < nsplit; ++z) dh += ws[(((size_t)z * 2 + d) * B + b) * H + u];
+    const int t = d == 0 ? Tn - 1 - s : s;
+    cell_bwd<T>(dhseq, gsv, csv, dgates, dc, B, Tn, H, d, t, b, u, dh);
+  }
+}
+
+int step_bwd_oneshot(const bf16* dhseq, const bf16* whh_t, const bf16* gsv, const float* csv, bf16* dgates, float* dc,
+                     float* ws, int B, int Tn, int H, int s, hipStream_t st) {
+  Pair<RowMajorK<bf16>> la, lb;
+  for (int d = 0; d < 2; ++d) {
+    const int t = d == 0 ? Tn - 1 - s : s;  // time processed now
+    const int tn = d == 0 ? t + 1 : t - 1;  // time processed at step s-1
+    RowMajorK<bf16> a{dgates + (size_t)(d * Tn + tn) * B * 4 * H, 4 * H, B, 4 * H};  // dgates of step s-1
+    RowMajorK<bf16> b{whh_t + (size_t)d * H * 4 * H, 4 * H, H, 4 * H};               // W_hh'^T [H][4H]
+    (d ? la.b : la.a) = a;
+    (d ? lb.b : lb.a) = b;
+  }
+  const int ns = bptt_splits(H);
+  BpttSlabEpi ep{ws, B, H, 0};
+  int rc = launch_oneshot<BPTT_KC>(la, lb, ep, B, H, 4 * H, ns, st, 2);
+  if (rc) return rc;
+  const long n = 2L * B * H;
+  hipLaunchKernelGGL(bptt_cell_kernel<bf16>, dim3(grid_for(n)), dim3(256), 0, st, ws, ns, dhseq, gsv, csv, dgates, dc,
+                     B, Tn, H, s);
+  return (int)hipGetLastError();
 }
 
 template <typename T>
@@ -308,10 +363,16 @@ int crnn_lstm_step_fwd(int dtype, const void* xg, const void* whh, void* hseq, v
                             : step_fwd_t<float>(xg, whh, hseq, gsv, csv, B, T, H, step, st);
 }
 
-int crnn_lstm_step_bwd(int dtype, const void* dhseq, const void* whh, const void* gsv, const float* csv, void* dgates,
-                       float* dc, int B, int T, int H, int step, void* stream) {
+size_t crnn_lstm_bptt_workspace(int B, int H) { return (size_t)bptt_splits(H) * 2 * B * H * sizeof(float); }
+
+int crnn_lstm_step_bwd(int dtype, const void* dhseq, const void* whh, const void* whh_t, const void* gsv,
+                       const float* csv, void* dgates, float* dc, float* ws, int B, int T, int H, int step,
+                       void* stream) {
   if (H % 8) return crnn_set_error(hipErrorInvalidValue, "lstm: H must be a multiple of 8");
   hipStream_t st = (hipStream_t)stream;
+  if (dtype == CRNN_BF16 && whh_t && ws && step > 0 && H % 16 == 0)
+    return step_bwd_oneshot((const bf16*)dhseq, (const bf16*)whh_t, (const bf16*)gsv, csv, (bf16*)dgates, dc, ws, B, T,
+                            H, step, st);
   return dtype == CRNN_BF16 ? step_bwd_t<bf16>(dhseq, whh, gsv, csv, dgates, dc, B, T, H, step, st)
                             : step_bwd_t<float>(dhseq, whh, gsv, csv, dgates, dc, B, T, H, step, st);
 }

@@ -167,9 +167,13 @@ def _pack_lstm(w_ih, w_hh, b_ih, b_hh, H, dtype, L):
     return wih, whh, bias
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("BTHI", [(3, 5, 32, 64), (16, 8, 64, 128)])
-def test_bilstm_fwd_bwd(BTHI, dtype):
+@pytest.mark.parametrize("dtype,BTHI,oneshot", [
+    (torch.float32, (3, 5, 32, 64), False), (torch.float32, (16, 8, 64, 128), False),
+    (torch.bfloat16, (3, 5, 32, 64), False), (torch.bfloat16, (16, 8, 64, 128), True),
+    (torch.bfloat16, (3, 5, 32, 64), True), (torch.bfloat16, (64, 6, 512, 512), True)])
+def test_bilstm_fwd_bwd(BTHI, dtype, oneshot):
+    """bf16 steps run the one-shot LDS-DMA GEMM (forward: fused cell; backward with whh_t: split-K
+    partials + sum/cell pass; H = 512 -> 4 splits); oneshot=False passes no whh_t (staged kernel)."""
     L = _L()
     import crnn_oracle as O
     B, T, H, In = BTHI
@@ -212,9 +216,11 @@ def test_bilstm_fwd_bwd(BTHI, dtype):
     dh = dh_out.to(DEV, dtype).contiguous()
     dg = torch.empty(2, T, B, 4 * H, dtype=dtype, device=DEV)
     dc = torch.empty(2, B, H, device=DEV)
+    whh_t = whh.transpose(1, 2).contiguous() if oneshot else None
+    bws = torch.empty(L.lib().crnn_lstm_bptt_workspace(B, H) // 4, device=DEV)
     for s in range(T):
-        L.call("crnn_lstm_step_bwd", dt, dh.data_ptr(), whh.data_ptr(), gsv.data_ptr(), csv.data_ptr(),
-               dg.data_ptr(), dc.data_ptr(), B, T, H, s, st)
+        L.call("crnn_lstm_step_bwd", dt, dh.data_ptr(), whh.data_ptr(), None if whh_t is None else whh_t.data_ptr(),
+               gsv.data_ptr(), csv.data_ptr(), dg.data_ptr(), dc.data_ptr(), bws.data_ptr(), B, T, H, s, st)
     dwhh = torch.empty(2, 4 * H, H, device=DEV)
     dwih = torch.empty(2, 4 * H, In, device=DEV)
     db = torch.empty(2, 4 * H, device=DEV)
