@@ -45,6 +45,10 @@ extern "C" {
 
 int crnn_version(void);
 const char* crnn_last_error_string(void);
+/* tuning switches, process-wide (benchmark A/B only; defaults are the measured-best settings) */
+enum { CRNN_OPT_GEMM_STAGGER = 0, /* 256-row conv GEMM: waves 4-7 one barrier behind waves 0-3 */
+       CRNN_OPT_COUNT = 1 };
+int crnn_set_option(int key, int value);
 
 /* ------------------------------------------------------------------ layout */
 /* fp32 NCHW image batch -> dtype NHWC with channels zero-padded to Cp. */

@@ -43,11 +43,14 @@ class PackJob(C.Structure):  # crnn_pack_job
                 ("src2", vp), ("perm", vp), ("dst", vp)]
 
 
+OPT_GEMM_STAGGER = 0   # crnn_set_option keys (include/crnn_hip.h)
+
 PACK_CONV, PACK_ROWS, PACK_ROWS_SUM, PACK_TRANSPOSE = 0, 1, 2, 3
 
 _SIGS = {
     "crnn_pack_batch": ([i32, vp, i32, i64, vp], i32),
     "crnn_version": ([], i32),
+    "crnn_set_option": ([i32, i32], i32),
     "crnn_last_error_string": ([], C.c_char_p),
     "crnn_nchw_to_nhwc": ([i32, vp, vp, i32, i32, i32, i32, i32, vp], i32),
     "crnn_cast_f32": ([i32, vp, vp, i64, vp], i32),

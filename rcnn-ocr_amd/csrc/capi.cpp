@@ -13,6 +13,17 @@ int crnn_set_error(int code, const char* msg) {
 
 extern "C" int crnn_version(void) { return 100; }
 
+// tuning switches (A/B in one process); defaults are the measured-best settings
+static int g_opts[CRNN_OPT_COUNT] = {1};
+
+int crnn_option(int key) { return (key >= 0 && key < CRNN_OPT_COUNT) ? g_opts[key] : 0; }
+
+extern "C" int crnn_set_option(int key, int value) {
+  if (key < 0 || key >= CRNN_OPT_COUNT) return crnn_set_error((int)hipErrorInvalidValue, "crnn_set_option: bad key");
+  g_opts[key] = value;
+  return 0;
+}
+
 extern "C" const char* crnn_last_error_string(void) {
   if (g_err[0]) return g_err;
   return hipGetErrorString(hipGetLastError());

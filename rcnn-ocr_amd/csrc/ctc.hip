@@ -178,7 +178,7 @@ int crnn_ctc_loss(const float* logits, int ldc, int B, int T, int C, const int* 
   if (sm > 160 * 1024) return crnn_set_error(hipErrorInvalidValue, "ctc_loss: T x (2*Lmax+1) too large for LDS");
   static bool attr_set = false;
   if (!attr_set) {
-    hipFuncSetAttribute((const void*)ctc_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)ctc_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
   hipLaunchKernelGGL(ctc_kernel, dim3(B), dim3(256), sm, (hipStream_t)stream, logits, ldc, T, C, targets, Lmax, lengths,

@@ -26,6 +26,9 @@
 #pragma once
 #include "gemm.hpp"
 
+#include "crnn_hip.h"
+int crnn_option(int key);  // capi.cpp (crnn_set_option)
+
 namespace gemm {
 
 typedef __attribute__((address_space(3))) void lds_void_t;
@@ -184,7 +187,7 @@ __device__ __forceinline__ uint32_t lds_addr(const char* p) {
 
 template <int BM, int BN, class LA, class LB, class EPI>
 __global__ __launch_bounds__(512) void gemm256_kernel(LA la, LB lb, EPI epi, int M, int N, int K, int klen,
-                                                      int tiles_m, int tiles_n, int nsplit) {
+                                                      int tiles_m, int tiles_n, int nsplit, int stagger) {
   using T = bf16;
   static_assert(BM == 256 && (BN == 256 || BN == 128), "tile");
   constexpr int KS = 64;
@@ -244,6 +247,9 @@ __global__ __launch_bounds__(512) void gemm256_kernel(LA la, LB lb, EPI epi, int
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   raw_barrier();
+  // ping-pong: waves 4-7 (wr == 1, one per SIMD) run one barrier behind waves 0-3, so each SIMD
+  // alternates one wave's MFMA cluster with its partner's ds_read / LDS-DMA issue segment
+  if (stagger && wr == 1) raw_barrier();
 
   bf16x8 af[MQ][2], bfr[NI][2];
   for (int t = 0; t < nk; ++t) {
@@ -260,8 +266,8 @@ __global__ __launch_bounds__(512) void gemm256_kernel(LA la, LB lb, EPI epi, int
     oa.template load<0, MQ>(af, As, lA, wr * WM, lane);
     ob.template load<0, NQ>(*reinterpret_cast<bf16x8(*)[NQ][2]>(&bfr[0]), Bs, lB, wc * WN, lane);
     if (n1) oa.issue(la, ra, sA0 + (b ^ 1) * STAGE, 1, pa1);
-    raw_barrier();
     lds_wait_all();
+    raw_barrier();
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
@@ -274,8 +280,8 @@ __global__ __launch_bounds__(512) void gemm256_kernel(LA la, LB lb, EPI epi, int
     // ---- P2: quadrant (0,1)
     ob.template load<1, NQ>(*reinterpret_cast<bf16x8(*)[NQ][2]>(&bfr[NQ]), Bs, lB, wc * WN, lane);
     if (n2) oa.issue(la, ra, sA0 + b * STAGE, 0, pa2);
-    raw_barrier();
     lds_wait_all();
+    raw_barrier();
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
@@ -288,8 +294,8 @@ __global__ __launch_bounds__(512) void gemm256_kernel(LA la, LB lb, EPI epi, int
     // ---- P3: quadrant (1,1)
     oa.template load<1, MQ>(af, As, lA, wr * WM, lane);
     if (n2) ob.issue(lb, rb, sB0 + b * STAGE, 0, pb2);
-    raw_barrier();
     lds_wait_all();
+    raw_barrier();
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
@@ -318,6 +324,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(LA la, LB lb, EPI epi, int
     __builtin_amdgcn_s_setprio(0);
     raw_barrier();
   }
+  if (stagger && wr == 0) raw_barrier();
 
   const int mr = lane & 15, nq = 4 * (lane >> 4);
 #pragma unroll
@@ -336,7 +343,7 @@ inline int launch256(const LA& la, const LB& lb, const EPI& epi, int M, int N, i
   const int klen = split_len(K, nsplit);
   nsplit = K > 0 ? (K + klen - 1) / klen : 1;
   hipLaunchKernelGGL((gemm256_kernel<BM, BN, LA, LB, EPI>), dim3(tm * tn * nsplit), dim3(512), 0, st, la, lb, epi,
-                     M, N, K, klen, tm, tn, nsplit);
+                     M, N, K, klen, tm, tn, nsplit, crnn_option(CRNN_OPT_GEMM_STAGGER));
   return (int)hipGetLastError();
 }
 

@@ -40,11 +40,17 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--only", default=None)
     ap.add_argument("--layer", type=int, default=None)
+    ap.add_argument("--opt", default=None, help="A/B a crnn_set_option key: KEY=V0,V1 (e.g. 0=0,1)")
     a = ap.parse_args()
     dev = torch.device("cuda")
     T = torch.bfloat16
     s = L.stream_ptr()
     tot = {}
+    key, variants = None, [("", None)]
+    if a.opt:
+        ks, vs = a.opt.split("=")
+        key = int(ks)
+        variants = [(f"[{v}]", int(v)) for v in vs.split(",")]
     for li, (name, cs, h, w) in enumerate(geometries(a.batch, 32, 256)):
         if a.layer is not None and li != a.layer:
             continue
@@ -76,17 +82,20 @@ def main():
                 continue
             if k == "dgrad" and name == "stem0":
                 continue
-            for _ in range(3):
-                fn()
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            for _ in range(a.iters):
-                fn()
-            e1.record()
-            torch.cuda.synchronize()
-            ms = e0.elapsed_time(e1) / a.iters
-            tot[k] = tot.get(k, 0.0) + ms
-            line += f" {k} {ms * 1e3:7.1f}us {flop / ms / 1e9:6.0f}TF |"
+            for tag, val in variants:
+                if key is not None:
+                    L.call("crnn_set_option", key, val)
+                for _ in range(3):
+                    fn()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(a.iters):
+                    fn()
+                e1.record()
+                torch.cuda.synchronize()
+                ms = e0.elapsed_time(e1) / a.iters
+                tot[k + tag] = tot.get(k + tag, 0.0) + ms
+                line += f" {k}{tag} {ms * 1e3:7.1f}us {flop / ms / 1e9:6.0f}TF |"
         print(line, flush=True)
     print("sum of distinct-geometry times (ms):", {k: round(v, 3) for k, v in tot.items()})
 
