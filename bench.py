@@ -76,6 +76,22 @@ def cpu_baseline(args, threads):
                       f"hidden {args.hidden}; {dt:.1f} s"}
 
 
+def lstm_roofline(lstm, args, eng):
+    """HBM roofline of the BiLSTM recurrence (north star: >= 40% on the step at B=256): algorithmic
+    bytes per step (CRNNEngine.lstm_step_bytes) x steps / measured sweep time."""
+    out = {}
+    for k, (n, ms, byt) in lstm.items():
+        gbs = byt / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
+        out[k] = {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                  "frac": round(gbs / PEAK_HBM_GBS, 4), "traffic": None,
+                  "sweeps_per_step": n // args.steps, "us_per_sweep": round(ms / n * 1e3, 2),
+                  "us_per_timestep": round(ms / n / (args.width // 8) * 1e3, 3),
+                  "algorithmic_bytes_per_timestep": byt / n / (args.width // 8)}
+    out["kernel"] = ("persistent whole-sequence BiLSTM (lstm_seq.hip)" if eng._seq_ok(args.batch)
+                     else "per-step BiLSTM launches (lstm.hip)")
+    return out
+
+
 def main():
     args = parse()
     from crnn_hip import dist as D
@@ -143,6 +159,7 @@ def main():
     final_loss = float(loss.item())
 
     if rank == 0:
+        lstm = {k: timing.pop(k) for k in ("lstm_fwd", "lstm_bwd") if k in timing}
         conv_launches = sum(v[0] for v in timing.values())
         conv_ms = sum(v[1] for v in timing.values())
         conv_flop = sum(v[2] for v in timing.values())
@@ -177,6 +194,7 @@ def main():
                          "kernel_ms_per_step": round(conv_ms / args.steps, 3),
                          "timing": "HIP events around every conv launch on the launch stream, timed region"},
             "kernels": per_kind,
+            "roofline_lstm": lstm_roofline(lstm, args, eng),
             "final_loss": round(final_loss, 4),
         }
         if world == 1 and not args.no_cpu_baseline:

@@ -219,6 +219,23 @@ int crnn_lstm_dbias(int dtype, const void* dgates, float* b_fwd, float* b2_fwd, 
 size_t crnn_lstm_dbias_workspace(int H);
 /* dx [B][T][In] (dtype) = sum_dir dgates . W_ih'  (wih packed [2][4H][In]) */
 int crnn_lstm_dx(int dtype, const void* dgates, const void* wih, void* dx, int B, int T, int H, int In, void* stream);
+/* Persistent whole-sequence recurrence (bf16 only; replaces the T per-step launches of
+ * crnn_lstm_step_fwd / crnn_lstm_step_bwd with ONE launch per layer and direction pair, same
+ * buffers and results). Supported when crnn_lstm_seq_supported() != 0: B % 32 == 0,
+ * H in {256, 512, 768} and 2*(B/32)*(H/32) workgroups <= the device's CU count (all resident).
+ * ws: crnn_lstm_seq_workspace(B) bytes of device memory, zeroed by the call itself:
+ * [2*B/32] step counters then one error word (non-zero after a bounded wait timed out, in which
+ * case the outputs carry NaN). */
+int crnn_lstm_seq_supported(int dtype, int B, int H);
+/* diagnostics: record per-phase s_memrealtime stamps of the following persistent launches into a
+ * device buffer of (grid * T * 8) u64 (NULL: off) */
+int crnn_lstm_seq_debug_stamps(unsigned long long* buf);
+size_t crnn_lstm_seq_workspace(int B);
+int crnn_lstm_seq_fwd(const void* xg, const void* whh, void* hseq, void* gsv, float* csv, unsigned* ws, int B, int T,
+                      int H, void* stream);
+/* BPTT: dhseq [B][T][2H] upstream grad, whh_t [2][H][4H] -> dgates [2][T][B][4H] */
+int crnn_lstm_seq_bwd(const void* dhseq, const void* whh_t, const void* gsv, const float* csv, void* dgates,
+                      unsigned* ws, int B, int T, int H, void* stream);
 
 /* ------------------------------------------------------------------ CTC */
 /* Per-sample log-space CTC over logits [B][T][ldc] (fp32, C classes, blank = 0, input length T).

@@ -90,6 +90,11 @@ _SIGS = {
     "crnn_lstm_dwih": ([i32, vp, vp, vp, vp, i32, i32, i32, i32, i32, vp], i32),
     "crnn_lstm_dbias": ([i32, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, vp], i32),
     "crnn_lstm_dbias_workspace": ([i32], sz),
+    "crnn_lstm_seq_supported": ([i32, i32, i32], i32),
+    "crnn_lstm_seq_workspace": ([i32], sz),
+    "crnn_lstm_seq_debug_stamps": ([vp], i32),
+    "crnn_lstm_seq_fwd": ([vp, vp, vp, vp, vp, vp, i32, i32, i32, vp], i32),
+    "crnn_lstm_seq_bwd": ([vp, vp, vp, vp, vp, vp, i32, i32, i32, vp], i32),
     "crnn_lstm_dx": ([i32, vp, vp, vp, i32, i32, i32, i32, vp], i32),
     "crnn_ctc_loss": ([vp, i32, i32, i32, i32, vp, i32, vp, vp, vp, i32, vp], i32),
     "crnn_ctc_reduce_mean": ([vp, vp, i32, vp, vp], i32),

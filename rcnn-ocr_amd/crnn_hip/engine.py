@@ -19,6 +19,7 @@ Data layout in HBM (all activations NHWC, compute dtype T = bf16 | fp32):
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Tuple
 
@@ -226,18 +227,43 @@ class CRNNEngine:
         self.timers = [] if on else None
 
     def _conv_call(self, kind, flops, name, *args):
-        if getattr(self, "timers", None) is None:
-            call(name, *args)
-            return
-        a = torch.cuda.Event(enable_timing=True)
-        b = torch.cuda.Event(enable_timing=True)
-        a.record()
+        t0 = self._mark()
         call(name, *args)
+        self._record(kind, flops, t0)
+
+    def _mark(self):
+        """start event on the current (launch) stream when timing is on, else None"""
+        if getattr(self, "timers", None) is None:
+            return None
+        a = torch.cuda.Event(enable_timing=True)
+        a.record()
+        return a
+
+    def _record(self, kind, work, start):
+        if start is None:
+            return
+        b = torch.cuda.Event(enable_timing=True)
         b.record()
-        self.timers.append((kind, flops, a, b))
+        self.timers.append((kind, work, start, b))
+
+    @staticmethod
+    def lstm_step_bytes(B, H, T):
+        """algorithmic HBM bytes of ONE forward recurrence step of one layer, both directions
+        (SURVEY.md §8d): W_hh + precomputed x-gates + h_{t-1} read / h_t write + c read/write (fp32)."""
+        s = 2 if T == torch.bfloat16 else 4
+        return 2 * (4 * H * H * s + B * 4 * H * s + 2 * B * H * s + 2 * B * H * 4)
+
+    @staticmethod
+    def lstm_bptt_step_bytes(B, H, T):
+        """the BPTT step's counterpart: W_hh + dgates_{t'} read + dgates_t write + saved gates read +
+        dh read + c_t, c_{t-1} read (fp32), both directions."""
+        s = 2 if T == torch.bfloat16 else 4
+        return 2 * (4 * H * H * s + 3 * B * 4 * H * s + B * H * s + 2 * B * H * 4)
 
     def conv_timing(self):
-        """{kind: (launches, total_ms, total_flop)} since enable_timing(); clears the list."""
+        """{kind: (launches, total_ms, total_work)} since enable_timing(); clears the list. Kinds:
+        conv fwd / dgrad / wgrad (work = FLOP) and lstm_fwd / lstm_bwd (recurrence sweeps, work =
+        algorithmic bytes)."""
         out = {}
         for kind, flops, a, b in self.timers or []:
             n, ms, fl = out.get(kind, (0, 0.0, 0.0))
@@ -259,6 +285,22 @@ class CRNNEngine:
         return t
 
     # ------------------------------------------------------------------ helpers
+    # persistent whole-sequence BiLSTM kernels (lstm_seq.hip): bf16, supported shapes only;
+    # CRNN_LSTM_PER_STEP=1 forces the per-step launches (A/B and fallback coverage)
+    use_seq = os.environ.get("CRNN_LSTM_PER_STEP", "0") != "1"
+
+    def _seq_ok(self, B):
+        return self.use_seq and bool(L.lib().crnn_lstm_seq_supported(self.dt, B, self.H))
+
+    def _seq_ws(self, B):
+        n = (L.lib().crnn_lstm_seq_workspace(B) + 3) // 4
+        return self.ws.get("rnn.seq_ws", (n,), torch.int32)
+
+    def seq_status(self) -> int:
+        """error word of the last persistent BiLSTM launch (0 = ok; non-zero: a bounded wait timed out)."""
+        t = self.ws.bufs.get("rnn.seq_ws")
+        return 0 if t is None else int(t[-1].item() if t.numel() else 0)
+
     def _bn_finalize(self, prefix, psum, psq, rows, count, train, tag, rpp=1):
         C = psum.shape[-1] if psum is not None else self.p[prefix + ".weight"].numel()
         ws = self.ws
@@ -417,8 +459,14 @@ class CRNNEngine:
             gsv = ws.get(f"r{l}.gates", (2, Tn, B, 4 * Hd), T)
             csv = ws.get(f"r{l}.c", (2, Tn, B, Hd), torch.float32)
             whh = self.packed[pre + ".whh"]
-            for st in range(Tn):
-                call("crnn_lstm_step_fwd", dt, ptr(xg), ptr(whh), ptr(hseq), ptr(gsv), ptr(csv), B, Tn, Hd, st, s)
+            t0 = self._mark()
+            if self._seq_ok(B):
+                call("crnn_lstm_seq_fwd", ptr(xg), ptr(whh), ptr(hseq), ptr(gsv), ptr(csv), ptr(self._seq_ws(B)), B,
+                     Tn, Hd, s)
+            else:
+                for st in range(Tn):
+                    call("crnn_lstm_step_fwd", dt, ptr(xg), ptr(whh), ptr(hseq), ptr(gsv), ptr(csv), B, Tn, Hd, st, s)
+            self._record("lstm_fwd", Tn * self.lstm_step_bytes(B, Hd, T), t0)
             out = ws.get(f"r{l}.out", (B, Tn, Hd), T)
             call("crnn_gemm_nt", dt, ptr(hseq), 2 * Hd, ptr(self.packed[pre + ".lin"]), 2 * Hd, ptr(out), Hd,
                  ptr(self.p[pre + ".linear.bias"]), B * Tn, Hd, 2 * Hd, 0, 0, s)
@@ -546,10 +594,16 @@ class CRNNEngine:
             dg = ws.get("rnn.dgates", (2, Tn, B, 4 * Hd), T)
             dc = ws.get("rnn.dc", (2, B, Hd), torch.float32)
             whh, whh_t = self.packed[pre + ".whh"], self.packed[pre + ".whh_t"]
-            bws = ws.get("rnn.bptt_ws", (L.lib().crnn_lstm_bptt_workspace(B, Hd) // 4,), torch.float32)
-            for stp in range(Tn):
-                call("crnn_lstm_step_bwd", dt, ptr(dh), ptr(whh), ptr(whh_t), ptr(r["gates"]), ptr(r["c"]), ptr(dg),
-                     ptr(dc), ptr(bws), B, Tn, Hd, stp, s)
+            t0 = self._mark()
+            if self._seq_ok(B):
+                call("crnn_lstm_seq_bwd", ptr(dh), ptr(whh_t), ptr(r["gates"]), ptr(r["c"]), ptr(dg),
+                     ptr(self._seq_ws(B)), B, Tn, Hd, s)
+            else:
+                bws = ws.get("rnn.bptt_ws", (L.lib().crnn_lstm_bptt_workspace(B, Hd) // 4,), torch.float32)
+                for stp in range(Tn):
+                    call("crnn_lstm_step_bwd", dt, ptr(dh), ptr(whh), ptr(whh_t), ptr(r["gates"]), ptr(r["c"]),
+                         ptr(dg), ptr(dc), ptr(bws), B, Tn, Hd, stp, s)
+            self._record("lstm_bwd", Tn * self.lstm_bptt_step_bytes(B, Hd, T), t0)
             rr = pre + ".rnn."
             gq = lambda n: ptr(self._gview(rr + n))
             # gradients straight into the parameters' .grad views (reference row order)

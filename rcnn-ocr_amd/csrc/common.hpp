@@ -101,6 +101,13 @@ __device__ __forceinline__ float tanhf_(float x) {
   return copysignf(t, x);
 }
 
+// bf16-path variants: hardware reciprocal (1 ulp) instead of the IEEE division sequence
+__device__ __forceinline__ float sigmoid_fast(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
+__device__ __forceinline__ float tanh_fast(float x) {
+  float e = __expf(-2.f * fabsf(x));
+  return copysignf((1.f - e) * __builtin_amdgcn_rcpf(1.f + e), x);
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -1,0 +1,415 @@
+// Persistent BiLSTM recurrence (bf16): the whole T-step sweep of one layer — forward recurrence
+// or BPTT — in ONE launch, both directions, W_hh resident in registers for all T steps.
+// Reference: nn.LSTM(in, H, bidirectional=True, batch_first=True), model/model.py:152-163
+// (gate order i,f,g,o; h0 = c0 = 0); the per-step kernels in lstm.hip compute the same thing
+// one launch per step (and remain the fp32 / unsupported-shape path).
+//
+// Decomposition (B = batch, H = hidden, T = steps): one workgroup per
+//   (direction d, batch slice bs of SEQ_S = 32 samples, unit slice ns of SEQ_U = 32 units),
+// 2 * (B/32) * (H/32) workgroups, 4 waves each, at most one per CU (all must be co-resident:
+// the host checks the grid against the CU count). The step GEMM's K is split over the 4 waves
+// (each wave holds its K-quarter of the W_hh slice as MFMA fragments in VGPRs, loaded once), the
+// four partial tiles are summed through LDS, and the cell math runs on the summed tile.
+//
+//   forward  step: gates[b][4u+q] = xg[b][t][d][4u+q] + sum_k h_{t-1}[b][k] W_hh'[4u+q][k]
+//                  (W_hh' = gate-interleaved packing, lstm.hip) -> c, h; saves gates, c for BPTT
+//   BPTT     step: dh_rec[b][u]   = sum_g dgates_{t'}[b][g] W_hh'[g][u]   (t' = the step before)
+//                  -> cell backward -> dgates_t (and the running dc, kept in registers)
+//
+// Per-step hand-off (cdna_hip_programming.md Guideline 16, MI355X_MICROARCH.md "Valid forms",
+// first table row): the only data crossing workgroups are h_t (forward) / dgates_t (BPTT) of a
+// batch slice, consumed by the 16..24 workgroups of the same (d, bs). Producers store them with
+// write-through (sc1) 16-B stores, every storing wave drains vmcnt(0), the workgroup barriers,
+// then ONE lane adds 1 (agent scope) to the slice's counter. A consumer's wave 0 polls that
+// counter with sc1 loads until it reaches (unit slices) x (steps done), the workgroup barriers,
+// and every load of the handed-off bytes is an sc1 buffer load to registers. Counters are zeroed
+// by a memset in the launch function. Every spin is bounded: on time-out the kernel records an
+// error word (ws[2*B/32], see include/crnn_hip.h) and the step's outputs carry NaN.
+#include "gemm.hpp"
+#include "crnn_internal.hpp"
+
+using namespace gemm;
+
+namespace {
+
+constexpr int SEQ_S = 32;  // samples per workgroup
+constexpr int SEQ_U = 32;  // hidden units per workgroup
+constexpr unsigned long long SEQ_TIMEOUT_TICKS = 50000000ull;  // s_memrealtime @100 MHz: 0.5 s per wait
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7fffffff, 0x00020000);
+}
+// write-through (sc1) 16-B load / store: the hand-off's only access kinds for shared bytes
+__device__ __forceinline__ bf16x8 ld_sc1(__amdgpu_buffer_rsrc_t r, uint32_t byteoff) {
+  return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(r, byteoff, 0, 16));
+}
+__device__ __forceinline__ void st_sc1(__amdgpu_buffer_rsrc_t r, uint32_t byteoff, bf16x8 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, byteoff, 0, 16);
+}
+
+// one lane: wait until *cnt >= target (relaxed agent-scope sc1 polls, s_sleep between polls)
+__device__ __noinline__ bool seq_wait(unsigned* cnt, unsigned target, unsigned* err) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+    if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return false;
+    if (__builtin_amdgcn_s_memrealtime() - t0 > SEQ_TIMEOUT_TICKS) {
+      __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+  return true;
+}
+
+// every storing wave drains its stores, the workgroup joins, one lane signals
+__device__ __forceinline__ void seq_publish(unsigned* cnt) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// optional per-phase timestamps (s_memrealtime, 10 ns) of workgroup `id`, step s: stamps[(id*T+s)*8+p]
+#define SEQ_STAMP(p)                                                                              \
+  if (stamps && threadIdx.x == 0) stamps[((size_t)blockIdx.x * Tn + s) * 8 + (p)] = __builtin_amdgcn_s_memrealtime()
+
+__device__ __forceinline__ void seq_coords(int nsl, int nbs, int& d, int& bs, int& ns) {
+  // logical id = (d * nbs + bs) * nsl + ns; xcd_remap keeps a (d, bs) group's workgroups together
+  const int nwg = 2 * nbs * nsl;
+  const int id = xcd_remap(blockIdx.x, nwg);
+  ns = id % nsl;
+  bs = (id / nsl) % nbs;
+  d = id / (nsl * nbs);
+}
+
+// ---------------------------------------------------------------- forward sweep
+// wave w: K-quarter [w*H/4, (w+1)*H/4); partial tile 32 samples x 128 gate rows (2 x 8 fragments).
+// It finalises fragment blocks q = 0..3: (i, j) = (q & 1, 2w + (q >> 1)).
+template <int H>
+__global__ __launch_bounds__(256) void lstm_seq_fwd_kernel(const bf16* __restrict__ xg, const bf16* __restrict__ whh,
+                                                           bf16* hseq, bf16* __restrict__ gsv, float* __restrict__ csv,
+                                                           unsigned* cnt, unsigned* err, int B, int Tn,
+                                                           unsigned long long* stamps) {
+  constexpr int KW = H / 4, KK = KW / 32;
+  constexpr int GR = 4 * SEQ_U, NJ = GR / 16;  // 128 gate rows, 8 fragments
+  constexpr int H4 = 4 * H;
+  static_assert(H % 128 == 0, "H");
+  // LDS: partials [wave][i][j][lane] f32x4 (64 KB) + h tile [32][32] bf16 (2 KB)
+  __shared__ __attribute__((aligned(16))) f32x4 part[4][2][NJ][64];
+  __shared__ __attribute__((aligned(16))) bf16 htile[SEQ_S][SEQ_U];
+
+  const int nsl = H / SEQ_U, nbs = B / SEQ_S;
+  int d, bs, ns;
+  seq_coords(nsl, nbs, d, bs, ns);
+  const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int b0 = bs * SEQ_S, n0 = ns * GR;
+  unsigned* mycnt = cnt + d * nbs + bs;
+
+  // W_hh' slice fragments: rows n0 + 16j + c, k = w*KW + 32kk + 8g
+  // register slot kk holds K-chunk (kk + rot) % KK: the 16 workgroups of a (d, bs) group read the
+  // handed-off h in rotated chunk order, spreading their simultaneous requests over memory channels
+  const int rot = ns % KK;
+  bf16x8 wf[NJ][KK];
+  {
+    const bf16* wb = whh + (size_t)d * H4 * H;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk) {
+        const int kc = kk + rot < KK ? kk + rot : kk + rot - KK;
+        wf[j][kk] = *reinterpret_cast<const bf16x8*>(wb + (size_t)(n0 + 16 * j + c) * H + w * KW + 32 * kc + 8 * g);
+      }
+  }
+  const __amdgpu_buffer_rsrc_t rh = rsrc_of(hseq);
+  float cst[4] = {0.f, 0.f, 0.f, 0.f};
+  f32x4 xv[4];
+  auto load_xg = [&](int t) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int i = q & 1, j = 2 * w + (q >> 1);
+      const int b = b0 + 16 * i + c, n = n0 + 16 * j + 4 * g;
+      xv[q] = ld4f<bf16>(xg + ((size_t)b * Tn + t) * 2 * H4 + d * H4 + n);
+    }
+  };
+  load_xg(d == 0 ? 0 : Tn - 1);
+
+  for (int s = 0; s < Tn; ++s) {
+    const int t = d == 0 ? s : Tn - 1 - s;
+    const int tp = d == 0 ? t - 1 : t + 1;
+    f32x4 sum[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) sum[q] = xv[q];
+    bool ok = true;
+    SEQ_STAMP(0);
+    if (s > 0) {
+      __shared__ int okflag;
+      if (threadIdx.x == 0) okflag = seq_wait(mycnt, (unsigned)(nsl * s), err) ? 1 : 0;
+      __syncthreads();
+      SEQ_STAMP(1);
+      ok = okflag != 0;
+      // A fragments: h_{tp}[b0 + 16i + c][w*KW + 32kk + 8g] (sc1: handed-off bytes)
+      bf16x8 af[2][KK];
+      const uint32_t abase = (uint32_t)((((size_t)b0 + c) * Tn + tp) * 2 * H + d * H + w * KW + 8 * g) * 2u;
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int kc = kk + rot < KK ? kk + rot : kk + rot - KK;
+          af[i][kk] = ld_sc1(rh, abase + (uint32_t)(i * 16 * Tn * 2 * H * 2 + kc * 64));
+        }
+      f32x4 acc[2][NJ];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) mma<bf16>(acc[i][j], wf[j][kk], af[i][kk]);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) part[w][i][j][lane] = acc[i][j];
+      SEQ_STAMP(2);
+      __syncthreads();
+      SEQ_STAMP(3);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int i = q & 1, j = 2 * w + (q >> 1);
+#pragma unroll
+        for (int ww = 0; ww < 4; ++ww) sum[q] += part[ww][i][j][lane];
+      }
+    }
+    // cell update for the 4 blocks: lane holds gates (i,f,g,o) of unit n/4 for one sample
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int i = q & 1, j = 2 * w + (q >> 1);
+      const int bl = 16 * i + c, b = b0 + bl;
+      const int n = n0 + 16 * j + 4 * g, u = n >> 2;
+      f32x4 v = sum[q];
+      const float ig = sigmoid_fast(v[0]), fg = sigmoid_fast(v[1]), gg = tanh_fast(v[2]), og = sigmoid_fast(v[3]);
+      float cc = fg * cst[q] + ig * gg;
+      float hh = og * tanh_fast(cc);
+      if (!ok) hh = cc = __builtin_nanf("");
+      cst[q] = cc;
+      csv[((size_t)(d * Tn + t) * B + b) * H + u] = cc;
+      st4<bf16>(gsv + ((size_t)(d * Tn + t) * B + b) * H4 + n, f32x4{ig, fg, gg, og});
+      htile[bl][4 * j + g] = (bf16)hh;
+    }
+    SEQ_STAMP(4);
+    __syncthreads();
+    // publish h_t of this (samples, units) tile: 32 rows x 64 B, 16 B per lane (waves 0-1)
+    if (threadIdx.x < 128) {
+      const int row = threadIdx.x >> 2, ch = threadIdx.x & 3;
+      const bf16x8 hv = *reinterpret_cast<const bf16x8*>(&htile[row][8 * ch]);
+      st_sc1(rh, (uint32_t)((((size_t)(b0 + row) * Tn + t) * 2 * H + d * H + ns * SEQ_U + 8 * ch) * sizeof(bf16)), hv);
+    }
+    SEQ_STAMP(5);
+    seq_publish(mycnt);
+    SEQ_STAMP(6);
+    if (s + 1 < Tn) load_xg(d == 0 ? t + 1 : t - 1);
+  }
+}
+
+// ---------------------------------------------------------------- BPTT sweep
+// wave w: K-quarter [w*H, (w+1)*H) of the 4H gate columns; partial tile 32 samples x 32 units
+// (2 x 2 fragments); it finalises block (i, j) = (w & 1, w >> 1): 16 samples x 16 units, one
+// sample and 4 consecutive units per lane.
+template <int H>
+__global__ __launch_bounds__(256) void lstm_seq_bwd_kernel(const bf16* __restrict__ dhseq, const bf16* __restrict__ whh_t,
+                                                           const bf16* __restrict__ gsv, const float* __restrict__ csv,
+                                                           bf16* dgates, unsigned* cnt, unsigned* err, int B, int Tn,
+                                                           unsigned long long* stamps) {
+  constexpr int KW = H, KK = KW / 32;
+  constexpr int H4 = 4 * H;
+  static_assert(H % 32 == 0, "H");
+  __shared__ __attribute__((aligned(16))) f32x4 part[4][2][2][64];
+
+  const int nsl = H / SEQ_U, nbs = B / SEQ_S;
+  int d, bs, ns;
+  seq_coords(nsl, nbs, d, bs, ns);
+  const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int b0 = bs * SEQ_S, u0 = ns * SEQ_U;
+  unsigned* mycnt = cnt + d * nbs + bs;
+
+  // W_hh'^T slice fragments: rows u0 + 16j + c of whh_t[d] ([H][4H]), k = w*KW + 32kk + 8g
+  const int rot = (ns * KK / nsl) % KK;   // rotated K-chunk order, as in the forward kernel
+  bf16x8 wf[2][KK];
+  {
+    const bf16* wb = whh_t + (size_t)d * H * H4;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk) {
+        const int kc = kk + rot < KK ? kk + rot : kk + rot - KK;
+        wf[j][kk] = *reinterpret_cast<const bf16x8*>(wb + (size_t)(u0 + 16 * j + c) * H4 + w * KW + 32 * kc + 8 * g);
+      }
+  }
+  const __amdgpu_buffer_rsrc_t rg = rsrc_of(dgates);
+  const int fi = w & 1, fj = w >> 1;
+  const int bl = 16 * fi + c, b = b0 + bl;
+  const int u = u0 + 16 * fj + 4 * g;  // this lane's 4 units u..u+3
+  float dcs[4] = {0.f, 0.f, 0.f, 0.f};
+
+  // per-step saved-forward inputs of this lane (independent of the recurrence: prefetched)
+  bf16x8 gv0, gv1;
+  f32x4 cv, cpv, dhv;
+  auto load_in = [&](int t) {
+    const size_t gi = ((size_t)(d * Tn + t) * B + b) * H4 + 4 * u;
+    gv0 = *reinterpret_cast<const bf16x8*>(gsv + gi);
+    gv1 = *reinterpret_cast<const bf16x8*>(gsv + gi + 8);
+    cv = *reinterpret_cast<const f32x4*>(csv + ((size_t)(d * Tn + t) * B + b) * H + u);
+    const int tf = d == 0 ? t - 1 : t + 1;
+    const bool has_prev = d == 0 ? t > 0 : t < Tn - 1;
+    cpv = has_prev ? *reinterpret_cast<const f32x4*>(csv + ((size_t)(d * Tn + tf) * B + b) * H + u)
+                   : f32x4{0.f, 0.f, 0.f, 0.f};
+    dhv = ld4f<bf16>(dhseq + ((size_t)b * Tn + t) * 2 * H + d * H + u);
+  };
+  load_in(d == 0 ? Tn - 1 : 0);
+
+  for (int s = 0; s < Tn; ++s) {
+    const int t = d == 0 ? Tn - 1 - s : s;
+    const int tn = d == 0 ? t + 1 : t - 1;  // time of the previous BPTT step
+    f32x4 dh = dhv;
+    bool ok = true;
+    SEQ_STAMP(0);
+    if (s > 0) {
+      __shared__ int okflag;
+      if (threadIdx.x == 0) okflag = seq_wait(mycnt, (unsigned)(nsl * s), err) ? 1 : 0;
+      __syncthreads();
+      SEQ_STAMP(1);
+      ok = okflag != 0;
+      bf16x8 af[2][KK];
+      const uint32_t abase = (uint32_t)((((size_t)(d * Tn + tn) * B + b0 + c) * H4 + w * KW + 8 * g) * 2u);
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int kc = kk + rot < KK ? kk + rot : kk + rot - KK;
+          af[i][kk] = ld_sc1(rg, abase + (uint32_t)(i * 16 * H4 * 2 + kc * 64));
+        }
+      f32x4 acc[2][2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) mma<bf16>(acc[i][j], wf[j][kk], af[i][kk]);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) part[w][i][j][lane] = acc[i][j];
+      SEQ_STAMP(2);
+      __syncthreads();
+      SEQ_STAMP(3);
+#pragma unroll
+      for (int ww = 0; ww < 4; ++ww) dh += part[ww][fi][fj][lane];
+    }
+    // cell backward of units u..u+3 (lstm.hip cell_bwd)
+    bf16x8 out0, out1;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const bf16x8& gv = r < 2 ? gv0 : gv1;
+      const int o = (r & 1) * 4;
+      const float ig = (float)gv[o], fg = (float)gv[o + 1], gg = (float)gv[o + 2], og = (float)gv[o + 3];
+      const float tc = tanh_fast(cv[r]);
+      const float dcv = dcs[r] + dh[r] * og * (1.f - tc * tc);
+      const float do_ = dh[r] * tc;
+      const float di = dcv * gg, dg = dcv * ig, df = dcv * cpv[r];
+      dcs[r] = dcv * fg;
+      float q0 = di * ig * (1.f - ig), q1 = df * fg * (1.f - fg), q2 = dg * (1.f - gg * gg), q3 = do_ * og * (1.f - og);
+      if (!ok) q0 = q1 = q2 = q3 = __builtin_nanf("");
+      bf16x8& ov = r < 2 ? out0 : out1;
+      ov[o] = (bf16)q0;
+      ov[o + 1] = (bf16)q1;
+      ov[o + 2] = (bf16)q2;
+      ov[o + 3] = (bf16)q3;
+    }
+    const uint32_t go = (uint32_t)((((size_t)(d * Tn + t) * B + b) * H4 + 4 * u) * sizeof(bf16));
+    SEQ_STAMP(4);
+    st_sc1(rg, go, out0);
+    st_sc1(rg, go + 16, out1);
+    SEQ_STAMP(5);
+    seq_publish(mycnt);
+    SEQ_STAMP(6);
+    if (s + 1 < Tn) load_in(d == 0 ? t - 1 : t + 1);
+  }
+}
+
+int g_cus = -1;
+unsigned long long* g_stamps = nullptr;  // crnn_lstm_seq_debug_stamps
+
+int seq_grid(int B, int H) { return 2 * (B / SEQ_S) * (H / SEQ_U); }
+
+}  // namespace
+
+extern "C" {
+
+int crnn_lstm_seq_supported(int dtype, int B, int H) {
+  if (dtype != CRNN_BF16 || B % SEQ_S || !(H == 256 || H == 512 || H == 768)) return 0;
+  if (g_cus < 0) {
+    int dev = 0;
+    hipDeviceProp_t p;
+    if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&p, dev) != hipSuccess) return 0;
+    g_cus = p.multiProcessorCount;
+  }
+  return seq_grid(B, H) <= g_cus ? 1 : 0;
+}
+
+// diagnostics: per-phase timestamps of the NEXT persistent launches into `buf` (device,
+// grid * T * 8 u64), NULL to stop. Not for production paths.
+int crnn_lstm_seq_debug_stamps(unsigned long long* buf) {
+  g_stamps = buf;
+  return 0;
+}
+
+size_t crnn_lstm_seq_workspace(int B) { return (size_t)((2 * (B / SEQ_S) + 1 + 3) / 4 * 16); }
+
+int crnn_lstm_seq_fwd(const void* xg, const void* whh, void* hseq, void* gsv, float* csv, unsigned* ws, int B, int T,
+                      int H, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (!crnn_lstm_seq_supported(CRNN_BF16, B, H)) return crnn_set_error(hipErrorInvalidValue, "lstm_seq: unsupported shape");
+  const int nbs = B / SEQ_S;
+  hipError_t e = hipMemsetAsync(ws, 0, crnn_lstm_seq_workspace(B), st);
+  if (e != hipSuccess) return (int)e;
+  unsigned* cnt = ws;
+  unsigned* err = ws + 2 * nbs;
+  const dim3 grid(seq_grid(B, H)), block(256);
+#define SEQ_FWD(HH)                                                                                                 \
+  hipLaunchKernelGGL(lstm_seq_fwd_kernel<HH>, grid, block, 0, st, (const bf16*)xg, (const bf16*)whh, (bf16*)hseq,   \
+                     (bf16*)gsv, csv, cnt, err, B, T, g_stamps)
+  if (H == 256) SEQ_FWD(256);
+  else if (H == 512) SEQ_FWD(512);
+  else SEQ_FWD(768);
+#undef SEQ_FWD
+  return (int)hipGetLastError();
+}
+
+int crnn_lstm_seq_bwd(const void* dhseq, const void* whh_t, const void* gsv, const float* csv, void* dgates,
+                      unsigned* ws, int B, int T, int H, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (!crnn_lstm_seq_supported(CRNN_BF16, B, H)) return crnn_set_error(hipErrorInvalidValue, "lstm_seq: unsupported shape");
+  const int nbs = B / SEQ_S;
+  hipError_t e = hipMemsetAsync(ws, 0, crnn_lstm_seq_workspace(B), st);
+  if (e != hipSuccess) return (int)e;
+  unsigned* cnt = ws;
+  unsigned* err = ws + 2 * nbs;
+  const dim3 grid(seq_grid(B, H)), block(256);
+#define SEQ_BWD(HH)                                                                                                   \
+  hipLaunchKernelGGL(lstm_seq_bwd_kernel<HH>, grid, block, 0, st, (const bf16*)dhseq, (const bf16*)whh_t,           \
+                     (const bf16*)gsv, csv, (bf16*)dgates, cnt, err, B, T, g_stamps)
+  if (H == 256) SEQ_BWD(256);
+  else if (H == 512) SEQ_BWD(512);
+  else SEQ_BWD(768);
+#undef SEQ_BWD
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

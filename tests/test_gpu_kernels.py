@@ -170,10 +170,13 @@ def _pack_lstm(w_ih, w_hh, b_ih, b_hh, H, dtype, L):
 @pytest.mark.parametrize("dtype,BTHI,oneshot", [
     (torch.float32, (3, 5, 32, 64), False), (torch.float32, (16, 8, 64, 128), False),
     (torch.bfloat16, (3, 5, 32, 64), False), (torch.bfloat16, (16, 8, 64, 128), True),
-    (torch.bfloat16, (3, 5, 32, 64), True), (torch.bfloat16, (64, 6, 512, 512), True)])
+    (torch.bfloat16, (3, 5, 32, 64), True), (torch.bfloat16, (64, 6, 512, 512), True),
+    (torch.bfloat16, (64, 6, 512, 512), "seq"), (torch.bfloat16, (32, 7, 256, 128), "seq"),
+    (torch.bfloat16, (64, 5, 768, 512), "seq"), (torch.bfloat16, (256, 4, 512, 512), "seq")])
 def test_bilstm_fwd_bwd(BTHI, dtype, oneshot):
     """bf16 steps run the one-shot LDS-DMA GEMM (forward: fused cell; backward with whh_t: split-K
-    partials + sum/cell pass; H = 512 -> 4 splits); oneshot=False passes no whh_t (staged kernel)."""
+    partials + sum/cell pass; H = 512 -> 4 splits); oneshot=False passes no whh_t (staged kernel);
+    "seq" runs the persistent whole-sequence kernels (lstm_seq.hip), one launch per sweep."""
     L = _L()
     import crnn_oracle as O
     B, T, H, In = BTHI
@@ -208,9 +211,18 @@ def test_bilstm_fwd_bwd(BTHI, dtype, oneshot):
     hseq = torch.empty(B, T, 2 * H, dtype=dtype, device=DEV)
     gsv = torch.empty(2, T, B, 4 * H, dtype=dtype, device=DEV)
     csv = torch.empty(2, T, B, H, device=DEV)
-    for s in range(T):
-        L.call("crnn_lstm_step_fwd", dt, xg.data_ptr(), whh.data_ptr(), hseq.data_ptr(), gsv.data_ptr(),
-               csv.data_ptr(), B, T, H, s, st)
+    seq = oneshot == "seq"
+    if seq:
+        assert L.lib().crnn_lstm_seq_supported(dt, B, H) == 1
+        sws = torch.full((L.lib().crnn_lstm_seq_workspace(B) // 4,), 7, dtype=torch.int32, device=DEV)
+        L.call("crnn_lstm_seq_fwd", xg.data_ptr(), whh.data_ptr(), hseq.data_ptr(), gsv.data_ptr(), csv.data_ptr(),
+               sws.data_ptr(), B, T, H, st)
+        assert int(sws[-1].item()) == 0   # no timed-out wait
+        assert int(sws[: 2 * (B // 32)].min().item()) == H // 32 * T   # every slice published every step
+    else:
+        for s in range(T):
+            L.call("crnn_lstm_step_fwd", dt, xg.data_ptr(), whh.data_ptr(), hseq.data_ptr(), gsv.data_ptr(),
+                   csv.data_ptr(), B, T, H, s, st)
     tol = 2e-5 if dtype == torch.float32 else 3e-2
     assert relerr(hseq.float().cpu(), href.detach()) < tol
     dh = dh_out.to(DEV, dtype).contiguous()
@@ -218,9 +230,20 @@ def test_bilstm_fwd_bwd(BTHI, dtype, oneshot):
     dc = torch.empty(2, B, H, device=DEV)
     whh_t = whh.transpose(1, 2).contiguous() if oneshot else None
     bws = torch.empty(L.lib().crnn_lstm_bptt_workspace(B, H) // 4, device=DEV)
-    for s in range(T):
-        L.call("crnn_lstm_step_bwd", dt, dh.data_ptr(), whh.data_ptr(), None if whh_t is None else whh_t.data_ptr(),
-               gsv.data_ptr(), csv.data_ptr(), dg.data_ptr(), dc.data_ptr(), bws.data_ptr(), B, T, H, s, st)
+    if seq:
+        L.call("crnn_lstm_seq_bwd", dh.data_ptr(), whh_t.data_ptr(), gsv.data_ptr(), csv.data_ptr(), dg.data_ptr(),
+               sws.data_ptr(), B, T, H, st)
+        assert int(sws[-1].item()) == 0
+        # the per-step path on the same saved forward agrees to bf16 rounding of dgates
+        dg2 = torch.empty_like(dg)
+        for s in range(T):
+            L.call("crnn_lstm_step_bwd", dt, dh.data_ptr(), whh.data_ptr(), whh_t.data_ptr(), gsv.data_ptr(),
+                   csv.data_ptr(), dg2.data_ptr(), dc.data_ptr(), bws.data_ptr(), B, T, H, s, st)
+        assert relerr(dg.float().cpu(), dg2.float().cpu()) < 2e-2
+    else:
+        for s in range(T):
+            L.call("crnn_lstm_step_bwd", dt, dh.data_ptr(), whh.data_ptr(), None if whh_t is None else whh_t.data_ptr(),
+                   gsv.data_ptr(), csv.data_ptr(), dg.data_ptr(), dc.data_ptr(), bws.data_ptr(), B, T, H, s, st)
     dwhh = torch.empty(2, 4 * H, H, device=DEV)
     dwih = torch.empty(2, 4 * H, In, device=DEV)
     db = torch.empty(2, 4 * H, device=DEV)

@@ -1,0 +1,78 @@
+"""Phase timing of the persistent BiLSTM kernels (lstm_seq.hip) from in-kernel s_memrealtime
+stamps (10 ns ticks). Prints per-phase medians and the hand-off latency (last producer's signal of
+step s-1 -> consumer past its wait at step s).   python tools/lstm_stamps.py [B T H]"""
+import os
+import sys
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "rcnn-ocr_amd"))
+from crnn_hip import _lib as L  # noqa: E402
+
+PH = ["start", "waited", "mfma+part", "reduced", "epilogue", "stored", "published"]
+
+
+def run(kind, B, T, H):
+    dev = torch.device("cuda")
+    st = L.stream_ptr()
+    g = torch.Generator(device="cpu").manual_seed(0)
+    xg = (torch.randn(B, T, 2, 4 * H, generator=g) * 0.5).to(dev, torch.bfloat16)
+    whh = (torch.randn(2, 4 * H, H, generator=g) / H ** 0.5).to(dev, torch.bfloat16)
+    whh_t = whh.transpose(1, 2).contiguous()
+    hseq = torch.zeros(B, T, 2 * H, device=dev, dtype=torch.bfloat16)
+    gsv = torch.zeros(2, T, B, 4 * H, device=dev, dtype=torch.bfloat16)
+    csv = torch.zeros(2, T, B, H, device=dev)
+    dg = torch.zeros(2, T, B, 4 * H, device=dev, dtype=torch.bfloat16)
+    ws = torch.zeros(L.lib().crnn_lstm_seq_workspace(B) // 4 + 4, dtype=torch.int32, device=dev)
+    grid = 2 * (B // 32) * (H // 32)
+    stamps = torch.zeros(grid * T * 8, dtype=torch.int64, device=dev)
+
+    def fwd():
+        L.call("crnn_lstm_seq_fwd", xg.data_ptr(), whh.data_ptr(), hseq.data_ptr(), gsv.data_ptr(), csv.data_ptr(),
+               ws.data_ptr(), B, T, H, st)
+
+    def bwd():
+        L.call("crnn_lstm_seq_bwd", hseq.data_ptr(), whh_t.data_ptr(), gsv.data_ptr(), csv.data_ptr(), dg.data_ptr(),
+               ws.data_ptr(), B, T, H, st)
+
+    fwd()
+    fn = fwd if kind == "fwd" else bwd
+    for _ in range(3):
+        fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(10):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) / 10 * 1e3
+    L.call("crnn_lstm_seq_debug_stamps", stamps.data_ptr())
+    fn()
+    torch.cuda.synchronize()
+    L.call("crnn_lstm_seq_debug_stamps", None)
+    s = stamps.view(grid, T, 8).cpu().numpy().astype(np.int64)
+    print(f"{kind}: B={B} T={T} H={H} grid={grid}: {us:.1f} us/sweep = {us / T:.2f} us/step (no stamps)")
+    steps = slice(2, T - 1)
+    d = s[:, steps, :]
+    for p in range(1, 7):
+        if p in (1, 2, 3):   # only for s > 0
+            pass
+        dt = (d[:, :, p] - d[:, :, p - 1]) * 10 / 1e3
+        print(f"  {PH[p - 1]:>10s} -> {PH[p]:<10s} median {np.median(dt):6.3f} us  p90 {np.percentile(dt, 90):6.3f}")
+    per_step = (s[:, 1:, 0] - s[:, :-1, 0]) * 10 / 1e3
+    print(f"  step period median {np.median(per_step):.3f} us")
+    # hand-off: group = same (d, bs); physical block -> logical via the same xcd remap is not needed:
+    # use all producers' published stamps of step s-1 vs this block's waited stamp at s (upper bound)
+    nb = s.shape[0]
+    last_pub = s[:, :-1, 6].max(axis=0)   # over all blocks
+    wait_done = s[:, 1:, 1]
+    lat = (wait_done - last_pub[None, :]) * 10 / 1e3
+    print(f"  last publish (any block, step s-1) -> waited (step s): median {np.median(lat):.3f} us")
+
+
+if __name__ == "__main__":
+    B, T, H = (int(a) for a in sys.argv[1:4]) if len(sys.argv) > 3 else (256, 32, 512)
+    run("fwd", B, T, H)
+    run("bwd", B, T, H)
