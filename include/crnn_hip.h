@@ -134,6 +134,9 @@ int crnn_maxpool_bwd(int dtype, const void* z, const float* scale, const float* 
 #define CRNN_BNG_RELU 1  /* g = dy * (z*scale+shift > 0)             */
 #define CRNN_BNG_RESID 2 /* g = dy * (y > 0)                         */
 #define CRNN_BNG_SE 3    /* g = dy * (y > 0) * s[b][c] + dpool[b][c] */
+#define CRNN_BNG_POOL 4  /* BN -> ReLU -> MaxPool2d(2,2): dy = POOLED grad [B][H/2][W/2][C],   \
+                            HW = full-res W (even H, W); g = dy at the window's first max of \
+                            relu(z*scale+shift) when > 0, else 0 (crnn_maxpool_bwd fused)  */
 typedef struct {
   const void* dy;
   const void* z;

@@ -705,12 +705,11 @@ class CRNNEngine:
         if self.debug:
             self.dbg["dpool"] = dp[: B * (st["h1"] // 2) * (st["w1"] // 2) * 128].clone()
         h1, w1 = st["h1"], st["w1"]
-        dyf = bufs[o1][: B * h1 * w1 * 128]
-        call("crnn_maxpool_bwd", dt, ptr(st["z1"]), ptr(st["sc1"]), ptr(st["sh1"]), ptr(dp), ptr(dyf), B, h1, w1,
-             128, s)
+        # BN -> ReLU -> MaxPool backward in one pass pair (CRNN_BNG_POOL: the pooled gradient is
+        # routed to each window's first maximum inside the BN-backward reduce / apply kernels)
         dz1 = bufs[o2][: B * h1 * w1 * 128]
-        self._bn_bwd(1, dyf, st["z1"], (st["m1"], st["i1"], st["sc1"], st["sh1"]), self.stem1.bn, B * h1 * w1, 128,
-                     out=dz1, accumulate_params=accumulate)
+        self._bn_bwd(4, dp, st["z1"], (st["m1"], st["i1"], st["sc1"], st["sh1"]), self.stem1.bn, B * h1 * w1, 128,
+                     HW=w1, out=dz1, accumulate_params=accumulate)
         self._wgrad(self.stem1, dz1, st["a0"], B, h1, w1)
         da0 = bufs[o1][: B * h1 * w1 * 64]
         self._conv_call("dgrad", self.conv_flops(self.stem1, B, h1, w1), "crnn_conv_dgrad", dt, self.stem1.desc(B, h1, w1), ptr(dz1), ptr(self.packed[self.stem1.name]),

@@ -426,90 +426,269 @@ __global__ void maxpool_bwd_kernel(const T* __restrict__ z, const float* __restr
 }
 
 // ------------------------------------------------------------ SE
-__global__ void se_mlp_fwd_kernel(const float* __restrict__ pooled, const float* __restrict__ w1,
-                                  const float* __restrict__ w2, float* __restrict__ hid, float* __restrict__ s,
-                                  int C, int Cr) {
-  extern __shared__ float sm[];  // pooled[C], hid[Cr]
-  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  float* p = sm;
-  float* h = sm + C;
-  for (int c = tid; c < C; c += blockDim.x) p[c] = pooled[(size_t)b * C + c];
+// SELayer.fc (model/seresnet31.py:9-14, 16-20): Linear(C, C/16, bias=False) -> ReLU ->
+// Linear(C/16, C, bias=False) -> Sigmoid on the pooled [B][C] vector, and its backward.
+// Tiny GEMMs whose cost is memory round trips, not FLOPs: every global access is a 16-B vector,
+// all of a phase's loads are issued before its first FMA, and they are UNCONDITIONAL (clamped
+// addresses, masked values) — a load under a runtime condition makes hipcc branch around it and
+// wait for it on the spot (cdna_hip_programming.md §5, trap 4(c)), serialising the batch.
+// C is a template parameter (the SE-ResNet31 widths 256 / 512; Cr = C/16); SB samples per block
+// share each weight read.
+constexpr int SE_SB = 4;
+
+// butterfly reduce-scatter: 32 values per lane summed over the 64 lanes of the wave; on return
+// v[0] of lanes 2i and 2i+1 holds the full sum of value i (halving exchanges at xor 32..2, then 1)
+__device__ __forceinline__ void reduce_scatter32(float (&v)[32], int lane) {
+#pragma unroll
+  for (int step = 0; step < 5; ++step) {
+    const int o = 32 >> step, h = 16 >> step;
+    const bool hi = (lane & o) != 0;
+#pragma unroll
+    for (int i = 0; i < h; ++i) {
+      const float send = hi ? v[i] : v[i + h];
+      const float keep = hi ? v[i + h] : v[i];
+      v[i] = keep + __shfl_xor(send, o, 64);
+    }
+  }
+  v[0] += __shfl_xor(v[0], 1, 64);
+}
+
+// sum over aligned groups of G (2, 4 or 8) lanes with DPP moves; every lane gets its group's sum
+template <int CTRL> __device__ __forceinline__ float dppf(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+template <int G> __device__ __forceinline__ float rowgroup_sum(float v) {
+  static_assert(G == 2 || G == 4 || G == 8, "group");
+  v += dppf<0xB1>(v);                        // quad_perm [1,0,3,2]
+  if constexpr (G >= 4) v += dppf<0x4E>(v);  // quad_perm [2,3,0,1]
+  if constexpr (G >= 8) v += dppf<0x141>(v); // row_half_mirror: quad 0 <-> quad 1 of each 8
+  return v;
+}
+
+__device__ __forceinline__ float dot4(f32x4 a, f32x4 b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2] + a[3] * b[3]; }
+
+template <int C>
+__global__ __launch_bounds__(256) void se_mlp_fwd_kernel(const float* __restrict__ pooled, const float* __restrict__ w1,
+                                                         const float* __restrict__ w2, float* __restrict__ hid,
+                                                         float* __restrict__ s, int B) {
+  constexpr int Cr = C / 16, KC = C / 256;   // KC: 16-B column pieces per lane per w1 row
+  __shared__ __attribute__((aligned(16))) float p[SE_SB][C];
+  __shared__ __attribute__((aligned(16))) float h[SE_SB][Cr];
+  const int b0 = blockIdx.x * SE_SB, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int nb = min(SE_SB, B - b0);
+#pragma unroll
+  for (int q = 0; q < SE_SB * C / 1024; ++q) {
+    const int i = 4 * tid + 1024 * q, sb = i / C;
+    const f32x4 v = *reinterpret_cast<const f32x4*>(pooled + (size_t)(b0 + min(sb, nb - 1)) * C + i % C);
+    *reinterpret_cast<f32x4*>(&p[0][0] + i) = sb < nb ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
   __syncthreads();
-  for (int r = wid; r < Cr; r += blockDim.x / 64) {
-    float acc = 0.f;
-    for (int c = lane; c < C; c += 64) acc += p[c] * w1[(size_t)r * C + c];
-    acc = wave_sum(acc);
-    if (lane == 0) {
-      h[r] = fmaxf(acc, 0.f);
-      hid[(size_t)b * Cr + r] = h[r];
+  // hidden = relu(p . W1^T): thread (row r = tid % Cr, channel chunk ck = tid / Cr of CK channels)
+  // accumulates its chunk's dot products for the SB samples; chunks fold through LDS (no
+  // cross-lane shuffles)
+  {
+    constexpr int NCK = 256 / Cr, CK = C / NCK;
+    __shared__ float red[NCK][SE_SB][Cr];
+    const int r = tid % Cr, ck = tid / Cr, cbeg = ck * CK;
+    f32x4 wv[CK / 4];
+#pragma unroll
+    for (int q = 0; q < CK / 4; ++q) wv[q] = *reinterpret_cast<const f32x4*>(w1 + (size_t)r * C + cbeg + 4 * q);
+#pragma unroll
+    for (int sb = 0; sb < SE_SB; ++sb) {
+      float a = 0.f;
+#pragma unroll
+      for (int q = 0; q < CK / 4; ++q) a += dot4(*reinterpret_cast<const f32x4*>(&p[sb][cbeg + 4 * q]), wv[q]);
+      red[ck][sb][r] = a;
+    }
+    __syncthreads();
+    if (tid < SE_SB * Cr) {
+      const int sb = tid / Cr, rr = tid % Cr;
+      float a = 0.f;
+#pragma unroll
+      for (int k = 0; k < NCK; ++k) a += red[k][sb][rr];
+      a = fmaxf(a, 0.f);
+      h[sb][rr] = a;
+      if (sb < nb) hid[(size_t)(b0 + sb) * Cr + rr] = a;
     }
   }
   __syncthreads();
-  for (int c = tid; c < C; c += blockDim.x) {
-    float acc = 0.f;
-    for (int r = 0; r < Cr; ++r) acc += h[r] * w2[(size_t)c * Cr + r];
-    s[(size_t)b * C + c] = 1.f / (1.f + expf(-acc));
+  // s = sigmoid(h . W2^T): lane = (row group rg = lane % G of 4 hidden units, channel sub-row
+  // cs = lane / G): one instruction reads R whole w2 rows (contiguous); the G lanes of a row fold
+  // their 4-unit partials with DPP moves (quad / half-row permutes, no LDS round trip)
+  {
+    constexpr int G = Cr / 4, R = 64 / G, CQ = C / 4, NI = CQ / R;
+    const int rg = lane % G, cs = lane / G, cbeg = wid * CQ;
+    f32x4 wv[NI];
+#pragma unroll
+    for (int k = 0; k < NI; ++k) wv[k] = *reinterpret_cast<const f32x4*>(w2 + (size_t)(cbeg + k * R + cs) * Cr + 4 * rg);
+#pragma unroll
+    for (int k = 0; k < NI; ++k) {
+      const int c = cbeg + k * R + cs;
+      float out = 0.f;
+#pragma unroll
+      for (int sb = 0; sb < SE_SB; ++sb) {
+        float a = dot4(*reinterpret_cast<const f32x4*>(&h[sb][4 * rg]), wv[k]);
+        a = rowgroup_sum<G>(a);
+        out = rg == sb ? a : out;
+      }
+      if (rg < nb) s[(size_t)(b0 + rg) * C + c] = 1.f / (1.f + expf(-out));
+    }
   }
 }
 
-__global__ void se_mlp_bwd_kernel(const float* __restrict__ ds, const float* __restrict__ hid,
-                                  const float* __restrict__ s, const float* __restrict__ w1,
-                                  const float* __restrict__ w2, float* __restrict__ dsig, float* __restrict__ dhid,
-                                  float* __restrict__ dpool, int C, int Cr, float inv_hw) {
-  extern __shared__ float sm[];  // dsig[C], dhid[Cr]
-  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  float* dg = sm;
-  float* dh = sm + C;
-  for (int c = tid; c < C; c += blockDim.x) {
-    float sv = s[(size_t)b * C + c];
-    float v = ds[(size_t)b * C + c] * sv * (1.f - sv);
-    dg[c] = v;
-    dsig[(size_t)b * C + c] = v;
+// backward for SB samples per block: dsig = ds*s(1-s); dhid = (hid>0) * W2^T dsig;
+// dpool = W1^T dhid / HW (the pool's mean folded in)
+template <int C>
+__global__ __launch_bounds__(256) void se_mlp_bwd_kernel(const float* __restrict__ ds, const float* __restrict__ hid,
+                                                         const float* __restrict__ s, const float* __restrict__ w1,
+                                                         const float* __restrict__ w2, float* __restrict__ dsig,
+                                                         float* __restrict__ dhid, float* __restrict__ dpool, int B,
+                                                         float inv_hw) {
+  constexpr int Cr = C / 16;
+  constexpr int G = Cr / 4, R = 64 / G;   // lanes per w2 row (16 B each), w2 rows per wave-instruction
+  constexpr int CQ = C / 4, NI = CQ / R;  // channels per wave, load instructions per lane
+  __shared__ __attribute__((aligned(16))) float dg[SE_SB][C];
+  __shared__ __attribute__((aligned(16))) float red[4][SE_SB][Cr];
+  __shared__ __attribute__((aligned(16))) float dh[SE_SB][Cr];
+  const int b0 = blockIdx.x * SE_SB, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int nb = min(SE_SB, B - b0);
+#pragma unroll
+  for (int q = 0; q < SE_SB * C / 1024; ++q) {
+    const int i = 4 * tid + 1024 * q, sb = i / C;
+    const size_t o = (size_t)(b0 + min(sb, nb - 1)) * C + i % C;
+    const f32x4 sv = *reinterpret_cast<const f32x4*>(s + o);
+    const f32x4 dv = *reinterpret_cast<const f32x4*>(ds + o);
+    f32x4 v;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = dv[e] * sv[e] * (1.f - sv[e]);
+    if (sb < nb) *reinterpret_cast<f32x4*>(dsig + o) = v;
+    *reinterpret_cast<f32x4*>(&dg[0][0] + i) = sb < nb ? v : f32x4{0.f, 0.f, 0.f, 0.f};
   }
   __syncthreads();
-  for (int r = wid; r < Cr; r += blockDim.x / 64) {
-    float acc = 0.f;
-    for (int c = lane; c < C; c += 64) acc += dg[c] * w2[(size_t)c * Cr + r];
-    acc = wave_sum(acc);
-    if (lane == 0) {
-      float v = hid[(size_t)b * Cr + r] > 0.f ? acc : 0.f;
-      dh[r] = v;
-      dhid[(size_t)b * Cr + r] = v;
+  // W2^T dg: lane = (row group rg = lane % G, channel sub-row cs = lane / G); wave w sums the
+  // channels [w*CQ, (w+1)*CQ): NI 16-B loads per lane, all issued first
+  {
+    const int rg = lane % G, cs = lane / G, cbeg = wid * CQ;
+    f32x4 wv[NI];
+#pragma unroll
+    for (int k = 0; k < NI; ++k) wv[k] = *reinterpret_cast<const f32x4*>(w2 + (size_t)(cbeg + k * R + cs) * Cr + 4 * rg);
+    f32x4 acc[SE_SB];
+#pragma unroll
+    for (int sb = 0; sb < SE_SB; ++sb) {
+      acc[sb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k = 0; k < NI; ++k) acc[sb] += dg[sb][cbeg + k * R + cs] * wv[k];
     }
+    // fold the R channel sub-rows (lanes with equal rg): xor over the lane bits above G
+#pragma unroll
+    for (int sb = 0; sb < SE_SB; ++sb)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int o = G; o < 64; o <<= 1) acc[sb][e] += __shfl_xor(acc[sb][e], o, 64);
+    if (cs == 0)
+#pragma unroll
+      for (int sb = 0; sb < SE_SB; ++sb) *reinterpret_cast<f32x4*>(&red[wid][sb][4 * rg]) = acc[sb];
   }
   __syncthreads();
-  for (int c = tid; c < C; c += blockDim.x) {
-    float acc = 0.f;
-    for (int r = 0; r < Cr; ++r) acc += dh[r] * w1[(size_t)r * C + c];
-    dpool[(size_t)b * C + c] = acc * inv_hw;
+  if (tid < SE_SB * Cr) {
+    const int sb = tid / Cr, r = tid % Cr;
+    const float a = red[0][sb][r] + red[1][sb][r] + red[2][sb][r] + red[3][sb][r];
+    const float hv = hid[(size_t)(b0 + min(sb, nb - 1)) * Cr + r];
+    const float v = sb < nb && hv > 0.f ? a : 0.f;
+    dh[sb][r] = v;
+    if (sb < nb) dhid[(size_t)(b0 + sb) * Cr + r] = v;
+  }
+  __syncthreads();
+  // dpool: thread = 4 consecutive channels, w1 columns by 16-B loads over all Cr rows
+  if (4 * tid < C) {
+    const int c4 = 4 * tid;
+    f32x4 wv[Cr];
+#pragma unroll
+    for (int r = 0; r < Cr; ++r) wv[r] = *reinterpret_cast<const f32x4*>(w1 + (size_t)r * C + c4);
+#pragma unroll
+    for (int sb = 0; sb < SE_SB; ++sb) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int r = 0; r < Cr; ++r) acc += dh[sb][r] * wv[r];
+      if (sb < nb) *reinterpret_cast<f32x4*>(dpool + (size_t)(b0 + sb) * C + c4) = acc * inv_hw;
+    }
   }
 }
 
 // dw2[c][r] = sum_b dsig[b][c] hid[b][r] ; dw1[r][c] = sum_b dhid[b][r] pooled[b][c]
-// block = 64 channels x 4 batch lanes for one r; batch split over the lanes, LDS combine.
+// block (x, y): 64 channels (16 groups of 4, one 16-B load each) x rows r0 = 8y .. 8y+7;
+// 16 batch lanes (4 per wave x 4 waves) take interleaved samples; fixed-order combine
+// (shuffles inside a wave, then LDS across waves): deterministic.
+template <int C>
 __global__ __launch_bounds__(256) void se_wgrad_kernel(const float* __restrict__ dsig, const float* __restrict__ hid,
                                                        const float* __restrict__ dhid,
                                                        const float* __restrict__ pooled, float* __restrict__ dw1,
-                                                       float* __restrict__ dw2, int B, int C, int Cr, int accumulate) {
-  __shared__ float red[2][4][64];
-  const int lc = threadIdx.x & 63, ln = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + lc, r = blockIdx.y;
-  float a2 = 0.f, a1 = 0.f;
-  if (c < C)
-    for (int b = ln; b < B; b += 4) {
-      a2 += dsig[(size_t)b * C + c] * hid[(size_t)b * Cr + r];
-      a1 += dhid[(size_t)b * Cr + r] * pooled[(size_t)b * C + c];
+                                                       float* __restrict__ dw2, int B, int accumulate) {
+  constexpr int Cr = C / 16;
+  __shared__ __attribute__((aligned(16))) f32x4 red[4][16][16];   // [wave][value][c-group]
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int cgp = lane & 15, bl = (lane >> 4) + 4 * wid;         // channel group, batch lane 0..15
+  const int c4 = blockIdx.x * 64 + 4 * cgp, r0 = blockIdx.y * 8;
+  f32x4 a2[8], a1[8];   // a2[rr] = dw2[c4..c4+3][r0+rr], a1[rr] = dw1[r0+rr][c4..c4+3]
+#pragma unroll
+  for (int rr = 0; rr < 8; ++rr) a2[rr] = a1[rr] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int bb = bl; bb < B; bb += 64) {   // 4 samples per lane per batch, all loads first
+    f32x4 dv[4], pv[4], hv[4][2], dhv[4][2];
+    float mk[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int b = min(bb + 16 * j, B - 1);   // clamped: the value is masked below
+      mk[j] = bb + 16 * j < B ? 1.f : 0.f;
+      dv[j] = *reinterpret_cast<const f32x4*>(dsig + (size_t)b * C + c4);
+      pv[j] = *reinterpret_cast<const f32x4*>(pooled + (size_t)b * C + c4);
+#pragma unroll
+      for (int hq = 0; hq < 2; ++hq) {
+        hv[j][hq] = *reinterpret_cast<const f32x4*>(hid + (size_t)b * Cr + r0 + 4 * hq);
+        dhv[j][hq] = *reinterpret_cast<const f32x4*>(dhid + (size_t)b * Cr + r0 + 4 * hq);
+      }
     }
-  red[0][ln][lc] = a2;
-  red[1][ln][lc] = a1;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const f32x4 dm = dv[j] * mk[j], pm = pv[j] * mk[j];
+#pragma unroll
+      for (int rr = 0; rr < 8; ++rr) {
+        a2[rr] += dm * hv[j][rr >> 2][rr & 3];
+        a1[rr] += dhv[j][rr >> 2][rr & 3] * pm;
+      }
+    }
+  }
+  // fold the 4 batch lanes of this wave (lane bits 4, 5), then the 4 waves
+#pragma unroll
+  for (int rr = 0; rr < 8; ++rr)
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int o = 16; o < 64; o <<= 1) {
+        a2[rr][e] += __shfl_xor(a2[rr][e], o, 64);
+        a1[rr][e] += __shfl_xor(a1[rr][e], o, 64);
+      }
+  if (lane < 16)
+#pragma unroll
+    for (int rr = 0; rr < 8; ++rr) {
+      red[wid][rr][cgp] = a2[rr];
+      red[wid][8 + rr][cgp] = a1[rr];
+    }
   __syncthreads();
-  if (ln != 0 || c >= C) return;
-  const float v2 = red[0][0][lc] + red[0][1][lc] + red[0][2][lc] + red[0][3][lc];
-  const float v1 = red[1][0][lc] + red[1][1][lc] + red[1][2][lc] + red[1][3][lc];
-  float* p2 = dw2 + (size_t)c * Cr + r;
-  float* p1 = dw1 + (size_t)r * C + c;
-  *p2 = accumulate ? *p2 + v2 : v2;
-  *p1 = accumulate ? *p1 + v1 : v1;
+  // finalise: thread (value k = tid / 16, c-group = tid % 16)
+  const int k = threadIdx.x >> 4, cg2 = threadIdx.x & 15;
+  const int rr = k & 7, r = r0 + rr, cc = blockIdx.x * 64 + 4 * cg2;
+  const f32x4 v = red[0][k][cg2] + red[1][k][cg2] + red[2][k][cg2] + red[3][k][cg2];
+  if (k < 8) {   // dw2[cc + e][r], stride Cr
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float* p = dw2 + (size_t)(cc + e) * Cr + r;
+      *p = accumulate ? *p + v[e] : v[e];
+    }
+  } else {
+    f32x4* p = reinterpret_cast<f32x4*>(dw1 + (size_t)r * C + cc);
+    *p = accumulate ? *p + v : v;
+  }
 }
 
 // ------------------------------------------------------------ height collapse
@@ -704,6 +883,46 @@ __device__ __forceinline__ void bng(const crnn_bn_bwd_desc& d, size_t o, const f
   }
 }
 
+// CRNN_BNG_POOL — BN -> ReLU -> MaxPool2d(2,2) of the stem (model/seresnet31.py:83-88) with the
+// max-pool backward fused in: d.dy is the POOLED gradient [B][H/2][W/2][C] and d.HW the full-res
+// width W. Window i (pooled pixel) covers full-res rows (2*(i / Wo) + dh) * W + 2*(i % Wo) + dw; the
+// gradient of each row is dpool at the window's first maximum of relu(z*scale+shift) (torch's
+// max_pool2d index, scan order h then w) when that value is > 0, else 0.
+template <typename T>
+__device__ __forceinline__ void pool_window(const crnn_bn_bwd_desc& d, const FastDiv& dWo, long i, int c8,
+                                            const float* sc, const float* sh, float (&z)[4][8], float (&g)[4][8],
+                                            size_t (&o)[4]) {
+  uint32_t wo;
+  const uint32_t bho = dWo.divmod((uint32_t)i, wo);
+  const int W = d.HW;
+  float best[8];
+  int arg[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    best[k] = -INFINITY;
+    arg[k] = 0;
+  }
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    o[t] = ((size_t)(2 * bho + (t >> 1)) * W + 2 * wo + (t & 1)) * d.C + c8;
+    unpack8<T>(ld8<T>((const T*)d.z + o[t]), z[t]);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float v = fmaxf(z[t][k] * sc[k] + sh[k], 0.f);
+      if (v > best[k]) {
+        best[k] = v;
+        arg[k] = t;
+      }
+    }
+  }
+  float dp[8];
+  unpack8<T>(ld8<T>((const T*)d.dy + (size_t)i * d.C + c8), dp);
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) g[t][k] = (arg[k] == t && z[t][k] * sc[k] + sh[k] > 0.f) ? dp[k] : 0.f;
+}
+
 template <typename T, int MODE>
 __global__ __launch_bounds__(NT) void bnb_reduce_kernel(crnn_bn_bwd_desc d, FastDiv dHW, long rpb,
                                                         float* __restrict__ p0, float* __restrict__ p1) {
@@ -713,14 +932,29 @@ __global__ __launch_bounds__(NT) void bnb_reduce_kernel(crnn_bn_bwd_desc d, Fast
   float mean[8], inv[8], sc[8], sh[8], s8[8], dp8[8], a0[8], a1[8];
   ld8f(d.mean + q.c8, mean);
   ld8f(d.invstd + q.c8, inv);
-  if (MODE == CRNN_BNG_RELU) {
+  if (MODE == CRNN_BNG_RELU || MODE == CRNN_BNG_POOL) {
     ld8f(d.scale + q.c8, sc);
     ld8f(d.shift + q.c8, sh);
   }
 #pragma unroll
   for (int i = 0; i < 8; ++i) a0[i] = a1[i] = 0.f;
-  const long m0 = blockIdx.x * rpb, m1 = min(d.M, m0 + rpb);
+  const long mend = MODE == CRNN_BNG_POOL ? d.M / 4 : d.M;  // pool mode: rows = windows
+  const long m0 = blockIdx.x * rpb, m1 = min(mend, m0 + rpb);
   uint32_t cb = 0xffffffffu;
+  if constexpr (MODE == CRNN_BNG_POOL) {
+    for (long m = m0 + q.r; m < m1; m += q.rl) {
+      float z[4][8], g[4][8];
+      size_t o[4];
+      pool_window<T>(d, dHW, m, q.c8, sc, sh, z, g, o);
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          a0[i] += g[t][i];
+          a1[i] += g[t][i] * ((z[t][i] - mean[i]) * inv[i]);
+        }
+    }
+  } else
   for (long m = m0 + q.r; m < m1; m += q.rl) {
     const size_t o = (size_t)m * C + q.c8;
     if constexpr (MODE == CRNN_BNG_SE) {
@@ -778,12 +1012,28 @@ __global__ __launch_bounds__(NT) void bnb_apply_kernel(crnn_bn_bwd_desc d, FastD
       Cg[i] = A[i] * g1[i];
     }
   }
-  if (MODE == CRNN_BNG_RELU) {
+  if (MODE == CRNN_BNG_RELU || MODE == CRNN_BNG_POOL) {
     ld8f(d.scale + q.c8, sc);
     ld8f(d.shift + q.c8, sh);
   }
-  const long m0 = blockIdx.x * rpb, m1 = min(d.M, m0 + rpb);
+  const long mend = MODE == CRNN_BNG_POOL ? d.M / 4 : d.M;
+  const long m0 = blockIdx.x * rpb, m1 = min(mend, m0 + rpb);
   uint32_t cb = 0xffffffffu;
+  if constexpr (MODE == CRNN_BNG_POOL) {
+    for (long m = m0 + q.r; m < m1; m += q.rl) {
+      float z[4][8], g[4][8];
+      size_t o[4];
+      pool_window<T>(d, dHW, m, q.c8, sc, sh, z, g, o);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        float out[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) out[i] = A[i] * g[t][i] - Bx[i] * ((z[t][i] - mean[i]) * inv[i]) - Cg[i];
+        st8<T>(dz + o[t], pack8<T>(out));
+      }
+    }
+    return;
+  }
   for (long m = m0 + q.r; m < m1; m += q.rl) {
     const size_t o = (size_t)m * C + q.c8;
     if constexpr (MODE == CRNN_BNG_SE) {
@@ -928,11 +1178,15 @@ inline void stream_grid(long M, int C, int* blocks, long* rpb) {
 namespace {
 template <typename T>
 int bnb_reduce_launch(const crnn_bn_bwd_desc* d, float* pg, float* pgx, int rows, hipStream_t st) {
-  const long rpb = (d->M + rows - 1) / rows;
+  const bool pool = d->mode == CRNN_BNG_POOL;
+  const long rpb = ((pool ? d->M / 4 : d->M) + rows - 1) / rows;
   const int rl = NT / (d->C / 8);
   const size_t sm = (size_t)2 * rl * d->C * sizeof(float);
-  const FastDiv dHW(d->HW > 0 ? d->HW : 1);
+  const FastDiv dHW(pool ? d->HW / 2 : (d->HW > 0 ? d->HW : 1));  // pool mode: pooled width Wo
   switch (d->mode) {
+    case CRNN_BNG_POOL:
+      hipLaunchKernelGGL((bnb_reduce_kernel<T, CRNN_BNG_POOL>), dim3(rows), dim3(NT), sm, st, *d, dHW, rpb, pg, pgx);
+      break;
     case CRNN_BNG_PLAIN:
       hipLaunchKernelGGL((bnb_reduce_kernel<T, CRNN_BNG_PLAIN>), dim3(rows), dim3(NT), sm, st, *d, dHW, rpb, pg, pgx);
       break;
@@ -952,9 +1206,13 @@ template <typename T>
 int bnb_apply_launch(const crnn_bn_bwd_desc* d, const float* mg, const float* mgx, void* dz, hipStream_t st) {
   int nb;
   long rpb;
-  stream_grid(d->M, d->C, &nb, &rpb);
-  const FastDiv dHW(d->HW > 0 ? d->HW : 1);
+  const bool pool = d->mode == CRNN_BNG_POOL;
+  stream_grid(pool ? d->M / 4 : d->M, d->C, &nb, &rpb);
+  const FastDiv dHW(pool ? d->HW / 2 : (d->HW > 0 ? d->HW : 1));
   switch (d->mode) {
+    case CRNN_BNG_POOL:
+      hipLaunchKernelGGL((bnb_apply_kernel<T, CRNN_BNG_POOL>), dim3(nb), dim3(NT), 0, st, *d, dHW, mg, mgx, (T*)dz, rpb);
+      break;
     case CRNN_BNG_PLAIN:
       hipLaunchKernelGGL((bnb_apply_kernel<T, CRNN_BNG_PLAIN>), dim3(nb), dim3(NT), 0, st, *d, dHW, mg, mgx, (T*)dz, rpb);
       break;
@@ -1063,8 +1321,12 @@ int crnn_se_pool(int dtype, const void* z2, const float* scale, const float* shi
 
 int crnn_se_mlp_fwd(const float* pooled, const float* w1, const float* w2, float* hid, float* s, int B, int C, int Cr,
                     void* stream) {
-  hipLaunchKernelGGL(se_mlp_fwd_kernel, dim3(B), dim3(256), (C + Cr) * sizeof(float), (hipStream_t)stream, pooled, w1,
-                     w2, hid, s, C, Cr);
+  if (Cr * 16 != C || (C != 256 && C != 512)) return crnn_set_error(hipErrorInvalidValue, "se_mlp: C in {256, 512}, Cr = C/16");
+  const dim3 grid((B + SE_SB - 1) / SE_SB);
+  if (C == 256)
+    hipLaunchKernelGGL(se_mlp_fwd_kernel<256>, grid, dim3(256), 0, (hipStream_t)stream, pooled, w1, w2, hid, s, B);
+  else
+    hipLaunchKernelGGL(se_mlp_fwd_kernel<512>, grid, dim3(256), 0, (hipStream_t)stream, pooled, w1, w2, hid, s, B);
   return (int)hipGetLastError();
 }
 
@@ -1094,10 +1356,16 @@ int crnn_se_mlp_bwd(const float* ds, const float* pooled, const float* hid, cons
                     const float* w2, float* dsig, float* dhid, float* dpool, float* dw1, float* dw2, int B, int C,
                     int Cr, int HW, int accumulate, void* stream) {
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(se_mlp_bwd_kernel, dim3(B), dim3(256), (C + Cr) * sizeof(float), st, ds, hid, s, w1, w2, dsig,
-                     dhid, dpool, C, Cr, 1.f / (float)HW);
-  hipLaunchKernelGGL(se_wgrad_kernel, dim3((C + 63) / 64, Cr), dim3(256), 0, st, dsig, hid, dhid, pooled, dw1, dw2, B,
-                     C, Cr, accumulate);
+  if (Cr * 16 != C || (C != 256 && C != 512)) return crnn_set_error(hipErrorInvalidValue, "se_mlp: C in {256, 512}, Cr = C/16");
+  const dim3 grid((B + SE_SB - 1) / SE_SB), wgrid(C / 64, Cr / 8);
+  const float inv = 1.f / (float)HW;
+  if (C == 256) {
+    hipLaunchKernelGGL(se_mlp_bwd_kernel<256>, grid, dim3(256), 0, st, ds, hid, s, w1, w2, dsig, dhid, dpool, B, inv);
+    hipLaunchKernelGGL(se_wgrad_kernel<256>, wgrid, dim3(256), 0, st, dsig, hid, dhid, pooled, dw1, dw2, B, accumulate);
+  } else {
+    hipLaunchKernelGGL(se_mlp_bwd_kernel<512>, grid, dim3(256), 0, st, ds, hid, s, w1, w2, dsig, dhid, dpool, B, inv);
+    hipLaunchKernelGGL(se_wgrad_kernel<512>, wgrid, dim3(256), 0, st, dsig, hid, dhid, pooled, dw1, dw2, B, accumulate);
+  }
   return (int)hipGetLastError();
 }
 

@@ -334,11 +334,13 @@ def test_adamw_vs_oracle():
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_bn_bwd_and_se(dtype):
-    """BN train fwd + SE block tail + backward vs torch autograd."""
+@pytest.mark.parametrize("shape", [(3, 256, 4, 6), (70, 512, 2, 3), (133, 256, 1, 5)])
+def test_bn_bwd_and_se(dtype, shape):
+    """BN train fwd + SE block tail + backward vs torch autograd (ragged batch vs the SE kernels'
+    4-sample blocks and 16-lane batch split; C/16 = 16, 32)."""
     L = _L()
     g = torch.Generator().manual_seed(7)
-    B, C, H, W = 3, 64, 4, 6
+    B, C, H, W = shape
     HW = H * W
     Cr = C // 16
     z2 = torch.randn(B, C, H, W, generator=g).to(dtype).float()
@@ -573,3 +575,60 @@ def test_bn_finalize_shared_workspace_mixed_channels():
         torch.cuda.synchronize()
         assert relerr(dbet.cpu(), pg.double().sum(0)) < 1e-6, (C, rows)
         assert relerr(dgam.cpu(), pgx.double().sum(0)) < 1e-6, (C, rows)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape", [(3, 6, 10, 128), (2, 32, 64, 64)])
+def test_bn_bwd_pool_mode_matches_maxpool_then_relu_mode(dtype, shape):
+    """CRNN_BNG_POOL (BN -> ReLU -> MaxPool backward fused, the stem, model/seresnet31.py:83-88)
+    against the unfused crnn_maxpool_bwd + CRNN_BNG_RELU pair and torch autograd of
+    max_pool2d(relu(batch_norm(z)))."""
+    L = _L()
+    from crnn_hip._lib import BnBwdDesc
+    g = torch.Generator().manual_seed(5)
+    B, H, W, C = shape
+    M = B * H * W
+    z = torch.randn(B, C, H, W, generator=g).to(dtype).float()
+    z[:, :, 0, 0] = z[:, :, 0, 1]   # exact ties: routed to the first max in scan order
+    gamma = torch.rand(C, generator=g) + 0.5
+    beta = torch.randn(C, generator=g) * 0.3
+    dp = torch.randn(B, C, H // 2, W // 2, generator=g).to(dtype).float()
+    zr = z.clone().double().requires_grad_(True)
+    pr = [gamma.double().clone().requires_grad_(True), beta.double().clone().requires_grad_(True)]
+    u = F.batch_norm(zr, None, None, pr[0], pr[1], training=True, eps=1e-5)
+    F.max_pool2d(torch.relu(u), 2, 2).backward(dp.double())
+    z64 = z.double()
+    mean = z64.mean(dim=(0, 2, 3))
+    inv = 1 / torch.sqrt(z64.var(dim=(0, 2, 3), unbiased=False) + 1e-5)
+    sc, sh = gamma.double() * inv, beta.double() - mean * gamma.double() * inv
+    dev = lambda t: t.float().contiguous().to(DEV)
+    zd, dpd = to_nhwc(z, None, dtype), to_nhwc(dp, None, dtype)
+    meand, invd, scd, shd = dev(mean), dev(inv), dev(sc), dev(sh)
+    dt, st = L.dtype_code(dtype), L.stream_ptr()
+    rows = L.lib().crnn_bn_rows(M)
+    fws = torch.zeros(L.lib().crnn_bn_finalize_workspace(C) // 4, device=DEV)
+
+    def bwd(mode, dy, hw):
+        desc = BnBwdDesc(dy.data_ptr(), zd.data_ptr(), meand.data_ptr(), invd.data_ptr(), scd.data_ptr(),
+                         shd.data_ptr(), 0, 0, 0, mode, M, C, hw)
+        pg, pgx = torch.empty(rows, C, device=DEV), torch.empty(rows, C, device=DEV)
+        L.call("crnn_bn_bwd_reduce", dt, desc, pg.data_ptr(), pgx.data_ptr(), rows, st)
+        dgam, dbet, mg, mgx = [torch.empty(C, device=DEV) for _ in range(4)]
+        L.call("crnn_bn_bwd_finalize", pg.data_ptr(), pgx.data_ptr(), rows, C, M, dgam.data_ptr(), dbet.data_ptr(),
+               mg.data_ptr(), mgx.data_ptr(), 0, fws.data_ptr(), st)
+        dz = torch.empty(B, H, W, C, dtype=dtype, device=DEV)
+        L.call("crnn_bn_bwd_apply", dt, desc, mg.data_ptr(), mgx.data_ptr(), dz.data_ptr(), st)
+        return dz.float().cpu(), dgam.cpu(), dbet.cpu()
+
+    dfull = torch.empty(B, H, W, C, dtype=dtype, device=DEV)
+    L.call("crnn_maxpool_bwd", dt, zd.data_ptr(), scd.data_ptr(), shd.data_ptr(), dpd.data_ptr(), dfull.data_ptr(),
+           B, H, W, C, st)
+    dz_u, dgam_u, dbet_u = bwd(1, dfull, H * W)
+    dz_p, dgam_p, dbet_p = bwd(4, dpd, W)
+    torch.cuda.synchronize()
+    # fused == unfused up to the order of the fp32 partial sums
+    assert relerr(dbet_p, dbet_u) < 1e-5 and relerr(dgam_p, dgam_u) < 1e-5
+    assert relerr(dz_p, dz_u) < (1e-5 if dtype == torch.float32 else 1e-2)
+    tol = 1e-4 if dtype == torch.float32 else 3e-2
+    assert relerr(dz_p.permute(0, 3, 1, 2), zr.grad) < tol
+    assert relerr(dgam_p, pr[0].grad) < tol and relerr(dbet_p, pr[1].grad) < tol
