@@ -43,7 +43,7 @@ class PackJob(C.Structure):  # crnn_pack_job
                 ("src2", vp), ("perm", vp), ("dst", vp)]
 
 
-OPT_GEMM_STAGGER = 0   # crnn_set_option keys (include/crnn_hip.h)
+OPT_GEMM_STAGGER, OPT_GEMM_PERSISTENT = 0, 1   # crnn_set_option keys (include/crnn_hip.h)
 
 PACK_CONV, PACK_ROWS, PACK_ROWS_SUM, PACK_TRANSPOSE = 0, 1, 2, 3
 

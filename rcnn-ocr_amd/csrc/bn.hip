@@ -453,18 +453,6 @@ __device__ __forceinline__ void reduce_scatter32(float (&v)[32], int lane) {
   v[0] += __shfl_xor(v[0], 1, 64);
 }
 
-// sum over aligned groups of G (2, 4 or 8) lanes with DPP moves; every lane gets its group's sum
-template <int CTRL> __device__ __forceinline__ float dppf(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
-}
-template <int G> __device__ __forceinline__ float rowgroup_sum(float v) {
-  static_assert(G == 2 || G == 4 || G == 8, "group");
-  v += dppf<0xB1>(v);                        // quad_perm [1,0,3,2]
-  if constexpr (G >= 4) v += dppf<0x4E>(v);  // quad_perm [2,3,0,1]
-  if constexpr (G >= 8) v += dppf<0x141>(v); // row_half_mirror: quad 0 <-> quad 1 of each 8
-  return v;
-}
-
 __device__ __forceinline__ float dot4(f32x4 a, f32x4 b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2] + a[3] * b[3]; }
 
 template <int C>

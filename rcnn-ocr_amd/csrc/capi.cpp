@@ -14,7 +14,18 @@ int crnn_set_error(int code, const char* msg) {
 extern "C" int crnn_version(void) { return 100; }
 
 // tuning switches (A/B in one process); defaults are the measured-best settings
-static int g_opts[CRNN_OPT_COUNT] = {1};
+static int g_opts[CRNN_OPT_COUNT] = {1, 1, 1, 0};
+
+int crnn_cu_count() {
+  static int n = -1;
+  if (n < 0) {
+    int dev = 0;
+    hipDeviceProp_t p;
+    n = (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&p, dev) == hipSuccess) ? p.multiProcessorCount : 256;
+    if (n < 1) n = 256;
+  }
+  return n;
+}
 
 int crnn_option(int key) { return (key >= 0 && key < CRNN_OPT_COUNT) ? g_opts[key] : 0; }
 

@@ -108,6 +108,20 @@ __device__ __forceinline__ float tanh_fast(float x) {
   return copysignf((1.f - e) * __builtin_amdgcn_rcpf(1.f + e), x);
 }
 
+// sum over aligned groups of G (2, 4, 8 or 16) lanes with DPP moves (no LDS round trip, unlike
+// __shfl_xor's ds_bpermute); every lane of a group gets the same, lane-order-independent sum
+template <int CTRL> __device__ __forceinline__ float dppf(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+template <int G> __device__ __forceinline__ float rowgroup_sum(float v) {
+  static_assert(G == 2 || G == 4 || G == 8 || G == 16, "group");
+  v += dppf<0xB1>(v);                          // quad_perm [1,0,3,2]
+  if constexpr (G >= 4) v += dppf<0x4E>(v);    // quad_perm [2,3,0,1]
+  if constexpr (G >= 8) v += dppf<0x141>(v);   // row_half_mirror: quads 0 <-> 1 of each 8
+  if constexpr (G >= 16) v += dppf<0x140>(v);  // row_mirror: halves of each 16-lane row
+  return v;
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

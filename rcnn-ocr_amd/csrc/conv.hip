@@ -398,20 +398,35 @@ struct SlabEpi {
   __device__ __forceinline__ void stats(int, int, f32x4, f32x4) const {}
 };
 
-// sum split-K slabs [S][Co][KH*KW*Cip] and scatter into an OIHW fp32 gradient
-__global__ void wgrad_reduce_kernel(const float* __restrict__ ws, int S, float* __restrict__ dw,
-                                    int Co, int Ci, int Cip, int KH, int KW, float beta) {
+// sum split-K slabs [S][Co][KH*KW*Cip] and scatter into an OIHW fp32 gradient. A thread owns 4
+// consecutive k' (one tap, 4 channels: Cip % 8 == 0) of one output row: 16-B slab loads, 8 slabs
+// in flight per batch (the loop is otherwise latency-bound), fixed summation order.
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ ws, int S,
+                                                           float* __restrict__ dw, int Co, int Ci, int Cip, int KH,
+                                                           int KW, float beta) {
   const int Kp = KH * KW * Cip;
-  const long total = (long)Co * Kp;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    int co = (int)(i / Kp), k = (int)(i - (long)co * Kp);
-    int tap = k / Cip, ci = k - tap * Cip;
-    if (ci >= Ci) continue;
-    float s = 0.f;
-    for (int z = 0; z < S; ++z) s += ws[(size_t)z * total + i];
-    int kh = tap / KW, kw = tap - kh * KW;
-    size_t o = (((size_t)co * Ci + ci) * KH + kh) * KW + kw;
-    dw[o] = beta != 0.f ? beta * dw[o] + s : s;
+  const long total = (long)Co * Kp, n4 = total / 4;
+  for (long i4 = blockIdx.x * (long)blockDim.x + threadIdx.x; i4 < n4; i4 += (long)gridDim.x * blockDim.x) {
+    const long i = 4 * i4;
+    f32x4 s = {0.f, 0.f, 0.f, 0.f};
+    int z = 0;
+    for (; z + 8 <= S; z += 8) {
+      f32x4 v[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] = *reinterpret_cast<const f32x4*>(ws + (size_t)(z + q) * total + i);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) s += v[q];
+    }
+    for (; z < S; ++z) s += *reinterpret_cast<const f32x4*>(ws + (size_t)z * total + i);
+    const int co = (int)(i / Kp), k = (int)(i - (long)co * Kp);
+    const int tap = k / Cip, ci = k - tap * Cip;
+    const int kh = tap / KW, kw = tap - kh * KW;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      if (ci + e >= Ci) break;
+      const size_t o = (((size_t)co * Ci + ci + e) * KH + kh) * KW + kw;
+      dw[o] = beta != 0.f ? beta * dw[o] + s[e] : s[e];
+    }
   }
 }
 
@@ -537,7 +552,7 @@ template <typename T> int conv_wgrad_t(const crnn_conv_desc* d, const void* dy, 
   if (rc) return rc;
   int ci_real = d->Ci_real > 0 ? d->Ci_real : g.Ci;
   long total = (long)g.Co * Kp;
-  int blocks = (int)((total + 255) / 256);
+  int blocks = (int)((total / 4 + 255) / 256);
   if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, ws, splits, dw, g.Co, ci_real,
                      g.Ci, g.KH, g.KW, beta);
@@ -577,11 +592,16 @@ void crnn_conv_wgrad_plan(int dtype, const crnn_conv_desc* d, int* bm, int* bn, 
   int Kp = d->KH * d->KW * d->Ci;
   if (dtype == CRNN_BF16 && d->Co % 256 == 0 && Kp % 128 == 0 && Mp >= 256L * 64) {
     // deep kernel: 1 block per CU, ~2 blocks per CU over the split-K grid, >= 8 K-tiles per split
+    // tuning (crnn_set_option CRNN_OPT_WGRAD_TILE): 0 = 256x256 when Kp allows, 1 = 256x128
+    // (twice the tiles, about half the split-K slabs), 2.. = target grid of 128 * value blocks
+    const int opt = crnn_option(CRNN_OPT_WGRAD_TILE);
     *bm = 256;
-    *bn = Kp % 256 == 0 ? 256 : 128;
+    *bn = (Kp % 256 == 0 && opt != 1) ? 256 : 128;
     long tiles = (long)(d->Co / 256) * (Kp / *bn);
-    long want = CRNN_WGRAD_BLOCKS / tiles;      // whole rounds of 1-block-per-CU waves
+    const long target = opt >= 2 ? 128L * opt : CRNN_WGRAD_BLOCKS;
+    long want = target / tiles;                 // whole rounds of 1-block-per-CU waves
     long maxs = (Mp + 512 - 1) / 512;
+    if (maxs > 128) maxs = 128;                 // >= 128 slabs cost more to reduce than CUs gain
     if (want > maxs) want = maxs;
     if (want < 1) want = 1;
     if (want > 256) want = 256;

@@ -282,9 +282,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(LA la, LB lb, EPI epi, int M,
 #pragma unroll
       for (int i = 0; i < MI; ++i) s += acc[i][j];
 #pragma unroll
-      for (int o = 1; o < 16; o <<= 1)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) s[r] += __shfl_xor(s[r], o, 64);
+      for (int r = 0; r < 4; ++r) s[r] = rowgroup_sum<16>(s[r]);   // the 16 rows of a lane row (DPP)
       const float inv_n = nval > 0 ? 1.f / (float)nval : 0.f;
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
@@ -296,9 +294,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(LA la, LB lb, EPI epi, int M,
         }
       }
 #pragma unroll
-      for (int o = 1; o < 16; o <<= 1)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) q[r] += __shfl_xor(q[r], o, 64);
+      for (int r = 0; r < 4; ++r) q[r] = rowgroup_sum<16>(q[r]);
       if (mr == 0) epi.stats(m_tile * 2 + wm, n0 + wn * WN + j * 16 + nq, s, q);
     }
   }
@@ -366,10 +362,15 @@ template <typename T> struct ColMajorK {
   typedef int Prep;
   __device__ __forceinline__ Ctx row_ctx(int r8) const { return Ctx{(uint32_t)r8, r8 < rows}; }
   __device__ __forceinline__ Prep prep(int k0) const { return k0; }
-  __device__ __forceinline__ typename VT<T>::v8 load(const Ctx& c, Prep k0, int kofs) const {
+  __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc() const {
+    return mk_rsrc(p, (uint32_t)((size_t)K * ld * sizeof(T)));
+  }
+  __device__ __forceinline__ uint32_t offs(const Ctx& c, Prep k0, int kofs) const {
     const int k = k0 + kofs;
-    return bld8<T>(mk_rsrc(p, (uint32_t)((size_t)K * ld * sizeof(T))),
-                   boff<T>((uint32_t)k * (uint32_t)ld + c.off, c.ok && k < K));
+    return boff<T>((uint32_t)k * (uint32_t)ld + c.off, c.ok && k < K);
+  }
+  __device__ __forceinline__ typename VT<T>::v8 load(const Ctx& c, Prep k0, int kofs) const {
+    return bld8<T>(rsrc(), offs(c, k0, kofs));
   }
 };
 

@@ -28,6 +28,7 @@
 
 #include "crnn_hip.h"
 int crnn_option(int key);  // capi.cpp (crnn_set_option)
+int crnn_cu_count();       // capi.cpp: compute units of the current device (cached)
 
 namespace gemm {
 
@@ -68,9 +69,7 @@ __device__ __forceinline__ void wave_col_stats(const f32x4 (&acc)[MI][NI], const
 #pragma unroll
     for (int i = 0; i < MI; ++i) s += acc[i][j];
 #pragma unroll
-    for (int o = 1; o < 16; o <<= 1)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) s[r] += __shfl_xor(s[r], o, 64);
+    for (int r = 0; r < 4; ++r) s[r] = rowgroup_sum<16>(s[r]);   // the 16 rows of a lane row (DPP)
     const float inv_n = nval > 0 ? 1.f / (float)nval : 0.f;
 #pragma unroll
     for (int i = 0; i < MI; ++i) {
@@ -82,9 +81,7 @@ __device__ __forceinline__ void wave_col_stats(const f32x4 (&acc)[MI][NI], const
       }
     }
 #pragma unroll
-    for (int o = 1; o < 16; o <<= 1)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) q[r] += __shfl_xor(q[r], o, 64);
+    for (int r = 0; r < 4; ++r) q[r] = rowgroup_sum<16>(q[r]);
     if (mr == 0) epi.stats(prow, ncol0 + j * 16 + nq, s, q);
   }
 }
@@ -201,21 +198,52 @@ __global__ __launch_bounds__(512) void gemm256_kernel(LA la, LB lb, EPI epi, int
   constexpr int VM = OA::I + 2 * OB::I;          // DMA instructions of tile t+2 issued before the P4 wait
   __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
 
-  const int nwg = tiles_m * tiles_n * nsplit;
-  const int wg = xcd_remap(blockIdx.x, nwg);
-  const int n_tile = wg % tiles_n, m_tile = (wg / tiles_n) % tiles_m, kz = wg / (tiles_n * tiles_m);
-  const int m0 = m_tile * BM, n0 = n_tile * BN;
-  const int kbeg = kz * klen, kend = min(K, kbeg + klen);
-  const int nk = kend > kbeg ? (kend - kbeg + KS - 1) / KS : 0;
+  // Persistent over work items (tile, K-split): block lb takes items lb, lb + G, lb + 2G, ...
+  // (G = gridDim.x <= CU count) and runs their K-tiles as ONE flat sequence through the
+  // LDS-DMA ring, so the next item's first stages are in flight while the current item's last
+  // stages compute and while its epilogue runs. Positions u, u+1, u+2 of the sequence are
+  // tracked by cursors (item, K-tile index); the loaders' row contexts follow the item of the
+  // position being issued (re-initialised once per item, before the P2 issue that first needs it).
+  const int items = tiles_m * tiles_n * nsplit;
+  const int G = gridDim.x;
+  const int lb_id = xcd_remap(blockIdx.x, G);
+  if (lb_id >= items) return;
 
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = wid >> 2, wc = wid & 3;
 
+  struct Cur {
+    int it, t, nk, kb;  // item, K-tile within the item, K-tiles of the item, first k of the item
+  };
+  auto item_k = [&](Cur& c) {
+    const int kz = c.it / (tiles_n * tiles_m);
+    c.kb = kz * klen;
+    const int ke = min(K, c.kb + klen);
+    c.nk = ke > c.kb ? (ke - c.kb + KS - 1) / KS : 1;   // an empty split still owns one (masked) K-tile
+  };
+  auto advance = [&](Cur& c) {
+    if (++c.t == c.nk) {
+      c.it += G;
+      c.t = 0;
+      if (c.it < items) item_k(c);
+    }
+  };
+  auto tile_m0 = [&](int it) { return ((it / tiles_n) % tiles_m) * BM; };
+  auto tile_n0 = [&](int it) { return (it % tiles_n) * BN; };
+
   OA oa;
   OB ob;
-  oa.init(la, m0, wid, lane, wr);
-  ob.init(lb, n0, wid, lane, wc);
+  int ctx_it = lb_id;
+  oa.init(la, tile_m0(ctx_it), wid, lane, wr);
+  ob.init(lb, tile_n0(ctx_it), wid, lane, wc);
+  auto ensure_ctx = [&](int it) {
+    if (it != ctx_it) {
+      ctx_it = it;
+      oa.init(la, tile_m0(it), wid, lane, wr);
+      ob.init(lb, tile_n0(it), wid, lane, wc);
+    }
+  };
   const __amdgpu_buffer_rsrc_t ra = la.rsrc(), rb = lb.rsrc();
   char* const sA0 = smem;
   char* const sB0 = smem + OA::TB;
@@ -226,41 +254,51 @@ __global__ __launch_bounds__(512) void gemm256_kernel(LA la, LB lb, EPI epi, int
 #pragma unroll
     for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // ---- prologue: tile 0 whole, tile 1 except its A-half1 (issued in P1 of tile 0)
-  typename LA::Prep pa2 = la.prep(kbeg);
-  typename LB::Prep pb2 = lb.prep(kbeg);
-  if (nk > 0) {
-    oa.issue(la, ra, sA0, 0, pa2);
-    ob.issue(lb, rb, sB0, 0, pb2);
-    ob.issue(lb, rb, sB0, 1, pb2);
-    oa.issue(la, ra, sA0, 1, pa2);
+  Cur cur{lb_id, 0, 1, 0};
+  item_k(cur);
+  // ---- prologue: position 0 whole, position 1 except its A-half1 (issued in P1 of position 0)
+  {
+    const typename LA::Prep pa = la.prep(cur.kb);
+    const typename LB::Prep pb = lb.prep(cur.kb);
+    oa.issue(la, ra, sA0, 0, pa);
+    ob.issue(lb, rb, sB0, 0, pb);
+    ob.issue(lb, rb, sB0, 1, pb);
+    oa.issue(la, ra, sA0, 1, pa);
   }
-  typename LA::Prep pa1 = pa2;  // prep of tile t+1 (for its A-half1)
-  if (nk > 1) {
-    pa1 = la.prep(kbeg + KS);
-    const typename LB::Prep pb1 = lb.prep(kbeg + KS);
-    oa.issue(la, ra, sA0 + STAGE, 0, pa1);
-    ob.issue(lb, rb, sB0 + STAGE, 0, pb1);
-    ob.issue(lb, rb, sB0 + STAGE, 1, pb1);
+  Cur c1 = cur;
+  advance(c1);
+  if (c1.it < items) {
+    ensure_ctx(c1.it);
+    const int k1 = c1.kb + c1.t * KS;
+    const typename LA::Prep pa = la.prep(k1);
+    const typename LB::Prep pb = lb.prep(k1);
+    oa.issue(la, ra, sA0 + STAGE, 0, pa);
+    ob.issue(lb, rb, sB0 + STAGE, 0, pb);
+    ob.issue(lb, rb, sB0 + STAGE, 1, pb);
     asm volatile("s_waitcnt vmcnt(%0)" ::"i"(VM) : "memory");
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
+  Cur c2 = c1;
+  if (c2.it < items) advance(c2);
   raw_barrier();
   // ping-pong: waves 4-7 (wr == 1, one per SIMD) run one barrier behind waves 0-3, so each SIMD
   // alternates one wave's MFMA cluster with its partner's ds_read / LDS-DMA issue segment
   if (stagger && wr == 1) raw_barrier();
 
   bf16x8 af[MQ][2], bfr[NI][2];
-  for (int t = 0; t < nk; ++t) {
-    const int b = t & 1;
+  for (int u = 0; cur.it < items; ++u) {
+    const int b = u & 1;
     const char* As = smem + b * STAGE;
     const char* Bs = As + OA::TB;
     const uint32_t lA = lds_addr(As), lB = lds_addr(Bs);
-    const bool n1 = t + 1 < nk, n2 = t + 2 < nk;
+    const bool n1 = c1.it < items, n2 = c2.it < items;
+    typename LA::Prep pa2;
+    typename LB::Prep pb2;
+    typename LA::Prep pa1 = la.prep(c1.kb + c1.t * KS);   // A-half1 of position u+1 (ctx: c1's item)
     if (n2) {
-      pa2 = la.prep(kbeg + (t + 2) * KS);
-      pb2 = lb.prep(kbeg + (t + 2) * KS);
+      pa2 = la.prep(c2.kb + c2.t * KS);
+      pb2 = lb.prep(c2.kb + c2.t * KS);
     }
     // ---- P1: quadrant (0,0)
     oa.template load<0, MQ>(af, As, lA, wr * WM, lane);
@@ -279,7 +317,10 @@ __global__ __launch_bounds__(512) void gemm256_kernel(LA la, LB lb, EPI epi, int
     raw_barrier();
     // ---- P2: quadrant (0,1)
     ob.template load<1, NQ>(*reinterpret_cast<bf16x8(*)[NQ][2]>(&bfr[NQ]), Bs, lB, wc * WN, lane);
-    if (n2) oa.issue(la, ra, sA0 + b * STAGE, 0, pa2);
+    if (n2) {
+      ensure_ctx(c2.it);
+      oa.issue(la, ra, sA0 + b * STAGE, 0, pa2);
+    }
     lds_wait_all();
     raw_barrier();
     __builtin_amdgcn_s_setprio(1);
@@ -312,7 +353,6 @@ __global__ __launch_bounds__(512) void gemm256_kernel(LA la, LB lb, EPI epi, int
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    pa1 = pa2;
     raw_barrier();
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -323,15 +363,27 @@ __global__ __launch_bounds__(512) void gemm256_kernel(LA la, LB lb, EPI epi, int
         for (int j = 0; j < NQ; ++j) mma<T>(acc[MQ + i][j], bfr[j][kk], af[i][kk]);
     __builtin_amdgcn_s_setprio(0);
     raw_barrier();
+    // ---- item finished: epilogue (registers + global stores only; the next item's first
+    // stages are already in flight), then a fresh accumulator
+    if (cur.t == cur.nk - 1) {
+      const int m0 = tile_m0(cur.it), n0 = tile_n0(cur.it), kz = cur.it / (tiles_n * tiles_m);
+      const int mr = lane & 15, nq = 4 * (lane >> 4);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j) epi.store(m0 + wr * WM + i * 16 + mr, n0 + wc * WN + j * 16 + nq, acc[i][j], kz);
+      if constexpr (EPI::kStats)
+        wave_col_stats<MI, NI>(acc, epi, M, m0 + wr * WM, (m0 / BM) * 2 + wr, n0 + wc * WN, lane);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    cur = c1;
+    c1 = c2;
+    if (c2.it < items) advance(c2);
   }
   if (stagger && wr == 0) raw_barrier();
-
-  const int mr = lane & 15, nq = 4 * (lane >> 4);
-#pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int j = 0; j < NI; ++j) epi.store(m0 + wr * WM + i * 16 + mr, n0 + wc * WN + j * 16 + nq, acc[i][j], kz);
-  if constexpr (EPI::kStats) wave_col_stats<MI, NI>(acc, epi, M, m0 + wr * WM, m_tile * 2 + wr, n0 + wc * WN, lane);
 }
 
 // nsplit: split-K factor (K ranges of split_len(K, nsplit), multiples of 64)
@@ -342,7 +394,11 @@ inline int launch256(const LA& la, const LB& lb, const EPI& epi, int M, int N, i
   const int tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN;
   const int klen = split_len(K, nsplit);
   nsplit = K > 0 ? (K + klen - 1) / klen : 1;
-  hipLaunchKernelGGL((gemm256_kernel<BM, BN, LA, LB, EPI>), dim3(tm * tn * nsplit), dim3(512), 0, st, la, lb, epi,
+  // persistent grid: at most one block per CU (1 block/CU by LDS); each block loops over items
+  const int items = tm * tn * nsplit;
+  const int ncu = crnn_option(CRNN_OPT_GEMM_PERSISTENT) ? crnn_cu_count() : items;
+  const int grid = items < ncu ? items : ncu;
+  hipLaunchKernelGGL((gemm256_kernel<BM, BN, LA, LB, EPI>), dim3(grid), dim3(512), 0, st, la, lb, epi,
                      M, N, K, klen, tm, tn, nsplit, crnn_option(CRNN_OPT_GEMM_STAGGER));
   return (int)hipGetLastError();
 }

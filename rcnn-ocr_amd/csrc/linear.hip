@@ -2,6 +2,7 @@
 // model/model.py:157,162; CTC head) and their gradients, on the
 // shared MFMA GEMM core.
 #include "gemm.hpp"
+#include "gemm256.hpp"
 #include "crnn_internal.hpp"
 
 using namespace gemm;
@@ -54,6 +55,16 @@ template <typename T> struct OutEpi {
 template <typename T, class LA, class LB>
 int run(const LA& la, const LB& lb, const OutEpi<T>& ep, int M, int N, int K, int splits, hipStream_t st) {
   long work = (long)M * N;
+  if constexpr (sizeof(T) == 2) {
+    // the deep 256-row kernel when the grid alone fills most CUs (no split-K for these outputs)
+    const long cu = crnn_cu_count();
+    if (crnn_option(CRNN_OPT_DEEP_LINEAR) && splits == 1 && K >= 256) {
+      const long t256 = (long)((M + 255) / 256) * ((N + 255) / 256);
+      const long t128 = (long)((M + 255) / 256) * ((N + 127) / 128);
+      if (N >= 256 && t256 * 4 >= cu * 3) return launch256<256, 256>(la, lb, ep, M, N, K, st);
+      if (N >= 128 && t128 * 4 >= cu * 3) return launch256<256, 128>(la, lb, ep, M, N, K, st);
+    }
+  }
   if (M >= 128 && N >= 128 && work >= 128L * 128 * 128) return launch<T, 128, 128>(la, lb, ep, M, N, K, splits, st);
   if (work >= 64L * 64 * 128) return launch<T, 64, 64>(la, lb, ep, M, N, K, splits, st);
   return launch<T, 32, 32>(la, lb, ep, M, N, K, splits, st);

@@ -12,6 +12,7 @@
 // epilogue runs the cell backward of step s (again one lane per (b, 4 units)).
 #include "gemm.hpp"
 #include "gemm_oneshot.hpp"
+#include "gemm256.hpp"
 #include "crnn_internal.hpp"
 
 using namespace gemm;
@@ -209,14 +210,19 @@ template <typename T> struct HPrevB {
   typedef int Prep;
   __device__ __forceinline__ Ctx row_ctx(int r8) const { return Ctx{r8, r8 < H}; }
   __device__ __forceinline__ Prep prep(int k0) const { return k0; }
-  __device__ __forceinline__ typename VT<T>::v8 load(const Ctx& c, Prep k0, int kofs) const {
+  __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc() const {
+    return mk_rsrc(hseq, (uint32_t)((size_t)B * Tn * 2 * H * sizeof(T)));
+  }
+  __device__ __forceinline__ uint32_t offs(const Ctx& c, Prep k0, int kofs) const {
     const int k = k0 + kofs;
     uint32_t bu;
     const int t = (int)dB.divmod((uint32_t)k, bu), b = (int)bu;
     const int tp = d == 0 ? t - 1 : t + 1;
     const bool ok = c.ok && k < Tn * B && tp >= 0 && tp < Tn;
-    const uint32_t off = (uint32_t)(((b * Tn + tp) * 2 * H) + d * H + c.j);
-    return bld8<T>(mk_rsrc(hseq, (uint32_t)((size_t)B * Tn * 2 * H * sizeof(T))), boff<T>(off, ok));
+    return boff<T>((uint32_t)(((b * Tn + tp) * 2 * H) + d * H + c.j), ok);
+  }
+  __device__ __forceinline__ typename VT<T>::v8 load(const Ctx& c, Prep k0, int kofs) const {
+    return bld8<T>(rsrc(), offs(c, k0, kofs));
   }
 };
 // B (dW_ih): x rows i, k = t*B + b : x[b][t][i]
@@ -229,13 +235,17 @@ template <typename T> struct XB {
   typedef int Prep;
   __device__ __forceinline__ Ctx row_ctx(int r8) const { return Ctx{r8, r8 < In}; }
   __device__ __forceinline__ Prep prep(int k0) const { return k0; }
-  __device__ __forceinline__ typename VT<T>::v8 load(const Ctx& c, Prep k0, int kofs) const {
+  __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc() const {
+    return mk_rsrc(x, (uint32_t)((size_t)B * Tn * In * sizeof(T)));
+  }
+  __device__ __forceinline__ uint32_t offs(const Ctx& c, Prep k0, int kofs) const {
     const int k = k0 + kofs;
     uint32_t bu;
     const int t = (int)dB.divmod((uint32_t)k, bu), b = (int)bu;
-    const bool ok = c.ok && k < Tn * B;
-    return bld8<T>(mk_rsrc(x, (uint32_t)((size_t)B * Tn * In * sizeof(T))),
-                   boff<T>((uint32_t)((b * Tn + t) * In + c.i), ok));
+    return boff<T>((uint32_t)((b * Tn + t) * In + c.i), c.ok && k < Tn * B);
+  }
+  __device__ __forceinline__ typename VT<T>::v8 load(const Ctx& c, Prep k0, int kofs) const {
+    return bld8<T>(rsrc(), offs(c, k0, kofs));
   }
 };
 

@@ -1,0 +1,69 @@
+"""A/B microbenchmark of the BiLSTM / linear GEMM entry points at the bench shapes (B=256, T=32,
+H=512): crnn_set_option(KEY, v) for v in VALS, timed in one process.
+    python tools/gemmbench.py [KEY=V0,V1]"""
+import os
+import sys
+
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "rcnn-ocr_amd"))
+from crnn_hip import _lib as L  # noqa: E402
+
+
+def main():
+    key, vals = 2, [0, 1]
+    if len(sys.argv) > 1:
+        k, v = sys.argv[1].split("=")
+        key, vals = int(k), [int(x) for x in v.split(",")]
+    dev = torch.device("cuda")
+    st = L.stream_ptr()
+    B, T, H, In = 256, 32, 512, 512
+    M = B * T
+    bf = torch.bfloat16
+    x = torch.randn(M, In, device=dev).to(bf)
+    wih = (torch.randn(8 * H, In, device=dev) * 0.05).to(bf)
+    bias = torch.randn(8 * H, device=dev)
+    xg = torch.empty(M, 8 * H, device=dev, dtype=bf)
+    hseq = torch.randn(M, 2 * H, device=dev).to(bf)
+    lin = (torch.randn(H, 2 * H, device=dev) * 0.05).to(bf)
+    out = torch.empty(M, H, device=dev, dtype=bf)
+    dx = torch.randn(M, H, device=dev).to(bf)
+    dh = torch.empty(M, 2 * H, device=dev, dtype=bf)
+    dlw = torch.empty(H, 2 * H, device=dev)
+    dg = torch.randn(2, T, B, 4 * H, device=dev).to(bf)
+    dW = torch.empty(2, 4 * H, H, device=dev)
+    dxl = torch.empty(B, T, In, device=dev, dtype=bf)
+    ops = {
+        "xg nt 8192x4096x512": lambda: L.call("crnn_gemm_nt", L.BF16, x.data_ptr(), In, wih.data_ptr(), In, xg.data_ptr(),
+                                              8 * H, bias.data_ptr(), M, 8 * H, In, 0, 0, st),
+        "lin fwd nt 8192x512x1024": lambda: L.call("crnn_gemm_nt", L.BF16, hseq.data_ptr(), 2 * H, lin.data_ptr(), 2 * H,
+                                                   out.data_ptr(), H, None, M, H, 2 * H, 0, 0, st),
+        "lin bwd nn 8192x1024x512": lambda: L.call("crnn_gemm_nn", L.BF16, dx.data_ptr(), H, lin.data_ptr(), 2 * H,
+                                                   dh.data_ptr(), 2 * H, M, 2 * H, H, 0, 0, st),
+        "lin wgrad tn 512x1024x8192": lambda: L.call("crnn_gemm_tn", L.BF16, dx.data_ptr(), H, hseq.data_ptr(), 2 * H,
+                                                     dlw.data_ptr(), 2 * H, H, 2 * H, M, 0, st),
+        "dwhh (2 dirs)": lambda: L.call("crnn_lstm_dwhh", L.BF16, dg.data_ptr(), hseq.data_ptr(), dW[0].data_ptr(),
+                                        dW[1].data_ptr(), B, T, H, 0, st),
+        "dwih (2 dirs)": lambda: L.call("crnn_lstm_dwih", L.BF16, dg.data_ptr(), x.data_ptr(), dW[0].data_ptr(),
+                                        dW[1].data_ptr(), B, T, H, In, 0, st),
+        "lstm dx": lambda: L.call("crnn_lstm_dx", L.BF16, dg.data_ptr(), wih.data_ptr(), dxl.data_ptr(), B, T, H, In, st),
+    }
+    for name, fn in ops.items():
+        line = f"{name:28s}"
+        for v in vals:
+            L.call("crnn_set_option", key, v)
+            for _ in range(3):
+                fn()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(20):
+                fn()
+            e1.record()
+            torch.cuda.synchronize()
+            line += f" | opt{key}={v}: {e0.elapsed_time(e1) / 20 * 1e3:8.1f} us"
+        print(line, flush=True)
+
+
+if __name__ == "__main__":
+    main()
