@@ -198,6 +198,11 @@ int crnn_gemm_nn(int dtype, const void* A, int lda, const void* B, int ldb, void
 int crnn_gemm_tn(int dtype, const void* A, int lda, const void* B, int ldb, float* C, int ldc,
                  int M, int N, int K, int accumulate, void* stream);
 /* out[n] (+)= sum_m X[m][n]  (bias gradients), X dtype or fp32 */
+/* bf16 C (fp32, ldc) (+)= A^T B as above via split-K fp32 slabs + one reduce (deterministic);
+ * ws: crnn_gemm_tn_workspace(M, N, K) bytes */
+size_t crnn_gemm_tn_workspace(int M, int N, int K);
+int crnn_gemm_tn_slab(const void* A, int lda, const void* B, int ldb, float* C, int ldc, int M, int N, int K,
+                      int accumulate, float* ws, size_t ws_bytes, void* stream);
 int crnn_colsum(int dtype, const void* X, int ld, long M, int N, float* out, int accumulate, int x_f32, void* stream);
 
 /* ------------------------------------------------------------------ BiLSTM */
@@ -226,6 +231,13 @@ int crnn_lstm_dbias(int dtype, const void* dgates, float* b_fwd, float* b2_fwd, 
 size_t crnn_lstm_dbias_workspace(int H);
 /* dx [B][T][In] (dtype) = sum_dir dgates . W_ih'  (wih packed [2][4H][In]) */
 int crnn_lstm_dx(int dtype, const void* dgates, const void* wih, void* dx, int B, int T, int H, int In, void* stream);
+/* bf16: all four weight gradients of a layer (dW_ih and dW_hh, both directions, reference row
+ * order, fp32, += if accumulate) in one batched split-K GEMM launch + one slab reduce. x [B][T][In],
+ * hseq [B][T][2H], dgates [2][T][B][4H]; ws: crnn_lstm_wgrad_workspace bytes. */
+size_t crnn_lstm_wgrad_workspace(int B, int T, int H, int In);
+int crnn_lstm_wgrad(const void* dgates, const void* x, const void* hseq, float* dwih_f, float* dwih_r, float* dwhh_f,
+                    float* dwhh_r, float* ws, size_t ws_bytes, int B, int T, int H, int In, int accumulate,
+                    void* stream);
 /* Persistent whole-sequence recurrence (bf16 only; replaces the T per-step launches of
  * crnn_lstm_step_fwd / crnn_lstm_step_bwd with ONE launch per layer and direction pair, same
  * buffers and results). Supported when crnn_lstm_seq_supported() != 0: B % 32 == 0,

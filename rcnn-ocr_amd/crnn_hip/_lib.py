@@ -82,6 +82,8 @@ _SIGS = {
     "crnn_gemm_nt": ([i32, vp, i32, vp, i32, vp, i32, vp, i32, i32, i32, i32, i32, vp], i32),
     "crnn_gemm_nn": ([i32, vp, i32, vp, i32, vp, i32, i32, i32, i32, i32, i32, vp], i32),
     "crnn_gemm_tn": ([i32, vp, i32, vp, i32, vp, i32, i32, i32, i32, i32, vp], i32),
+    "crnn_gemm_tn_workspace": ([i32, i32, i32], sz),
+    "crnn_gemm_tn_slab": ([vp, i32, vp, i32, vp, i32, i32, i32, i32, i32, vp, sz, vp], i32),
     "crnn_colsum": ([i32, vp, i32, i64, i32, vp, i32, i32, vp], i32),
     "crnn_lstm_step_fwd": ([i32, vp, vp, vp, vp, vp, i32, i32, i32, i32, vp], i32),
     "crnn_lstm_step_bwd": ([i32, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, vp], i32),
@@ -95,6 +97,8 @@ _SIGS = {
     "crnn_lstm_seq_debug_stamps": ([vp], i32),
     "crnn_lstm_seq_fwd": ([vp, vp, vp, vp, vp, vp, i32, i32, i32, vp], i32),
     "crnn_lstm_seq_bwd": ([vp, vp, vp, vp, vp, vp, i32, i32, i32, vp], i32),
+    "crnn_lstm_wgrad_workspace": ([i32, i32, i32, i32], sz),
+    "crnn_lstm_wgrad": ([vp, vp, vp, vp, vp, vp, vp, vp, sz, i32, i32, i32, i32, i32, vp], i32),
     "crnn_lstm_dx": ([i32, vp, vp, vp, i32, i32, i32, i32, vp], i32),
     "crnn_ctc_loss": ([vp, i32, i32, i32, i32, vp, i32, vp, vp, vp, i32, vp], i32),
     "crnn_ctc_reduce_mean": ([vp, vp, i32, vp, vp], i32),

@@ -574,7 +574,7 @@ class CRNNEngine:
         dlT = ws.get("head.dlT", (B, Tn, self.Cpad), T)
         call("crnn_cast_f32", dt, ptr(dlogits), ptr(dlT), M * self.Cpad, s)
         hw_g = ws.get("head.dw", (self.Cpad, Hd), torch.float32)
-        call("crnn_gemm_tn", dt, ptr(dlT), self.Cpad, ptr(sv["enc"]), Hd, ptr(hw_g), Hd, self.Cpad, Hd, M, 0, s)
+        self._gemm_tn(dlT, self.Cpad, sv["enc"], Hd, hw_g, Hd, self.Cpad, Hd, M, 0)
         self._store_grad("ctc_head.weight", hw_g[: self.C], accumulate)
         call("crnn_colsum", L.F32, ptr(dlogits), self.Cpad, M, self.C, ptr(grads["ctc_head.bias"]), acc, 1, s)
         dx = ws.get("rnn.dx_head", (B, Tn, Hd), T)
@@ -588,8 +588,7 @@ class CRNNEngine:
             dh = ws.get("rnn.dhseq", (B, Tn, 2 * Hd), T)
             call("crnn_gemm_nn", dt, ptr(dx), Hd, ptr(self.packed[pre + ".lin"]), 2 * Hd, ptr(dh), 2 * Hd, M,
                  2 * Hd, Hd, 0, 0, s)
-            call("crnn_gemm_tn", dt, ptr(dx), Hd, ptr(r["hseq"]), 2 * Hd, ptr(grads[pre + ".linear.weight"]),
-                 2 * Hd, Hd, 2 * Hd, M, acc, s)
+            self._gemm_tn(dx, Hd, r["hseq"], 2 * Hd, grads[pre + ".linear.weight"], 2 * Hd, Hd, 2 * Hd, M, acc)
             call("crnn_colsum", dt, ptr(dx), Hd, M, Hd, ptr(grads[pre + ".linear.bias"]), acc, 0, s)
             dg = ws.get("rnn.dgates", (2, Tn, B, 4 * Hd), T)
             dc = ws.get("rnn.dc", (2, B, Hd), torch.float32)
@@ -607,10 +606,17 @@ class CRNNEngine:
             rr = pre + ".rnn."
             gq = lambda n: ptr(self._gview(rr + n))
             # gradients straight into the parameters' .grad views (reference row order)
-            call("crnn_lstm_dwhh", dt, ptr(dg), ptr(r["hseq"]), gq("weight_hh_l0"), gq("weight_hh_l0_reverse"),
-                 B, Tn, Hd, acc, s)
-            call("crnn_lstm_dwih", dt, ptr(dg), ptr(r["x"]), gq("weight_ih_l0"), gq("weight_ih_l0_reverse"),
-                 B, Tn, Hd, ind, acc, s)
+            if T == torch.bfloat16:   # all four in one batched split-K launch + slab reduce
+                need = L.lib().crnn_lstm_wgrad_workspace(B, Tn, Hd, ind)
+                wgw = ws.get("rnn.wgrad_ws", ((need + 3) // 4,), torch.float32)
+                call("crnn_lstm_wgrad", ptr(dg), ptr(r["x"]), ptr(r["hseq"]), gq("weight_ih_l0"),
+                     gq("weight_ih_l0_reverse"), gq("weight_hh_l0"), gq("weight_hh_l0_reverse"), ptr(wgw),
+                     wgw.numel() * 4, B, Tn, Hd, ind, acc, s)
+            else:
+                call("crnn_lstm_dwhh", dt, ptr(dg), ptr(r["hseq"]), gq("weight_hh_l0"), gq("weight_hh_l0_reverse"),
+                     B, Tn, Hd, acc, s)
+                call("crnn_lstm_dwih", dt, ptr(dg), ptr(r["x"]), gq("weight_ih_l0"), gq("weight_ih_l0_reverse"),
+                     B, Tn, Hd, ind, acc, s)
             dbws = ws.get("rnn.dbws", (L.lib().crnn_lstm_dbias_workspace(Hd) // 4,), torch.float32)
             call("crnn_lstm_dbias", dt, ptr(dg), gq("bias_ih_l0"), gq("bias_hh_l0"), gq("bias_ih_l0_reverse"),
                  gq("bias_hh_l0_reverse"), ptr(dbws), B, Tn, Hd, acc, s)
@@ -718,6 +724,16 @@ class CRNNEngine:
         self._bn_bwd(1, da0, st["z0"], (st["m0"], st["i0"], st["sc0"], st["sh0"]), self.stem0.bn, B * h1 * w1, 64,
                      out=dz0, accumulate_params=accumulate)
         self._wgrad(self.stem0, dz0, st["x0"], B, st["H"], st["W"])
+
+    def _gemm_tn(self, A, lda, Bm, ldb, C, ldc, M, N, K, acc):
+        """C (fp32) (+)= A^T B: bf16 through split-K slabs + reduce (crnn_gemm_tn_slab), fp32 direct."""
+        if self.dtype == torch.bfloat16:
+            need = L.lib().crnn_gemm_tn_workspace(M, N, K)
+            w = self.ws.get(f"tn.ws.{need}", (need // 4 + 4,), torch.float32)
+            call("crnn_gemm_tn_slab", ptr(A), lda, ptr(Bm), ldb, ptr(C), ldc, M, N, K, acc, ptr(w), w.numel() * 4,
+                 L.stream_ptr())
+        else:
+            call("crnn_gemm_tn", self.dt, ptr(A), lda, ptr(Bm), ldb, ptr(C), ldc, M, N, K, acc, L.stream_ptr())
 
     def _scratch_elems(self, sv):
         st = sv["stem"]

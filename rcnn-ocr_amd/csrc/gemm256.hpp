@@ -184,7 +184,8 @@ __device__ __forceinline__ uint32_t lds_addr(const char* p) {
 
 template <int BM, int BN, class LA, class LB, class EPI>
 __global__ __launch_bounds__(512) void gemm256_kernel(LA la, LB lb, EPI epi, int M, int N, int K, int klen,
-                                                      int tiles_m, int tiles_n, int nsplit, int stagger) {
+                                                      int tiles_m, int tiles_n, int nsplit, int stagger,
+                                                      int nbatch) {
   using T = bf16;
   static_assert(BM == 256 && (BN == 256 || BN == 128), "tile");
   constexpr int KS = 64;
@@ -204,7 +205,9 @@ __global__ __launch_bounds__(512) void gemm256_kernel(LA la, LB lb, EPI epi, int
   // stages compute and while its epilogue runs. Positions u, u+1, u+2 of the sequence are
   // tracked by cursors (item, K-tile index); the loaders' row contexts follow the item of the
   // position being issued (re-initialised once per item, before the P2 issue that first needs it).
-  const int items = tiles_m * tiles_n * nsplit;
+  // item = ((batch * nsplit + split) * tiles_m + m_tile) * tiles_n + n_tile; a batch entry is an
+  // independent GEMM whose loaders / epilogue are selected by set_batch (nbatch > 1 only)
+  const int items = tiles_m * tiles_n * nsplit * nbatch;
   const int G = gridDim.x;
   const int lb_id = xcd_remap(blockIdx.x, G);
   if (lb_id >= items) return;
@@ -217,7 +220,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(LA la, LB lb, EPI epi, int
     int it, t, nk, kb;  // item, K-tile within the item, K-tiles of the item, first k of the item
   };
   auto item_k = [&](Cur& c) {
-    const int kz = c.it / (tiles_n * tiles_m);
+    const int kz = (c.it / (tiles_n * tiles_m)) % nsplit;
     c.kb = kz * klen;
     const int ke = min(K, c.kb + klen);
     c.nk = ke > c.kb ? (ke - c.kb + KS - 1) / KS : 1;   // an empty split still owns one (masked) K-tile
@@ -232,19 +235,26 @@ __global__ __launch_bounds__(512) void gemm256_kernel(LA la, LB lb, EPI epi, int
   auto tile_m0 = [&](int it) { return ((it / tiles_n) % tiles_m) * BM; };
   auto tile_n0 = [&](int it) { return (it % tiles_n) * BN; };
 
+  auto item_b = [&](int it) { return it / (tiles_n * tiles_m * nsplit); };
+  auto select_batch = [&](int bz) {
+    if constexpr (has_set_batch<LA>::value) la.set_batch(bz);
+    if constexpr (has_set_batch<LB>::value) lb.set_batch(bz);
+  };
   OA oa;
   OB ob;
   int ctx_it = lb_id;
+  if (nbatch > 1) select_batch(item_b(ctx_it));
   oa.init(la, tile_m0(ctx_it), wid, lane, wr);
   ob.init(lb, tile_n0(ctx_it), wid, lane, wc);
   auto ensure_ctx = [&](int it) {
     if (it != ctx_it) {
       ctx_it = it;
+      if (nbatch > 1) select_batch(item_b(it));
       oa.init(la, tile_m0(it), wid, lane, wr);
       ob.init(lb, tile_n0(it), wid, lane, wc);
     }
   };
-  const __amdgpu_buffer_rsrc_t ra = la.rsrc(), rb = lb.rsrc();
+  __amdgpu_buffer_rsrc_t ra = la.rsrc(), rb = lb.rsrc();
   char* const sA0 = smem;
   char* const sB0 = smem + OA::TB;
 
@@ -269,6 +279,10 @@ __global__ __launch_bounds__(512) void gemm256_kernel(LA la, LB lb, EPI epi, int
   advance(c1);
   if (c1.it < items) {
     ensure_ctx(c1.it);
+    if (nbatch > 1) {
+      ra = la.rsrc();
+      rb = lb.rsrc();
+    }
     const int k1 = c1.kb + c1.t * KS;
     const typename LA::Prep pa = la.prep(k1);
     const typename LB::Prep pb = lb.prep(k1);
@@ -318,7 +332,13 @@ __global__ __launch_bounds__(512) void gemm256_kernel(LA la, LB lb, EPI epi, int
     // ---- P2: quadrant (0,1)
     ob.template load<1, NQ>(*reinterpret_cast<bf16x8(*)[NQ][2]>(&bfr[NQ]), Bs, lB, wc * WN, lane);
     if (n2) {
-      ensure_ctx(c2.it);
+      if (nbatch > 1 && c2.it != ctx_it) {
+        ensure_ctx(c2.it);
+        ra = la.rsrc();
+        rb = lb.rsrc();
+      } else {
+        ensure_ctx(c2.it);
+      }
       oa.issue(la, ra, sA0 + b * STAGE, 0, pa2);
     }
     lds_wait_all();
@@ -366,7 +386,9 @@ __global__ __launch_bounds__(512) void gemm256_kernel(LA la, LB lb, EPI epi, int
     // ---- item finished: epilogue (registers + global stores only; the next item's first
     // stages are already in flight), then a fresh accumulator
     if (cur.t == cur.nk - 1) {
-      const int m0 = tile_m0(cur.it), n0 = tile_n0(cur.it), kz = cur.it / (tiles_n * tiles_m);
+      const int m0 = tile_m0(cur.it), n0 = tile_n0(cur.it), kz = (cur.it / (tiles_n * tiles_m)) % nsplit;
+      if constexpr (has_set_batch<EPI>::value)
+        if (nbatch > 1) epi.set_batch(item_b(cur.it));
       const int mr = lane & 15, nq = 4 * (lane >> 4);
 #pragma unroll
       for (int i = 0; i < MI; ++i)
@@ -387,19 +409,20 @@ __global__ __launch_bounds__(512) void gemm256_kernel(LA la, LB lb, EPI epi, int
 }
 
 // nsplit: split-K factor (K ranges of split_len(K, nsplit), multiples of 64)
+// nbatch: independent GEMMs of one shape in one launch (loaders / epilogue with set_batch(int))
 template <int BM, int BN, class LA, class LB, class EPI>
 inline int launch256(const LA& la, const LB& lb, const EPI& epi, int M, int N, int K, hipStream_t st,
-                     int nsplit = 1) {
+                     int nsplit = 1, int nbatch = 1) {
   if (M <= 0 || N <= 0) return 0;
   const int tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN;
   const int klen = split_len(K, nsplit);
   nsplit = K > 0 ? (K + klen - 1) / klen : 1;
   // persistent grid: at most one block per CU (1 block/CU by LDS); each block loops over items
-  const int items = tm * tn * nsplit;
+  const int items = tm * tn * nsplit * nbatch;
   const int ncu = crnn_option(CRNN_OPT_GEMM_PERSISTENT) ? crnn_cu_count() : items;
   const int grid = items < ncu ? items : ncu;
   hipLaunchKernelGGL((gemm256_kernel<BM, BN, LA, LB, EPI>), dim3(grid), dim3(512), 0, st, la, lb, epi,
-                     M, N, K, klen, tm, tn, nsplit, crnn_option(CRNN_OPT_GEMM_STAGGER));
+                     M, N, K, klen, tm, tn, nsplit, crnn_option(CRNN_OPT_GEMM_STAGGER), nbatch);
   return (int)hipGetLastError();
 }
 

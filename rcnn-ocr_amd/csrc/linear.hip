@@ -113,6 +113,49 @@ int gemm_tn_t(const void* A, int lda, const void* B, int ldb, float* C, int ldc,
   return launch<T, 32, 32>(la, lb, ep, M, N, K, splits, st);
 }
 
+// split-K partials of C = A^T B into fp32 slabs [S][M][N] (deterministic; fp32 atomics from every
+// split are several times slower on this chip), then one fixed-order reduce into C (ldc, +=)
+struct TnSlabEpi {
+  static constexpr bool kStats = false;
+  float* ws;
+  int M, N;
+  __device__ __forceinline__ void store(int m, int n, f32x4 v, int kz) const {
+    if (m < M && n < N) *reinterpret_cast<f32x4*>(ws + ((size_t)kz * M + m) * N + n) = v;
+  }
+  __device__ __forceinline__ void stats(int, int, f32x4, f32x4) const {}
+};
+
+__global__ __launch_bounds__(256) void tn_reduce_kernel(const float* __restrict__ ws, int S, int M, int N,
+                                                        float* __restrict__ C, int ldc, int accumulate) {
+  const long total = (long)M * N;
+  for (long i4 = blockIdx.x * (long)blockDim.x + threadIdx.x; 4 * i4 < total; i4 += (long)gridDim.x * blockDim.x) {
+    const long i = 4 * i4;
+    f32x4 s = {0.f, 0.f, 0.f, 0.f};
+    int z = 0;
+    for (; z + 8 <= S; z += 8) {
+      f32x4 v[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] = *reinterpret_cast<const f32x4*>(ws + (size_t)(z + q) * total + i);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) s += v[q];
+    }
+    for (; z < S; ++z) s += *reinterpret_cast<const f32x4*>(ws + (size_t)z * total + i);
+    const int m = (int)(i / N), n = (int)(i - (long)m * N);
+    float* o = C + (size_t)m * ldc + n;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = accumulate ? o[e] + s[e] : s[e];
+  }
+}
+
+inline int tn_slab_splits(int M, int N, int K) {
+  const long tiles = (long)((M + 127) / 128) * ((N + 127) / 128);
+  long s = (256 + tiles - 1) / tiles;
+  const long smax = (K + 16 * 64 - 1) / (16 * 64);   // >= 16 K-tiles per split
+  if (s > smax) s = smax;
+  if (s < 1) s = 1;
+  return eff_splits(K, (int)s);
+}
+
 // out[n] += sum over a row chunk; grid (ceil(N/64), row chunks)
 template <typename T>
 __global__ void colsum_kernel(const T* __restrict__ X, int ld, long M, int N, long rpc, float* __restrict__ out) {
@@ -170,6 +213,27 @@ int crnn_colsum(int dtype, const void* X, int ld, long M, int N, float* out, int
     hipLaunchKernelGGL(colsum_kernel<float>, grid, dim3(256), 0, st, (const float*)X, ld, M, N, rpc, out);
   else
     hipLaunchKernelGGL(colsum_kernel<bf16>, grid, dim3(256), 0, st, (const bf16*)X, ld, M, N, rpc, out);
+  return (int)hipGetLastError();
+}
+
+size_t crnn_gemm_tn_workspace(int M, int N, int K) {
+  return (size_t)tn_slab_splits(M, N, K) * M * N * sizeof(float);
+}
+
+int crnn_gemm_tn_slab(const void* A, int lda, const void* B, int ldb, float* C, int ldc, int M, int N, int K,
+                      int accumulate, float* ws, size_t ws_bytes, void* stream) {
+  if (M % 8 || N % 8 || lda % 8 || ldb % 8) return crnn_set_error(hipErrorInvalidValue, "gemm_tn: M/N/ld must be multiples of 8");
+  if (ws_bytes < crnn_gemm_tn_workspace(M, N, K)) return crnn_set_error(hipErrorInvalidValue, "gemm_tn: workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  const int S = tn_slab_splits(M, N, K);
+  ColMajorK<bf16> la{(const bf16*)A, lda, M, K};
+  ColMajorK<bf16> lb{(const bf16*)B, ldb, N, K};
+  TnSlabEpi ep{ws, M, N};
+  int rc = launch<bf16, 128, 128>(la, lb, ep, M, N, K, S, st);
+  if (rc) return rc;
+  int blocks = (int)(((long)M * N / 4 + 255) / 256);
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(tn_reduce_kernel, dim3(blocks), dim3(256), 0, st, ws, S, M, N, C, ldc, accumulate);
   return (int)hipGetLastError();
 }
 

@@ -361,6 +361,112 @@ template <typename T> struct StoreEpi {
   __device__ __forceinline__ void stats(int, int, f32x4, f32x4) const {}
 };
 
+// ---- all four weight-gradient GEMMs of a layer in one launch (bf16):
+//   batch bz = 2*d + kind:  kind 0  dW_ih[d] = dgates[d]^T x          ([4H][In])
+//                           kind 1  dW_hh[d] = dgates[d]^T h_prev[d]  ([4H][H])
+// split-K over ~one block per CU into fp32 slabs [bz][split][4H][N] (N = max(In, H)), then one
+// reduce that sums the splits in fixed order and scatters packed gate rows (4j+q) to the
+// reference rows (q*H + j). Four GEMMs share the grid, so each needs ~4x fewer splits than alone.
+// batch-selectable loaders: the batch entry's parameters are derived arithmetically from bz
+// (an array of per-batch loader copies indexed at run time would live in scratch memory)
+template <typename T> struct GateWA {   // A rows g' (packed gate), k = t*B + b: dgates[d][k][g']
+  static constexpr bool kRowVec = true;
+  const T* dg;
+  int H4, K, d;
+  struct Ctx { uint32_t off; bool ok; };
+  typedef int Prep;
+  __device__ __forceinline__ void set_batch(int bz) { d = bz >> 1; }
+  __device__ __forceinline__ Ctx row_ctx(int r8) const { return Ctx{(uint32_t)r8, r8 < H4}; }
+  __device__ __forceinline__ Prep prep(int k0) const { return k0; }
+  __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc() const {
+    return mk_rsrc(dg + (size_t)d * K * H4, (uint32_t)((size_t)K * H4 * sizeof(T)));
+  }
+  __device__ __forceinline__ uint32_t offs(const Ctx& c, Prep k0, int kofs) const {
+    const int k = k0 + kofs;
+    return boff<T>((uint32_t)k * (uint32_t)H4 + c.off, c.ok && k < K);
+  }
+};
+
+template <typename T> struct GateWB {   // B rows n, k = t*B + b: x[b][t][n] (kind 0) or h_{t-1}[b][d][n] (kind 1)
+  static constexpr bool kRowVec = true;
+  const T* x;
+  const T* hseq;
+  int B, Tn, H, In, d, kind;
+  FastDiv dB;
+  struct Ctx { int j; bool ok; };
+  typedef int Prep;
+  __device__ __forceinline__ void set_batch(int bz) {
+    d = bz >> 1;
+    kind = bz & 1;
+  }
+  __device__ __forceinline__ Ctx row_ctx(int r8) const { return Ctx{r8, r8 < (kind ? H : In)}; }
+  __device__ __forceinline__ Prep prep(int k0) const { return k0; }
+  __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc() const {
+    return kind == 0 ? mk_rsrc(x, (uint32_t)((size_t)B * Tn * In * sizeof(T)))
+                     : mk_rsrc(hseq, (uint32_t)((size_t)B * Tn * 2 * H * sizeof(T)));
+  }
+  __device__ __forceinline__ uint32_t offs(const Ctx& c, Prep k0, int kofs) const {
+    const int k = k0 + kofs;
+    uint32_t bu;
+    const int t = (int)dB.divmod((uint32_t)k, bu), b = (int)bu;
+    if (kind == 0) return boff<T>((uint32_t)((b * Tn + t) * In + c.j), c.ok && k < Tn * B);
+    const int tp = d == 0 ? t - 1 : t + 1;
+    const bool ok = c.ok && k < Tn * B && tp >= 0 && tp < Tn;
+    return boff<T>((uint32_t)(((b * Tn + tp) * 2 * H) + d * H + c.j), ok);
+  }
+};
+
+struct BatchSlabEpi {
+  static constexpr bool kStats = false;
+  float* ws;  // [NB][nsplit][M][N]
+  int M, N, nsplit, bz;
+  __device__ __forceinline__ void set_batch(int b) { bz = b; }
+  __device__ __forceinline__ void store(int m, int n, f32x4 v, int kz) const {
+    if (m < M && n < N) *reinterpret_cast<f32x4*>(ws + (((size_t)bz * nsplit + kz) * M + m) * N + n) = v;
+  }
+  __device__ __forceinline__ void stats(int, int, f32x4, f32x4) const {}
+};
+
+struct GateOut {
+  float* p[4];   // [bz] destination, [4H][cols] reference gate order
+  int cols[4];
+};
+
+__global__ __launch_bounds__(256) void gate_slab_reduce_kernel(const float* __restrict__ ws, int S, int H, int N,
+                                                               GateOut out, int accumulate) {
+  const int bz = blockIdx.y, H4 = 4 * H, cols = out.cols[bz];
+  const long total = (long)H4 * N;
+  for (long i4 = blockIdx.x * (long)blockDim.x + threadIdx.x; 4 * i4 < total; i4 += (long)gridDim.x * blockDim.x) {
+    const long i = 4 * i4;
+    const int gp = (int)(i / N), n = (int)(i - (long)gp * N);
+    if (n >= cols) continue;
+    f32x4 s = {0.f, 0.f, 0.f, 0.f};
+    const float* base = ws + (size_t)bz * S * total + i;
+    int z = 0;
+    for (; z + 4 <= S; z += 4) {
+      f32x4 v[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = *reinterpret_cast<const f32x4*>(base + (size_t)(z + q) * total);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) s += v[q];
+    }
+    for (; z < S; ++z) s += *reinterpret_cast<const f32x4*>(base + (size_t)z * total);
+    float* o = out.p[bz] + (size_t)((gp & 3) * H + (gp >> 2)) * cols + n;
+    if (accumulate) s += *reinterpret_cast<const f32x4*>(o);
+    *reinterpret_cast<f32x4*>(o) = s;
+  }
+}
+
+inline int lstm_wgrad_splits(int B, int T, int H, int In) {
+  const int N = In > H ? In : H, K = T * B;
+  const long tiles = 4L * ((4 * H + 255) / 256) * ((N + 255) / 256);
+  long s = (crnn_cu_count() + tiles - 1) / tiles;
+  const long smax = K / (64 * 8);
+  if (s > smax) s = smax;
+  if (s < 1) s = 1;
+  return eff_splits(K, (int)s);
+}
+
 }  // namespace
 
 extern "C" {
@@ -452,6 +558,32 @@ int crnn_lstm_dx(int dtype, const void* dgates, const void* wih, void* dx, int B
   ColMajorK<float> lb{(const float*)wih, In, In, K};
   StoreEpi<float> ep{(float*)dx, M, In};
   return launch<float, 64, 64>(la, lb, ep, M, In, K, 1, st);
+}
+
+size_t crnn_lstm_wgrad_workspace(int B, int T, int H, int In) {
+  const int N = In > H ? In : H;
+  return (size_t)4 * lstm_wgrad_splits(B, T, H, In) * 4 * H * N * sizeof(float);
+}
+
+int crnn_lstm_wgrad(const void* dgates, const void* x, const void* hseq, float* dwih_f, float* dwih_r, float* dwhh_f,
+                    float* dwhh_r, float* ws, size_t ws_bytes, int B, int T, int H, int In, int accumulate,
+                    void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (In % 8 || H % 8) return crnn_set_error(hipErrorInvalidValue, "lstm_wgrad: In, H must be multiples of 8");
+  if (ws_bytes < crnn_lstm_wgrad_workspace(B, T, H, In))
+    return crnn_set_error(hipErrorInvalidValue, "lstm_wgrad: workspace too small");
+  const int N = In > H ? In : H, K = T * B, S = lstm_wgrad_splits(B, T, H, In);
+  GateWA<bf16> la{(const bf16*)dgates, 4 * H, K, 0};
+  GateWB<bf16> lb{(const bf16*)x, (const bf16*)hseq, B, T, H, In, 0, 0, FastDiv(B)};
+  BatchSlabEpi ep{ws, 4 * H, N, S, 0};
+  int rc = launch256<256, 256>(la, lb, ep, 4 * H, N, K, st, S, 4);
+  if (rc) return rc;
+  GateOut go{{dwih_f, dwhh_f, dwih_r, dwhh_r}, {In, H, In, H}};
+  const long n4 = (long)4 * H * N / 4;
+  int bx = (int)((n4 + 255) / 256);
+  if (bx > 1024) bx = 1024;
+  hipLaunchKernelGGL(gate_slab_reduce_kernel, dim3(bx, 4), dim3(256), 0, st, ws, S, H, N, go, accumulate);
+  return (int)hipGetLastError();
 }
 
 }  // extern "C"

@@ -156,6 +156,14 @@ def test_gemm_nt_nn_tn(mnk, dtype):
         Atd, Btd = At.to(DEV, dtype), Bt.to(DEV, dtype)  # keep both alive across the call
         L.call("crnn_gemm_tn", dt, Atd.data_ptr(), M, Btd.data_ptr(), N, C3.data_ptr(), N, M, N, K, 0, st)
         assert relerr(C3.cpu(), At.t() @ Bt) < tol
+        if dtype == torch.bfloat16:   # split-K slab path, overwrite then accumulate
+            need = L.lib().crnn_gemm_tn_workspace(M, N, K)
+            wsb = torch.empty(need // 4 + 4, device=DEV)
+            C4 = torch.full((M, N), 7.0, device=DEV)
+            for accm in (0, 1):
+                L.call("crnn_gemm_tn_slab", Atd.data_ptr(), M, Btd.data_ptr(), N, C4.data_ptr(), N, M, N, K, accm,
+                       wsb.data_ptr(), need, st)
+            assert relerr(C4.cpu(), 2 * (At.t() @ Bt)) < tol
 
 
 def _pack_lstm(w_ih, w_hh, b_ih, b_hh, H, dtype, L):
@@ -249,6 +257,18 @@ def test_bilstm_fwd_bwd(BTHI, dtype, oneshot):
     db = torch.empty(2, 4 * H, device=DEV)
     L.call("crnn_lstm_dwhh", dt, dg.data_ptr(), hseq.data_ptr(), dwhh[0].data_ptr(), dwhh[1].data_ptr(), B, T, H, 0, st)
     L.call("crnn_lstm_dwih", dt, dg.data_ptr(), xd.data_ptr(), dwih[0].data_ptr(), dwih[1].data_ptr(), B, T, H, In, 0, st)
+    if dtype == torch.bfloat16:
+        # batched one-launch weight gradients == the two per-kind calls (up to fp32 summation order),
+        # in both overwrite and accumulate modes
+        need = L.lib().crnn_lstm_wgrad_workspace(B, T, H, In)
+        wgw = torch.empty(need // 4 + 4, device=DEV)
+        w2 = [torch.full_like(dwih[0], 0.5), torch.full_like(dwih[1], 0.5), torch.full_like(dwhh[0], 0.5),
+              torch.full_like(dwhh[1], 0.5)]
+        for accm in (0, 1):
+            L.call("crnn_lstm_wgrad", dg.data_ptr(), xd.data_ptr(), hseq.data_ptr(), w2[0].data_ptr(), w2[1].data_ptr(),
+                   w2[2].data_ptr(), w2[3].data_ptr(), wgw.data_ptr(), need, B, T, H, In, accm, st)
+        for got, ref in zip(w2, [dwih[0], dwih[1], dwhh[0], dwhh[1]]):
+            assert relerr(got.cpu(), 2 * ref.cpu()) < 1e-5
     db2 = torch.full((2, 4 * H), 3.0, device=DEV)
     dbws = torch.empty(L.lib().crnn_lstm_dbias_workspace(H) // 4, device=DEV)
     L.call("crnn_lstm_dbias", dt, dg.data_ptr(), db[0].data_ptr(), db2[0].data_ptr(), db[1].data_ptr(), None,

@@ -34,6 +34,11 @@ def main():
     dg = torch.randn(2, T, B, 4 * H, device=dev).to(bf)
     dW = torch.empty(2, 4 * H, H, device=dev)
     dxl = torch.empty(B, T, In, device=dev, dtype=bf)
+    dW4 = torch.empty(4, 4 * H, H, device=dev)
+    tnneed = L.lib().crnn_gemm_tn_workspace(H, 2 * H, M)
+    tnw = torch.empty(tnneed // 4 + 4, device=dev)
+    need = L.lib().crnn_lstm_wgrad_workspace(B, T, H, In)
+    wgw = torch.empty(need // 4 + 4, device=dev)
     ops = {
         "xg nt 8192x4096x512": lambda: L.call("crnn_gemm_nt", L.BF16, x.data_ptr(), In, wih.data_ptr(), In, xg.data_ptr(),
                                               8 * H, bias.data_ptr(), M, 8 * H, In, 0, 0, st),
@@ -43,10 +48,15 @@ def main():
                                                    dh.data_ptr(), 2 * H, M, 2 * H, H, 0, 0, st),
         "lin wgrad tn 512x1024x8192": lambda: L.call("crnn_gemm_tn", L.BF16, dx.data_ptr(), H, hseq.data_ptr(), 2 * H,
                                                      dlw.data_ptr(), 2 * H, H, 2 * H, M, 0, st),
+        "lin wgrad tn slab": lambda: L.call("crnn_gemm_tn_slab", dx.data_ptr(), H, hseq.data_ptr(), 2 * H,
+                                            dlw.data_ptr(), 2 * H, H, 2 * H, M, 0, tnw.data_ptr(), tnneed, st),
         "dwhh (2 dirs)": lambda: L.call("crnn_lstm_dwhh", L.BF16, dg.data_ptr(), hseq.data_ptr(), dW[0].data_ptr(),
                                         dW[1].data_ptr(), B, T, H, 0, st),
         "dwih (2 dirs)": lambda: L.call("crnn_lstm_dwih", L.BF16, dg.data_ptr(), x.data_ptr(), dW[0].data_ptr(),
                                         dW[1].data_ptr(), B, T, H, In, 0, st),
+        "lstm wgrad batched (4)": lambda: L.call("crnn_lstm_wgrad", dg.data_ptr(), x.data_ptr(), hseq.data_ptr(),
+                                                 dW4[0].data_ptr(), dW4[1].data_ptr(), dW4[2].data_ptr(),
+                                                 dW4[3].data_ptr(), wgw.data_ptr(), need, B, T, H, In, 0, st),
         "lstm dx": lambda: L.call("crnn_lstm_dx", L.BF16, dg.data_ptr(), wih.data_ptr(), dxl.data_ptr(), B, T, H, In, st),
     }
     for name, fn in ops.items():
