@@ -123,13 +123,16 @@ def main():
     grads, _ = model._grad_views()
     opt = FusedAdamW(model, lr=1e-4, weight_decay=1e-2)
     inv_world = 1.0 / world
+    # DP: bucketed RCCL all-reduce of the flat gradient, issued stage by stage during the backward
+    # (head / BiLSTM first, stem last) so it overlaps the remaining backward kernels
+    reducer = D.OverlappedAllReduce(model._flat_grad, model.flat_offsets()) if world > 1 else None
 
     def step():
         eng.forward(x, train=True, save_for_backward=True)
         loss, dl = eng.ctc(eng.logits_padded(), tg, tl)
-        eng.backward(dl, grads, accumulate=False)
-        if world > 1:
-            D.allreduce_grads(model._flat_grad)
+        eng.backward(dl, grads, accumulate=False, stage_done=reducer.ready if reducer else None)
+        if reducer is not None:
+            reducer.finish()
         opt.step(grad_scale=inv_world)
         return loss
 
@@ -154,6 +157,13 @@ def main():
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
+    divergence = None
+    if world > 1:   # replicas must hold identical weights after the timed steps (same reduced grads)
+        c = model._flat_param.double().sum().reshape(1)
+        cmax, cmin = c.clone(), c.clone()
+        dist.all_reduce(cmax, op=dist.ReduceOp.MAX)
+        dist.all_reduce(cmin, op=dist.ReduceOp.MIN)
+        divergence = float((cmax - cmin).item())
     lines = args.batch * world * args.steps
     value = lines / elapsed
     final_loss = float(loss.item())
@@ -196,6 +206,8 @@ def main():
             "kernels": per_kind,
             "roofline_lstm": lstm_roofline(lstm, args, eng),
             "final_loss": round(final_loss, 4),
+            "dp": ({"allreduce": "RCCL sum of the flat fp32 gradient, bucketed and overlapped with the backward",
+                    "param_checksum_spread": divergence} if world > 1 else None),
         }
         if world == 1 and not args.no_cpu_baseline:
             try:

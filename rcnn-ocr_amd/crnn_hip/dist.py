@@ -2,9 +2,15 @@
 
 The path shards by sample: every rank runs the full train step on its own
 batch shard; BatchNorm uses per-rank batch statistics (the reference's plain BatchNorm2d,
-no SyncBN). The only exchange is a sum all-reduce of the flat fp32 gradient buffer,
-issued in buckets so several collectives are in flight at once; the optimizer then scales
-by 1/world. Parameters are broadcast from rank 0 once at start.
+no SyncBN). The only exchange is a sum all-reduce of the flat fp32 gradient buffer; the
+optimizer then scales by 1/world. Parameters are broadcast from rank 0 once at start.
+
+Overlap (OverlappedAllReduce): the flat buffer is laid out in parameter order (stem first, CTC
+head last) and the backward finalises gradients from the end of it towards the start, stage by
+stage (CRNNEngine.backward's stage_done hook). Each time the final region grows by at least
+min_bucket bytes its new part is all-reduced asynchronously on RCCL's stream while the backward
+kernels of the earlier layers keep running; finish() issues the remainder and makes the compute
+stream wait for every collective before the optimizer step.
 """
 from __future__ import annotations
 
@@ -26,11 +32,13 @@ def init_from_env(backend: Optional[str] = None):
     """init_process_group from torchrun's env (MASTER_ADDR/PORT, RANK, WORLD_SIZE);
     backend 'nccl' (= RCCL on ROCm) for HIP devices, 'gloo' for CPU tests."""
     world, rank, local = env_world()
+    if os.environ.get("CRNN_SHARE_DEVICE") == "1":   # rehearsal only: every rank on device 0
+        local = 0
     if world <= 1 or dist.is_initialized():
         return world, rank, local
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     if backend is None:
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        backend = os.environ.get("CRNN_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
     if backend == "nccl":
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -58,3 +66,41 @@ def allreduce_grads(flat_grad: torch.Tensor, bucket_bytes: int = BUCKET_BYTES):
              for s in reversed(buckets(flat_grad.numel(), flat_grad.element_size(), bucket_bytes))]
     for w in works:
         w.wait()
+
+
+class OverlappedAllReduce:
+    """bucketed sum all-reduce of a flat gradient buffer, overlapped with the backward: call
+    ready(prefixes) from CRNNEngine.backward's stage_done hook, then finish()."""
+
+    def __init__(self, flat_grad: torch.Tensor, offsets, min_bucket_bytes: int = 8 << 20):
+        """offsets: {param name: (start, numel)} into flat_grad (the model's flat layout)."""
+        self.flat = flat_grad
+        self.offsets = offsets
+        self.min_elems = max(1, min_bucket_bytes // flat_grad.element_size())
+        self.active = dist.is_initialized() and dist.get_world_size() > 1
+        self.reset()
+
+    def reset(self):
+        self.hi = self.flat.numel()      # [hi, end) already issued
+        self.lo = self.hi                # [lo, end) final
+        self.works = []
+
+    def ready(self, prefixes):
+        starts = [s for k, (s, n) in self.offsets.items() if any(k.startswith(p) for p in prefixes)]
+        if starts:
+            self.lo = min(self.lo, min(starts))
+        if self.active and self.hi - self.lo >= self.min_elems:
+            self._issue(self.lo, self.hi)
+
+    def _issue(self, lo, hi):
+        self.works.append(dist.all_reduce(self.flat[lo:hi], async_op=True))
+        self.hi = lo
+
+    def finish(self):
+        if self.active:
+            if self.hi > 0:
+                self._issue(0, self.hi)
+            for w in self.works:
+                w.wait()
+        self.reset()
+

@@ -556,8 +556,14 @@ class CRNNEngine:
         upd(self.co1, h, w)
         return cap
 
-    def backward(self, dlogits: torch.Tensor, grads: Dict[str, torch.Tensor], accumulate: bool = False):
-        """Full backward from d loss / d logits [B,T,Cpad] fp32 into `grads` (fp32, reference layouts)."""
+    def backward(self, dlogits: torch.Tensor, grads: Dict[str, torch.Tensor], accumulate: bool = False,
+                 stage_done=None):
+        """Full backward from d loss / d logits [B,T,Cpad] fp32 into `grads` (fp32, reference layouts).
+        stage_done(prefixes): called (host side, after the stage's kernels are enqueued) each time the
+        gradients of every parameter under the given name prefixes are final — CTC head + BiLSTM, then
+        conv_out, each residual block (last to first), the stem — so a data-parallel caller can start
+        their all-reduce while the rest of the backward runs."""
+        done = stage_done if stage_done is not None else (lambda prefixes: None)
         sv = self._saved
         if sv is None:
             raise RuntimeError("forward(save_for_backward=True) must precede backward")
@@ -626,6 +632,7 @@ class CRNNEngine:
         dseq = dx  # [B, T, 512]
         if self.debug:
             self.dbg["dseq"] = dseq.clone()
+        done(["ctc_head.", "enc_rnn."])
         # ---- conv_out + height collapse
         co = sv["co"]
         big = self._scratch_elems(sv)
@@ -652,6 +659,7 @@ class CRNNEngine:
         dy = bufB[: B * co["h"] * co["w"] * 512]
         self._conv_call("dgrad", self.conv_flops(self.co0, B, co["h"], co["w"]), "crnn_conv_dgrad", dt, self.co0.desc(B, co["h"], co["w"]), ptr(dz0), ptr(self.packed[self.co0.name]),
              ptr(dy), None, None, 0, s)
+        done(["cnn.conv_out."])
         # ---- residual blocks, reverse
         bufs = [bufA, bufB, bufC]
         cur = 1  # dy lives in bufB
@@ -705,6 +713,7 @@ class CRNNEngine:
                 self._conv_call("dgrad", self.conv_flops(blk.ds, B, h, w), "crnn_conv_dgrad", dt, blk.ds.desc(B, h, w), ptr(dzd), ptr(self.packed[blk.ds.name]),
                      ptr(dxb), None, None, 1, s)
                 cur = o2
+            done([blk.prefix + "."])
         # ---- stem
         o1, o2 = [k for k in range(3) if k != cur]
         dp = bufs[cur]
@@ -724,6 +733,7 @@ class CRNNEngine:
         self._bn_bwd(1, da0, st["z0"], (st["m0"], st["i0"], st["sc0"], st["sh0"]), self.stem0.bn, B * h1 * w1, 64,
                      out=dz0, accumulate_params=accumulate)
         self._wgrad(self.stem0, dz0, st["x0"], B, st["H"], st["W"])
+        done(["cnn.conv0."])
 
     def _gemm_tn(self, A, lda, Bm, ldb, C, ldc, M, N, K, acc):
         """C (fp32) (+)= A^T B: bf16 through split-K slabs + reduce (crnn_gemm_tn_slab), fp32 direct."""

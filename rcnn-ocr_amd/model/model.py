@@ -118,6 +118,14 @@ class RCNN(nn.Module):
         self._flat_param, self._flat_grad = flat, gflat
         self._grad_offsets = None
 
+    def flat_offsets(self):
+        """{parameter name: (start, numel)} in the flat buffer (parameter order: stem first, head last)."""
+        out, off = {}, 0
+        for n, p in self.named_parameters():
+            out[n] = (off, p.numel())
+            off += p.numel()
+        return out
+
     def _grad_views(self):
         """(name -> grad tensor, accumulate?) ; re-attaches flat views after zero_grad(set_to_none=True)."""
         params = list(self.named_parameters())

@@ -61,7 +61,19 @@ def _worker(rank, world, port, q):
         part = grads(x[2 * rank:2 * rank + 2], tg[2 * rank:2 * rank + 2], tl[2 * rank:2 * rank + 2])
         D.allreduce_grads(part)
         ok_dp = torch.allclose(part, full, rtol=1e-4, atol=1e-5)
-        q.put((rank, ok_sum, ok_bc, ok_dp))
+        # overlapped reducer: stage-wise readiness in backward order, every element reduced exactly once
+        offs = {"cnn.conv0.0.weight": (0, 100), "cnn.layer1.0.conv1.weight": (100, 300),
+                "cnn.conv_out.0.weight": (400, 200), "enc_rnn.0.linear.weight": (600, 300),
+                "ctc_head.weight": (900, 100)}
+        ok_ov = True
+        for mb in (4, 4 * 250, 4 * 5000):   # every stage its own bucket / merged / all at finish()
+            g2 = torch.arange(1000, dtype=torch.float32) * (rank + 1)
+            red = D.OverlappedAllReduce(g2, offs, min_bucket_bytes=mb)
+            for pre in (["ctc_head.", "enc_rnn."], ["cnn.conv_out."], ["cnn.layer1.0."], ["cnn.conv0."]):
+                red.ready(pre)
+            red.finish()
+            ok_ov = ok_ov and torch.allclose(g2, torch.arange(1000, dtype=torch.float32) * 3)
+        q.put((rank, ok_sum, ok_bc, ok_dp and ok_ov))
     finally:
         dist.destroy_process_group()
 
