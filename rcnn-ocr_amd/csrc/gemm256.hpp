@@ -182,8 +182,170 @@ __device__ __forceinline__ uint32_t lds_addr(const char* p) {
   return (uint32_t)(size_t)((const __attribute__((address_space(3))) char*)p);
 }
 
+// One block per work item (the default): the K-loop above, block-level.
 template <int BM, int BN, class LA, class LB, class EPI>
 __global__ __launch_bounds__(512) void gemm256_kernel(LA la, LB lb, EPI epi, int M, int N, int K, int klen,
+                                                      int tiles_m, int tiles_n, int nsplit, int stagger,
+                                                      int nbatch) {
+  using T = bf16;
+  static_assert(BM == 256 && (BN == 256 || BN == 128), "tile");
+  constexpr int KS = 64;
+  constexpr int WM = BM / 2, WN = BN / 4;        // per-wave output block
+  constexpr int MI = WM / 16, NI = WN / 16;      // 16x16 fragments per wave
+  constexpr int MQ = MI / 2, NQ = NI / 2;        // fragments per quadrant
+  constexpr int QM = WM / 2, QN = WN / 2;        // quadrant extent
+  using OA = Op256<LA, BM, QM>;
+  using OB = Op256<LB, BN, QN>;
+  constexpr int STAGE = OA::TB + OB::TB;
+  constexpr int VM = OA::I + 2 * OB::I;          // DMA instructions of tile t+2 issued before the P4 wait
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+
+  // one work item per block: ((batch * nsplit + split) * tiles_m + m_tile) * tiles_n + n_tile
+  const int nwg = tiles_m * tiles_n * nsplit * nbatch;
+  const int wg = xcd_remap(blockIdx.x, nwg);
+  const int n_tile = wg % tiles_n, m_tile = (wg / tiles_n) % tiles_m, kz = (wg / (tiles_n * tiles_m)) % nsplit;
+  if (nbatch > 1) {
+    const int bz = wg / (tiles_n * tiles_m * nsplit);
+    if constexpr (has_set_batch<LA>::value) la.set_batch(bz);
+    if constexpr (has_set_batch<LB>::value) lb.set_batch(bz);
+    if constexpr (has_set_batch<EPI>::value) epi.set_batch(bz);
+  }
+  const int m0 = m_tile * BM, n0 = n_tile * BN;
+  const int kbeg = kz * klen, kend = min(K, kbeg + klen);
+  const int nk = kend > kbeg ? (kend - kbeg + KS - 1) / KS : 0;
+
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wid >> 2, wc = wid & 3;
+
+  OA oa;
+  OB ob;
+  oa.init(la, m0, wid, lane, wr);
+  ob.init(lb, n0, wid, lane, wc);
+  const __amdgpu_buffer_rsrc_t ra = la.rsrc(), rb = lb.rsrc();
+  char* const sA0 = smem;
+  char* const sB0 = smem + OA::TB;
+
+  f32x4 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // ---- prologue: tile 0 whole, tile 1 except its A-half1 (issued in P1 of tile 0)
+  typename LA::Prep pa2 = la.prep(kbeg);
+  typename LB::Prep pb2 = lb.prep(kbeg);
+  if (nk > 0) {
+    oa.issue(la, ra, sA0, 0, pa2);
+    ob.issue(lb, rb, sB0, 0, pb2);
+    ob.issue(lb, rb, sB0, 1, pb2);
+    oa.issue(la, ra, sA0, 1, pa2);
+  }
+  typename LA::Prep pa1 = pa2;  // prep of tile t+1 (for its A-half1)
+  if (nk > 1) {
+    pa1 = la.prep(kbeg + KS);
+    const typename LB::Prep pb1 = lb.prep(kbeg + KS);
+    oa.issue(la, ra, sA0 + STAGE, 0, pa1);
+    ob.issue(lb, rb, sB0 + STAGE, 0, pb1);
+    ob.issue(lb, rb, sB0 + STAGE, 1, pb1);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(VM) : "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  raw_barrier();
+  // ping-pong: waves 4-7 (wr == 1, one per SIMD) run one barrier behind waves 0-3, so each SIMD
+  // alternates one wave's MFMA cluster with its partner's ds_read / LDS-DMA issue segment
+  if (stagger && wr == 1) raw_barrier();
+
+  bf16x8 af[MQ][2], bfr[NI][2];
+  for (int t = 0; t < nk; ++t) {
+    const int b = t & 1;
+    const char* As = smem + b * STAGE;
+    const char* Bs = As + OA::TB;
+    const uint32_t lA = lds_addr(As), lB = lds_addr(Bs);
+    const bool n1 = t + 1 < nk, n2 = t + 2 < nk;
+    if (n2) {
+      pa2 = la.prep(kbeg + (t + 2) * KS);
+      pb2 = lb.prep(kbeg + (t + 2) * KS);
+    }
+    // ---- P1: quadrant (0,0)
+    oa.template load<0, MQ>(af, As, lA, wr * WM, lane);
+    ob.template load<0, NQ>(*reinterpret_cast<bf16x8(*)[NQ][2]>(&bfr[0]), Bs, lB, wc * WN, lane);
+    if (n1) oa.issue(la, ra, sA0 + (b ^ 1) * STAGE, 1, pa1);
+    lds_wait_all();
+    raw_barrier();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < MQ; ++i)
+#pragma unroll
+        for (int j = 0; j < NQ; ++j) mma<T>(acc[i][j], bfr[j][kk], af[i][kk]);
+    __builtin_amdgcn_s_setprio(0);
+    raw_barrier();
+    // ---- P2: quadrant (0,1)
+    ob.template load<1, NQ>(*reinterpret_cast<bf16x8(*)[NQ][2]>(&bfr[NQ]), Bs, lB, wc * WN, lane);
+    if (n2) oa.issue(la, ra, sA0 + b * STAGE, 0, pa2);
+    lds_wait_all();
+    raw_barrier();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < MQ; ++i)
+#pragma unroll
+        for (int j = NQ; j < NI; ++j) mma<T>(acc[i][j], bfr[j][kk], af[i][kk]);
+    __builtin_amdgcn_s_setprio(0);
+    raw_barrier();
+    // ---- P3: quadrant (1,1)
+    oa.template load<1, MQ>(af, As, lA, wr * WM, lane);
+    if (n2) ob.issue(lb, rb, sB0 + b * STAGE, 0, pb2);
+    lds_wait_all();
+    raw_barrier();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < MQ; ++i)
+#pragma unroll
+        for (int j = NQ; j < NI; ++j) mma<T>(acc[MQ + i][j], bfr[j][kk], af[i][kk]);
+    __builtin_amdgcn_s_setprio(0);
+    raw_barrier();
+    // ---- P4: quadrant (1,0)
+    if (n2) {
+      ob.issue(lb, rb, sB0 + b * STAGE, 1, pb2);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(VM) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    pa1 = pa2;
+    raw_barrier();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < MQ; ++i)
+#pragma unroll
+        for (int j = 0; j < NQ; ++j) mma<T>(acc[MQ + i][j], bfr[j][kk], af[i][kk]);
+    __builtin_amdgcn_s_setprio(0);
+    raw_barrier();
+  }
+  if (stagger && wr == 0) raw_barrier();
+
+  const int mr = lane & 15, nq = 4 * (lane >> 4);
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) epi.store(m0 + wr * WM + i * 16 + mr, n0 + wc * WN + j * 16 + nq, acc[i][j], kz);
+  if constexpr (EPI::kStats) wave_col_stats<MI, NI>(acc, epi, M, m0 + wr * WM, m_tile * 2 + wr, n0 + wc * WN, lane);
+}
+
+// Persistent variant (crnn_set_option CRNN_OPT_GEMM_PERSISTENT): grid <= CU count, every block
+// loops over work items with one continuous LDS-DMA pipeline across item boundaries. Measured no
+// faster on this path's shapes (the short-K stem conv included) and slower on some, so it is off
+// by default and kept for A/B.
+template <int BM, int BN, class LA, class LB, class EPI>
+__global__ __launch_bounds__(512) void gemm256p_kernel(LA la, LB lb, EPI epi, int M, int N, int K, int klen,
                                                       int tiles_m, int tiles_n, int nsplit, int stagger,
                                                       int nbatch) {
   using T = bf16;
@@ -417,12 +579,15 @@ inline int launch256(const LA& la, const LB& lb, const EPI& epi, int M, int N, i
   const int tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN;
   const int klen = split_len(K, nsplit);
   nsplit = K > 0 ? (K + klen - 1) / klen : 1;
-  // persistent grid: at most one block per CU (1 block/CU by LDS); each block loops over items
   const int items = tm * tn * nsplit * nbatch;
-  const int ncu = crnn_option(CRNN_OPT_GEMM_PERSISTENT) ? crnn_cu_count() : items;
-  const int grid = items < ncu ? items : ncu;
-  hipLaunchKernelGGL((gemm256_kernel<BM, BN, LA, LB, EPI>), dim3(grid), dim3(512), 0, st, la, lb, epi,
-                     M, N, K, klen, tm, tn, nsplit, crnn_option(CRNN_OPT_GEMM_STAGGER), nbatch);
+  const int ncu = crnn_cu_count();
+  const int popt = crnn_option(CRNN_OPT_GEMM_PERSISTENT);   // 1: when items > CUs, 2: always
+  if ((popt == 1 && items > ncu) || popt == 2)
+    hipLaunchKernelGGL((gemm256p_kernel<BM, BN, LA, LB, EPI>), dim3(items < ncu ? items : ncu), dim3(512), 0, st, la, lb, epi,
+                       M, N, K, klen, tm, tn, nsplit, crnn_option(CRNN_OPT_GEMM_STAGGER), nbatch);
+  else
+    hipLaunchKernelGGL((gemm256_kernel<BM, BN, LA, LB, EPI>), dim3(items), dim3(512), 0, st, la, lb, epi,
+                       M, N, K, klen, tm, tn, nsplit, crnn_option(CRNN_OPT_GEMM_STAGGER), nbatch);
   return (int)hipGetLastError();
 }
 
