@@ -76,6 +76,17 @@ def cpu_baseline(args, threads):
                       f"hidden {args.hidden}; {dt:.1f} s"}
 
 
+def pmc_traffic():
+    """latest committed PMC summary (tools/gpu_pmc.sh + tools/pmc_traffic.py -> profiles/*_pmc_traffic.json):
+    measured HBM bytes per launch of the hot kernels; None when absent."""
+    import glob
+    fs = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_traffic.json")))
+    if not fs:
+        return None, None
+    with open(fs[-1]) as f:
+        return json.load(f), os.path.relpath(fs[-1], REPO)
+
+
 def lstm_roofline(lstm, args, eng):
     """HBM roofline of the BiLSTM recurrence (north star: >= 40% on the step at B=256): algorithmic
     bytes per step (CRNNEngine.lstm_step_bytes) x steps / measured sweep time."""
@@ -87,8 +98,14 @@ def lstm_roofline(lstm, args, eng):
                   "sweeps_per_step": n // args.steps, "us_per_sweep": round(ms / n * 1e3, 2),
                   "us_per_timestep": round(ms / n / (args.width // 8) * 1e3, 3),
                   "algorithmic_bytes_per_timestep": byt / n / (args.width // 8)}
-    out["kernel"] = ("persistent whole-sequence BiLSTM (lstm_seq.hip)" if eng._seq_ok(args.batch)
-                     else "per-step BiLSTM launches (lstm.hip)")
+    seq = eng._seq_ok(args.batch)
+    out["kernel"] = ("persistent whole-sequence BiLSTM (lstm_seq.hip)" if seq else "per-step BiLSTM launches (lstm.hip)")
+    pmc, src = pmc_traffic()
+    if pmc and seq and args.batch == 256 and args.hidden == 512:   # the configuration the PMC pass measured
+        for k in ("lstm_fwd", "lstm_bwd"):
+            if k in out and k in pmc:
+                out[k]["traffic"] = pmc[k]["hbm_bytes_per_launch"]
+                out[k]["traffic_note"] = f"HBM bytes per sweep launch, {src}"
     return out
 
 
@@ -174,6 +191,13 @@ def main():
         conv_ms = sum(v[1] for v in timing.values())
         conv_flop = sum(v[2] for v in timing.values())
         achieved = conv_flop / (conv_ms * 1e-3) / 1e12 if conv_ms > 0 else 0.0
+        pmc, src = pmc_traffic()
+        conv_traffic = conv_traffic_note = conv_mfma_busy = None
+        if pmc and "conv" in pmc and args.batch == 256 and args.width == 256 and dtype == torch.bfloat16:
+            conv_traffic = pmc["conv"]["hbm_bytes_per_launch"]
+            conv_mfma_busy = pmc["conv"].get("mfma_busy_frac")
+            conv_traffic_note = (f"measured HBM bytes per conv launch (mean over fwd/dgrad/wgrad launches, "
+                                 f"2*FETCH_SIZE + WRITE_SIZE), {src}; algorithmic per-launch FLOPs above")
         per_kind = {k: {"launches_per_step": v[0] // args.steps, "ms_per_step": round(v[1] / args.steps, 3),
                         "tflops": round(v[2] / (v[1] * 1e-3) / 1e12, 1) if v[1] > 0 else None}
                     for k, v in timing.items()}
@@ -198,7 +222,8 @@ def main():
                        "parallelism": f"dp{world}" if world > 1 else "single"},
             "roofline": {"bound": "mfma", "kernel": "implicit-GEMM conv (fwd+dgrad+wgrad, all 28 convs)",
                          "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                         "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": conv_traffic,
+                         "traffic_note": conv_traffic_note, "mfma_busy_frac_pmc": conv_mfma_busy,
                          "algorithmic_flop_per_step": conv_flop / args.steps,
                          "launches_per_step": conv_launches // args.steps,
                          "kernel_ms_per_step": round(conv_ms / args.steps, 3),
