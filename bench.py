@@ -41,7 +41,15 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=32, help="batch of the CPU baseline sample")
     ap.add_argument("--cpu-steps", type=int, default=6)
-    return ap.parse_args()
+    ap.add_argument("--mode", default="train", choices=["train", "infer"],
+                    help="train: BASELINE configs[2]/[3] (the headline); infer: configs[1] (eval forward + greedy "
+                         "CTC decode on device)")
+    ap.add_argument("--config", default=None, choices=["long"],
+                    help="long: BASELINE configs[4] shapes (32x1024 crops, 4x768 BiLSTM, batch 64/GPU)")
+    a = ap.parse_args()
+    if a.config == "long":
+        a.width, a.hidden, a.layers, a.batch = 1024, 768, 4, 64
+    return a
 
 
 def cpu_baseline(args, threads):
@@ -59,6 +67,10 @@ def cpu_baseline(args, threads):
     x, _, tg, tl = synthetic_batch(args.cpu_sample, args.height, args.width, T, C, seed=99)
 
     def step():
+        if args.mode == "infer":
+            with torch.no_grad():
+                O.head(O.encode(x, p, O.Ctx(train=False), args.layers), p).argmax(-1)
+            return
         opt.zero_grad(set_to_none=True)
         logits = O.head(O.encode(x, p, O.Ctx(train=True), args.layers), p)
         O.ctc_loss(logits, tg, tl).backward()
@@ -71,7 +83,7 @@ def cpu_baseline(args, threads):
     dt = time.perf_counter() - t0
     return {"value": round(args.cpu_sample * args.cpu_steps / dt, 3), "unit": "text-lines/s",
             "cores": threads, "kind": "port",
-            "sample": f"oracle/crnn_oracle.py fp32 torch-CPU train step (fwd + numpy CTC + bwd + AdamW), "
+            "sample": f"oracle/crnn_oracle.py fp32 torch-CPU {'eval forward + argmax' if args.mode == 'infer' else 'train step (fwd + numpy CTC + bwd + AdamW)'}, "
                       f"B={args.cpu_sample} x {args.cpu_steps} steps (+1 warm-up) at {args.height}x{args.width}, "
                       f"hidden {args.hidden}; {dt:.1f} s"}
 
@@ -101,7 +113,7 @@ def lstm_roofline(lstm, args, eng):
     seq = eng._seq_ok(args.batch)
     out["kernel"] = ("persistent whole-sequence BiLSTM (lstm_seq.hip)" if seq else "per-step BiLSTM launches (lstm.hip)")
     pmc, src = pmc_traffic()
-    if pmc and seq and args.batch == 256 and args.hidden == 512:   # the configuration the PMC pass measured
+    if pmc and seq and args.mode == "train" and args.batch == 256 and args.hidden == 512:   # the PMC pass's config
         for k in ("lstm_fwd", "lstm_bwd"):
             if k in out and k in pmc:
                 out[k]["traffic"] = pmc[k]["hbm_bytes_per_launch"]
@@ -127,7 +139,7 @@ def main():
     model = RCNN(num_classes=C, hidden_size=args.hidden, blank_id=None, num_rnn_layers=args.layers,
                  compute_dtype=dtype)
     model.load_state_dict(recipe_state_dict(O.param_shapes(args.hidden, C, args.layers), 0), strict=False)
-    model = model.to(dev).train()
+    model = model.to(dev).train(args.mode == "train")
     x, _, tg, tl = synthetic_batch(args.batch, args.height, args.width, T, C, seed=1234 + rank)
     x = x.to(dev)
     tg = tg.to(dev, torch.int32)
@@ -144,7 +156,20 @@ def main():
     # (head / BiLSTM first, stem last) so it overlaps the remaining backward kernels
     reducer = D.OverlappedAllReduce(model._flat_grad, model.flat_offsets()) if world > 1 else None
 
+    ids = torch.empty(args.batch, T, dtype=torch.int32, device=dev)
+    lens = torch.empty(args.batch, dtype=torch.int32, device=dev)
+    from crnn_hip._lib import call, stream_ptr
+
+    def infer_step():
+        eng.forward(x, train=False, save_for_backward=False)
+        lg = eng.logits_padded()
+        call("crnn_ctc_greedy", lg.data_ptr(), lg.shape[-1], args.batch, T, C, ids.data_ptr(), lens.data_ptr(),
+             stream_ptr())
+        return lens
+
     def step():
+        if args.mode == "infer":
+            return infer_step()
         eng.forward(x, train=True, save_for_backward=True)
         loss, dl = eng.ctc(eng.logits_padded(), tg, tl)
         eng.backward(dl, grads, accumulate=False, stage_done=reducer.ready if reducer else None)
@@ -183,7 +208,7 @@ def main():
         divergence = float((cmax - cmin).item())
     lines = args.batch * world * args.steps
     value = lines / elapsed
-    final_loss = float(loss.item())
+    final_loss = float(loss.float().mean().item())
 
     if rank == 0:
         lstm = {k: timing.pop(k) for k in ("lstm_fwd", "lstm_bwd") if k in timing}
@@ -193,7 +218,8 @@ def main():
         achieved = conv_flop / (conv_ms * 1e-3) / 1e12 if conv_ms > 0 else 0.0
         pmc, src = pmc_traffic()
         conv_traffic = conv_traffic_note = conv_mfma_busy = None
-        if pmc and "conv" in pmc and args.batch == 256 and args.width == 256 and dtype == torch.bfloat16:
+        if pmc and "conv" in pmc and args.mode == "train" and args.batch == 256 and args.width == 256 \
+                and dtype == torch.bfloat16:
             conv_traffic = pmc["conv"]["hbm_bytes_per_launch"]
             conv_mfma_busy = pmc["conv"].get("mfma_busy_frac")
             conv_traffic_note = (f"measured HBM bytes per conv launch (mean over fwd/dgrad/wgrad launches, "
@@ -202,7 +228,10 @@ def main():
                         "tflops": round(v[2] / (v[1] * 1e-3) / 1e12, 1) if v[1] > 0 else None}
                     for k, v in timing.items()}
         out = {
-            "metric": METRIC,
+            "metric": (METRIC if args.mode == "train" and args.config is None else
+                       "text-lines/sec (train step incl. CTC bwd), long lines: B=64/GPU, 32x1024 crops, 4x768 BiLSTM"
+                       if args.mode == "train" else
+                       "text-lines/sec (inference: eval forward + greedy CTC decode), B=256, 32x256 crops, 1 MI355X"),
             "value": round(value, 2),
             "unit": "text-lines/s",
             "n_gpus": world,
@@ -214,8 +243,12 @@ def main():
             "vs_baseline": None,
             "dtype": "bf16" if dtype == torch.bfloat16 else "fp32",
             "data": "synthetic (seeded 32xW uint8 crops with white padding, random labels; recipe-init weights)",
-            "config": {"workload": "train step: SE-ResNet31 + 2x512 BiLSTM + CTC head, fwd + CTC bwd + AdamW "
-                                   "(BASELINE configs[2]/[3])",
+            "config": {"workload": (f"train step: SE-ResNet31 + {args.layers}x{args.hidden} BiLSTM + CTC head, fwd + "
+                                    f"CTC bwd + AdamW (BASELINE " + ("configs[4])" if args.config == "long" else
+                                                                    "configs[2]/[3])")
+                                    if args.mode == "train" else
+                                    f"inference: SE-ResNet31 + {args.layers}x{args.hidden} BiLSTM + CTC head, eval "
+                                    f"forward + on-device greedy decode (BASELINE configs[1])"),
                        "global_batch": args.batch * world, "per_gpu_batch": args.batch,
                        "crop": f"{args.height}x{args.width}", "seq_len": T, "hidden": args.hidden,
                        "rnn_layers": args.layers, "num_classes": C,
