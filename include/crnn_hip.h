@@ -52,7 +52,9 @@ enum { CRNN_OPT_GEMM_STAGGER = 0,    /* 256-row conv GEMM: waves 4-7 one barrier
                                         tiles > CUs, 2 always */
        CRNN_OPT_DEEP_LINEAR = 2,     /* bf16 crnn_gemm_nt/nn on the 256-row kernel when its grid fills the chip */
        CRNN_OPT_WGRAD_TILE = 3,      /* conv wgrad plan: 0 = 256x256, 1 = 256x128 tiles, n >= 2: ~128n blocks */
-       CRNN_OPT_COUNT = 4 };
+       CRNN_OPT_LSTM_TILE = 4,       /* persistent BiLSTM workgroup tile: 0 = auto, 1 = 32 samples x 32 units,
+                                        2 = 16 x 32, 3 = 16 x 64 (when the grid fits the CUs) */
+       CRNN_OPT_COUNT = 5 };
 int crnn_set_option(int key, int value);
 
 /* ------------------------------------------------------------------ layout */
@@ -241,12 +243,17 @@ int crnn_lstm_wgrad(const void* dgates, const void* x, const void* hseq, float* 
                     void* stream);
 /* Persistent whole-sequence recurrence (bf16 only; replaces the T per-step launches of
  * crnn_lstm_step_fwd / crnn_lstm_step_bwd with ONE launch per layer and direction pair, same
- * buffers and results). Supported when crnn_lstm_seq_supported() != 0: B % 32 == 0,
- * H in {256, 512, 768} and 2*(B/32)*(H/32) workgroups <= the device's CU count (all resident).
+ * buffers and results). One workgroup per (direction, S samples, U units), S x U chosen per
+ * sweep by crnn_lstm_seq_config() among 16 x 32, 32 x 32 and 16 x 64 (H <= 512) such that the
+ * grid 2*(B/S)*(H/U) fits the device's CU count (all resident); H in {256, 512, 768}.
  * ws: crnn_lstm_seq_workspace(B) bytes of device memory, zeroed by the call itself:
- * [2*B/32] step counters then one error word (non-zero after a bounded wait timed out, in which
- * case the outputs carry NaN). */
+ * [2*(B/16+1)] step counters (the first 2*B/S used; counter of slice (d, bs) = d*(B/S)+bs reaches
+ * (H/U)*T) then one error word (non-zero after a bounded wait timed out, in which case the outputs
+ * carry NaN). */
 int crnn_lstm_seq_supported(int dtype, int B, int H);
+/* the (samples, units) workgroup tile the forward (bwd = 0) or BPTT (bwd = 1) sweep uses for
+ * (B, H); 0 if unsupported */
+int crnn_lstm_seq_config(int B, int H, int bwd, int* S, int* U);
 /* diagnostics: record per-phase s_memrealtime stamps of the following persistent launches into a
  * device buffer of (grid * T * 8) u64 (NULL: off) */
 int crnn_lstm_seq_debug_stamps(unsigned long long* buf);

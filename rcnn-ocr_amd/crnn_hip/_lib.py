@@ -43,7 +43,8 @@ class PackJob(C.Structure):  # crnn_pack_job
                 ("src2", vp), ("perm", vp), ("dst", vp)]
 
 
-OPT_GEMM_STAGGER, OPT_GEMM_PERSISTENT = 0, 1   # crnn_set_option keys (include/crnn_hip.h)
+# crnn_set_option keys (include/crnn_hip.h)
+OPT_GEMM_STAGGER, OPT_GEMM_PERSISTENT, OPT_DEEP_LINEAR, OPT_WGRAD_TILE, OPT_LSTM_TILE = 0, 1, 2, 3, 4
 
 PACK_CONV, PACK_ROWS, PACK_ROWS_SUM, PACK_TRANSPOSE = 0, 1, 2, 3
 
@@ -94,6 +95,7 @@ _SIGS = {
     "crnn_lstm_dbias_workspace": ([i32], sz),
     "crnn_lstm_seq_supported": ([i32, i32, i32], i32),
     "crnn_lstm_seq_workspace": ([i32], sz),
+    "crnn_lstm_seq_config": ([i32, i32, i32, vp, vp], i32),
     "crnn_lstm_seq_debug_stamps": ([vp], i32),
     "crnn_lstm_seq_fwd": ([vp, vp, vp, vp, vp, vp, i32, i32, i32, vp], i32),
     "crnn_lstm_seq_bwd": ([vp, vp, vp, vp, vp, vp, i32, i32, i32, vp], i32),

@@ -5,6 +5,8 @@
 
 // records a message for crnn_last_error_string() and returns `code`
 int crnn_set_error(int code, const char* msg);
+// crnn_set_option() values (capi.cpp)
+int crnn_option(int key);
 
 inline int grid_for(long n, int block = 256, int cap = 8192) {
   long g = (n + block - 1) / block;

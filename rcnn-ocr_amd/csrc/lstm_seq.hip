@@ -5,8 +5,8 @@
 // one launch per step (and remain the fp32 / unsupported-shape path).
 //
 // Decomposition (B = batch, H = hidden, T = steps): one workgroup per
-//   (direction d, batch slice bs of SEQ_S = 32 samples, unit slice ns of SEQ_U = 32 units),
-// 2 * (B/32) * (H/32) workgroups, 4 waves each, at most one per CU (all must be co-resident:
+//   (direction d, batch slice bs of S samples, unit slice ns of U units), S x U = 16 x 64,
+// 16 x 32 or 32 x 32 (seq_config), 2 * (B/S) * (H/U) workgroups, 4 waves each, at most one per CU (all must be co-resident:
 // the host checks the grid against the CU count). The step GEMM's K is split over the 4 waves
 // (each wave holds its K-quarter of the W_hh slice as MFMA fragments in VGPRs, loaded once), the
 // four partial tiles are summed through LDS, and the cell math runs on the summed tile.
@@ -24,7 +24,7 @@
 // counter with sc1 loads until it reaches (unit slices) x (steps done), the workgroup barriers,
 // and every load of the handed-off bytes is an sc1 buffer load to registers. Counters are zeroed
 // by a memset in the launch function. Every spin is bounded: on time-out the kernel records an
-// error word (ws[2*B/32], see include/crnn_hip.h) and the step's outputs carry NaN.
+// error word (ws[2*(B/16+1)], see include/crnn_hip.h) and the step's outputs carry NaN.
 #include "gemm.hpp"
 #include "crnn_internal.hpp"
 
@@ -32,8 +32,6 @@ using namespace gemm;
 
 namespace {
 
-constexpr int SEQ_S = 32;  // samples per workgroup
-constexpr int SEQ_U = 32;  // hidden units per workgroup
 constexpr unsigned long long SEQ_TIMEOUT_TICKS = 50000000ull;  // s_memrealtime @100 MHz: 0.5 s per wait
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* p) {
@@ -82,32 +80,35 @@ __device__ __forceinline__ void seq_coords(int nsl, int nbs, int& d, int& bs, in
 }
 
 // ---------------------------------------------------------------- forward sweep
-// wave w: K-quarter [w*H/4, (w+1)*H/4); partial tile 32 samples x 128 gate rows (2 x 8 fragments).
-// It finalises fragment blocks q = 0..3: (i, j) = (q & 1, 2w + (q >> 1)).
-template <int H>
+// Workgroup = (direction, S samples, U units = 4U gate rows); wave w holds the K-quarter
+// [w*H/4, (w+1)*H/4) of the W_hh' slice (NJ = 4U/16 row fragments x KK k-steps) in VGPRs and
+// computes an S x 4U partial tile; the partials are summed through LDS and wave w finalises the
+// fragment blocks bi = w*QB .. w*QB+QB-1 (QB = MI*NJ/4), bi -> (i = bi / NJ, j = bi % NJ).
+template <int H, int S, int U>
 __global__ __launch_bounds__(256) void lstm_seq_fwd_kernel(const bf16* __restrict__ xg, const bf16* __restrict__ whh,
                                                            bf16* hseq, bf16* __restrict__ gsv, float* __restrict__ csv,
                                                            unsigned* cnt, unsigned* err, int B, int Tn,
                                                            unsigned long long* stamps) {
   constexpr int KW = H / 4, KK = KW / 32;
-  constexpr int GR = 4 * SEQ_U, NJ = GR / 16;  // 128 gate rows, 8 fragments
+  constexpr int GR = 4 * U, NJ = GR / 16, MI = S / 16;
+  constexpr int QB = MI * NJ / 4;   // blocks finalised per wave
   constexpr int H4 = 4 * H;
-  static_assert(H % 128 == 0, "H");
-  // LDS: partials [wave][i][j][lane] f32x4 (64 KB) + h tile [32][32] bf16 (2 KB)
-  __shared__ __attribute__((aligned(16))) f32x4 part[4][2][NJ][64];
-  __shared__ __attribute__((aligned(16))) bf16 htile[SEQ_S][SEQ_U];
+  static_assert(H % 128 == 0 && S % 16 == 0 && U % 16 == 0 && (MI * NJ) % 4 == 0, "shape");
+  static_assert(S * U / 8 <= 256, "publish: one 16-B store per thread");
+  __shared__ __attribute__((aligned(16))) f32x4 part[4][MI][NJ][64];
+  __shared__ __attribute__((aligned(16))) bf16 htile[S][U];
 
-  const int nsl = H / SEQ_U, nbs = B / SEQ_S;
+  const int nsl = H / U, nbs = B / S;
   int d, bs, ns;
   seq_coords(nsl, nbs, d, bs, ns);
   const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int b0 = bs * SEQ_S, n0 = ns * GR;
+  const int b0 = bs * S, n0 = ns * GR;
   unsigned* mycnt = cnt + d * nbs + bs;
 
-  // W_hh' slice fragments: rows n0 + 16j + c, k = w*KW + 32kk + 8g
-  // register slot kk holds K-chunk (kk + rot) % KK: the 16 workgroups of a (d, bs) group read the
-  // handed-off h in rotated chunk order, spreading their simultaneous requests over memory channels
+  // W_hh' slice fragments: rows n0 + 16j + c, k = w*KW + 32kc + 8g; register slot kk holds K-chunk
+  // kc = (kk + rot) % KK: the workgroups of a (d, bs) group read the handed-off h in rotated chunk
+  // order, spreading their simultaneous requests over memory channels
   const int rot = ns % KK;
   bf16x8 wf[NJ][KK];
   {
@@ -121,14 +122,16 @@ __global__ __launch_bounds__(256) void lstm_seq_fwd_kernel(const bf16* __restric
       }
   }
   const __amdgpu_buffer_rsrc_t rh = rsrc_of(hseq);
-  float cst[4] = {0.f, 0.f, 0.f, 0.f};
-  f32x4 xv[4];
+  float cst[QB];
+#pragma unroll
+  for (int q = 0; q < QB; ++q) cst[q] = 0.f;
+  bf16x4 xv[QB];  // raw prefetch: converted at the step's use, not at the load
   auto load_xg = [&](int t) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int i = q & 1, j = 2 * w + (q >> 1);
+    for (int q = 0; q < QB; ++q) {
+      const int bi = w * QB + q, i = bi / NJ, j = bi % NJ;
       const int b = b0 + 16 * i + c, n = n0 + 16 * j + 4 * g;
-      xv[q] = ld4f<bf16>(xg + ((size_t)b * Tn + t) * 2 * H4 + d * H4 + n);
+      xv[q] = *reinterpret_cast<const bf16x4*>(xg + ((size_t)b * Tn + t) * 2 * H4 + d * H4 + n);
     }
   };
   load_xg(d == 0 ? 0 : Tn - 1);
@@ -136,9 +139,10 @@ __global__ __launch_bounds__(256) void lstm_seq_fwd_kernel(const bf16* __restric
   for (int s = 0; s < Tn; ++s) {
     const int t = d == 0 ? s : Tn - 1 - s;
     const int tp = d == 0 ? t - 1 : t + 1;
-    f32x4 sum[4];
+    f32x4 sum[QB];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) sum[q] = xv[q];
+    for (int q = 0; q < QB; ++q)
+      sum[q] = f32x4{(float)xv[q][0], (float)xv[q][1], (float)xv[q][2], (float)xv[q][3]};
     bool ok = true;
     SEQ_STAMP(0);
     if (s > 0) {
@@ -147,101 +151,114 @@ __global__ __launch_bounds__(256) void lstm_seq_fwd_kernel(const bf16* __restric
       __syncthreads();
       SEQ_STAMP(1);
       ok = okflag != 0;
-      // A fragments: h_{tp}[b0 + 16i + c][w*KW + 32kk + 8g] (sc1: handed-off bytes)
-      bf16x8 af[2][KK];
+      // A fragments: h_{tp}[b0 + 16i + c][w*KW + 32kc + 8g] (sc1: handed-off bytes)
+      bf16x8 af[MI][KK];
       const uint32_t abase = (uint32_t)((((size_t)b0 + c) * Tn + tp) * 2 * H + d * H + w * KW + 8 * g) * 2u;
 #pragma unroll
       for (int kk = 0; kk < KK; ++kk)
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
+        for (int i = 0; i < MI; ++i) {
           const int kc = kk + rot < KK ? kk + rot : kk + rot - KK;
           af[i][kk] = ld_sc1(rh, abase + (uint32_t)(i * 16 * Tn * 2 * H * 2 + kc * 64));
         }
-      f32x4 acc[2][NJ];
+      // every hand-off load in flight before the first MFMA (else the scheduler interleaves them
+      // with the MFMAs one load at a time, each behind a vmcnt(0))
+      __builtin_amdgcn_sched_barrier(0);
+      f32x4 acc[MI][NJ];
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int kk = 0; kk < KK; ++kk)
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < MI; ++i)
 #pragma unroll
           for (int j = 0; j < NJ; ++j) mma<bf16>(acc[i][j], wf[j][kk], af[i][kk]);
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < NJ; ++j) part[w][i][j][lane] = acc[i][j];
       SEQ_STAMP(2);
       __syncthreads();
       SEQ_STAMP(3);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int i = q & 1, j = 2 * w + (q >> 1);
+      for (int q = 0; q < QB; ++q) {
+        const int bi = w * QB + q, i = bi / NJ, j = bi % NJ;
 #pragma unroll
         for (int ww = 0; ww < 4; ++ww) sum[q] += part[ww][i][j][lane];
       }
     }
-    // cell update for the 4 blocks: lane holds gates (i,f,g,o) of unit n/4 for one sample
+    // cell update: lane holds gates (i,f,g,o) of unit n/4 for one sample, per block
+    f32x4 gq[QB];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int i = q & 1, j = 2 * w + (q >> 1);
-      const int bl = 16 * i + c, b = b0 + bl;
-      const int n = n0 + 16 * j + 4 * g, u = n >> 2;
+    for (int q = 0; q < QB; ++q) {
+      const int bi = w * QB + q, i = bi / NJ, j = bi % NJ;
       f32x4 v = sum[q];
       const float ig = sigmoid_fast(v[0]), fg = sigmoid_fast(v[1]), gg = tanh_fast(v[2]), og = sigmoid_fast(v[3]);
       float cc = fg * cst[q] + ig * gg;
       float hh = og * tanh_fast(cc);
       if (!ok) hh = cc = __builtin_nanf("");
       cst[q] = cc;
-      csv[((size_t)(d * Tn + t) * B + b) * H + u] = cc;
-      st4<bf16>(gsv + ((size_t)(d * Tn + t) * B + b) * H4 + n, f32x4{ig, fg, gg, og});
-      htile[bl][4 * j + g] = (bf16)hh;
+      gq[q] = f32x4{ig, fg, gg, og};
+      htile[16 * i + c][4 * j + g] = (bf16)hh;
     }
     SEQ_STAMP(4);
     __syncthreads();
-    // publish h_t of this (samples, units) tile: 32 rows x 64 B, 16 B per lane (waves 0-1)
-    if (threadIdx.x < 128) {
-      const int row = threadIdx.x >> 2, ch = threadIdx.x & 3;
+    // publish h_t of this (samples, units) tile: S rows x 2U bytes, one 16-B sc1 store per thread
+    if (threadIdx.x < S * U / 8) {
+      const int row = threadIdx.x / (U / 8), ch = threadIdx.x % (U / 8);
       const bf16x8 hv = *reinterpret_cast<const bf16x8*>(&htile[row][8 * ch]);
-      st_sc1(rh, (uint32_t)((((size_t)(b0 + row) * Tn + t) * 2 * H + d * H + ns * SEQ_U + 8 * ch) * sizeof(bf16)), hv);
+      st_sc1(rh, (uint32_t)((((size_t)(b0 + row) * Tn + t) * 2 * H + d * H + ns * U + 8 * ch) * sizeof(bf16)), hv);
     }
     SEQ_STAMP(5);
     seq_publish(mycnt);
     SEQ_STAMP(6);
-    if (s + 1 < Tn) load_xg(d == 0 ? t + 1 : t - 1);
+    // saved-forward stores for BPTT, off the hand-off's critical path (issued after the signal;
+    // the next step's vmcnt(0) drains them long after they completed)
+#pragma unroll
+    for (int q = 0; q < QB; ++q) {
+      const int bi = w * QB + q, i = bi / NJ, j = bi % NJ;
+      const int b = b0 + 16 * i + c;
+      const int n = n0 + 16 * j + 4 * g, u = n >> 2;
+      csv[((size_t)(d * Tn + t) * B + b) * H + u] = cst[q];
+      st4<bf16>(gsv + ((size_t)(d * Tn + t) * B + b) * H4 + n, gq[q]);
+    }
+    // next step's input rows, unconditionally (a load under a runtime branch gets a vmcnt(0) at
+    // the join, which would stall on the stores above): the last step re-reads its own row
+    load_xg(s + 1 < Tn ? (d == 0 ? t + 1 : t - 1) : t);
   }
 }
 
 // ---------------------------------------------------------------- BPTT sweep
-// wave w: K-quarter [w*H, (w+1)*H) of the 4H gate columns; partial tile 32 samples x 32 units
-// (2 x 2 fragments); it finalises block (i, j) = (w & 1, w >> 1): 16 samples x 16 units, one
-// sample and 4 consecutive units per lane.
-template <int H>
+// wave w: K-quarter [w*H, (w+1)*H) of the 4H gate columns; partial tile S samples x U units
+// (MI x NU fragments); waves w < MI*NU finalise block (i, j) = (w % MI, w / MI): 16 samples x 16
+// units, one sample and 4 consecutive units per lane.
+template <int H, int S, int U>
 __global__ __launch_bounds__(256) void lstm_seq_bwd_kernel(const bf16* __restrict__ dhseq, const bf16* __restrict__ whh_t,
                                                            const bf16* __restrict__ gsv, const float* __restrict__ csv,
                                                            bf16* dgates, unsigned* cnt, unsigned* err, int B, int Tn,
                                                            unsigned long long* stamps) {
   constexpr int KW = H, KK = KW / 32;
-  constexpr int H4 = 4 * H;
-  static_assert(H % 32 == 0, "H");
-  __shared__ __attribute__((aligned(16))) f32x4 part[4][2][2][64];
+  constexpr int H4 = 4 * H, MI = S / 16, NU = U / 16, NBLK = MI * NU;
+  static_assert(H % 32 == 0 && NBLK <= 4 && S % 16 == 0 && U % 16 == 0, "shape");
+  __shared__ __attribute__((aligned(16))) f32x4 part[4][MI][NU][64];
 
-  const int nsl = H / SEQ_U, nbs = B / SEQ_S;
+  const int nsl = H / U, nbs = B / S;
   int d, bs, ns;
   seq_coords(nsl, nbs, d, bs, ns);
   const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int b0 = bs * SEQ_S, u0 = ns * SEQ_U;
+  const int b0 = bs * S, u0 = ns * U;
   unsigned* mycnt = cnt + d * nbs + bs;
 
-  // W_hh'^T slice fragments: rows u0 + 16j + c of whh_t[d] ([H][4H]), k = w*KW + 32kk + 8g
+  // W_hh'^T slice fragments: rows u0 + 16j + c of whh_t[d] ([H][4H]), k = w*KW + 32kc + 8g
   const int rot = (ns * KK / nsl) % KK;   // rotated K-chunk order, as in the forward kernel
-  bf16x8 wf[2][KK];
+  bf16x8 wf[NU][KK];
   {
     const bf16* wb = whh_t + (size_t)d * H * H4;
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < NU; ++j)
 #pragma unroll
       for (int kk = 0; kk < KK; ++kk) {
         const int kc = kk + rot < KK ? kk + rot : kk + rot - KK;
@@ -249,14 +266,17 @@ __global__ __launch_bounds__(256) void lstm_seq_bwd_kernel(const bf16* __restric
       }
   }
   const __amdgpu_buffer_rsrc_t rg = rsrc_of(dgates);
-  const int fi = w & 1, fj = w >> 1;
+  const bool fin = w < NBLK;
+  const int fi = fin ? w % MI : 0, fj = fin ? w / MI : 0;
   const int bl = 16 * fi + c, b = b0 + bl;
   const int u = u0 + 16 * fj + 4 * g;  // this lane's 4 units u..u+3
   float dcs[4] = {0.f, 0.f, 0.f, 0.f};
 
-  // per-step saved-forward inputs of this lane (independent of the recurrence: prefetched)
+  // per-step saved-forward inputs of this lane (independent of the recurrence: prefetched;
+  // loads are unconditional — the t-1 of the first step reads a clamped row and is masked)
   bf16x8 gv0, gv1;
   f32x4 cv, cpv, dhv;
+  float has_prev_f = 0.f;
   auto load_in = [&](int t) {
     const size_t gi = ((size_t)(d * Tn + t) * B + b) * H4 + 4 * u;
     gv0 = *reinterpret_cast<const bf16x8*>(gsv + gi);
@@ -264,8 +284,9 @@ __global__ __launch_bounds__(256) void lstm_seq_bwd_kernel(const bf16* __restric
     cv = *reinterpret_cast<const f32x4*>(csv + ((size_t)(d * Tn + t) * B + b) * H + u);
     const int tf = d == 0 ? t - 1 : t + 1;
     const bool has_prev = d == 0 ? t > 0 : t < Tn - 1;
-    cpv = has_prev ? *reinterpret_cast<const f32x4*>(csv + ((size_t)(d * Tn + tf) * B + b) * H + u)
-                   : f32x4{0.f, 0.f, 0.f, 0.f};
+    const int tfc = has_prev ? tf : t;
+    cpv = *reinterpret_cast<const f32x4*>(csv + ((size_t)(d * Tn + tfc) * B + b) * H + u);
+    has_prev_f = has_prev ? 1.f : 0.f;
     dhv = ld4f<bf16>(dhseq + ((size_t)b * Tn + t) * 2 * H + d * H + u);
   };
   load_in(d == 0 ? Tn - 1 : 0);
@@ -282,85 +303,152 @@ __global__ __launch_bounds__(256) void lstm_seq_bwd_kernel(const bf16* __restric
       __syncthreads();
       SEQ_STAMP(1);
       ok = okflag != 0;
-      bf16x8 af[2][KK];
+      bf16x8 af[MI][KK];
       const uint32_t abase = (uint32_t)((((size_t)(d * Tn + tn) * B + b0 + c) * H4 + w * KW + 8 * g) * 2u);
 #pragma unroll
       for (int kk = 0; kk < KK; ++kk)
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
+        for (int i = 0; i < MI; ++i) {
           const int kc = kk + rot < KK ? kk + rot : kk + rot - KK;
           af[i][kk] = ld_sc1(rg, abase + (uint32_t)(i * 16 * H4 * 2 + kc * 64));
         }
-      f32x4 acc[2][2];
+      __builtin_amdgcn_sched_barrier(0);  // all loads issued first (forward sweep)
+      f32x4 acc[MI][NU];
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < MI; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < NU; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int kk = 0; kk < KK; ++kk)
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < MI; ++i)
 #pragma unroll
-          for (int j = 0; j < 2; ++j) mma<bf16>(acc[i][j], wf[j][kk], af[i][kk]);
+          for (int j = 0; j < NU; ++j) mma<bf16>(acc[i][j], wf[j][kk], af[i][kk]);
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < MI; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) part[w][i][j][lane] = acc[i][j];
+        for (int j = 0; j < NU; ++j) part[w][i][j][lane] = acc[i][j];
       SEQ_STAMP(2);
       __syncthreads();
       SEQ_STAMP(3);
+      if (fin)
 #pragma unroll
-      for (int ww = 0; ww < 4; ++ww) dh += part[ww][fi][fj][lane];
+        for (int ww = 0; ww < 4; ++ww) dh += part[ww][fi][fj][lane];
     }
-    // cell backward of units u..u+3 (lstm.hip cell_bwd)
-    bf16x8 out0, out1;
+    if (fin) {
+      // cell backward of units u..u+3 (lstm.hip cell_bwd)
+      bf16x8 out0, out1;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const bf16x8& gv = r < 2 ? gv0 : gv1;
-      const int o = (r & 1) * 4;
-      const float ig = (float)gv[o], fg = (float)gv[o + 1], gg = (float)gv[o + 2], og = (float)gv[o + 3];
-      const float tc = tanh_fast(cv[r]);
-      const float dcv = dcs[r] + dh[r] * og * (1.f - tc * tc);
-      const float do_ = dh[r] * tc;
-      const float di = dcv * gg, dg = dcv * ig, df = dcv * cpv[r];
-      dcs[r] = dcv * fg;
-      float q0 = di * ig * (1.f - ig), q1 = df * fg * (1.f - fg), q2 = dg * (1.f - gg * gg), q3 = do_ * og * (1.f - og);
-      if (!ok) q0 = q1 = q2 = q3 = __builtin_nanf("");
-      bf16x8& ov = r < 2 ? out0 : out1;
-      ov[o] = (bf16)q0;
-      ov[o + 1] = (bf16)q1;
-      ov[o + 2] = (bf16)q2;
-      ov[o + 3] = (bf16)q3;
+      for (int r = 0; r < 4; ++r) {
+        const bf16x8& gv = r < 2 ? gv0 : gv1;
+        const int o = (r & 1) * 4;
+        const float ig = (float)gv[o], fg = (float)gv[o + 1], gg = (float)gv[o + 2], og = (float)gv[o + 3];
+        const float tc = tanh_fast(cv[r]);
+        const float dcv = dcs[r] + dh[r] * og * (1.f - tc * tc);
+        const float do_ = dh[r] * tc;
+        const float di = dcv * gg, dg = dcv * ig, df = dcv * cpv[r] * has_prev_f;
+        dcs[r] = dcv * fg;
+        float q0 = di * ig * (1.f - ig), q1 = df * fg * (1.f - fg), q2 = dg * (1.f - gg * gg), q3 = do_ * og * (1.f - og);
+        if (!ok) q0 = q1 = q2 = q3 = __builtin_nanf("");
+        bf16x8& ov = r < 2 ? out0 : out1;
+        ov[o] = (bf16)q0;
+        ov[o + 1] = (bf16)q1;
+        ov[o + 2] = (bf16)q2;
+        ov[o + 3] = (bf16)q3;
+      }
+      SEQ_STAMP(4);
+      const uint32_t go = (uint32_t)((((size_t)(d * Tn + t) * B + b) * H4 + 4 * u) * sizeof(bf16));
+      st_sc1(rg, go, out0);
+      st_sc1(rg, go + 16, out1);
     }
-    const uint32_t go = (uint32_t)((((size_t)(d * Tn + t) * B + b) * H4 + 4 * u) * sizeof(bf16));
-    SEQ_STAMP(4);
-    st_sc1(rg, go, out0);
-    st_sc1(rg, go + 16, out1);
     SEQ_STAMP(5);
     seq_publish(mycnt);
     SEQ_STAMP(6);
-    if (s + 1 < Tn) load_in(d == 0 ? t - 1 : t + 1);
+    // unconditional prefetch (see the forward sweep); non-finalising waves read valid rows unused
+    load_in(s + 1 < Tn ? (d == 0 ? t - 1 : t + 1) : t);
   }
 }
 
 int g_cus = -1;
 unsigned long long* g_stamps = nullptr;  // crnn_lstm_seq_debug_stamps
 
-int seq_grid(int B, int H) { return 2 * (B / SEQ_S) * (H / SEQ_U); }
+int cu_count() {
+  if (g_cus < 0) {
+    int dev = 0;
+    hipDeviceProp_t p;
+    g_cus = (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&p, dev) == hipSuccess) ? p.multiProcessorCount : 0;
+  }
+  return g_cus;
+}
+
+// (samples, units) per workgroup: 16 samples halve the per-step hand-off each workgroup gathers;
+// 64 units (H <= 512: the W_hh slice still fits the VGPRs) keep the grid at <= one per CU
+bool seq_config(int B, int H, bool bwd, int& S, int& U) {
+  if (!(H == 256 || H == 512 || H == 768)) return false;
+  const int ncu = cu_count();
+  // preference order measured on MI355X (profiles/r01k_lstm_tiles.log): 16 samples halve the
+  // hand-off bytes each workgroup gathers per step; 16 x 64 over 16 x 32 where both fit
+  static const int order[2][3][2] = {{{16, 64}, {16, 32}, {32, 32}}, {{16, 64}, {16, 32}, {32, 32}}};
+  const int force = crnn_option(CRNN_OPT_LSTM_TILE);  // 1: 32x32, 2: 16x32, 3: 16x64 only
+  for (int k = 0; k < 3; ++k) {
+    const int s = order[bwd][k][0], u = order[bwd][k][1];
+    if (force >= 1 && force <= 3 && (s == 32 ? 1 : u == 32 ? 2 : 3) != force) continue;
+    if (u == 64 && H > 512) continue;  // the 4U x H/4 W_hh slice must stay in VGPRs
+    if (B % s || 2 * (B / s) * (H / u) > ncu) continue;
+    S = s;
+    U = u;
+    return true;
+  }
+  return false;
+}
+
+template <int H>
+int launch_fwd(int S, int U, dim3 grid, hipStream_t st, const bf16* xg, const bf16* whh, bf16* hseq, bf16* gsv,
+               float* csv, unsigned* cnt, unsigned* err, int B, int T) {
+  if constexpr (H <= 512) {  // 16 x 64 would spill at H = 768 (seq_config never picks it)
+    if (S == 16 && U == 64) {
+      hipLaunchKernelGGL((lstm_seq_fwd_kernel<H, 16, 64>), grid, dim3(256), 0, st, xg, whh, hseq, gsv, csv, cnt, err, B, T, g_stamps);
+      return (int)hipGetLastError();
+    }
+  }
+  if (S == 16)
+    hipLaunchKernelGGL((lstm_seq_fwd_kernel<H, 16, 32>), grid, dim3(256), 0, st, xg, whh, hseq, gsv, csv, cnt, err, B, T, g_stamps);
+  else
+    hipLaunchKernelGGL((lstm_seq_fwd_kernel<H, 32, 32>), grid, dim3(256), 0, st, xg, whh, hseq, gsv, csv, cnt, err, B, T, g_stamps);
+  return (int)hipGetLastError();
+}
+
+template <int H>
+int launch_bwd(int S, int U, dim3 grid, hipStream_t st, const bf16* dhseq, const bf16* whh_t, const bf16* gsv,
+               const float* csv, bf16* dg, unsigned* cnt, unsigned* err, int B, int T) {
+  if constexpr (H <= 512) {
+    if (S == 16 && U == 64) {
+      hipLaunchKernelGGL((lstm_seq_bwd_kernel<H, 16, 64>), grid, dim3(256), 0, st, dhseq, whh_t, gsv, csv, dg, cnt, err, B, T, g_stamps);
+      return (int)hipGetLastError();
+    }
+  }
+  if (S == 16)
+    hipLaunchKernelGGL((lstm_seq_bwd_kernel<H, 16, 32>), grid, dim3(256), 0, st, dhseq, whh_t, gsv, csv, dg, cnt, err, B, T, g_stamps);
+  else
+    hipLaunchKernelGGL((lstm_seq_bwd_kernel<H, 32, 32>), grid, dim3(256), 0, st, dhseq, whh_t, gsv, csv, dg, cnt, err, B, T, g_stamps);
+  return (int)hipGetLastError();
+}
 
 }  // namespace
 
 extern "C" {
 
 int crnn_lstm_seq_supported(int dtype, int B, int H) {
-  if (dtype != CRNN_BF16 || B % SEQ_S || !(H == 256 || H == 512 || H == 768)) return 0;
-  if (g_cus < 0) {
-    int dev = 0;
-    hipDeviceProp_t p;
-    if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&p, dev) != hipSuccess) return 0;
-    g_cus = p.multiProcessorCount;
-  }
-  return seq_grid(B, H) <= g_cus ? 1 : 0;
+  int S, U;
+  return dtype == CRNN_BF16 && seq_config(B, H, false, S, U) && seq_config(B, H, true, S, U) ? 1 : 0;
+}
+
+int crnn_lstm_seq_config(int B, int H, int bwd, int* S, int* U) {
+  int s = 0, u = 0;
+  const int ok = seq_config(B, H, bwd != 0, s, u) ? 1 : 0;
+  if (S) *S = ok ? s : 0;
+  if (U) *U = ok ? u : 0;
+  return ok;
 }
 
 // diagnostics: per-phase timestamps of the NEXT persistent launches into `buf` (device,
@@ -370,46 +458,39 @@ int crnn_lstm_seq_debug_stamps(unsigned long long* buf) {
   return 0;
 }
 
-size_t crnn_lstm_seq_workspace(int B) { return (size_t)((2 * (B / SEQ_S) + 1 + 3) / 4 * 16); }
+// counters: one per (direction, batch slice) of the smallest slice (16 samples), then the error word
+size_t crnn_lstm_seq_workspace(int B) { return (size_t)((2 * (B / 16 + 1) + 1 + 3) / 4 * 16); }
 
 int crnn_lstm_seq_fwd(const void* xg, const void* whh, void* hseq, void* gsv, float* csv, unsigned* ws, int B, int T,
                       int H, void* stream) {
   hipStream_t st = (hipStream_t)stream;
-  if (!crnn_lstm_seq_supported(CRNN_BF16, B, H)) return crnn_set_error(hipErrorInvalidValue, "lstm_seq: unsupported shape");
-  const int nbs = B / SEQ_S;
+  int S, U;
+  if (!seq_config(B, H, false, S, U)) return crnn_set_error(hipErrorInvalidValue, "lstm_seq: unsupported shape");
   hipError_t e = hipMemsetAsync(ws, 0, crnn_lstm_seq_workspace(B), st);
   if (e != hipSuccess) return (int)e;
   unsigned* cnt = ws;
-  unsigned* err = ws + 2 * nbs;
-  const dim3 grid(seq_grid(B, H)), block(256);
-#define SEQ_FWD(HH)                                                                                                 \
-  hipLaunchKernelGGL(lstm_seq_fwd_kernel<HH>, grid, block, 0, st, (const bf16*)xg, (const bf16*)whh, (bf16*)hseq,   \
-                     (bf16*)gsv, csv, cnt, err, B, T, g_stamps)
-  if (H == 256) SEQ_FWD(256);
-  else if (H == 512) SEQ_FWD(512);
-  else SEQ_FWD(768);
-#undef SEQ_FWD
-  return (int)hipGetLastError();
+  unsigned* err = ws + 2 * (B / 16 + 1);
+  const dim3 grid(2 * (B / S) * (H / U));
+  const bf16 *x = (const bf16*)xg, *w = (const bf16*)whh;
+  if (H == 256) return launch_fwd<256>(S, U, grid, st, x, w, (bf16*)hseq, (bf16*)gsv, csv, cnt, err, B, T);
+  if (H == 512) return launch_fwd<512>(S, U, grid, st, x, w, (bf16*)hseq, (bf16*)gsv, csv, cnt, err, B, T);
+  return launch_fwd<768>(S, U, grid, st, x, w, (bf16*)hseq, (bf16*)gsv, csv, cnt, err, B, T);
 }
 
 int crnn_lstm_seq_bwd(const void* dhseq, const void* whh_t, const void* gsv, const float* csv, void* dgates,
                       unsigned* ws, int B, int T, int H, void* stream) {
   hipStream_t st = (hipStream_t)stream;
-  if (!crnn_lstm_seq_supported(CRNN_BF16, B, H)) return crnn_set_error(hipErrorInvalidValue, "lstm_seq: unsupported shape");
-  const int nbs = B / SEQ_S;
+  int S, U;
+  if (!seq_config(B, H, true, S, U)) return crnn_set_error(hipErrorInvalidValue, "lstm_seq: unsupported shape");
   hipError_t e = hipMemsetAsync(ws, 0, crnn_lstm_seq_workspace(B), st);
   if (e != hipSuccess) return (int)e;
   unsigned* cnt = ws;
-  unsigned* err = ws + 2 * nbs;
-  const dim3 grid(seq_grid(B, H)), block(256);
-#define SEQ_BWD(HH)                                                                                                   \
-  hipLaunchKernelGGL(lstm_seq_bwd_kernel<HH>, grid, block, 0, st, (const bf16*)dhseq, (const bf16*)whh_t,           \
-                     (const bf16*)gsv, csv, (bf16*)dgates, cnt, err, B, T, g_stamps)
-  if (H == 256) SEQ_BWD(256);
-  else if (H == 512) SEQ_BWD(512);
-  else SEQ_BWD(768);
-#undef SEQ_BWD
-  return (int)hipGetLastError();
+  unsigned* err = ws + 2 * (B / 16 + 1);
+  const dim3 grid(2 * (B / S) * (H / U));
+  const bf16 *dh = (const bf16*)dhseq, *wt = (const bf16*)whh_t, *gv = (const bf16*)gsv;
+  if (H == 256) return launch_bwd<256>(S, U, grid, st, dh, wt, gv, csv, (bf16*)dgates, cnt, err, B, T);
+  if (H == 512) return launch_bwd<512>(S, U, grid, st, dh, wt, gv, csv, (bf16*)dgates, cnt, err, B, T);
+  return launch_bwd<768>(S, U, grid, st, dh, wt, gv, csv, (bf16*)dgates, cnt, err, B, T);
 }
 
 }  // extern "C"

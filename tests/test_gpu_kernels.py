@@ -180,12 +180,33 @@ def _pack_lstm(w_ih, w_hh, b_ih, b_hh, H, dtype, L):
     (torch.bfloat16, (3, 5, 32, 64), False), (torch.bfloat16, (16, 8, 64, 128), True),
     (torch.bfloat16, (3, 5, 32, 64), True), (torch.bfloat16, (64, 6, 512, 512), True),
     (torch.bfloat16, (64, 6, 512, 512), "seq"), (torch.bfloat16, (32, 7, 256, 128), "seq"),
-    (torch.bfloat16, (64, 5, 768, 512), "seq"), (torch.bfloat16, (256, 4, 512, 512), "seq")])
+    (torch.bfloat16, (64, 5, 768, 512), "seq"), (torch.bfloat16, (256, 4, 512, 512), "seq"),
+    (torch.bfloat16, (64, 6, 512, 512), "seq1"), (torch.bfloat16, (64, 6, 512, 512), "seq2"),
+    (torch.bfloat16, (32, 5, 256, 128), "seq1"), (torch.bfloat16, (32, 5, 768, 128), "seq2"),
+    (torch.bfloat16, (64, 5, 768, 512), "seq1"), (torch.bfloat16, (64, 5, 512, 256), "seq3")])
 def test_bilstm_fwd_bwd(BTHI, dtype, oneshot):
     """bf16 steps run the one-shot LDS-DMA GEMM (forward: fused cell; backward with whh_t: split-K
     partials + sum/cell pass; H = 512 -> 4 splits); oneshot=False passes no whh_t (staged kernel);
-    "seq" runs the persistent whole-sequence kernels (lstm_seq.hip), one launch per sweep."""
+    "seq" runs the persistent whole-sequence kernels (lstm_seq.hip), one launch per sweep, with the
+    automatic workgroup tile; "seqN" forces tile N (CRNN_OPT_LSTM_TILE: 1 = 32x32, 2 = 16x32, 3 = 16x64)."""
     L = _L()
+    force = int(oneshot[3:]) if isinstance(oneshot, str) and len(oneshot) > 3 else 0
+    L.call("crnn_set_option", L.OPT_LSTM_TILE, force)
+    try:
+        _bilstm_case(L, BTHI, dtype, oneshot)
+    finally:
+        L.call("crnn_set_option", L.OPT_LSTM_TILE, 0)
+
+
+def seq_tile(B, H, bwd=0):
+    import ctypes
+    L = _L()
+    S, U = ctypes.c_int(0), ctypes.c_int(0)
+    assert L.lib().crnn_lstm_seq_config(B, H, bwd, ctypes.byref(S), ctypes.byref(U)) == 1
+    return S.value, U.value
+
+
+def _bilstm_case(L, BTHI, dtype, oneshot):
     import crnn_oracle as O
     B, T, H, In = BTHI
     g = torch.Generator().manual_seed(3)
@@ -219,14 +240,15 @@ def test_bilstm_fwd_bwd(BTHI, dtype, oneshot):
     hseq = torch.empty(B, T, 2 * H, dtype=dtype, device=DEV)
     gsv = torch.empty(2, T, B, 4 * H, dtype=dtype, device=DEV)
     csv = torch.empty(2, T, B, H, device=DEV)
-    seq = oneshot == "seq"
+    seq = isinstance(oneshot, str) and oneshot.startswith("seq")
     if seq:
         assert L.lib().crnn_lstm_seq_supported(dt, B, H) == 1
         sws = torch.full((L.lib().crnn_lstm_seq_workspace(B) // 4,), 7, dtype=torch.int32, device=DEV)
         L.call("crnn_lstm_seq_fwd", xg.data_ptr(), whh.data_ptr(), hseq.data_ptr(), gsv.data_ptr(), csv.data_ptr(),
                sws.data_ptr(), B, T, H, st)
         assert int(sws[-1].item()) == 0   # no timed-out wait
-        assert int(sws[: 2 * (B // 32)].min().item()) == H // 32 * T   # every slice published every step
+        S, U = seq_tile(B, H)
+        assert int(sws[: 2 * (B // S)].min().item()) == H // U * T   # every slice published every step
     else:
         for s in range(T):
             L.call("crnn_lstm_step_fwd", dt, xg.data_ptr(), whh.data_ptr(), hseq.data_ptr(), gsv.data_ptr(),
@@ -242,6 +264,8 @@ def test_bilstm_fwd_bwd(BTHI, dtype, oneshot):
         L.call("crnn_lstm_seq_bwd", dh.data_ptr(), whh_t.data_ptr(), gsv.data_ptr(), csv.data_ptr(), dg.data_ptr(),
                sws.data_ptr(), B, T, H, st)
         assert int(sws[-1].item()) == 0
+        S, U = seq_tile(B, H, 1)
+        assert int(sws[: 2 * (B // S)].min().item()) == H // U * T
         # the per-step path on the same saved forward agrees to bf16 rounding of dgates
         dg2 = torch.empty_like(dg)
         for s in range(T):

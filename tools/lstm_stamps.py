@@ -1,6 +1,8 @@
 """Phase timing of the persistent BiLSTM kernels (lstm_seq.hip) from in-kernel s_memrealtime
 stamps (10 ns ticks). Prints per-phase medians and the hand-off latency (last producer's signal of
-step s-1 -> consumer past its wait at step s).   python tools/lstm_stamps.py [B T H]"""
+step s-1 -> consumer past its wait at step s), for every workgroup tile (CRNN_OPT_LSTM_TILE) the
+shape supports, in one process.   python tools/lstm_stamps.py [B T H]"""
+import ctypes
 import os
 import sys
 
@@ -26,7 +28,11 @@ def run(kind, B, T, H):
     csv = torch.zeros(2, T, B, H, device=dev)
     dg = torch.zeros(2, T, B, 4 * H, device=dev, dtype=torch.bfloat16)
     ws = torch.zeros(L.lib().crnn_lstm_seq_workspace(B) // 4 + 4, dtype=torch.int32, device=dev)
-    grid = 2 * (B // 32) * (H // 32)
+    S, U = ctypes.c_int(0), ctypes.c_int(0)
+    if not L.lib().crnn_lstm_seq_config(B, H, int(kind == "bwd"), ctypes.byref(S), ctypes.byref(U)):
+        return
+    S, U = S.value, U.value
+    grid = 2 * (B // S) * (H // U)
     stamps = torch.zeros(grid * T * 8, dtype=torch.int64, device=dev)
 
     def fwd():
@@ -53,7 +59,7 @@ def run(kind, B, T, H):
     torch.cuda.synchronize()
     L.call("crnn_lstm_seq_debug_stamps", None)
     s = stamps.view(grid, T, 8).cpu().numpy().astype(np.int64)
-    print(f"{kind}: B={B} T={T} H={H} grid={grid}: {us:.1f} us/sweep = {us / T:.2f} us/step (no stamps)")
+    print(f"{kind}: B={B} T={T} H={H} tile {S}x{U} grid={grid}: {us:.1f} us/sweep = {us / T:.2f} us/step (no stamps)")
     steps = slice(2, T - 1)
     d = s[:, steps, :]
     for p in range(1, 7):
@@ -74,5 +80,8 @@ def run(kind, B, T, H):
 
 if __name__ == "__main__":
     B, T, H = (int(a) for a in sys.argv[1:4]) if len(sys.argv) > 3 else (256, 32, 512)
-    run("fwd", B, T, H)
-    run("bwd", B, T, H)
+    for force in (1, 2, 3):
+        L.call("crnn_set_option", L.OPT_LSTM_TILE, force)
+        run("fwd", B, T, H)
+        run("bwd", B, T, H)
+    L.call("crnn_set_option", L.OPT_LSTM_TILE, 0)
