@@ -16,6 +16,15 @@
 
 using namespace gemm;
 
+// conv_halo.hip: direct 3x3 / stride-1 kernel for the full-resolution stem conv
+bool conv_halo_fits(const crnn_conv_desc* d, bool dgrad);
+int conv_halo_fwd(const crnn_conv_desc* d, const void* x, const void* w, void* y, float* psum, float* psq,
+                  hipStream_t st);
+int conv_halo_dgrad(const crnn_conv_desc* d, const void* dy, const void* w, void* dx, hipStream_t st);
+static bool use_halo(int dtype, const crnn_conv_desc* d, bool dgrad) {
+  return dtype == CRNN_BF16 && crnn_option(CRNN_OPT_HALO_CONV) != 0 && conv_halo_fits(d, dgrad);
+}
+
 // target grid of the deep split-K wgrad (tuning knob; slab bytes grow with the split count)
 #ifndef CRNN_WGRAD_BLOCKS
 #define CRNN_WGRAD_BLOCKS 256
@@ -575,12 +584,14 @@ void crnn_conv_fwd_tile(int dtype, const crnn_conv_desc* d, int* bm, int* bn) {
 }
 
 int crnn_conv_stat_rows_per_partial(int dtype, const crnn_conv_desc* d) {
+  if (use_halo(dtype, d, false)) return 128;  // one partial per 128-pixel tile
   int bm, bn;
   crnn_conv_fwd_tile(dtype, d, &bm, &bn);
   return bm / 2;
 }
 
 int crnn_conv_stat_rows(int dtype, const crnn_conv_desc* d) {
+  if (use_halo(dtype, d, false)) return (int)((long)d->B * d->Ho * d->Wo / 128);
   int bm, bn;
   crnn_conv_fwd_tile(dtype, d, &bm, &bn);
   long M = (long)d->B * d->Ho * d->Wo;
@@ -629,6 +640,7 @@ int crnn_conv_fwd(int dtype, const crnn_conv_desc* d, const void* x, const void*
                   float* psum, float* psq, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if (d->Ci % 8 || d->Co % 8) return crnn_set_error(hipErrorInvalidValue, "conv_fwd: channels must be multiples of 8");
+  if (use_halo(dtype, d, false)) return conv_halo_fwd(d, x, w, y, psum, psq, st);
   return dtype == CRNN_BF16 ? conv_fwd_t<bf16>(d, x, w, y, psum, psq, st)
                             : conv_fwd_t<float>(d, x, w, y, psum, psq, st);
 }
@@ -637,6 +649,7 @@ int crnn_conv_dgrad(int dtype, const crnn_conv_desc* d, const void* dy, const vo
                     const void* dres, const void* yres, int accumulate, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if (d->Ci % 8 || d->Co % 8) return crnn_set_error(hipErrorInvalidValue, "conv_dgrad: channels must be multiples of 8");
+  if (dres == nullptr && !accumulate && use_halo(dtype, d, true)) return conv_halo_dgrad(d, dy, w, dx, st);
   return dtype == CRNN_BF16 ? conv_dgrad_t<bf16>(d, dy, w, dx, dres, yres, accumulate, st)
                             : conv_dgrad_t<float>(d, dy, w, dx, dres, yres, accumulate, st);
 }

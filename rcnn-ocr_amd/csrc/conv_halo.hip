@@ -1,0 +1,232 @@
+// Halo-tiled direct 3x3 convolution (stride 1, pad 1, NHWC bf16) for the full-resolution stem
+// conv of SE-ResNet31 (reference: model/seresnet31.py:82-86, nn.Conv2d(64, 128, 3, 1, 1)) — its
+// forward and its input gradient, which is the same convolution with flipped taps and transposed
+// weights.
+//
+// Why a separate kernel: at 32x256 with Ci = 64 the implicit GEMM (conv.hip) has K = 576, so
+// every 256 x 128 tile re-reads its 9x im2col rows and the whole 147 KB weight from L2 for only
+// nine 64-deep K-steps — the launch runs at the L2 bandwidth, ~0.5 PFLOP/s. Here:
+//   * one workgroup owns a BAND: one image, one 128-pixel half of the width, all H rows, and
+//     walks it top to bottom (persistent over the band's H tiles);
+//   * its weights live in VGPRs for the whole band (each wave holds the K x CO/4 slice it needs);
+//   * the input rows y-1, y, y+1 (+ halo columns) sit in a 4-slot LDS ring; row y+2 is fetched
+//     into registers while row y computes and written to the free slot afterwards, so each input
+//     byte crosses HBM -> LDS once per band;
+//   * A fragments come straight from the ring with ds_read_b128 (pixel pitch padded so the 16
+//     pixels of each lane group land on distinct banks).
+// Wave (pw, cw) of 8 (two per SIMD): 64 output pixels x CO/4 channels, MFMA 16x16x32 bf16, fp32
+// accumulate; each wave's weight slice (CO/4 x 9*CI) is 144 VGPRs.
+// The forward also emits the BatchNorm partial statistics of conv.hip's layout: one (sum, M2)
+// row per 128 output pixels (= one tile), from the fp32 accumulators.
+#include "gemm.hpp"
+#include "crnn_internal.hpp"
+
+using namespace gemm;
+
+namespace {
+
+constexpr int TW = 128;  // output pixels per tile: half of a 256-wide row
+
+template <int CI> struct Ring {
+  // bytes per halo pixel: (CI/8 + 2) 16-B slots, = 2 mod 4 slots, which keeps every ds_read_b128 lane
+  // group of an A fragment (16 pixels, 2 channel chunks) on distinct banks (enumerated offline)
+  static constexpr int PITCH = CI * 2 + 32;
+  static constexpr int SLOT = (TW + 2) * PITCH;  // one input row of the band + 2 halo columns
+  static constexpr int CH = CI / 8;              // 16-B chunks per pixel
+  static constexpr int NCHUNK = (TW + 2) * CH;
+  static constexpr int PER_T = (NCHUNK + 511) / 512;
+};
+
+// FLIP = false: y = conv(x, W), W packed [CO][3][3][CI] (conv.hip's OHWI pack).
+// FLIP = true : dx = conv(dy, W'), W'[o][t][c] = W[c][8 - t][o], read from the forward pack
+//               [CI][3][3][CO] (CI = forward Co, CO = forward Ci).
+template <int CI, int CO, bool FLIP>
+__global__ __launch_bounds__(512) void halo3x3_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wp,
+                                                      bf16* __restrict__ y, float* __restrict__ psum,
+                                                      float* __restrict__ psq, int H, int W, uint32_t xbytes) {
+  using R = Ring<CI>;
+  constexpr int KC = CI / 32;       // 32-deep k-steps per tap
+  constexpr int KS = 9 * KC;        // k-steps
+  constexpr int CW = CO / 4;        // output channels per wave
+  constexpr int NJ = CW / 16;       // channel fragments per wave
+  constexpr int MI = 4;             // 64 pixels per wave
+  static_assert(CI % 32 == 0 && CO % 32 == 0, "channels");
+  __shared__ __attribute__((aligned(16))) char ring[4 * R::SLOT];
+  __shared__ __attribute__((aligned(16))) f32x4 xst[4][2][CW / 4];  // [cw][sum | M2][channel quad] of the pw = 1 waves
+
+  const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int pw = wv & 1, cw = wv >> 1;
+  const int nxh = W / TW;
+  const int band = blockIdx.x;
+  const int b = band / nxh, x0 = (band - b * nxh) * TW;
+
+  // weights: slot ks of fragment j = output channel cw*CW + 16j + c, k = 32ks + 8g .. +7
+  bf16x8 wf[NJ][KS];
+  if constexpr (!FLIP) {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+        wf[j][ks] = *reinterpret_cast<const bf16x8*>(wp + (size_t)(cw * CW + 16 * j + c) * 9 * CI + 32 * ks + 8 * g);
+  } else {
+    // W' is a gather of the forward pack: build it in the (still unused) ring one half of the
+    // output channels at a time, [CO/2][9*CI] rows, coalesced global reads (o fastest)
+    static_assert((size_t)2 * CW * 9 * CI * 2 <= 4 * R::SLOT, "W' half fits the ring");
+    bf16* wl = reinterpret_cast<bf16*>(ring);
+#pragma unroll 1
+    for (int hh = 0; hh < 2; ++hh) {
+      for (int e = threadIdx.x; e < 2 * CW * 9 * CI; e += 512) {
+        const int o = e % (2 * CW), kk = e / (2 * CW), t = kk / CI, cc = kk % CI;  // kk = t * CI + cc
+        wl[o * 9 * CI + kk] = wp[((size_t)cc * 9 + (8 - t)) * CO + hh * 2 * CW + o];
+      }
+      __syncthreads();
+      if ((cw >> 1) == hh) {
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+#pragma unroll
+          for (int ks = 0; ks < KS; ++ks)
+            wf[j][ks] = *reinterpret_cast<const bf16x8*>(wl + ((cw & 1) * CW + 16 * j + c) * 9 * CI + 32 * ks + 8 * g);
+      }
+      __syncthreads();
+    }
+  }
+
+  const __amdgpu_buffer_rsrc_t rx = mk_rsrc(x, xbytes);
+  u32x4 pre[R::PER_T];
+  // input row r of image b, columns x0-1 .. x0+TW, into registers (zeros outside the image:
+  // out-of-range buffer offsets read 0, so the loads carry no branches)
+  auto load_row = [&](int r) {
+#pragma unroll
+    for (int i = 0; i < R::PER_T; ++i) {
+      const int q = threadIdx.x + 512 * i;
+      const int px = q / R::CH, ch = q % R::CH;
+      const int xc = x0 - 1 + px;
+      const bool ok = q < R::NCHUNK && r >= 0 && r < H && xc >= 0 && xc < W;
+      const uint32_t off = ok ? ((((uint32_t)b * H + r) * W + xc) * CI + ch * 8) * 2u : OOB;
+      pre[i] = __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0);
+    }
+  };
+  auto store_row = [&](int r) {
+    char* s = ring + ((r + 1) & 3) * R::SLOT;
+#pragma unroll
+    for (int i = 0; i < R::PER_T; ++i) {
+      const int q = threadIdx.x + 512 * i;
+      const int px = q / R::CH, ch = q % R::CH;
+      if (q < R::NCHUNK) *reinterpret_cast<u32x4*>(s + px * R::PITCH + ch * 16) = pre[i];
+    }
+  };
+  load_row(-1);
+  store_row(-1);
+  load_row(0);
+  store_row(0);
+  load_row(1);
+  store_row(1);
+  __syncthreads();
+
+  const uint32_t abase = (uint32_t)((pw * 64 + c) * R::PITCH + 16 * g);
+  for (int yy = 0; yy < H; ++yy) {
+    load_row(yy + 2);  // lands while this row computes; stored to the free slot below
+    f32x4 acc[MI][NJ];
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) {
+      const char* rowp = ring + ((yy + kh) & 3) * R::SLOT + abase;  // input row yy - 1 + kh
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+        for (int kc = 0; kc < KC; ++kc) {
+          bf16x8 af[MI];
+#pragma unroll
+          for (int i = 0; i < MI; ++i)
+            af[i] = *reinterpret_cast<const bf16x8*>(rowp + (16 * i + kw) * R::PITCH + kc * 64);
+#pragma unroll
+          for (int i = 0; i < MI; ++i)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) mma<bf16>(acc[i][j], wf[j][(kh * 3 + kw) * KC + kc], af[i]);
+        }
+    }
+    store_row(yy + 2);
+
+    // outputs: lane (c, g) of fragment (i, j) = pixel pw*64 + 16i + c, channels co .. co+3
+    const size_t m0 = ((size_t)b * H + yy) * W + x0;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+        st4<bf16>(y + (m0 + pw * 64 + 16 * i + c) * CO + cw * CW + 16 * j + 4 * g, acc[i][j]);
+
+    if (psum != nullptr) {
+      // per-wave (sum, M2) over its 64 pixels, Chan-combined with the other pixel half
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        f32x4 s = {0.f, 0.f, 0.f, 0.f}, q = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < MI; ++i) s += acc[i][j];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s[r] = rowgroup_sum<16>(s[r]);
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float dv = acc[i][j][r] - s[r] * (1.f / 64.f);
+            q[r] += dv * dv;
+          }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) q[r] = rowgroup_sum<16>(q[r]);
+        if (pw == 1 && c == 0) {
+          xst[cw][0][4 * j + g] = s;
+          xst[cw][1][4 * j + g] = q;
+        }
+        acc[0][j] = s;  // keep this wave's (sum, M2) for the combine
+        acc[1][j] = q;
+      }
+      __syncthreads();
+      if (pw == 0 && c == 0) {
+        const size_t prow = m0 / TW;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const f32x4 s1 = xst[cw][0][4 * j + g], q1 = xst[cw][1][4 * j + g];
+          const f32x4 s0 = acc[0][j], q0 = acc[1][j];
+          const f32x4 dm = (s0 - s1) * (1.f / 64.f);
+          const int co = cw * CW + 16 * j + 4 * g;
+          *reinterpret_cast<f32x4*>(psum + prow * CO + co) = s0 + s1;
+          *reinterpret_cast<f32x4*>(psq + prow * CO + co) = q0 + q1 + dm * dm * 32.f;  // n0 n1 / n = 32
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+}  // namespace
+
+// conv.hip dispatch: the halo kernel covers 3x3 / stride 1 / pad 1 convolutions whose width is a
+// multiple of 128 and whose (Ci, Co) has an instance; dgrad = the same kernel on the flipped weights
+bool conv_halo_fits(const crnn_conv_desc* d, bool dgrad) {
+  if (!(d->KH == 3 && d->KW == 3 && d->sh == 1 && d->sw == 1 && d->ph == 1 && d->pw == 1)) return false;
+  if (d->Ho != d->Hi || d->Wo != d->Wi || d->Wi % TW || d->Hi < 1) return false;
+  if (d->Ci_real > 0 && d->Ci_real != d->Ci) return false;
+  (void)dgrad;
+  return d->Ci == 64 && d->Co == 128;
+}
+
+int conv_halo_fwd(const crnn_conv_desc* d, const void* x, const void* w, void* y, float* psum, float* psq,
+                  hipStream_t st) {
+  const dim3 grid(d->B * (d->Wi / TW));
+  const uint32_t xbytes = (uint32_t)((size_t)d->B * d->Hi * d->Wi * d->Ci * 2);
+  hipLaunchKernelGGL((halo3x3_kernel<64, 128, false>), grid, dim3(512), 0, st, (const bf16*)x, (const bf16*)w,
+                     (bf16*)y, psum, psq, d->Hi, d->Wi, xbytes);
+  return (int)hipGetLastError();
+}
+
+int conv_halo_dgrad(const crnn_conv_desc* d, const void* dy, const void* w, void* dx, hipStream_t st) {
+  const dim3 grid(d->B * (d->Wi / TW));
+  const uint32_t dybytes = (uint32_t)((size_t)d->B * d->Ho * d->Wo * d->Co * 2);
+  hipLaunchKernelGGL((halo3x3_kernel<128, 64, true>), grid, dim3(512), 0, st, (const bf16*)dy, (const bf16*)w,
+                     (bf16*)dx, (float*)nullptr, (float*)nullptr, d->Hi, d->Wi, dybytes);
+  return (int)hipGetLastError();
+}

@@ -60,6 +60,10 @@ CONVS_DEEP = [
     (256, 256, 8, 64, 512, (3, 3), (2, 2), (1, 1)),
     (52, 256, 16, 63, 256, (3, 3), (1, 1), (1, 1)),
     (128, 128, 16, 64, 256, (1, 1), (2, 2), (0, 0)),
+    # the stem conv on the halo-tiled direct kernel (conv_halo.hip): full 256 width, and an odd
+    # number of 128-pixel tiles
+    (4, 64, 6, 256, 128, (3, 3), (1, 1), (1, 1)),
+    (3, 64, 5, 128, 128, (3, 3), (1, 1), (1, 1)),
 ]
 
 
@@ -123,6 +127,49 @@ def test_conv_fwd_dgrad_wgrad(cfg, dtype):
     dw = torch.full((Co, Ci, k[0], k[1]), 7.0, device=DEV)
     L.call("crnn_conv_wgrad", dt, d, dyd.data_ptr(), xd.data_ptr(), dw.data_ptr(), ws.data_ptr(), need, 0.0, st)
     assert relerr(dw.cpu(), wr.grad) < (1e-5 if dtype == torch.float32 else 1e-2)
+
+
+def test_conv_halo_vs_gemm():
+    """The stem conv (64 -> 128, 3x3, 32x256) on the halo kernel and on the implicit GEMM
+    (CRNN_OPT_HALO_CONV = 0) of the same inputs: outputs, BN partial statistics and dx agree to
+    fp32 summation order (bf16 outputs: within one rounding step)."""
+    L = _L()
+    B, Ci, H, W, Co = 8, 64, 32, 256, 128
+    g = torch.Generator().manual_seed(5)
+    x = (torch.randn(B, H, W, Ci, generator=g)).to(DEV, torch.bfloat16)
+    w = (torch.randn(Co, Ci, 3, 3, generator=g) / 24).to(DEV)
+    dy = torch.randn(B, H, W, Co, generator=g).to(DEV, torch.bfloat16)
+    dt = L.BF16
+    st = L.stream_ptr()
+    d = L.ConvDesc(B, H, W, Ci, H, W, Co, 3, 3, 1, 1, 1, 1, Ci)
+    wd = torch.empty(Co, 3, 3, Ci, dtype=torch.bfloat16, device=DEV)
+    L.call("crnn_pack_conv_weight", dt, w.data_ptr(), wd.data_ptr(), Co, Ci, 3, 3, Ci, st)
+    out = {}
+    for opt in (1, 0):
+        L.call("crnn_set_option", L.OPT_HALO_CONV, opt)
+        try:
+            rows = L.lib().crnn_conv_stat_rows(dt, d)
+            rpp = L.lib().crnn_conv_stat_rows_per_partial(dt, d)
+            y = torch.empty(B, H, W, Co, dtype=torch.bfloat16, device=DEV)
+            ps = torch.empty(rows, Co, device=DEV)
+            pq = torch.empty(rows, Co, device=DEV)
+            L.call("crnn_conv_fwd", dt, d, x.data_ptr(), wd.data_ptr(), y.data_ptr(), ps.data_ptr(), pq.data_ptr(), st)
+            dx = torch.empty(B, H, W, Ci, dtype=torch.bfloat16, device=DEV)
+            L.call("crnn_conv_dgrad", dt, d, dy.data_ptr(), wd.data_ptr(), dx.data_ptr(), None, None, 0, st)
+            torch.cuda.synchronize()
+            M = B * H * W
+            n = rpp
+            mean = ps.double().sum(0) / M
+            var = (pq.double().sum(0) + (n * (ps.double() / n - mean) ** 2).sum(0)) / M
+            out[opt] = (y.float(), mean, var, dx.float(), rows, rpp)
+        finally:
+            L.call("crnn_set_option", L.OPT_HALO_CONV, 1)
+    (y1, m1, v1, dx1, r1, p1), (y0, m0, v0, dx0, r0, p0) = out[1], out[0]
+    assert r1 * p1 == r0 * p0 == B * H * W
+    assert float((y1 - y0).abs().max()) <= 2 ** -7 * float(y0.abs().max())
+    assert relerr(y1, y0) < 2e-3
+    assert relerr(m1, m0) < 1e-5 and relerr(v1, v0) < 1e-5
+    assert relerr(dx1, dx0) < 2e-3
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
