@@ -584,14 +584,14 @@ void crnn_conv_fwd_tile(int dtype, const crnn_conv_desc* d, int* bm, int* bn) {
 }
 
 int crnn_conv_stat_rows_per_partial(int dtype, const crnn_conv_desc* d) {
-  if (use_halo(dtype, d, false)) return 128;  // one partial per 128-pixel tile
+  if (use_halo(dtype, d, false)) return 64;  // one partial per wave: 64 pixels
   int bm, bn;
   crnn_conv_fwd_tile(dtype, d, &bm, &bn);
   return bm / 2;
 }
 
 int crnn_conv_stat_rows(int dtype, const crnn_conv_desc* d) {
-  if (use_halo(dtype, d, false)) return (int)((long)d->B * d->Ho * d->Wo / 128);
+  if (use_halo(dtype, d, false)) return (int)((long)d->B * d->Ho * d->Wo / 64);
   int bm, bn;
   crnn_conv_fwd_tile(dtype, d, &bm, &bn);
   long M = (long)d->B * d->Ho * d->Wo;

@@ -16,8 +16,8 @@
 //     pixels of each lane group land on distinct banks).
 // Wave (pw, cw) of 8 (two per SIMD): 64 output pixels x CO/4 channels, MFMA 16x16x32 bf16, fp32
 // accumulate; each wave's weight slice (CO/4 x 9*CI) is 144 VGPRs.
-// The forward also emits the BatchNorm partial statistics of conv.hip's layout: one (sum, M2)
-// row per 128 output pixels (= one tile), from the fp32 accumulators.
+// The forward also emits BatchNorm partial statistics in conv.hip's (sum, M2) layout, one partial
+// row per 64 output pixels (one wave's share of a tile), from the fp32 accumulators.
 #include "gemm.hpp"
 #include "crnn_internal.hpp"
 
@@ -52,7 +52,6 @@ __global__ __launch_bounds__(512) void halo3x3_kernel(const bf16* __restrict__ x
   constexpr int MI = 4;             // 64 pixels per wave
   static_assert(CI % 32 == 0 && CO % 32 == 0, "channels");
   __shared__ __attribute__((aligned(16))) char ring[4 * R::SLOT];
-  __shared__ __attribute__((aligned(16))) f32x4 xst[4][2][CW / 4];  // [cw][sum | M2][channel quad] of the pw = 1 waves
 
   const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -71,14 +70,18 @@ __global__ __launch_bounds__(512) void halo3x3_kernel(const bf16* __restrict__ x
         wf[j][ks] = *reinterpret_cast<const bf16x8*>(wp + (size_t)(cw * CW + 16 * j + c) * 9 * CI + 32 * ks + 8 * g);
   } else {
     // W' is a gather of the forward pack: build it in the (still unused) ring one half of the
-    // output channels at a time, [CO/2][9*CI] rows, coalesced global reads (o fastest)
+    // output channels at a time, [CO/2][9*CI] rows
     static_assert((size_t)2 * CW * 9 * CI * 2 <= 4 * R::SLOT, "W' half fits the ring");
     bf16* wl = reinterpret_cast<bf16*>(ring);
 #pragma unroll 1
     for (int hh = 0; hh < 2; ++hh) {
-      for (int e = threadIdx.x; e < 2 * CW * 9 * CI; e += 512) {
-        const int o = e % (2 * CW), kk = e / (2 * CW), t = kk / CI, cc = kk % CI;  // kk = t * CI + cc
-        wl[o * 9 * CI + kk] = wp[((size_t)cc * 9 + (8 - t)) * CO + hh * 2 * CW + o];
+      // a thread moves 8 consecutive o of one kk = t * CI + cc: one 16-B global read, 8 LDS
+      // writes whose lanes differ in kk (consecutive addresses, no bank conflicts)
+      for (int e = threadIdx.x; e < 2 * CW / 8 * 9 * CI; e += 512) {
+        const int kk = e % (9 * CI), o8 = e / (9 * CI), t = kk / CI, cc = kk % CI;
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(wp + ((size_t)cc * 9 + (8 - t)) * CO + hh * 2 * CW + 8 * o8);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) wl[(8 * o8 + q) * 9 * CI + kk] = v[q];
       }
       __syncthreads();
       if ((cw >> 1) == hh) {
@@ -132,22 +135,30 @@ __global__ __launch_bounds__(512) void halo3x3_kernel(const bf16* __restrict__ x
     for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const char* rowp[3];  // input rows yy - 1 .. yy + 1
 #pragma unroll
-    for (int kh = 0; kh < 3; ++kh) {
-      const char* rowp = ring + ((yy + kh) & 3) * R::SLOT + abase;  // input row yy - 1 + kh
+    for (int kh = 0; kh < 3; ++kh) rowp[kh] = ring + ((yy + kh) & 3) * R::SLOT + abase;
+    // k-step ks = (kh, kw, kc): A fragments of step ks+1 are read while step ks multiplies
+    // (software double buffer; the scheduling barrier keeps the compiler from sinking the reads
+    // next to their MFMAs)
+    bf16x8 af[2][MI];
+    auto read_a = [&](int ks, bf16x8 (&a)[MI]) {
+      const int kh = ks / (3 * KC), kw = (ks / KC) % 3, kc = ks % KC;
 #pragma unroll
-      for (int kw = 0; kw < 3; ++kw)
+      for (int i = 0; i < MI; ++i)
+        a[i] = *reinterpret_cast<const bf16x8*>(rowp[kh] + (16 * i + kw) * R::PITCH + kc * 64);
+    };
+    read_a(0, af[0]);
 #pragma unroll
-        for (int kc = 0; kc < KC; ++kc) {
-          bf16x8 af[MI];
+    for (int ks = 0; ks < KS; ++ks) {
+      if (ks + 1 < KS) read_a(ks + 1, af[(ks + 1) & 1]);
 #pragma unroll
-          for (int i = 0; i < MI; ++i)
-            af[i] = *reinterpret_cast<const bf16x8*>(rowp + (16 * i + kw) * R::PITCH + kc * 64);
+      for (int i = 0; i < MI; ++i)
 #pragma unroll
-          for (int i = 0; i < MI; ++i)
-#pragma unroll
-            for (int j = 0; j < NJ; ++j) mma<bf16>(acc[i][j], wf[j][(kh * 3 + kw) * KC + kc], af[i]);
-        }
+        for (int j = 0; j < NJ; ++j) mma<bf16>(acc[i][j], wf[j][ks], af[ks & 1][i]);
+      if (ks + 1 < KS) __builtin_amdgcn_sched_group_barrier(0x100, MI, 0);  // the DS reads first,
+      __builtin_amdgcn_sched_group_barrier(0x008, MI * NJ, 0);             // then the MFMAs
+      __builtin_amdgcn_sched_barrier(0);
     }
     store_row(yy + 2);
 
@@ -160,7 +171,9 @@ __global__ __launch_bounds__(512) void halo3x3_kernel(const bf16* __restrict__ x
         st4<bf16>(y + (m0 + pw * 64 + 16 * i + c) * CO + cw * CW + 16 * j + 4 * g, acc[i][j]);
 
     if (psum != nullptr) {
-      // per-wave (sum, M2) over its 64 pixels, Chan-combined with the other pixel half
+      // BN partial statistics: (sum, M2 about the partial mean) of this wave's 64 pixels, one
+      // partial row per 64 pixels (crnn_conv_stat_rows_per_partial), straight from the accumulators
+      const size_t prow = (m0 + pw * 64) / 64;
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         f32x4 s = {0.f, 0.f, 0.f, 0.f}, q = {0.f, 0.f, 0.f, 0.f};
@@ -177,24 +190,10 @@ __global__ __launch_bounds__(512) void halo3x3_kernel(const bf16* __restrict__ x
           }
 #pragma unroll
         for (int r = 0; r < 4; ++r) q[r] = rowgroup_sum<16>(q[r]);
-        if (pw == 1 && c == 0) {
-          xst[cw][0][4 * j + g] = s;
-          xst[cw][1][4 * j + g] = q;
-        }
-        acc[0][j] = s;  // keep this wave's (sum, M2) for the combine
-        acc[1][j] = q;
-      }
-      __syncthreads();
-      if (pw == 0 && c == 0) {
-        const size_t prow = m0 / TW;
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-          const f32x4 s1 = xst[cw][0][4 * j + g], q1 = xst[cw][1][4 * j + g];
-          const f32x4 s0 = acc[0][j], q0 = acc[1][j];
-          const f32x4 dm = (s0 - s1) * (1.f / 64.f);
+        if (c == 0) {
           const int co = cw * CW + 16 * j + 4 * g;
-          *reinterpret_cast<f32x4*>(psum + prow * CO + co) = s0 + s1;
-          *reinterpret_cast<f32x4*>(psq + prow * CO + co) = q0 + q1 + dm * dm * 32.f;  // n0 n1 / n = 32
+          *reinterpret_cast<f32x4*>(psum + prow * CO + co) = s;
+          *reinterpret_cast<f32x4*>(psq + prow * CO + co) = q;
         }
       }
     }
