@@ -55,7 +55,8 @@ enum { CRNN_OPT_GEMM_STAGGER = 0,    /* 256-row conv GEMM: waves 4-7 one barrier
        CRNN_OPT_LSTM_TILE = 4,       /* persistent BiLSTM workgroup tile: 0 = auto, 1 = 32 samples x 32 units,
                                         2 = 16 x 32, 3 = 16 x 64 (when the grid fits the CUs) */
        CRNN_OPT_HALO_CONV = 5,       /* full-resolution 3x3 stride-1 convs (the stem's 64 -> 128) on the
-                                        halo-tiled direct kernel (conv_halo.hip): 1 = on (default), 0 = GEMM */
+                                        halo-tiled direct kernel (conv_halo.hip): 1 = on (default), 0 = GEMM,
+                                        n >= 2: on, with n-row bands for the MFMA-bound instances */
        CRNN_OPT_COUNT = 6 };
 int crnn_set_option(int key, int value);
 

@@ -1,7 +1,7 @@
-// Halo-tiled direct 3x3 convolution (stride 1, pad 1, NHWC bf16) for the full-resolution stem
-// conv of SE-ResNet31 (reference: model/seresnet31.py:82-86, nn.Conv2d(64, 128, 3, 1, 1)) — its
-// forward and its input gradient, which is the same convolution with flipped taps and transposed
-// weights.
+// Halo-tiled direct 3x3 convolution (stride 1, pad 1, NHWC bf16) for the two full-resolution stem
+// convs of SE-ResNet31 (reference: model/seresnet31.py:82-86, nn.Conv2d(3, 64, 3, 1, 1) and
+// nn.Conv2d(64, 128, 3, 1, 1)) — their forward, and the second one's input gradient, which is the
+// same convolution with flipped taps and transposed weights.
 //
 // Why a separate kernel: at 32x256 with Ci = 64 the implicit GEMM (conv.hip) has K = 576, so
 // every 256 x 128 tile re-reads its 9x im2col rows and the whole 147 KB weight from L2 for only
@@ -30,7 +30,8 @@ constexpr int TW = 128;  // output pixels per tile: half of a 256-wide row
 template <int CI> struct Ring {
   // bytes per halo pixel: (CI/8 + 2) 16-B slots, = 2 mod 4 slots, which keeps every ds_read_b128 lane
   // group of an A fragment (16 pixels, 2 channel chunks) on distinct banks (enumerated offline)
-  static constexpr int PITCH = CI * 2 + 32;
+  // (CI = 8, the 3-channel input conv: one 16-B slot per pixel, taps packed along k instead)
+  static constexpr int PITCH = CI >= 32 ? CI * 2 + 32 : CI * 2;
   static constexpr int SLOT = (TW + 2) * PITCH;  // one input row of the band + 2 halo columns
   static constexpr int CH = CI / 8;              // 16-B chunks per pixel
   static constexpr int NCHUNK = (TW + 2) * CH;
@@ -43,22 +44,27 @@ template <int CI> struct Ring {
 template <int CI, int CO, bool FLIP>
 __global__ __launch_bounds__(512) void halo3x3_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wp,
                                                       bf16* __restrict__ y, float* __restrict__ psum,
-                                                      float* __restrict__ psq, int H, int W, uint32_t xbytes) {
+                                                      float* __restrict__ psq, int H, int W, int RB, uint32_t xbytes) {
   using R = Ring<CI>;
-  constexpr int KC = CI / 32;       // 32-deep k-steps per tap
-  constexpr int KS = 9 * KC;        // k-steps
+  // CI = 8 (TAPK): a 32-deep k-step holds 4 taps x 8 channels, lane group g takes tap 4ks + g
+  // (taps 9..11 of the last step: zero weights, any finite data)
+  constexpr bool TAPK = CI == 8;
+  constexpr int KC = TAPK ? 1 : CI / 32;  // 32-deep k-steps per tap
+  constexpr int KS = TAPK ? 3 : 9 * KC;   // k-steps
   constexpr int CW = CO / 4;        // output channels per wave
   constexpr int NJ = CW / 16;       // channel fragments per wave
   constexpr int MI = 4;             // 64 pixels per wave
-  static_assert(CI % 32 == 0 && CO % 32 == 0, "channels");
+  static_assert((CI % 32 == 0 || TAPK) && CO % 32 == 0 && !(TAPK && FLIP), "channels");
   __shared__ __attribute__((aligned(16))) char ring[4 * R::SLOT];
 
   const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int pw = wv & 1, cw = wv >> 1;
-  const int nxh = W / TW;
+  // band = (image b, 128-column half xh, chunk of RB rows starting at r0)
+  const int nxh = W / TW, nrc = H / RB;
   const int band = blockIdx.x;
-  const int b = band / nxh, x0 = (band - b * nxh) * TW;
+  const int b = band / (nxh * nrc), xh = (band / nrc) % nxh, r0 = (band % nrc) * RB;
+  const int x0 = xh * TW;
 
   // weights: slot ks of fragment j = output channel cw*CW + 16j + c, k = 32ks + 8g .. +7
   bf16x8 wf[NJ][KS];
@@ -67,7 +73,12 @@ __global__ __launch_bounds__(512) void halo3x3_kernel(const bf16* __restrict__ x
     for (int j = 0; j < NJ; ++j)
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks)
-        wf[j][ks] = *reinterpret_cast<const bf16x8*>(wp + (size_t)(cw * CW + 16 * j + c) * 9 * CI + 32 * ks + 8 * g);
+        if constexpr (TAPK) {
+          const bf16x8 v = *reinterpret_cast<const bf16x8*>(wp + (size_t)(cw * CW + 16 * j + c) * 72 + 8 * min(4 * ks + g, 8));
+          wf[j][ks] = 4 * ks + g < 9 ? v : bf16x8{};
+        } else {
+          wf[j][ks] = *reinterpret_cast<const bf16x8*>(wp + (size_t)(cw * CW + 16 * j + c) * 9 * CI + 32 * ks + 8 * g);
+        }
   } else {
     // W' is a gather of the forward pack: build it in the (still unused) ring one half of the
     // output channels at a time, [CO/2][9*CI] rows
@@ -119,31 +130,38 @@ __global__ __launch_bounds__(512) void halo3x3_kernel(const bf16* __restrict__ x
       if (q < R::NCHUNK) *reinterpret_cast<u32x4*>(s + px * R::PITCH + ch * 16) = pre[i];
     }
   };
-  load_row(-1);
-  store_row(-1);
-  load_row(0);
-  store_row(0);
-  load_row(1);
-  store_row(1);
+  load_row(r0 - 1);
+  store_row(r0 - 1);
+  load_row(r0);
+  store_row(r0);
+  load_row(r0 + 1);
+  store_row(r0 + 1);
   __syncthreads();
 
-  const uint32_t abase = (uint32_t)((pw * 64 + c) * R::PITCH + 16 * g);
-  for (int yy = 0; yy < H; ++yy) {
+  const uint32_t abase = (uint32_t)((pw * 64 + c) * R::PITCH + (TAPK ? 0 : 16 * g));
+  for (int yy = r0; yy < r0 + RB; ++yy) {
     load_row(yy + 2);  // lands while this row computes; stored to the free slot below
     f32x4 acc[MI][NJ];
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const char* rowp[3];  // input rows yy - 1 .. yy + 1
+    const char* rowp[3];  // input rows yy - 1 .. yy + 1 (TAPK: this lane's tap of k-step kh)
 #pragma unroll
-    for (int kh = 0; kh < 3; ++kh) rowp[kh] = ring + ((yy + kh) & 3) * R::SLOT + abase;
+    for (int kh = 0; kh < 3; ++kh) {
+      if constexpr (TAPK) {
+        const int t = min(4 * kh + g, 8), th = t / 3;
+        rowp[kh] = ring + ((yy + th) & 3) * R::SLOT + abase + (t - 3 * th) * R::PITCH;
+      } else {
+        rowp[kh] = ring + ((yy + kh) & 3) * R::SLOT + abase;
+      }
+    }
     // k-step ks = (kh, kw, kc): A fragments of step ks+1 are read while step ks multiplies
     // (software double buffer; the scheduling barrier keeps the compiler from sinking the reads
     // next to their MFMAs)
     bf16x8 af[2][MI];
     auto read_a = [&](int ks, bf16x8 (&a)[MI]) {
-      const int kh = ks / (3 * KC), kw = (ks / KC) % 3, kc = ks % KC;
+      const int kh = TAPK ? ks : ks / (3 * KC), kw = TAPK ? 0 : (ks / KC) % 3, kc = ks % KC;
 #pragma unroll
       for (int i = 0; i < MI; ++i)
         a[i] = *reinterpret_cast<const bf16x8*>(rowp[kh] + (16 * i + kw) * R::PITCH + kc * 64);
@@ -204,21 +222,39 @@ __global__ __launch_bounds__(512) void halo3x3_kernel(const bf16* __restrict__ x
 }  // namespace
 
 // conv.hip dispatch: the halo kernel covers 3x3 / stride 1 / pad 1 convolutions whose width is a
-// multiple of 128 and whose (Ci, Co) has an instance; dgrad = the same kernel on the flipped weights
+// multiple of 128 and whose (Ci, Co) has an instance — the stem's (8 = 3 padded, 64) and (64, 128);
+// dgrad = the same kernel on the flipped weights (64, 128 only: the input conv needs no dx)
 bool conv_halo_fits(const crnn_conv_desc* d, bool dgrad) {
   if (!(d->KH == 3 && d->KW == 3 && d->sh == 1 && d->sw == 1 && d->ph == 1 && d->pw == 1)) return false;
   if (d->Ho != d->Hi || d->Wo != d->Wi || d->Wi % TW || d->Hi < 1) return false;
-  if (d->Ci_real > 0 && d->Ci_real != d->Ci) return false;
-  (void)dgrad;
-  return d->Ci == 64 && d->Co == 128;
+  if (dgrad) return d->Ci == 64 && d->Co == 128;
+  return (d->Ci == 64 && d->Co == 128) || (d->Ci == 8 && d->Co == 64);
+}
+
+// rows per band: the memory-bound input conv (few FLOPs per row, several workgroups per CU) takes
+// short bands so more of them are in flight; the MFMA-bound ones walk the whole height
+// (tuning: CRNN_OPT_HALO_CONV = n >= 2 sets n rows for the others, when it divides H)
+static int band_rows(int H, int ci) {
+  if (ci == 8)
+    for (int rb : {8, 4, 2})
+      if (H % rb == 0 && H > rb) return rb;
+  const int opt = crnn_option(CRNN_OPT_HALO_CONV);
+  if (opt >= 2 && H % opt == 0) return opt;
+  if (ci == 64 && H % 16 == 0 && H > 16) return 16;  // 4 bands per CU: measured 7 % faster than H
+  return H;
 }
 
 int conv_halo_fwd(const crnn_conv_desc* d, const void* x, const void* w, void* y, float* psum, float* psq,
                   hipStream_t st) {
-  const dim3 grid(d->B * (d->Wi / TW));
+  const int rb = band_rows(d->Hi, d->Ci);
+  const dim3 grid(d->B * (d->Wi / TW) * (d->Hi / rb));
   const uint32_t xbytes = (uint32_t)((size_t)d->B * d->Hi * d->Wi * d->Ci * 2);
-  hipLaunchKernelGGL((halo3x3_kernel<64, 128, false>), grid, dim3(512), 0, st, (const bf16*)x, (const bf16*)w,
-                     (bf16*)y, psum, psq, d->Hi, d->Wi, xbytes);
+  if (d->Ci == 8)
+    hipLaunchKernelGGL((halo3x3_kernel<8, 64, false>), grid, dim3(512), 0, st, (const bf16*)x, (const bf16*)w,
+                       (bf16*)y, psum, psq, d->Hi, d->Wi, rb, xbytes);
+  else
+    hipLaunchKernelGGL((halo3x3_kernel<64, 128, false>), grid, dim3(512), 0, st, (const bf16*)x, (const bf16*)w,
+                       (bf16*)y, psum, psq, d->Hi, d->Wi, rb, xbytes);
   return (int)hipGetLastError();
 }
 
@@ -226,6 +262,6 @@ int conv_halo_dgrad(const crnn_conv_desc* d, const void* dy, const void* w, void
   const dim3 grid(d->B * (d->Wi / TW));
   const uint32_t dybytes = (uint32_t)((size_t)d->B * d->Ho * d->Wo * d->Co * 2);
   hipLaunchKernelGGL((halo3x3_kernel<128, 64, true>), grid, dim3(512), 0, st, (const bf16*)dy, (const bf16*)w,
-                     (bf16*)dx, (float*)nullptr, (float*)nullptr, d->Hi, d->Wi, dybytes);
+                     (bf16*)dx, (float*)nullptr, (float*)nullptr, d->Hi, d->Wi, d->Hi, dybytes);
   return (int)hipGetLastError();
 }

@@ -64,6 +64,7 @@ CONVS_DEEP = [
     # number of 128-pixel tiles
     (4, 64, 6, 256, 128, (3, 3), (1, 1), (1, 1)),
     (3, 64, 5, 128, 128, (3, 3), (1, 1), (1, 1)),
+    (4, 3, 5, 256, 64, (3, 3), (1, 1), (1, 1)),   # the input conv (3 -> 8 padded channels, taps along k)
 ]
 
 
