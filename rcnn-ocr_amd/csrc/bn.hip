@@ -791,25 +791,27 @@ __global__ __launch_bounds__(256) void pack_batch_kernel(const crnn_pack_job* __
       if (jb.start >= e1) break;
       continue;
     }
+    // element index inside a job fits 32 bits (the largest tensor is 2.4 M elements): 32-bit
+    // divisions, not the 64-bit ones that dominated this kernel
     for (long g = a0 + threadIdx.x; g < a1; g += blockDim.x) {
-      const long i = g - jb.start;
+      const int i = (int)(g - jb.start);
       float v;
       if (jb.kind == CRNN_PACK_CONV) {
         const int Ci = jb.b, KH = jb.c, KW = jb.d, Cip = jb.e;
-        const int ci = (int)(i % Cip);
-        long t = i / Cip;
-        const int kw = (int)(t % KW);
+        const int ci = i % Cip;
+        int t = i / Cip;
+        const int kw = t % KW;
         t /= KW;
-        const int kh = (int)(t % KH), co = (int)(t / KH);
+        const int kh = t % KH, co = t / KH;
         v = ci < Ci ? jb.src[(((size_t)co * Ci + ci) * KH + kh) * KW + kw] : 0.f;
       } else if (jb.kind == CRNN_PACK_TRANSPOSE) {
         const int rows = jb.a;
-        const int c = (int)(i / rows), r = (int)(i - (long)c * rows);
+        const int c = i / rows, r = i - c * rows;
         const int sr = jb.perm ? jb.perm[r] : r;
         v = (r < jb.b && sr >= 0) ? jb.src[(size_t)sr * jb.c + c] : 0.f;
       } else {
         const int cols = jb.c;
-        const int r = (int)(i / cols), c = (int)(i - (long)r * cols);
+        const int r = i / cols, c = i - r * cols;
         const int sr = jb.perm ? jb.perm[r] : r;
         const bool ok = r < jb.b && sr >= 0;
         v = ok ? jb.src[(size_t)sr * cols + c] : 0.f;
@@ -1394,8 +1396,10 @@ int crnn_pack_conv_weight(int dtype, const float* w, void* out, int Co, int Ci, 
 
 int crnn_pack_batch(int dtype, const crnn_pack_job* jobs, int njobs, long total, void* stream) {
   if (njobs <= 0 || total <= 0) return 0;
-  long blocks = (total + 4095) / 4096;
-  if (blocks > 8192) blocks = 8192;
+  // ~4 elements per thread: the element loop is load-latency bound (one dependent load per
+  // element, strided for the conv repack), so parallelism comes from many small blocks
+  long blocks = (total + 1023) / 1024;
+  if (blocks > (1L << 20)) blocks = 1L << 20;
   const long chunk = (total + blocks - 1) / blocks;
   DISPATCH(dtype, hipLaunchKernelGGL(pack_batch_kernel<T>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
                                      jobs, njobs, total, chunk));

@@ -150,17 +150,56 @@ __global__ void greedy_kernel(const float* __restrict__ logits, int ldc, int B, 
   if (lane == 0) lens[b] = n;
 }
 
-__global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
-                             float* __restrict__ v, long n, float lr, float b1, float b2, float eps, float wd,
-                             float step_size, float inv_sqrt_bc2, float gs) {
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
-    float gr = g[i] * gs;
-    float pv = p[i] * (1.f - lr * wd);
-    float mv = m[i];
-    mv = mv + (1.f - b1) * (gr - mv);
-    float vv = v[i] * b2 + (1.f - b2) * gr * gr;
-    float denom = sqrtf(vv) * inv_sqrt_bc2 + eps;
-    pv -= step_size * mv / denom;
+__device__ __forceinline__ void adamw_elem(float& pv, float gr, float& mv, float& vv, float lr, float b1, float b2,
+                                           float eps, float wd, float step_size, float inv_sqrt_bc2) {
+  pv *= 1.f - lr * wd;
+  mv = mv + (1.f - b1) * (gr - mv);
+  vv = vv * b2 + (1.f - b2) * gr * gr;
+  const float denom = sqrtf(vv) * inv_sqrt_bc2 + eps;
+  pv -= step_size * mv / denom;
+}
+
+// VEC: one 16-B vector of p, g, m, v per thread and iteration (HBM-bound: 28 B per parameter),
+// the n % 4 tail elements by the first threads one at a time; !VEC (pointers not 16-B aligned):
+// one element per thread and iteration
+template <bool VEC>
+__global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                    float* __restrict__ m, float* __restrict__ v, long n, float lr,
+                                                    float b1, float b2, float eps, float wd, float step_size,
+                                                    float inv_sqrt_bc2, float gs) {
+  const long tid = blockIdx.x * (long)blockDim.x + threadIdx.x, nth = (long)gridDim.x * blockDim.x;
+  if constexpr (!VEC) {
+    for (long i = tid; i < n; i += nth) {
+      float pv = p[i], mv = m[i], vv = v[i];
+      adamw_elem(pv, g[i] * gs, mv, vv, lr, b1, b2, eps, wd, step_size, inv_sqrt_bc2);
+      p[i] = pv;
+      m[i] = mv;
+      v[i] = vv;
+    }
+    return;
+  }
+  const long n4 = n >> 2;
+  for (long i = tid; i < n4; i += nth) {
+    f32x4 pv = reinterpret_cast<const f32x4*>(p)[i];
+    const f32x4 gv = reinterpret_cast<const f32x4*>(g)[i];
+    f32x4 mv = reinterpret_cast<const f32x4*>(m)[i];
+    f32x4 vv = reinterpret_cast<const f32x4*>(v)[i];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float pe = pv[r], me = mv[r], ve = vv[r];
+      adamw_elem(pe, gv[r] * gs, me, ve, lr, b1, b2, eps, wd, step_size, inv_sqrt_bc2);
+      pv[r] = pe;
+      mv[r] = me;
+      vv[r] = ve;
+    }
+    reinterpret_cast<f32x4*>(p)[i] = pv;
+    reinterpret_cast<f32x4*>(m)[i] = mv;
+    reinterpret_cast<f32x4*>(v)[i] = vv;
+  }
+  const long i = 4 * n4 + tid;
+  if (i < n) {
+    float pv = p[i], mv = m[i], vv = v[i];
+    adamw_elem(pv, g[i] * gs, mv, vv, lr, b1, b2, eps, wd, step_size, inv_sqrt_bc2);
     p[i] = pv;
     m[i] = mv;
     v[i] = vv;
@@ -202,8 +241,13 @@ int crnn_adamw(float* p, const float* g, float* m, float* v, long n, float lr, f
   double bc2 = 1.0 - pow((double)beta2, (double)step);
   float step_size = (float)((double)lr / bc1);
   float inv_sqrt_bc2 = (float)(1.0 / sqrt(bc2));
-  hipLaunchKernelGGL(adamw_kernel, dim3(grid_for(n, 256, 16384)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n, lr,
-                     beta1, beta2, eps, weight_decay, step_size, inv_sqrt_bc2, grad_scale);
+  const bool vec = ((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) % 16 == 0;
+  if (vec)
+    hipLaunchKernelGGL(adamw_kernel<true>, dim3(grid_for((n + 3) / 4, 256, 8192)), dim3(256), 0, (hipStream_t)stream,
+                       p, g, m, v, n, lr, beta1, beta2, eps, weight_decay, step_size, inv_sqrt_bc2, grad_scale);
+  else
+    hipLaunchKernelGGL(adamw_kernel<false>, dim3(grid_for(n, 256, 16384)), dim3(256), 0, (hipStream_t)stream, p, g,
+                       m, v, n, lr, beta1, beta2, eps, weight_decay, step_size, inv_sqrt_bc2, grad_scale);
   return (int)hipGetLastError();
 }
 

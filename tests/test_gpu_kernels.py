@@ -407,7 +407,9 @@ def test_greedy_decode_golden(itos):
     assert texts == ref["texts"]
 
 
-def test_adamw_vs_oracle():
+@pytest.mark.parametrize("offset", [0, 1])
+def test_adamw_vs_oracle(offset):
+    """offset 0: 16-B aligned buffers (vector kernel + n % 4 tail); 1: misaligned (scalar kernel)"""
     L = _L()
     import crnn_oracle as O
     g = torch.Generator().manual_seed(6)
@@ -415,7 +417,8 @@ def test_adamw_vs_oracle():
     p = torch.randn(n, generator=g)
     m = torch.zeros(n)
     v = torch.zeros(n)
-    pd, md, vd = p.to(DEV), m.to(DEV), v.to(DEV)
+    pd, md, vd = (torch.zeros(n + offset, device=DEV)[offset:] for _ in range(3))
+    pd.copy_(p)
     pn, mn, vn = p.double().numpy(), m.double().numpy(), v.double().numpy()
     for step in range(1, 4):
         gr = torch.randn(n, generator=g)
