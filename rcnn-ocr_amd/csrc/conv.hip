@@ -21,6 +21,8 @@ bool conv_halo_fits(const crnn_conv_desc* d, bool dgrad);
 int conv_halo_fwd(const crnn_conv_desc* d, const void* x, const void* w, void* y, float* psum, float* psq,
                   hipStream_t st);
 int conv_halo_dgrad(const crnn_conv_desc* d, const void* dy, const void* w, void* dx, hipStream_t st);
+int conv_halo_wgrad_slabs(const crnn_conv_desc* d);
+int conv_halo_wgrad(const crnn_conv_desc* d, const void* dy, const void* x, float* ws, hipStream_t st);
 static bool use_halo(int dtype, const crnn_conv_desc* d, bool dgrad) {
   return dtype == CRNN_BF16 && crnn_option(CRNN_OPT_HALO_CONV) != 0 && conv_halo_fits(d, dgrad);
 }
@@ -547,10 +549,13 @@ template <typename T> int conv_wgrad_t(const crnn_conv_desc* d, const void* dy, 
   crnn_conv_wgrad_plan(sizeof(T) == 2 ? CRNN_BF16 : CRNN_F32, d, &bm, &bn, &splits);
   size_t need = (size_t)splits * g.Co * Kp * sizeof(float);
   if (ws_bytes < need) return crnn_set_error(hipErrorInvalidValue, "conv_wgrad: workspace too small");
+  int rc = 0;
+  if (bm == 0) {  // halo-tiled direct kernel (plan: bm = bn = 0), one slab per workgroup
+    rc = conv_halo_wgrad(d, dy, x, ws, st);
+  } else {
   WgradA<T> la{(const T*)dy, g.Co, Mp, nbytes((long)Mp * g.Co, sizeof(T))};
   WgradB<T> lb{(const T*)x, g, Kp, Mp, nbytes((long)g.B * g.Hi * g.Wi * g.Ci, sizeof(T))};
   SlabEpi ep{ws, g.Co, Kp};
-  int rc = 0;
   if constexpr (sizeof(T) == 2) {
     if (bm == 256 && bn == 256) rc = launch256<256, 256>(la, lb, ep, g.Co, Kp, Mp, st, splits);
     else if (bm == 256 && bn == 128) rc = launch256<256, 128>(la, lb, ep, g.Co, Kp, Mp, st, splits);
@@ -558,6 +563,7 @@ template <typename T> int conv_wgrad_t(const crnn_conv_desc* d, const void* dy, 
   if (bm == 256) {
   } else if (bm == 128) rc = launch<T, 128, 128>(la, lb, ep, g.Co, Kp, Mp, splits, st);
   else rc = launch<T, 64, 64>(la, lb, ep, g.Co, Kp, Mp, splits, st);
+  }
   if (rc) return rc;
   int ci_real = d->Ci_real > 0 ? d->Ci_real : g.Ci;
   long total = (long)g.Co * Kp;
@@ -599,6 +605,12 @@ int crnn_conv_stat_rows(int dtype, const crnn_conv_desc* d) {
 }
 
 void crnn_conv_wgrad_plan(int dtype, const crnn_conv_desc* d, int* bm, int* bn, int* splits) {
+  if (use_halo(dtype, d, true) && d->Ci == 64) {  // conv_halo.hip: bm = bn = 0, a slab per workgroup
+    *bm = 0;
+    *bn = 0;
+    *splits = conv_halo_wgrad_slabs(d);
+    return;
+  }
   long Mp = (long)d->B * d->Ho * d->Wo;
   int Kp = d->KH * d->KW * d->Ci;
   if (dtype == CRNN_BF16 && d->Co % 256 == 0 && Kp % 128 == 0 && Mp >= 256L * 64) {

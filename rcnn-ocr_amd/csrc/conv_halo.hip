@@ -219,6 +219,147 @@ __global__ __launch_bounds__(512) void halo3x3_kernel(const bf16* __restrict__ x
   }
 }
 
+
+// ------------------------------------------------------------------------------------------------
+// Weight gradient of the same convolution, dW[co][t][ci] = sum_p dy[p][co] x[p + t][ci]: a GEMM
+// with K = pixels, M = CO, N = 9*CI. A workgroup walks whole bands (as the forward does: x rows in
+// a 4-slot ring, the band's dy row as a 128 x CO tile, both double-buffered through registers)
+// and keeps its CO x 9*CI partial in accumulators across all of them; one fp32 slab per
+// workgroup, summed by conv.hip's wgrad_reduce_kernel. Both operands stay pixel-major in LDS (NHWC
+// rows as loaded) and are read with ds_read_b64_tr_b16. The k -> pixel map of a 32-deep k-step
+// puts the two 16-lane groups of each 32-lane half on 8 CONSECUTIVE pixel rows
+// (pixel = 16(g>>1) + 8h + 4(g&1) + q for lane group g, read h, block row q), and row pitches of
+// 20 and 36 8-byte chunks (mod 32) spread any 8 consecutive rows over distinct banks — for every
+// tap shift kw, so addresses are a per-lane base plus immediates (enumerated offline).
+// Wave (mw, nw) of 8: CO/2 output channels x 9*CI/4 k' columns (144 accumulator VGPRs).
+template <int CI, int CO>
+__global__ __launch_bounds__(512) void halo3x3_wgrad_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
+                                                            float* __restrict__ ws, int B, int H, int W,
+                                                            uint32_t dybytes, uint32_t xbytes) {
+  constexpr int XROW = CI * 2 + 32, DROW = CO * 2 + 32;  // padded pixel rows (bytes)
+  static_assert((XROW / 8) % 32 == 20 && (DROW / 8) % 32 == 4, "pitches of the conflict-free map");
+  constexpr int XSLOT = (TW + 2) * XROW, DTILE = TW * DROW;
+  constexpr int KP = 9 * CI;                      // k' = (tap, ci)
+  constexpr int MW = CO / 2, NW = KP / 4;         // per-wave block
+  constexpr int MF = MW / 16, NF = NW / 16;       // fragments
+  constexpr int XCH = CI / 8, DCH = CO / 8;       // 16-B chunks per pixel
+  constexpr int NT = 512;
+  constexpr int XPER = ((TW + 2) * XCH + NT - 1) / NT, DPER = (TW * DCH + NT - 1) / NT;
+  static_assert(NW % 16 == 0 && MW % 16 == 0 && (CI % 16) == 0, "shape");
+  __shared__ __attribute__((aligned(16))) char ring[4 * XSLOT];
+  __shared__ __attribute__((aligned(16))) char dyt[2][DTILE];
+
+  const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int mw = wv & 1, nw = wv >> 1;
+  const int nxh = W / TW, nbands = B * nxh;
+  const __amdgpu_buffer_rsrc_t rx = mk_rsrc(x, xbytes), rd = mk_rsrc(dy, dybytes);
+  // transposed-read lane roles: block row q, column quad p4; pixel of (h = 0, q) within a k-step
+  const int q = c >> 2, p4 = c & 3;
+  const int prow = 16 * (g >> 1) + 4 * (g & 1) + q;
+  const uint32_t dbase = (uint32_t)(prow * DROW + (mw * MW + 4 * p4) * 2);
+  const uint32_t xbase = (uint32_t)(prow * XROW + 4 * p4 * 2);
+
+  f32x4 acc[MF][NF];
+#pragma unroll
+  for (int i = 0; i < MF; ++i)
+#pragma unroll
+    for (int j = 0; j < NF; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  u32x4 xpre[XPER], dpre[DPER];
+  int b = 0, x0 = 0;
+  auto load_x = [&](int r) {
+#pragma unroll
+    for (int i = 0; i < XPER; ++i) {
+      const int e = threadIdx.x + NT * i, px = e / XCH, ch = e % XCH;
+      const int xc = x0 - 1 + px;
+      const bool ok = e < (TW + 2) * XCH && r >= 0 && r < H && xc >= 0 && xc < W;
+      xpre[i] = __builtin_amdgcn_raw_buffer_load_b128(rx, ok ? ((((uint32_t)b * H + r) * W + xc) * CI + ch * 8) * 2u : OOB, 0, 0);
+    }
+  };
+  auto store_x = [&](int r) {
+    char* s = ring + ((r + 1) & 3) * XSLOT;
+#pragma unroll
+    for (int i = 0; i < XPER; ++i) {
+      const int e = threadIdx.x + NT * i, px = e / XCH, ch = e % XCH;
+      if (e < (TW + 2) * XCH) *reinterpret_cast<u32x4*>(s + px * XROW + ch * 16) = xpre[i];
+    }
+  };
+  auto load_d = [&](int r) {
+#pragma unroll
+    for (int i = 0; i < DPER; ++i) {
+      const int e = threadIdx.x + NT * i, px = e / DCH, ch = e % DCH;
+      const bool ok = e < TW * DCH && r < H;
+      dpre[i] = __builtin_amdgcn_raw_buffer_load_b128(rd, ok ? ((((uint32_t)b * H + r) * W + x0 + px) * CO + ch * 8) * 2u : OOB, 0, 0);
+    }
+  };
+  auto store_d = [&](int r) {
+    char* s = dyt[r & 1];
+#pragma unroll
+    for (int i = 0; i < DPER; ++i) {
+      const int e = threadIdx.x + NT * i, px = e / DCH, ch = e % DCH;
+      if (e < TW * DCH) *reinterpret_cast<u32x4*>(s + px * DROW + ch * 16) = dpre[i];
+    }
+  };
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+  for (int band = blockIdx.x; band < nbands; band += gridDim.x) {
+    b = band / nxh;
+    x0 = (band - b * nxh) * TW;
+    load_x(-1);
+    store_x(-1);
+    load_x(0);
+    store_x(0);
+    load_x(1);
+    store_x(1);
+    load_d(0);
+    store_d(0);
+    __syncthreads();
+    for (int yy = 0; yy < H; ++yy) {
+      load_x(yy + 2);
+      load_d(yy + 1);
+      const char* dt = dyt[yy & 1] + dbase;
+      const char* sl[3];
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh) sl[kh] = ring + ((yy + kh) & 3) * XSLOT + xbase;
+#pragma unroll
+      for (int ks = 0; ks < TW / 32; ++ks) {
+        bf16x8 xa[MF];
+#pragma unroll
+        for (int i = 0; i < MF; ++i) {
+          const char* pa = dt + ks * 32 * DROW + i * 32;
+          s16x4 t2[2] = {__builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(pa)),
+                         __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(pa + 8 * DROW))};
+          xa[i] = *reinterpret_cast<const bf16x8*>(t2);
+        }
+#pragma unroll
+        for (int j = 0; j < NF; ++j) {
+          const int f = nw * NF + j, t = f / (CI / 16), ci0 = (f % (CI / 16)) * 16;
+          const int kh = t / 3, kw = t % 3;
+          const char* pb = sl[kh] + (ks * 32 + kw) * XROW + ci0 * 2;
+          s16x4 t2[2] = {__builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(pb)),
+                         __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(pb + 8 * XROW))};
+          const bf16x8 yb = *reinterpret_cast<const bf16x8*>(t2);
+#pragma unroll
+          for (int i = 0; i < MF; ++i) mma<bf16>(acc[i][j], xa[i], yb);
+        }
+      }
+      store_x(yy + 2);
+      store_d(yy + 1);
+      __syncthreads();
+    }
+  }
+  // slab [blockIdx.x][CO][KP]: lane (c, g) of fragment (i, j) holds rows co = 4g + r, column k' = c
+  float* slab = ws + (size_t)blockIdx.x * CO * KP;
+#pragma unroll
+  for (int i = 0; i < MF; ++i)
+#pragma unroll
+    for (int j = 0; j < NF; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        slab[(size_t)(mw * MW + 16 * i + 4 * g + r) * KP + nw * NW + 16 * j + c] = acc[i][j][r];
+}
+
 }  // namespace
 
 // conv.hip dispatch: the halo kernel covers 3x3 / stride 1 / pad 1 convolutions whose width is a
@@ -263,5 +404,22 @@ int conv_halo_dgrad(const crnn_conv_desc* d, const void* dy, const void* w, void
   const uint32_t dybytes = (uint32_t)((size_t)d->B * d->Ho * d->Wo * d->Co * 2);
   hipLaunchKernelGGL((halo3x3_kernel<128, 64, true>), grid, dim3(512), 0, st, (const bf16*)dy, (const bf16*)w,
                      (bf16*)dx, (float*)nullptr, (float*)nullptr, d->Hi, d->Wi, d->Hi, dybytes);
+  return (int)hipGetLastError();
+}
+
+// stem wgrad on the halo kernel: grid = slabs = min(bands, CUs)
+int conv_halo_wgrad_slabs(const crnn_conv_desc* d) {
+  const int bands = d->B * (d->Wi / TW);
+  int ncu = crnn_cu_count();
+  if (ncu <= 0) ncu = 256;
+  return bands < ncu ? bands : ncu;
+}
+
+int conv_halo_wgrad(const crnn_conv_desc* d, const void* dy, const void* x, float* ws, hipStream_t st) {
+  const int S = conv_halo_wgrad_slabs(d);
+  const uint32_t dybytes = (uint32_t)((size_t)d->B * d->Ho * d->Wo * d->Co * 2);
+  const uint32_t xbytes = (uint32_t)((size_t)d->B * d->Hi * d->Wi * d->Ci * 2);
+  hipLaunchKernelGGL((halo3x3_wgrad_kernel<64, 128>), dim3(S), dim3(512), 0, st, (const bf16*)dy, (const bf16*)x, ws,
+                     d->B, d->Hi, d->Wi, dybytes, xbytes);
   return (int)hipGetLastError();
 }

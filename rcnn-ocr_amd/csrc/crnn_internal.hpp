@@ -7,6 +7,8 @@
 int crnn_set_error(int code, const char* msg);
 // crnn_set_option() values (capi.cpp)
 int crnn_option(int key);
+// compute units of the current device (capi.cpp, cached)
+int crnn_cu_count();
 
 inline int grid_for(long n, int block = 256, int cap = 8192) {
   long g = (n + block - 1) / block;

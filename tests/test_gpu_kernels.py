@@ -131,9 +131,9 @@ def test_conv_fwd_dgrad_wgrad(cfg, dtype):
 
 
 def test_conv_halo_vs_gemm():
-    """The stem conv (64 -> 128, 3x3, 32x256) on the halo kernel and on the implicit GEMM
-    (CRNN_OPT_HALO_CONV = 0) of the same inputs: outputs, BN partial statistics and dx agree to
-    fp32 summation order (bf16 outputs: within one rounding step)."""
+    """The stem conv (64 -> 128, 3x3, 32x256) on the halo kernels and on the implicit GEMM
+    (CRNN_OPT_HALO_CONV = 0) of the same inputs: outputs, BN partial statistics, dx and dW agree
+    to fp32 summation order (bf16 outputs: within one rounding step)."""
     L = _L()
     B, Ci, H, W, Co = 8, 64, 32, 256, 128
     g = torch.Generator().manual_seed(5)
@@ -157,20 +157,25 @@ def test_conv_halo_vs_gemm():
             L.call("crnn_conv_fwd", dt, d, x.data_ptr(), wd.data_ptr(), y.data_ptr(), ps.data_ptr(), pq.data_ptr(), st)
             dx = torch.empty(B, H, W, Ci, dtype=torch.bfloat16, device=DEV)
             L.call("crnn_conv_dgrad", dt, d, dy.data_ptr(), wd.data_ptr(), dx.data_ptr(), None, None, 0, st)
+            need = L.lib().crnn_conv_wgrad_workspace(dt, d)
+            wsb = torch.empty(need // 4 + 1, device=DEV)
+            dw = torch.full((Co, Ci, 3, 3), 0.25, device=DEV)
+            L.call("crnn_conv_wgrad", dt, d, dy.data_ptr(), x.data_ptr(), dw.data_ptr(), wsb.data_ptr(), need, 1.0, st)
             torch.cuda.synchronize()
             M = B * H * W
             n = rpp
             mean = ps.double().sum(0) / M
             var = (pq.double().sum(0) + (n * (ps.double() / n - mean) ** 2).sum(0)) / M
-            out[opt] = (y.float(), mean, var, dx.float(), rows, rpp)
+            out[opt] = (y.float(), mean, var, dx.float(), rows, rpp, dw.clone())
         finally:
             L.call("crnn_set_option", L.OPT_HALO_CONV, 1)
-    (y1, m1, v1, dx1, r1, p1), (y0, m0, v0, dx0, r0, p0) = out[1], out[0]
+    (y1, m1, v1, dx1, r1, p1, w1), (y0, m0, v0, dx0, r0, p0, w0) = out[1], out[0]
     assert r1 * p1 == r0 * p0 == B * H * W
     assert float((y1 - y0).abs().max()) <= 2 ** -7 * float(y0.abs().max())
     assert relerr(y1, y0) < 2e-3
     assert relerr(m1, m0) < 1e-5 and relerr(v1, v0) < 1e-5
     assert relerr(dx1, dx0) < 2e-3
+    assert relerr(w1, w0) < 1e-5   # fp32 accumulation both ways (beta = 1 keeps the 0.25 start)
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
