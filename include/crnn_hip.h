@@ -174,6 +174,11 @@ int crnn_bn_rows(long M); /* partial rows used by the reduce kernels for M */
 /* ------------------------------------------------------------------ SE + residual */
 /* pooled[b][c] = mean_hw(z2*scale+shift) */
 int crnn_se_pool(int dtype, const void* z2, const float* scale, const float* shift, float* pooled, int B, int HW, int C, void* stream);
+/* the same pooled values in training mode from the SE conv's BN partial sums (crnn_conv_fwd psum,
+ * `rows` partial rows of rows_per_partial data rows): requires HW % rows_per_partial == 0 and
+ * rows * rows_per_partial == B * HW (partials tile each sample); no pass over z2 */
+int crnn_se_pool_partials(const float* psum, int rows, long rows_per_partial, const float* scale,
+                          const float* shift, float* pooled, int B, int HW, int C, void* stream);
 /* hid = relu(pooled W1^T) [B][Cr]; s = sigmoid(hid W2^T) [B][C] (fp32; W1 [Cr][C], W2 [C][Cr]) */
 int crnn_se_mlp_fwd(const float* pooled, const float* w1, const float* w2, float* hid, float* s, int B, int C, int Cr, void* stream);
 /* y = relu((z2*scale+shift)*s[b][c] + idn'), idn' = idn*iscale+ishift if iscale else idn */

@@ -147,6 +147,7 @@ class CRNNEngine:
         self.version_source = version_source
         self._saved = None
         self.debug = False      # when set, backward keeps copies of block-boundary gradients
+        self._last_partials = None  # (psum, rows, rows_per_partial) of the latest training-mode conv
         self.dbg: Dict[str, torch.Tensor] = {}
 
     # ------------------------------------------------------------------ weights
@@ -341,6 +342,7 @@ class CRNNEngine:
                             ptr(self.packed[cs.name]), ptr(z), ptr(psum), ptr(psq), s)
             rpp = L.lib().crnn_conv_stat_rows_per_partial(self.dt, d)
             stats = self._bn_finalize(cs.bn, psum, psq, rows, b * ho * wo, True, tag, rpp)
+            self._last_partials = (psum, rows, rpp)
         else:
             self._conv_call("fwd", self.conv_flops(cs, b, h, w), "crnn_conv_fwd", self.dt, d, ptr(x),
                             ptr(self.packed[cs.name]), ptr(z), None, None, s)
@@ -415,7 +417,12 @@ class CRNNEngine:
             pooled = ws.get(tag + ".pooled", (B, P), torch.float32)
             hid = ws.get(tag + ".hid", (B, Cr), torch.float32)
             se = ws.get(tag + ".s", (B, P), torch.float32)
-            call("crnn_se_pool", dt, ptr(z2), ptr(bs2), ptr(bh2), ptr(pooled), B, HW, P, s)
+            lp = self._last_partials if train else None
+            if lp is not None and HW % lp[2] == 0 and lp[1] * lp[2] == B * HW:
+                # squeeze from conv2's BN partial sums (no pass over z2)
+                call("crnn_se_pool_partials", ptr(lp[0]), lp[1], lp[2], ptr(bs2), ptr(bh2), ptr(pooled), B, HW, P, s)
+            else:
+                call("crnn_se_pool", dt, ptr(z2), ptr(bs2), ptr(bh2), ptr(pooled), B, HW, P, s)
             call("crnn_se_mlp_fwd", ptr(pooled), ptr(self.p[blk.prefix + ".se.fc.0.weight"]),
                  ptr(self.p[blk.prefix + ".se.fc.2.weight"]), ptr(hid), ptr(se), B, P, Cr, s)
             dsv = None

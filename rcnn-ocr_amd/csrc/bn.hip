@@ -1142,6 +1142,20 @@ __global__ __launch_bounds__(NT) void se_reduce_kernel(const T* __restrict__ z, 
   }
 }
 
+// SE squeeze from the conv's BatchNorm partial sums (training forward): when the partial rows
+// (rpp data rows each, conv.hip's FwdEpi / halo layout) tile every sample's HW rows exactly,
+// sum_hw z[b][c] is the sum of the sample's partial rows, so pooled = scale * that / HW + shift
+// needs no pass over z. Block per sample, thread per channel.
+__global__ void se_pool_partials_kernel(const float* __restrict__ psum, int per_b, const float* __restrict__ scale,
+                                        const float* __restrict__ shift, float* __restrict__ pooled, int HW, int C) {
+  const int b = blockIdx.x;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    float s = 0.f;
+    for (int k = 0; k < per_b; ++k) s += psum[((size_t)b * per_b + k) * C + c];
+    pooled[(size_t)b * C + c] = scale[c] * (s / (float)HW) + shift[c];
+  }
+}
+
 inline bool rowmap_ok(int C) { return C % 8 == 0 && C / 8 <= NT && NT % (C / 8) == 0; }
 
 // blocks for a row-streaming launch: enough to fill the chip, each a contiguous row chunk
@@ -1306,6 +1320,15 @@ int crnn_se_pool(int dtype, const void* z2, const float* scale, const float* shi
   DISPATCH(dtype, hipLaunchKernelGGL((se_reduce_kernel<T, 0>), dim3(B), dim3(NT), sm, (hipStream_t)stream,
                                      (const T*)z2, scale, shift, (const T*)nullptr, (const T*)nullptr, HW, C, pooled,
                                      1.f / (float)HW));
+  return (int)hipGetLastError();
+}
+
+int crnn_se_pool_partials(const float* psum, int rows, long rows_per_partial, const float* scale,
+                          const float* shift, float* pooled, int B, int HW, int C, void* stream) {
+  if (rows_per_partial <= 0 || HW % rows_per_partial || (long)rows * rows_per_partial != (long)B * HW)
+    return crnn_set_error(hipErrorInvalidValue, "se_pool_partials: partial rows must tile every sample");
+  hipLaunchKernelGGL(se_pool_partials_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, psum,
+                     (int)(HW / rows_per_partial), scale, shift, pooled, HW, C);
   return (int)hipGetLastError();
 }
 

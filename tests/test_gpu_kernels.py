@@ -178,6 +178,33 @@ def test_conv_halo_vs_gemm():
     assert relerr(w1, w0) < 1e-5   # fp32 accumulation both ways (beta = 1 keeps the 0.25 start)
 
 
+@pytest.mark.parametrize("hw", [(8, 64), (4, 32)])
+def test_se_pool_from_partials(hw):
+    """The SE squeeze from the conv's BN partial sums equals the pass over z2 (bf16 z2 rounding)."""
+    L = _L()
+    H, W = hw
+    B, C = 16, 256
+    g = torch.Generator().manual_seed(8)
+    x = torch.randn(B, H, W, C, generator=g).to(DEV, torch.bfloat16)
+    w = (torch.randn(C, C, 3, 3, generator=g) / 48).to(DEV)
+    dt, st = L.BF16, L.stream_ptr()
+    d = L.ConvDesc(B, H, W, C, H, W, C, 3, 3, 1, 1, 1, 1, C)
+    wd = torch.empty(C, 3, 3, C, dtype=torch.bfloat16, device=DEV)
+    L.call("crnn_pack_conv_weight", dt, w.data_ptr(), wd.data_ptr(), C, C, 3, 3, C, st)
+    rows, rpp = L.lib().crnn_conv_stat_rows(dt, d), L.lib().crnn_conv_stat_rows_per_partial(dt, d)
+    z = torch.empty(B, H, W, C, dtype=torch.bfloat16, device=DEV)
+    ps, pq = torch.empty(rows, C, device=DEV), torch.empty(rows, C, device=DEV)
+    L.call("crnn_conv_fwd", dt, d, x.data_ptr(), wd.data_ptr(), z.data_ptr(), ps.data_ptr(), pq.data_ptr(), st)
+    sc = torch.rand(C, generator=g).to(DEV) + 0.5
+    sh = torch.randn(C, generator=g).to(DEV)
+    p0, p1 = torch.empty(B, C, device=DEV), torch.empty(B, C, device=DEV)
+    L.call("crnn_se_pool", dt, z.data_ptr(), sc.data_ptr(), sh.data_ptr(), p0.data_ptr(), B, H * W, C, st)
+    L.call("crnn_se_pool_partials", ps.data_ptr(), rows, rpp, sc.data_ptr(), sh.data_ptr(), p1.data_ptr(), B,
+           H * W, C, st)
+    torch.cuda.synchronize()
+    assert relerr(p1, p0) < 2e-3
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("mnk", [(37, 50, 64), (256, 194, 512), (304, 1024, 256), (8, 16, 8), (200, 512, 8192),
                                  (512, 1024, 4096)])
