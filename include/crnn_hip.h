@@ -187,6 +187,18 @@ int crnn_se_residual_fwd(int dtype, const void* z2, const float* scale, const fl
 /* ds[b][c] = sum_hw dy*(y>0)*(z2*scale+shift) */
 int crnn_se_bwd_reduce(int dtype, const void* dy, const void* y, const void* z2, const float* scale, const float* shift,
                        float* ds, int B, int HW, int C, void* stream);
+/* SE block backward, one pass over (dy, y, z2) for both reductions (per sample b, channel c):
+ *   dy_m = dy * (y > 0), xhat = (z2 - mean) * invstd
+ *   abc[b][0][c] = sum_hw dy_m, abc[b][1][c] = sum_hw dy_m xhat, abc[b][2][c] = sum_hw xhat
+ *   ds[b][c] = sum_hw dy_m (z2 scale + shift) = gamma abc[1] + beta abc[0]
+ * crnn_se_bn_partials then gives the CRNN_BNG_SE BatchNorm sums as B partial rows for
+ * crnn_bn_bwd_finalize (rows = B): pg = s abc[0] + HW dpool, pgx = s abc[1] + dpool abc[2] —
+ * the same quantities crnn_bn_bwd_reduce computes with a second pass. */
+int crnn_se_bn_bwd_reduce(int dtype, const void* dy, const void* y, const void* z2, const float* mean,
+                          const float* invstd, const float* gamma, const float* beta, float* ds, float* abc, int B,
+                          int HW, int C, void* stream);
+int crnn_se_bn_partials(const float* abc, const float* s, const float* dpool, float* pg, float* pgx, int B, int HW,
+                        int C, void* stream);
 /* SE MLP backward: dsig, dhid (work [B][C] and [B][Cr]), dpool = W1^T dhid / HW; dw1/dw2 (fp32, written) */
 int crnn_se_mlp_bwd(const float* ds, const float* pooled, const float* hid, const float* s, const float* w1, const float* w2,
                     float* dsig, float* dhid, float* dpool, float* dw1, float* dw2, int B, int C, int Cr, int HW, int accumulate,

@@ -75,6 +75,8 @@ _SIGS = {
     "crnn_bn_rows": ([i64], i32),
     "crnn_se_pool": ([i32, vp, vp, vp, vp, i32, i32, i32, vp], i32),
     "crnn_se_pool_partials": ([vp, i32, i64, vp, vp, vp, i32, i32, i32, vp], i32),
+    "crnn_se_bn_bwd_reduce": ([i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, vp], i32),
+    "crnn_se_bn_partials": ([vp, vp, vp, vp, vp, i32, i32, i32, vp], i32),
     "crnn_se_mlp_fwd": ([vp, vp, vp, vp, vp, i32, i32, i32, vp], i32),
     "crnn_se_residual_fwd": ([i32, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, vp], i32),
     "crnn_se_bwd_reduce": ([i32, vp, vp, vp, vp, vp, vp, i32, i32, i32, vp], i32),

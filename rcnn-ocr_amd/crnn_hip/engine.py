@@ -513,16 +513,26 @@ class CRNNEngine:
 
     # ------------------------------------------------------------------ backward
     def _bn_bwd(self, mode, dy, z, stats, prefix, M, C, HW=1, y=None, se=None, dpool=None, out=None,
-                accumulate_params=False):
+                accumulate_params=False, se_abc=None):
+        """BN backward: per-channel sums of g (mode, crnn_hip.h CRNN_BNG_*) -> finalize -> apply.
+        se_abc = (abc, B): the SE mode's sums come from crnn_se_bn_bwd_reduce's per-sample terms
+        (no second pass over the tensor)."""
         mean, inv, sc, sh = stats
         ws = self.ws
         s = L.stream_ptr()
         d = BnBwdDesc(ptr(dy), ptr(z), ptr(mean), ptr(inv), ptr(sc), ptr(sh), ptr(y), ptr(se), ptr(dpool), mode,
                       M, C, HW)
-        rows = L.lib().crnn_bn_rows(M)
-        pg = ws.get("bnb.pg", (1024 * 512,), torch.float32)[: rows * C]
-        pgx = ws.get("bnb.pgx", (1024 * 512,), torch.float32)[: rows * C]
-        call("crnn_bn_bwd_reduce", self.dt, d, ptr(pg), ptr(pgx), rows, s)
+        if se_abc is not None:
+            abc, B = se_abc
+            rows = B
+            pg = ws.get("bnb.pg", (1024 * 512,), torch.float32)[: rows * C]
+            pgx = ws.get("bnb.pgx", (1024 * 512,), torch.float32)[: rows * C]
+            call("crnn_se_bn_partials", ptr(abc), ptr(se), ptr(dpool), ptr(pg), ptr(pgx), B, HW, C, s)
+        else:
+            rows = L.lib().crnn_bn_rows(M)
+            pg = ws.get("bnb.pg", (1024 * 512,), torch.float32)[: rows * C]
+            pgx = ws.get("bnb.pgx", (1024 * 512,), torch.float32)[: rows * C]
+            call("crnn_bn_bwd_reduce", self.dt, d, ptr(pg), ptr(pgx), rows, s)
         mg = ws.get("bnb.mg", (512,), torch.float32)
         mgx = ws.get("bnb.mgx", (512,), torch.float32)
         call("crnn_bn_bwd_finalize", ptr(pg), ptr(pgx), rows, C, M, ptr(self.g[prefix + ".weight"]),
@@ -683,8 +693,11 @@ class CRNNEngine:
             if self.debug:
                 self.dbg[f"dy.b{bi}"] = dyb.clone().view(B, ho, wo, P)
             ds = ws.get(f"se.ds{P}", (B, P), torch.float32)
-            call("crnn_se_bwd_reduce", dt, ptr(dyb), ptr(sb["y"]), ptr(sb["z2"]), ptr(sb["sc2"]), ptr(sb["sh2"]),
-                 ptr(ds), B, HW, P, s)
+            abc = ws.get(f"se.abc{P}", (B, 3, P), torch.float32)
+            bn2 = blk.conv2.bn
+            # one pass over (dy, y, z2) for the SE gate gradient AND the BN2 sums (crnn_hip.h)
+            call("crnn_se_bn_bwd_reduce", dt, ptr(dyb), ptr(sb["y"]), ptr(sb["z2"]), ptr(sb["m2"]), ptr(sb["i2"]),
+                 ptr(self.p[bn2 + ".weight"]), ptr(self.p[bn2 + ".bias"]), ptr(ds), ptr(abc), B, HW, P, s)
             dsig = ws.get(f"se.dsig{P}", (B, P), torch.float32)
             dhid = ws.get(f"se.dhid{P}", (B, Cr), torch.float32)
             dpool = ws.get(f"se.dpool{P}", (B, P), torch.float32)
@@ -694,7 +707,8 @@ class CRNNEngine:
                  ptr(self._gview(blk.prefix + ".se.fc.2.weight")), B, P, Cr, HW, acc, s)
             dz2 = bufs[o1][: Mo * P]
             self._bn_bwd(3, dyb, sb["z2"], (sb["m2"], sb["i2"], sb["sc2"], sb["sh2"]), blk.conv2.bn, Mo, P, HW=HW,
-                         y=sb["y"], se=sb["s"], dpool=dpool, out=dz2, accumulate_params=accumulate)
+                         y=sb["y"], se=sb["s"], dpool=dpool, out=dz2, accumulate_params=accumulate,
+                         se_abc=(abc, B))
             self._wgrad(blk.conv2, dz2, sb["a1"], B, ho, wo)
             da1 = bufs[o2][: Mo * P]
             self._conv_call("dgrad", self.conv_flops(blk.conv2, B, ho, wo), "crnn_conv_dgrad", dt, blk.conv2.desc(B, ho, wo), ptr(dz2), ptr(self.packed[blk.conv2.name]),

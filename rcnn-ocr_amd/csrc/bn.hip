@@ -1156,6 +1156,76 @@ __global__ void se_pool_partials_kernel(const float* __restrict__ psum, int per_
   }
 }
 
+// SE block backward, one pass for both reductions over the tensor (block per sample b):
+//   dy_m = dy * (y > 0), xhat = (z - mean) * invstd
+//   A = sum_hw dy_m, Bx = sum_hw dy_m xhat, Cx = sum_hw xhat        -> abc[b][3][C]
+//   ds[b][c] = sum_hw dy_m (z scale + shift) = gamma Bx + beta A     (the SE gate gradient)
+// The BN sums of g = dy_m s + dpool (CRNN_BNG_SE) then follow per sample without a second pass
+// (se_bn_partials_kernel): sum g = s A + HW dpool, sum g xhat = s Bx + dpool Cx.
+template <typename T>
+__global__ __launch_bounds__(NT) void se_bn_bwd_reduce_kernel(const T* __restrict__ dy, const T* __restrict__ y,
+                                                              const T* __restrict__ z, const float* __restrict__ meanp,
+                                                              const float* __restrict__ invp,
+                                                              const float* __restrict__ gamma,
+                                                              const float* __restrict__ beta, int HW, int C,
+                                                              float* __restrict__ ds, float* __restrict__ abc) {
+  extern __shared__ float red[];  // [3][rl][C]
+  const RowMap q = rowmap(C);
+  const int b = blockIdx.x;
+  float mean[8], inv[8], a[8], bx[8], cx[8];
+  ld8f(meanp + q.c8, mean);
+  ld8f(invp + q.c8, inv);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) a[i] = bx[i] = cx[i] = 0.f;
+  for (int hw = q.r; hw < HW; hw += q.rl) {
+    const size_t o = ((size_t)b * HW + hw) * C + q.c8;
+    float zz[8], dd[8], yy[8];
+    unpack8<T>(ld8<T>(z + o), zz);
+    unpack8<T>(ld8<T>(dy + o), dd);
+    unpack8<T>(ld8<T>(y + o), yy);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float xh = (zz[i] - mean[i]) * inv[i];
+      const float dm = yy[i] > 0.f ? dd[i] : 0.f;
+      a[i] += dm;
+      bx[i] += dm * xh;
+      cx[i] += xh;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    red[q.r * C + q.c8 + i] = a[i];
+    red[(q.rl + q.r) * C + q.c8 + i] = bx[i];
+    red[(2 * q.rl + q.r) * C + q.c8 + i] = cx[i];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += NT) {
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+    for (int k = 0; k < q.rl; ++k) {
+      s0 += red[k * C + c];
+      s1 += red[(q.rl + k) * C + c];
+      s2 += red[(2 * q.rl + k) * C + c];
+    }
+    float* o = abc + (size_t)b * 3 * C;
+    o[c] = s0;
+    o[C + c] = s1;
+    o[2 * C + c] = s2;
+    ds[(size_t)b * C + c] = gamma[c] * s1 + beta[c] * s0;
+  }
+}
+
+__global__ void se_bn_partials_kernel(const float* __restrict__ abc, const float* __restrict__ sg,
+                                      const float* __restrict__ dpool, int HW, int C, float* __restrict__ p0,
+                                      float* __restrict__ p1) {
+  const int b = blockIdx.x;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    const float* o = abc + (size_t)b * 3 * C;
+    const float sv = sg[(size_t)b * C + c], dp = dpool[(size_t)b * C + c];
+    p0[(size_t)b * C + c] = sv * o[c] + (float)HW * dp;
+    p1[(size_t)b * C + c] = sv * o[C + c] + dp * o[2 * C + c];
+  }
+}
+
 inline bool rowmap_ok(int C) { return C % 8 == 0 && C / 8 <= NT && NT % (C / 8) == 0; }
 
 // blocks for a row-streaming launch: enough to fill the chip, each a contiguous row chunk
@@ -1329,6 +1399,24 @@ int crnn_se_pool_partials(const float* psum, int rows, long rows_per_partial, co
     return crnn_set_error(hipErrorInvalidValue, "se_pool_partials: partial rows must tile every sample");
   hipLaunchKernelGGL(se_pool_partials_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, psum,
                      (int)(HW / rows_per_partial), scale, shift, pooled, HW, C);
+  return (int)hipGetLastError();
+}
+
+int crnn_se_bn_bwd_reduce(int dtype, const void* dy, const void* y, const void* z2, const float* mean,
+                          const float* invstd, const float* gamma, const float* beta, float* ds, float* abc, int B,
+                          int HW, int C, void* stream) {
+  if (!rowmap_ok(C)) return crnn_set_error(hipErrorInvalidValue, "se_bn_bwd_reduce: C/8 must divide 256");
+  size_t sm = (size_t)3 * (NT / (C / 8)) * C * sizeof(float);
+  DISPATCH(dtype, hipLaunchKernelGGL((se_bn_bwd_reduce_kernel<T>), dim3(B), dim3(NT), sm, (hipStream_t)stream,
+                                     (const T*)dy, (const T*)y, (const T*)z2, mean, invstd, gamma, beta, HW, C, ds,
+                                     abc));
+  return (int)hipGetLastError();
+}
+
+int crnn_se_bn_partials(const float* abc, const float* s, const float* dpool, float* pg, float* pgx, int B, int HW,
+                        int C, void* stream) {
+  hipLaunchKernelGGL(se_bn_partials_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, abc, s, dpool, HW, C, pg,
+                     pgx);
   return (int)hipGetLastError();
 }
 

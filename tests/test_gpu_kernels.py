@@ -178,6 +178,58 @@ def test_conv_halo_vs_gemm():
     assert relerr(w1, w0) < 1e-5   # fp32 accumulation both ways (beta = 1 keeps the 0.25 start)
 
 
+@pytest.mark.parametrize("BHWC", [(6, 40, 256), (5, 128, 512)])
+def test_se_bn_bwd_fused_reduce(BHWC):
+    """crnn_se_bn_bwd_reduce + crnn_se_bn_partials == crnn_se_bwd_reduce + crnn_bn_bwd_reduce
+    (CRNN_BNG_SE) through crnn_bn_bwd_finalize: ds, mean_g, mean_gx, dgamma, dbeta."""
+    L = _L()
+    B, HW, C = BHWC
+    g = torch.Generator().manual_seed(9)
+    M = B * HW
+    T = torch.bfloat16
+    dy = torch.randn(M, C, generator=g).to(DEV, T)
+    y = torch.randn(M, C, generator=g).to(DEV, T)
+    z = (torch.randn(M, C, generator=g) * 2 + 0.5).to(DEV, T)
+    zf = z.float()
+    mean = zf.mean(0)
+    inv = 1 / (zf.var(0, unbiased=False) + 1e-5).sqrt()
+    gamma = (torch.rand(C, generator=g) + 0.5).to(DEV)
+    beta = torch.randn(C, generator=g).to(DEV)
+    sc = gamma * inv
+    sh = beta - mean * sc
+    sg = torch.rand(B, C, generator=g).to(DEV)
+    dpool = (torch.randn(B, C, generator=g) * 1e-2).to(DEV)
+    st = L.stream_ptr()
+    fws = torch.zeros((L.lib().crnn_bn_finalize_workspace(512) + 3) // 4, device=DEV)
+    res = []
+    for fused in (False, True):
+        ds = torch.empty(B, C, device=DEV)
+        mg, mgx = torch.empty(C, device=DEV), torch.empty(C, device=DEV)
+        dga, dbe = torch.empty(C, device=DEV), torch.empty(C, device=DEV)
+        if fused:
+            abc = torch.empty(B, 3, C, device=DEV)
+            L.call("crnn_se_bn_bwd_reduce", L.BF16, dy.data_ptr(), y.data_ptr(), z.data_ptr(), mean.data_ptr(),
+                   inv.data_ptr(), gamma.data_ptr(), beta.data_ptr(), ds.data_ptr(), abc.data_ptr(), B, HW, C, st)
+            rows = B
+            pg, pgx = torch.empty(rows, C, device=DEV), torch.empty(rows, C, device=DEV)
+            L.call("crnn_se_bn_partials", abc.data_ptr(), sg.data_ptr(), dpool.data_ptr(), pg.data_ptr(),
+                   pgx.data_ptr(), B, HW, C, st)
+        else:
+            L.call("crnn_se_bwd_reduce", L.BF16, dy.data_ptr(), y.data_ptr(), z.data_ptr(), sc.data_ptr(),
+                   sh.data_ptr(), ds.data_ptr(), B, HW, C, st)
+            d = L.BnBwdDesc(dy.data_ptr(), z.data_ptr(), mean.data_ptr(), inv.data_ptr(), sc.data_ptr(), sh.data_ptr(),
+                            y.data_ptr(), sg.data_ptr(), dpool.data_ptr(), 3, M, C, HW)
+            rows = L.lib().crnn_bn_rows(M)
+            pg, pgx = torch.empty(rows, C, device=DEV), torch.empty(rows, C, device=DEV)
+            L.call("crnn_bn_bwd_reduce", L.BF16, d, pg.data_ptr(), pgx.data_ptr(), rows, st)
+        L.call("crnn_bn_bwd_finalize", pg.data_ptr(), pgx.data_ptr(), rows, C, M, dga.data_ptr(), dbe.data_ptr(),
+               mg.data_ptr(), mgx.data_ptr(), 0, fws.data_ptr(), st)
+        torch.cuda.synchronize()
+        res.append((ds.clone(), mg.clone(), mgx.clone(), dga.clone(), dbe.clone()))
+    for a, b in zip(res[0], res[1]):
+        assert relerr(b, a) < 1e-4
+
+
 @pytest.mark.parametrize("hw", [(8, 64), (4, 32)])
 def test_se_pool_from_partials(hw):
     """The SE squeeze from the conv's BN partial sums equals the pass over z2 (bf16 z2 rounding)."""
