@@ -170,7 +170,7 @@ def main():
     def step():
         if args.mode == "infer":
             return infer_step()
-        eng.forward(x, train=True, save_for_backward=True)
+        eng.forward(x, train=True, save_for_backward=True, dropout_p=model.enc_dropout.p)
         loss, dl = eng.ctc(eng.logits_padded(), tg, tl)
         eng.backward(dl, grads, accumulate=False, stage_done=reducer.ready if reducer else None)
         if reducer is not None:

@@ -65,6 +65,11 @@ int crnn_set_option(int key, int value);
 int crnn_nchw_to_nhwc(int dtype, const float* x, void* y, int B, int C, int H, int W, int Cp, void* stream);
 /* fp32 -> dtype cast of n contiguous elements. */
 int crnn_cast_f32(int dtype, const float* src, void* dst, long n, void* stream);
+/* dropout (reference: model/model.py:201,220 nn.Dropout(enc_dropout_p) on the encoder output):
+ * y[i] = x[i] / (1 - p) if hash(seed, i) >= p * 2^32 else 0 (in place allowed). The mask is a
+ * function of (seed, i) only, so the backward is the same call on dy with the same seed. Not
+ * torch's Philox stream: masks agree in distribution, not bit for bit. p in [0, 1). */
+int crnn_dropout(int dtype, const void* x, void* y, long n, float p, unsigned long long seed, void* stream);
 /* conv weight OIHW fp32 -> OHWI dtype with Ci zero-padded to Cip. */
 int crnn_pack_conv_weight(int dtype, const float* w, void* out, int Co, int Ci, int KH, int KW, int Cip, void* stream);
 /* row gather + cast: out[r][c] = src[perm[r]][c] (perm == NULL: identity), rows >= rows_src are zero.

@@ -55,6 +55,7 @@ _SIGS = {
     "crnn_last_error_string": ([], C.c_char_p),
     "crnn_nchw_to_nhwc": ([i32, vp, vp, i32, i32, i32, i32, i32, vp], i32),
     "crnn_cast_f32": ([i32, vp, vp, i64, vp], i32),
+    "crnn_dropout": ([i32, vp, vp, i64, f32, C.c_ulonglong, vp], i32),
     "crnn_pack_conv_weight": ([i32, vp, vp, i32, i32, i32, i32, i32, vp], i32),
     "crnn_pack_rows": ([i32, vp, vp, vp, i32, i32, i32, vp], i32),
     "crnn_conv_fwd": ([i32, C.POINTER(ConvDesc), vp, vp, vp, vp, vp, vp], i32),

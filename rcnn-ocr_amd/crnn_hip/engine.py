@@ -148,6 +148,8 @@ class CRNNEngine:
         self._saved = None
         self.debug = False      # when set, backward keeps copies of block-boundary gradients
         self._last_partials = None  # (psum, rows, rows_per_partial) of the latest training-mode conv
+        self._drop_seed = int(torch.initial_seed()) & 0xFFFFFFFFFFFFFFFF  # enc_dropout mask stream
+        self._drop_calls = 0
         self.dbg: Dict[str, torch.Tensor] = {}
 
     # ------------------------------------------------------------------ weights
@@ -374,8 +376,10 @@ class CRNNEngine:
 
     # ------------------------------------------------------------------ forward
     def forward(self, images: torch.Tensor, train: bool, update_running: bool = True,
-                save_for_backward: bool = False) -> torch.Tensor:
-        """images [B,3,H,W] fp32 (reference NCHW input) -> logits [B,T,C] fp32 (view)."""
+                save_for_backward: bool = False, dropout_p: float = 0.0) -> torch.Tensor:
+        """images [B,3,H,W] fp32 (reference NCHW input) -> logits [B,T,C] fp32 (view).
+        dropout_p: enc_dropout probability applied to the encoder output in training
+        (model/model.py:201,220); counter-based mask, regenerated in backward (crnn_dropout)."""
         L.require_device(images)
         self.pack()
         self.update_running = update_running
@@ -480,7 +484,16 @@ class CRNNEngine:
             rnn_saved.append(dict(x=xin, hseq=hseq, gates=gsv, c=csv, out=out))
             xin = out
         sv["rnn"] = rnn_saved
-        # enc_dropout (model/model.py:201,220): identity in eval; p=0 supported in train
+        # enc_dropout (model/model.py:201,220): identity in eval; in training a counter-based mask
+        # (crnn_dropout) whose seed is saved so the backward regenerates it
+        sv["drop"] = None
+        if train and dropout_p > 0.0:
+            self._drop_calls += 1
+            seed = (self._drop_seed + 0x9E3779B97F4A7C15 * self._drop_calls) & 0xFFFFFFFFFFFFFFFF
+            xdr = ws.get("enc.drop", (B, Tn, Hd), T)
+            call("crnn_dropout", dt, ptr(xin), ptr(xdr), B * Tn * Hd, float(dropout_p), seed, s)
+            sv["drop"] = (float(dropout_p), seed)
+            xin = xdr
         # CTC head
         logits = ws.get("logits", (B, Tn, self.Cpad), torch.float32)
         call("crnn_gemm_nt", dt, ptr(xin), Hd, ptr(self.packed["head.w"]), Hd, ptr(logits), self.Cpad,
@@ -603,6 +616,8 @@ class CRNNEngine:
         dx = ws.get("rnn.dx_head", (B, Tn, Hd), T)
         call("crnn_gemm_nn", dt, ptr(dlT), self.Cpad, ptr(self.packed["head.w"]), Hd, ptr(dx), Hd, M, Hd,
              self.Cpad, 0, 0, s)
+        if sv["drop"] is not None:  # enc_dropout backward: the forward's mask, from its seed
+            call("crnn_dropout", dt, ptr(dx), ptr(dx), M * Hd, sv["drop"][0], sv["drop"][1], s)
         # ---- BiLSTM stack, reverse
         for l in reversed(range(self.nl)):
             pre = f"enc_rnn.{l}"

@@ -46,7 +46,8 @@ class _EncodeFn(torch.autograd.Function):
     def forward(ctx, anchor, images, model, need_grad):
         eng = model._engine_for(images)
         logits = eng.forward(images, train=model.training, save_for_backward=need_grad,
-                             update_running=model.training)
+                             update_running=model.training,
+                             dropout_p=model.enc_dropout.p if model.training else 0.0)
         ctx.model = model
         return logits.clone()
 
@@ -174,9 +175,11 @@ class RCNN(nn.Module):
     def encode(self, x):
         """RCNN.encode (model/model.py:215-221): [B,3,H,W] -> [B, W/8, hidden] (inference)."""
         eng = self._engine_for(x)
+        p = self.enc_dropout.p if self.training else 0.0
         with torch.no_grad():
-            eng.forward(x, train=self.training, save_for_backward=False, update_running=self.training)
-        return eng.ws.bufs[f"r{self.num_rnn_layers - 1}.out"].float().clone()
+            eng.forward(x, train=self.training, save_for_backward=False, update_running=self.training, dropout_p=p)
+        key = "enc.drop" if p > 0.0 else f"r{self.num_rnn_layers - 1}.out"   # after enc_dropout (model.py:220)
+        return eng.ws.bufs[key].float().clone()
 
     def forward(self, x, text=None, is_train=True, batch_max_length=25):
         """CTC logits [B, T, num_classes] (fp32). `text`/`batch_max_length` are accepted for

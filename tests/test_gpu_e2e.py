@@ -21,9 +21,11 @@ def _gpu():
         pytest.skip("no HIP device")
 
 
-def build_model(sd, hidden, dtype):
+def build_model(sd, hidden, dtype, enc_dropout_p=0.0):
+    """enc_dropout_p = 0: the train-mode goldens were made with the reference's dropout off
+    (tests/golden/make_goldens.py); test_enc_dropout_train covers p > 0."""
     from model.model import RCNN
-    m = RCNN(num_classes=194, hidden_size=hidden, blank_id=None, compute_dtype=dtype)
+    m = RCNN(num_classes=194, hidden_size=hidden, blank_id=None, compute_dtype=dtype, enc_dropout_p=enc_dropout_p)
     missing, unexpected = m.load_state_dict(sd, strict=False)
     assert not unexpected, unexpected
     assert all(k.endswith("num_batches_tracked") for k in missing), missing
@@ -287,3 +289,39 @@ def test_train_step_bf16_runs_and_descends():
     print("losses", losses)
     assert all(np.isfinite(losses))
     assert losses[-1] < losses[0]
+
+
+def test_enc_dropout_train():
+    """enc_dropout (model/model.py:201,220) in training: the head sees the encoder output with a
+    Bernoulli(1 - p) mask scaled by 1/(1-p) (keep share within 4 sigma), the logits are the head
+    applied to exactly that tensor, the head-weight gradient is dlogits^T @ that tensor, and eval
+    mode applies no dropout. The mask stream is counter-based (crnn_dropout), not torch's Philox."""
+    from crnn_hip.ctc import ctc_loss
+    from crnn_hip.recipe import recipe_state_dict, synthetic_batch
+    p = 0.3
+    sd = recipe_state_dict(O.param_shapes(64, 194), 11)
+    model = build_model(sd, 64, torch.float32, enc_dropout_p=p).train()
+    x, _, tg, tl = synthetic_batch(4, 32, 128, 16, 194, seed=12)
+    x = x.to(DEV)
+    logits = model(x)
+    eng = model._engine
+    raw = eng.ws.bufs[f"r{model.num_rnn_layers - 1}.out"].float()
+    drop = eng.ws.bufs["enc.drop"].float()
+    kept = drop != 0
+    n = kept.numel()
+    share = float(kept.float().mean())
+    assert abs(share - (1 - p)) < 4 * ((p * (1 - p) / n) ** 0.5)
+    assert torch.allclose(drop[kept], raw[kept] / (1 - p), rtol=1e-6, atol=1e-6)
+    w = model.ctc_head.weight.detach()
+    b = model.ctc_head.bias.detach()
+    assert torch.allclose(logits.detach(), drop @ w.t() + b, rtol=1e-4, atol=1e-4)
+    logits.retain_grad()
+    ctc_loss(logits, tg, tl).backward()
+    gw = (logits.grad.reshape(-1, logits.shape[-1]).t() @ drop.reshape(-1, drop.shape[-1]))
+    assert float((model.ctc_head.weight.grad - gw).norm() / gw.norm()) < 1e-4
+    # a second training forward draws a new mask; eval applies none
+    model(x)
+    assert not torch.equal(eng.ws.bufs["enc.drop"] != 0, kept)
+    model.eval()
+    with torch.no_grad():
+        model(x)

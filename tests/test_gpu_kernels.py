@@ -178,6 +178,32 @@ def test_conv_halo_vs_gemm():
     assert relerr(w1, w0) < 1e-5   # fp32 accumulation both ways (beta = 1 keeps the 0.25 start)
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_dropout_mask(dtype):
+    """crnn_dropout: keep share ~ 1-p, kept values x/(1-p), the mask is a function of (seed, index)
+    (the backward regenerates it), other seeds give other masks, p = 0 is the identity."""
+    L = _L()
+    n, p = 1 << 20, 0.1
+    x = (torch.rand(n, generator=torch.Generator().manual_seed(3)) + 0.5).to(DEV, dtype)
+    st = L.stream_ptr()
+    dt = L.dtype_code(dtype)
+    ys = []
+    for seed in (7, 7, 8):
+        y = torch.empty_like(x)
+        L.call("crnn_dropout", dt, x.data_ptr(), y.data_ptr(), n, p, seed, st)
+        ys.append(y.float())
+    k = ys[0] != 0
+    share = float(k.float().mean())
+    assert abs(share - (1 - p)) < 4 * (p * (1 - p) / n) ** 0.5
+    tol = 1e-6 if dtype == torch.float32 else 8e-3
+    assert torch.allclose(ys[0][k], x.float()[k] / (1 - p), rtol=tol)
+    assert torch.equal(ys[0], ys[1])
+    assert float(((ys[2] != 0) != k).float().mean()) > 0.1
+    y0 = torch.empty_like(x)
+    L.call("crnn_dropout", dt, x.data_ptr(), y0.data_ptr(), n, 0.0, 7, st)
+    assert torch.equal(y0, x)
+
+
 @pytest.mark.parametrize("BHWC", [(6, 40, 256), (5, 128, 512)])
 def test_se_bn_bwd_fused_reduce(BHWC):
     """crnn_se_bn_bwd_reduce + crnn_se_bn_partials == crnn_se_bwd_reduce + crnn_bn_bwd_reduce
