@@ -500,6 +500,9 @@ int conv_dgrad_strided(const Geo& g, const void* dy, const void* w, void* dx, co
       }
       const int Hc = (g.Hi - pch + g.sh - 1) / g.sh, Wc = (g.Wi - pcw + g.sw - 1) / g.sw;
       if (Hc <= 0 || Wc <= 0) continue;
+      // a class no tap reaches contributes 0: with accumulate and no residual term it leaves dx
+      // as it is (the 1x1 stride-2 downsample: 3 of 4 classes), so skip its read + write pass
+      if (tt.n == 0 && accumulate && dres == nullptr) continue;
       const int M = g.B * Hc * Wc, N = g.Ci, K = tt.n * g.Co;
       FastDiv dWc(Wc), dHcWc(Hc * Wc);
       DgradClsA<T> la{(const T*)dy, g, tt, Hc, Wc, M, K, dWc, dHcWc, dyb};

@@ -122,6 +122,9 @@ def test_conv_fwd_dgrad_wgrad(cfg, dtype):
         L.call("crnn_conv_dgrad", dt, d, dyd.data_ptr(), wd.data_ptr(), dxd.data_ptr(), None, None, 0, st)
         dx = dxd.float().permute(0, 3, 1, 2).cpu()
         assert relerr(dx, xr.grad) < tol
+        # accumulate mode (dx += dgrad; the downsample branch of a block), incl. skipped classes
+        L.call("crnn_conv_dgrad", dt, d, dyd.data_ptr(), wd.data_ptr(), dxd.data_ptr(), None, None, 1, st)
+        assert relerr(dxd.float().permute(0, 3, 1, 2).cpu(), 2 * xr.grad) < tol
     # wgrad
     need = L.lib().crnn_conv_wgrad_workspace(dt, d)
     ws = torch.empty(need // 4 + 1, device=DEV)
