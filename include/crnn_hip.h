@@ -132,8 +132,9 @@ int crnn_bn_finalize(const float* psum, const float* psq, int rows, long rows_pe
                      const float* gamma, const float* beta,
                      float* running_mean, float* running_var, float momentum, float eps, int train,
                      float* mean, float* invstd, float* scale, float* shift, float* ws, void* stream);
-/* bytes of `ws` crnn_bn_finalize / crnn_bn_bwd_finalize need for C channels (chunk partials of the
- * two-launch combine); calls sharing one workspace must be stream-ordered. */
+/* bytes of `ws` crnn_bn_finalize / crnn_bn_bwd_finalize need for C channels: 64 ticket counters
+ * then the chunk partials. ZERO it once before first use (the one-launch path's counters re-arm
+ * themselves); calls sharing one workspace must be stream-ordered. */
 size_t crnn_bn_finalize_workspace(int C);
 /* per-channel (sum, M2) partials of an NHWC tensor [M][C] (for tensors not produced by a conv);
  * partial r covers ceil(M/rows) rows. */
