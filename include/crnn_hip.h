@@ -115,6 +115,16 @@ int crnn_conv_stat_rows(int dtype, const crnn_conv_desc* d);
 int crnn_conv_stat_rows_per_partial(int dtype, const crnn_conv_desc* d);
 /* dx[B][Hi][Wi][Ci] = dgrad(dy) (+= dx if accumulate) (+ dres*(yres>0) if dres != NULL). */
 int crnn_conv_dgrad(int dtype, const crnn_conv_desc* d, const void* dy, const void* w, void* dx, const void* dres, const void* yres, int accumulate, void* stream);
+/* dgrad fused with the BatchNorm backward sums of the layer before (conv input = ReLU(BN(z))):
+ * dx as crnn_conv_dgrad (no accumulate / residual), plus per partial row r (128 rows of dx)
+ * pg[r][c] = sum g, pgx[r][c] = sum g (z - mean) invstd with g = dx (z scale + shift > 0) — the
+ * CRNN_BNG_RELU sums crnn_bn_bwd_reduce would compute, from the fp32 accumulators; feed them to
+ * crnn_bn_bwd_finalize with rows = crnn_conv_dgrad_bnrelu_rows(). bf16, stride 1; rows = 0 means
+ * the geometry is not supported (use crnn_conv_dgrad + crnn_bn_bwd_reduce). */
+int crnn_conv_dgrad_bnrelu_rows(int dtype, const crnn_conv_desc* d);
+int crnn_conv_dgrad_bnrelu(int dtype, const crnn_conv_desc* d, const void* dy, const void* w, void* dx, const void* z,
+                           const float* mean, const float* invstd, const float* scale, const float* shift, float* pg,
+                           float* pgx, void* stream);
 /* dw_oihw (fp32, reference layout) = beta*dw + wgrad(dy, x); ws = split-K slabs. */
 int crnn_conv_wgrad(int dtype, const crnn_conv_desc* d, const void* dy, const void* x, float* dw_oihw, float* ws, size_t ws_bytes, float beta, void* stream);
 size_t crnn_conv_wgrad_workspace(int dtype, const crnn_conv_desc* d);

@@ -62,6 +62,8 @@ _SIGS = {
     "crnn_conv_stat_rows": ([i32, C.POINTER(ConvDesc)], i32),
     "crnn_conv_stat_rows_per_partial": ([i32, C.POINTER(ConvDesc)], i32),
     "crnn_conv_dgrad": ([i32, C.POINTER(ConvDesc), vp, vp, vp, vp, vp, i32, vp], i32),
+    "crnn_conv_dgrad_bnrelu_rows": ([i32, C.POINTER(ConvDesc)], i32),
+    "crnn_conv_dgrad_bnrelu": ([i32, C.POINTER(ConvDesc), vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp], i32),
     "crnn_conv_wgrad": ([i32, C.POINTER(ConvDesc), vp, vp, vp, vp, sz, f32, vp], i32),
     "crnn_conv_wgrad_workspace": ([i32, C.POINTER(ConvDesc)], sz),
     "crnn_bn_finalize": ([vp, vp, i32, i64, i32, i64, vp, vp, vp, vp, f32, f32, i32, vp, vp, vp, vp, vp, vp], i32),

@@ -526,16 +526,18 @@ class CRNNEngine:
 
     # ------------------------------------------------------------------ backward
     def _bn_bwd(self, mode, dy, z, stats, prefix, M, C, HW=1, y=None, se=None, dpool=None, out=None,
-                accumulate_params=False, se_abc=None):
+                accumulate_params=False, se_abc=None, sums=None):
         """BN backward: per-channel sums of g (mode, crnn_hip.h CRNN_BNG_*) -> finalize -> apply.
         se_abc = (abc, B): the SE mode's sums come from crnn_se_bn_bwd_reduce's per-sample terms
-        (no second pass over the tensor)."""
+        (no second pass over the tensor); sums = (pg, pgx, rows): given by the producing dgrad."""
         mean, inv, sc, sh = stats
         ws = self.ws
         s = L.stream_ptr()
         d = BnBwdDesc(ptr(dy), ptr(z), ptr(mean), ptr(inv), ptr(sc), ptr(sh), ptr(y), ptr(se), ptr(dpool), mode,
                       M, C, HW)
-        if se_abc is not None:
+        if sums is not None:   # (pg, pgx, rows) already produced (crnn_conv_dgrad_bnrelu)
+            pg, pgx, rows = sums
+        elif se_abc is not None:
             abc, B = se_abc
             rows = B
             pg = ws.get("bnb.pg", (1024 * 512,), torch.float32)[: rows * C]
@@ -726,11 +728,23 @@ class CRNNEngine:
                          se_abc=(abc, B))
             self._wgrad(blk.conv2, dz2, sb["a1"], B, ho, wo)
             da1 = bufs[o2][: Mo * P]
-            self._conv_call("dgrad", self.conv_flops(blk.conv2, B, ho, wo), "crnn_conv_dgrad", dt, blk.conv2.desc(B, ho, wo), ptr(dz2), ptr(self.packed[blk.conv2.name]),
-                 ptr(da1), None, None, 0, s)
+            d2 = blk.conv2.desc(B, ho, wo)
+            frows = L.lib().crnn_conv_dgrad_bnrelu_rows(dt, d2)
+            sums = None
+            if frows > 0 and frows * P <= 1024 * 512:
+                # dgrad + BN1's backward sums in the epilogue (no reduce pass over da1, z1)
+                pg = ws.get("bnb.pg", (1024 * 512,), torch.float32)[: frows * P]
+                pgx = ws.get("bnb.pgx", (1024 * 512,), torch.float32)[: frows * P]
+                self._conv_call("dgrad", self.conv_flops(blk.conv2, B, ho, wo), "crnn_conv_dgrad_bnrelu", dt, d2,
+                                ptr(dz2), ptr(self.packed[blk.conv2.name]), ptr(da1), ptr(sb["z1"]), ptr(sb["m1"]),
+                                ptr(sb["i1"]), ptr(sb["sc1"]), ptr(sb["sh1"]), ptr(pg), ptr(pgx), s)
+                sums = (pg, pgx, frows)
+            else:
+                self._conv_call("dgrad", self.conv_flops(blk.conv2, B, ho, wo), "crnn_conv_dgrad", dt, d2, ptr(dz2),
+                                ptr(self.packed[blk.conv2.name]), ptr(da1), None, None, 0, s)
             dz1 = bufs[o1][: Mo * P]
             self._bn_bwd(1, da1, sb["z1"], (sb["m1"], sb["i1"], sb["sc1"], sb["sh1"]), blk.conv1.bn, Mo, P,
-                         out=dz1, accumulate_params=accumulate)
+                         out=dz1, accumulate_params=accumulate, sums=sums)
             self._wgrad(blk.conv1, dz1, sb["x"], B, h, w)
             Ci = blk.conv1.ci
             dxb = bufs[o2][: B * h * w * Ci]

@@ -398,6 +398,62 @@ template <typename T> struct DgradEpi {
   __device__ __forceinline__ void stats(int, int, f32x4, f32x4) const {}
 };
 
+// dgrad of a conv whose input went through BN -> ReLU (the next layer's BN backward, CRNN_BNG_RELU):
+// stores dx and, per 128-row partial (the wave's rows of a 256-row tile), the BN sums
+// sum g and sum g x^ over its rows, g = dx * (z scale + shift > 0), x^ = (z - mean) invstd, from
+// the fp32 accumulators — the reduce pass over (dx, z) that would follow is not needed.
+template <typename T> struct DgradBnEpi {
+  static constexpr bool kStats = false;
+  static constexpr bool kTileHook = true;
+  T* dx;
+  int M, N;
+  const T* z;
+  const float* mean;
+  const float* inv;
+  const float* scale;
+  const float* shift;
+  float* pg;
+  float* pgx;
+  __device__ __forceinline__ void store(int m, int n, f32x4 v, int) const {
+    if (m < M && n < N) st4<T>(dx + (size_t)m * N + n, v);
+  }
+  __device__ __forceinline__ void stats(int, int, f32x4, f32x4) const {}
+  template <int MI, int NI>
+  __device__ __forceinline__ void tile(const f32x4 (&acc)[MI][NI], int Mr, int rbase, int prow, int ncol0,
+                                       int lane) const {
+    const int mr = lane & 15, nq = 4 * (lane >> 4);
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int n = ncol0 + j * 16 + nq;
+      const int nc = n < N ? n : N - 4;   // clamped: loads stay unconditional
+      const f32x4 mu = *reinterpret_cast<const f32x4*>(mean + nc), iv = *reinterpret_cast<const f32x4*>(inv + nc);
+      const f32x4 sc = *reinterpret_cast<const f32x4*>(scale + nc), sh = *reinterpret_cast<const f32x4*>(shift + nc);
+      f32x4 s = {0.f, 0.f, 0.f, 0.f}, q = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int m = rbase + i * 16 + mr;
+        const float ok = m < Mr ? 1.f : 0.f;
+        const f32x4 zz = ld4f<T>(z + (size_t)(m < Mr ? m : Mr - 1) * N + nc);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float g = (zz[r] * sc[r] + sh[r]) > 0.f ? acc[i][j][r] * ok : 0.f;
+          s[r] += g;
+          q[r] += g * ((zz[r] - mu[r]) * iv[r]);
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        s[r] = rowgroup_sum<16>(s[r]);
+        q[r] = rowgroup_sum<16>(q[r]);
+      }
+      if (mr == 0 && n < N) {
+        *reinterpret_cast<f32x4*>(pg + (size_t)prow * N + n) = s;
+        *reinterpret_cast<f32x4*>(pgx + (size_t)prow * N + n) = q;
+      }
+    }
+  }
+};
+
 struct SlabEpi {
   static constexpr bool kStats = false;
   float* ws;  // [nsplit][Mrows][N]
@@ -544,6 +600,29 @@ template <typename T> int conv_dgrad_t(const crnn_conv_desc* d, const void* dy, 
   return launch<T, 64, 64>(la, lb, ep, M, N, K, 1, st);
 }
 
+// stride-1 dgrad on the 256-row kernel with the BN-ReLU backward sums (DgradBnEpi); the number of
+// partial rows, or 0 when the geometry does not take the 256-row path (caller: unfused)
+inline int dgrad_bnrelu_rows(const crnn_conv_desc* d) {
+  if (d->sh != 1 || d->sw != 1 || d->Co % 64 || d->Ci % 8) return 0;
+  const long M = (long)d->B * d->Hi * d->Wi;
+  if (!deep_dgrad_bn<bf16>(M, d->Ci, d->Co, 128)) return 0;
+  return (int)((M + 255) / 256 * 2);
+}
+
+int conv_dgrad_bnrelu(const crnn_conv_desc* d, const void* dy, const void* w, void* dx, const void* z,
+                      const float* mean, const float* inv, const float* scale, const float* shift, float* pg,
+                      float* pgx, hipStream_t st) {
+  using T = bf16;
+  Geo g = geo(d);
+  const int M = g.B * g.Hi * g.Wi, N = g.Ci, K = g.KH * g.KW * g.Co;
+  DgradA<T> la{(const T*)dy, g, M, K, 0, 0, nbytes((long)g.B * g.Ho * g.Wo * g.Co, sizeof(T))};
+  DgradB<T> lb{(const T*)w, g, K, nbytes((long)g.Co * g.KH * g.KW * g.Ci, sizeof(T))};
+  DgradBnEpi<T> ep{(T*)dx, M, N, (const T*)z, mean, inv, scale, shift, pg, pgx};
+  const int deep = deep_dgrad_bn<T>(M, N, g.Co, 128);
+  if (deep == 256) return launch256<256, 256>(la, lb, ep, M, N, K, st);
+  return launch256<256, 128>(la, lb, ep, M, N, K, st);
+}
+
 template <typename T> int conv_wgrad_t(const crnn_conv_desc* d, const void* dy, const void* x, float* dw,
                                        float* ws, size_t ws_bytes, float beta, hipStream_t st) {
   Geo g = geo(d);
@@ -667,6 +746,18 @@ int crnn_conv_dgrad(int dtype, const crnn_conv_desc* d, const void* dy, const vo
   if (dres == nullptr && !accumulate && use_halo(dtype, d, true)) return conv_halo_dgrad(d, dy, w, dx, st);
   return dtype == CRNN_BF16 ? conv_dgrad_t<bf16>(d, dy, w, dx, dres, yres, accumulate, st)
                             : conv_dgrad_t<float>(d, dy, w, dx, dres, yres, accumulate, st);
+}
+
+int crnn_conv_dgrad_bnrelu_rows(int dtype, const crnn_conv_desc* d) {
+  return dtype == CRNN_BF16 ? dgrad_bnrelu_rows(d) : 0;
+}
+
+int crnn_conv_dgrad_bnrelu(int dtype, const crnn_conv_desc* d, const void* dy, const void* w, void* dx, const void* z,
+                           const float* mean, const float* invstd, const float* scale, const float* shift, float* pg,
+                           float* pgx, void* stream) {
+  if (dtype != CRNN_BF16 || dgrad_bnrelu_rows(d) == 0)
+    return crnn_set_error(hipErrorInvalidValue, "conv_dgrad_bnrelu: geometry not on the 256-row path");
+  return conv_dgrad_bnrelu(d, dy, w, dx, z, mean, invstd, scale, shift, pg, pgx, (hipStream_t)stream);
 }
 
 int crnn_conv_wgrad(int dtype, const crnn_conv_desc* d, const void* dy, const void* x, float* dw_oihw,

@@ -26,6 +26,7 @@
 #pragma once
 #include "gemm.hpp"
 
+#include <type_traits>
 #include "crnn_hip.h"
 int crnn_option(int key);  // capi.cpp (crnn_set_option)
 int crnn_cu_count();       // capi.cpp: compute units of the current device (cached)
@@ -54,6 +55,11 @@ __device__ __forceinline__ void raw_barrier() {
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
 }
+
+// optional epilogue hook: an EPI with `static constexpr bool kTileHook = true` gets
+// epi.tile<MI, NI>(acc, M, first row, partial row, first column, lane) after its stores
+template <class E, class = void> struct has_tile_hook : std::false_type {};
+template <class E> struct has_tile_hook<E, std::void_t<decltype(E::kTileHook)>> : std::bool_constant<E::kTileHook> {};
 
 // per-wave, per-column partial statistics (sum, sum of squared deviations from the partial
 // mean) over this wave's WM accumulator rows — the BN two-pass-in-registers epilogue
@@ -338,6 +344,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(LA la, LB lb, EPI epi, int
 #pragma unroll
     for (int j = 0; j < NI; ++j) epi.store(m0 + wr * WM + i * 16 + mr, n0 + wc * WN + j * 16 + nq, acc[i][j], kz);
   if constexpr (EPI::kStats) wave_col_stats<MI, NI>(acc, epi, M, m0 + wr * WM, m_tile * 2 + wr, n0 + wc * WN, lane);
+  if constexpr (has_tile_hook<EPI>::value) epi.template tile<MI, NI>(acc, M, m0 + wr * WM, m_tile * 2 + wr, n0 + wc * WN, lane);
 }
 
 // Persistent variant (crnn_set_option CRNN_OPT_GEMM_PERSISTENT): grid <= CU count, every block
@@ -558,6 +565,8 @@ __global__ __launch_bounds__(512) void gemm256p_kernel(LA la, LB lb, EPI epi, in
         for (int j = 0; j < NI; ++j) epi.store(m0 + wr * WM + i * 16 + mr, n0 + wc * WN + j * 16 + nq, acc[i][j], kz);
       if constexpr (EPI::kStats)
         wave_col_stats<MI, NI>(acc, epi, M, m0 + wr * WM, (m0 / BM) * 2 + wr, n0 + wc * WN, lane);
+      if constexpr (has_tile_hook<EPI>::value)
+        epi.template tile<MI, NI>(acc, M, m0 + wr * WM, (m0 / BM) * 2 + wr, n0 + wc * WN, lane);
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll

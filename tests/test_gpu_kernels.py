@@ -181,6 +181,57 @@ def test_conv_halo_vs_gemm():
     assert relerr(w1, w0) < 1e-5   # fp32 accumulation both ways (beta = 1 keeps the 0.25 start)
 
 
+@pytest.mark.parametrize("geo", [(64, 256, 8, 64, 256), (128, 512, 4, 32, 512), (70, 256, 8, 60, 256)])
+def test_dgrad_bnrelu_fused(geo):
+    """crnn_conv_dgrad_bnrelu == crnn_conv_dgrad + crnn_bn_bwd_reduce (CRNN_BNG_RELU) through
+    crnn_bn_bwd_finalize (incl. a ragged last tile)."""
+    L = _L()
+    B, Ci, H, W, Co = geo
+    g = torch.Generator().manual_seed(10)
+    T = torch.bfloat16
+    dt, st = L.BF16, L.stream_ptr()
+    d = L.ConvDesc(B, H, W, Ci, H, W, Co, 3, 3, 1, 1, 1, 1, Ci)
+    rows = L.lib().crnn_conv_dgrad_bnrelu_rows(dt, d)
+    assert rows > 0
+    w = (torch.randn(Co, Ci, 3, 3, generator=g) / 48).to(DEV)
+    wd = torch.empty(Co, 3, 3, Ci, dtype=T, device=DEV)
+    L.call("crnn_pack_conv_weight", dt, w.data_ptr(), wd.data_ptr(), Co, Ci, 3, 3, Ci, st)
+    dy = torch.randn(B, H, W, Co, generator=g).to(DEV, T)
+    M = B * H * W
+    z = (torch.randn(M, Ci, generator=g) * 1.5 + 0.2).to(DEV, T)
+    zf = z.float()
+    mean = zf.mean(0)
+    inv = 1 / (zf.var(0, unbiased=False) + 1e-5).sqrt()
+    gamma = (torch.rand(Ci, generator=g) + 0.5).to(DEV)
+    beta = torch.randn(Ci, generator=g).to(DEV) * 0.3
+    sc, sh = gamma * inv, beta - mean * gamma * inv
+    fws = torch.zeros((L.lib().crnn_bn_finalize_workspace(512) + 3) // 4, device=DEV)
+    out = []
+    for fused in (False, True):
+        dx = torch.empty(M, Ci, dtype=T, device=DEV)
+        mg, mgx = torch.empty(Ci, device=DEV), torch.empty(Ci, device=DEV)
+        dga, dbe = torch.empty(Ci, device=DEV), torch.empty(Ci, device=DEV)
+        if fused:
+            r = rows
+            pg, pgx = torch.empty(r, Ci, device=DEV), torch.empty(r, Ci, device=DEV)
+            L.call("crnn_conv_dgrad_bnrelu", dt, d, dy.data_ptr(), wd.data_ptr(), dx.data_ptr(), z.data_ptr(),
+                   mean.data_ptr(), inv.data_ptr(), sc.data_ptr(), sh.data_ptr(), pg.data_ptr(), pgx.data_ptr(), st)
+        else:
+            L.call("crnn_conv_dgrad", dt, d, dy.data_ptr(), wd.data_ptr(), dx.data_ptr(), None, None, 0, st)
+            bd = L.BnBwdDesc(dx.data_ptr(), z.data_ptr(), mean.data_ptr(), inv.data_ptr(), sc.data_ptr(),
+                             sh.data_ptr(), None, None, None, 1, M, Ci, 1)
+            r = L.lib().crnn_bn_rows(M)
+            pg, pgx = torch.empty(r, Ci, device=DEV), torch.empty(r, Ci, device=DEV)
+            L.call("crnn_bn_bwd_reduce", dt, bd, pg.data_ptr(), pgx.data_ptr(), r, st)
+        L.call("crnn_bn_bwd_finalize", pg.data_ptr(), pgx.data_ptr(), r, Ci, M, dga.data_ptr(), dbe.data_ptr(),
+               mg.data_ptr(), mgx.data_ptr(), 0, fws.data_ptr(), st)
+        torch.cuda.synchronize()
+        out.append((dx.float(), mg.clone(), mgx.clone(), dga.clone(), dbe.clone()))
+    assert torch.equal(out[0][0], out[1][0])
+    for a, b in zip(out[0][1:], out[1][1:]):
+        assert relerr(b, a) < 5e-3   # fp32 accumulators vs the bf16-rounded dx of the unfused pass
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_dropout_mask(dtype):
     """crnn_dropout: keep share ~ 1-p, kept values x/(1-p), the mask is a function of (seed, index)
