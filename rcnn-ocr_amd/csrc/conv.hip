@@ -687,7 +687,7 @@ int crnn_conv_stat_rows(int dtype, const crnn_conv_desc* d) {
 }
 
 void crnn_conv_wgrad_plan(int dtype, const crnn_conv_desc* d, int* bm, int* bn, int* splits) {
-  if (use_halo(dtype, d, true) && d->Ci == 64) {  // conv_halo.hip: bm = bn = 0, a slab per workgroup
+  if (use_halo(dtype, d, false)) {  // conv_halo.hip (the fwd instances): bm = bn = 0, slab per workgroup
     *bm = 0;
     *bn = 0;
     *splits = conv_halo_wgrad_slabs(d);

@@ -236,22 +236,28 @@ template <int CI, int CO>
 __global__ __launch_bounds__(512) void halo3x3_wgrad_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
                                                             float* __restrict__ ws, int B, int H, int W,
                                                             uint32_t dybytes, uint32_t xbytes) {
-  constexpr int XROW = CI * 2 + 32, DROW = CO * 2 + 32;  // padded pixel rows (bytes)
-  static_assert((XROW / 8) % 32 == 20 && (DROW / 8) % 32 == 4, "pitches of the conflict-free map");
+  // TAPK (CI = 8, the input conv): a 16-column k' fragment spans two taps; each lane's tap comes
+  // from its column quad, the 72 k' columns are padded to 5 fragments (extra columns not written)
+  constexpr bool TAPK = CI == 8;
+  constexpr int XROW = TAPK ? 32 : CI * 2 + 32, DROW = CO * 2 + 32;  // padded pixel rows (bytes)
+  static_assert((XROW / 8) % 8 == 4 && (DROW / 8) % 8 == 4, "pitches of the conflict-free map");
   constexpr int XSLOT = (TW + 2) * XROW, DTILE = TW * DROW;
   constexpr int KP = 9 * CI;                      // k' = (tap, ci)
-  constexpr int MW = CO / 2, NW = KP / 4;         // per-wave block
-  constexpr int MF = MW / 16, NF = NW / 16;       // fragments
+  constexpr int WVM = TAPK ? 4 : 2, WVN = 8 / WVM;  // waves along M (co) and N (k')
+  constexpr int MW = CO / WVM;                    // per-wave co
+  constexpr int NFT = (KP + 15) / 16;             // k' fragments in all
+  constexpr int NF = (NFT + WVN - 1) / WVN, NW = 16 * NF;  // per wave
+  constexpr int MF = MW / 16;
   constexpr int XCH = CI / 8, DCH = CO / 8;       // 16-B chunks per pixel
   constexpr int NT = 512;
   constexpr int XPER = ((TW + 2) * XCH + NT - 1) / NT, DPER = (TW * DCH + NT - 1) / NT;
-  static_assert(NW % 16 == 0 && MW % 16 == 0 && (CI % 16) == 0, "shape");
+  static_assert(MW % 16 == 0 && (CI % 16 == 0 || TAPK), "shape");
   __shared__ __attribute__((aligned(16))) char ring[4 * XSLOT];
   __shared__ __attribute__((aligned(16))) char dyt[2][DTILE];
 
   const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int mw = wv & 1, nw = wv >> 1;
+  const int mw = wv % WVM, nw = wv / WVM;
   const int nxh = W / TW, nbands = B * nxh;
   const __amdgpu_buffer_rsrc_t rx = mk_rsrc(x, xbytes), rd = mk_rsrc(dy, dybytes);
   // transposed-read lane roles: block row q, column quad p4; pixel of (h = 0, q) within a k-step
@@ -334,9 +340,18 @@ __global__ __launch_bounds__(512) void halo3x3_wgrad_kernel(const bf16* __restri
         }
 #pragma unroll
         for (int j = 0; j < NF; ++j) {
-          const int f = nw * NF + j, t = f / (CI / 16), ci0 = (f % (CI / 16)) * 16;
-          const int kh = t / 3, kw = t % 3;
-          const char* pb = sl[kh] + (ks * 32 + kw) * XROW + ci0 * 2;
+          const int f = nw * NF + j;
+          if (f >= NFT) break;  // wave-uniform
+          const char* pb;
+          if constexpr (TAPK) {
+            // columns 16f + 4p4 .. +3: tap 2f + p4/2 (clamped: its columns are not written), ci 4(p4&1)
+            const int t = min(2 * f + (p4 >> 1), 8), kh = t / 3, kw = t - 3 * kh;
+            pb = ring + ((yy + kh) & 3) * XSLOT + prow * XROW + (ks * 32 + kw) * XROW + 8 * (p4 & 1);
+          } else {
+            const int t = f / (CI / 16), ci0 = (f % (CI / 16)) * 16;
+            const int kh = t / 3, kw = t % 3;
+            pb = sl[kh] + (ks * 32 + kw) * XROW + ci0 * 2;
+          }
           s16x4 t2[2] = {__builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(pb)),
                          __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(pb + 8 * XROW))};
           const bf16x8 yb = *reinterpret_cast<const bf16x8*>(t2);
@@ -354,10 +369,12 @@ __global__ __launch_bounds__(512) void halo3x3_wgrad_kernel(const bf16* __restri
 #pragma unroll
   for (int i = 0; i < MF; ++i)
 #pragma unroll
-    for (int j = 0; j < NF; ++j)
+    for (int j = 0; j < NF; ++j) {
+      const int n = nw * NW + 16 * j + c;
+      if (n < KP)
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        slab[(size_t)(mw * MW + 16 * i + 4 * g + r) * KP + nw * NW + 16 * j + c] = acc[i][j][r];
+        for (int r = 0; r < 4; ++r) slab[(size_t)(mw * MW + 16 * i + 4 * g + r) * KP + n] = acc[i][j][r];
+    }
 }
 
 }  // namespace
@@ -419,7 +436,11 @@ int conv_halo_wgrad(const crnn_conv_desc* d, const void* dy, const void* x, floa
   const int S = conv_halo_wgrad_slabs(d);
   const uint32_t dybytes = (uint32_t)((size_t)d->B * d->Ho * d->Wo * d->Co * 2);
   const uint32_t xbytes = (uint32_t)((size_t)d->B * d->Hi * d->Wi * d->Ci * 2);
-  hipLaunchKernelGGL((halo3x3_wgrad_kernel<64, 128>), dim3(S), dim3(512), 0, st, (const bf16*)dy, (const bf16*)x, ws,
-                     d->B, d->Hi, d->Wi, dybytes, xbytes);
+  if (d->Ci == 8)
+    hipLaunchKernelGGL((halo3x3_wgrad_kernel<8, 64>), dim3(S), dim3(512), 0, st, (const bf16*)dy, (const bf16*)x, ws,
+                       d->B, d->Hi, d->Wi, dybytes, xbytes);
+  else
+    hipLaunchKernelGGL((halo3x3_wgrad_kernel<64, 128>), dim3(S), dim3(512), 0, st, (const bf16*)dy, (const bf16*)x,
+                       ws, d->B, d->Hi, d->Wi, dybytes, xbytes);
   return (int)hipGetLastError();
 }
