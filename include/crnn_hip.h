@@ -50,7 +50,7 @@ enum { CRNN_OPT_GEMM_STAGGER = 0,    /* 256-row conv GEMM: waves 4-7 one barrier
        CRNN_OPT_GEMM_PERSISTENT = 1, /* 256-row GEMM: <= 1 block per CU looping over tiles, one continuous
                                         LDS-DMA pipeline across tile boundaries; 0 (default) off, 1 when
                                         tiles > CUs, 2 always */
-       CRNN_OPT_DEEP_LINEAR = 2,     /* bf16 crnn_gemm_nt/nn on the 256-row kernel when its grid fills the chip */
+       CRNN_OPT_DEEP_LINEAR = 2,     /* bf16 crnn_gemm_nt/nn on the 256-row kernel when its grid fills the chip (default 1) */
        CRNN_OPT_WGRAD_TILE = 3,      /* conv wgrad plan: 0 = 256x256, 1 = 256x128 tiles, n >= 2: ~128n blocks */
        CRNN_OPT_LSTM_TILE = 4,       /* persistent BiLSTM workgroup tile: 0 = auto, 1 = 32 samples x 32 units,
                                         2 = 16 x 32, 3 = 16 x 64 (when the grid fits the CUs) */

@@ -8,6 +8,8 @@ SHAPES = [  # (name, M, N, K): fwd = (B*Ho*Wo, Co, 9*Ci)
     ("b3.c2 fwd", 256 * 4 * 32, 512, 4608),
     ("b0.c2 wgrad", 256, 2304, 256 * 8 * 64),
     ("b3.c2 wgrad", 512, 4608, 256 * 4 * 32),
+    ("lstm xg", 256 * 32, 4096, 512),
+    ("lstm dx", 256 * 32, 512, 4096),
 ]
 
 

@@ -1,6 +1,6 @@
 """A/B microbenchmark of the BiLSTM / linear GEMM entry points at the bench shapes (B=256, T=32,
 H=512): crnn_set_option(KEY, v) for v in VALS, timed in one process.
-    python tools/gemmbench.py [KEY=V0,V1]"""
+    python tools/gemmbench.py [KEY=V0,V1] [--set KEY=V ...]  (--set: fixed options for every variant)"""
 import os
 import sys
 
@@ -13,9 +13,18 @@ from crnn_hip import _lib as L  # noqa: E402
 
 def main():
     key, vals = 2, [0, 1]
-    if len(sys.argv) > 1:
-        k, v = sys.argv[1].split("=")
+    args = sys.argv[1:]
+    fixed = []
+    while "--set" in args:
+        i = args.index("--set")
+        k, v = args[i + 1].split("=")
+        fixed.append((int(k), int(v)))
+        del args[i:i + 2]
+    if args:
+        k, v = args[0].split("=")
         key, vals = int(k), [int(x) for x in v.split(",")]
+    for k, v in fixed:
+        L.call("crnn_set_option", k, v)
     dev = torch.device("cuda")
     st = L.stream_ptr()
     B, T, H, In = 256, 32, 512, 512
