@@ -17,7 +17,7 @@ def kind(name):
         return "lstm_fwd"
     if "lstm_seq_bwd" in name:
         return "lstm_bwd"
-    if "gemm" in name and CONV.search(name):
+    if ("gemm" in name and CONV.search(name)) or "halo3x3" in name:
         return "conv"
     return None
 
