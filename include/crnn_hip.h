@@ -300,6 +300,25 @@ int crnn_lstm_seq_fwd(const void* xg, const void* whh, void* hseq, void* gsv, fl
 int crnn_lstm_seq_bwd(const void* dhseq, const void* whh_t, const void* gsv, const float* csv, void* dgates,
                       unsigned* ws, int B, int T, int H, void* stream);
 
+/* ------------------------------------------------------------------ attention decoder (fp32)
+ * The reference's attention head (model/model.py:23-148), one decoder step
+ * per call sequence (host loop: crnn_hip/attn.py):
+ *   crnn_gemm_nt  proj_h = h W_h2h^T + b_h2h            (proj_H = enc W_i2h^T once per decode)
+ *   crnn_attn_context: alpha = softmax_t(score . tanh(proj_H[b,t] + proj_h[b])),
+ *                      ctx[b][0..C) (row stride ldc) = sum_t alpha enc[b,t]; alpha optional
+ *   crnn_gemm_nt  gates = hx W_cat^T, hx = [ctx | h] rows, W_cat = [W_ih[:, :C] | W_hh]
+ *   crnn_attn_cell: LSTMCell (i, f, g, o) with + b_ih + b_hh + W_ih[:, C + ch[b * ch_stride]]
+ *                   (the one-hot input); writes h, c, hx[b][C + j] and hs (optional)
+ *   crnn_gemm_nt  logits = h W_gen^T + b_gen
+ *   crnn_attn_out: blank column masked to -1e4, logits -> probs_t (optional), argmax -> ch */
+int crnn_attn_context(const float* projH, const float* projh, const float* score, const float* enc, float* ctx,
+                      int ldc, float* alpha, int B, int T, int H, int C, void* stream);
+int crnn_attn_cell(const float* gates, const float* b_ih, const float* b_hh, const float* w_ih, int ldw, const int* ch,
+                   int ch_stride, float* h, float* c, float* hx, int ldx, float* hs, int ld_hs, int B, int H, int C,
+                   void* stream);
+int crnn_attn_out(const float* logits, int ldl, int B, int V, int blank, float* probs_t, int ldp, int* ch,
+                  void* stream);
+
 /* ------------------------------------------------------------------ CTC */
 /* Per-sample log-space CTC over logits [B][T][ldc] (fp32, C classes, blank = 0, input length T).
  * loss[b] = -log p(target_b); dlogits (may be NULL) = grad of the 'mean' reduction

@@ -199,6 +199,63 @@ class _CTC(torch.autograd.Function):
         return g * go, None, None, None, None
 
 
+# ---------------------------------------------------------------- attention decoder
+# Parameters keyed by the reference's Attention state_dict (model/model.py:23-79):
+# attention_cell.{i2h.weight, h2h.weight, h2h.bias, score.weight, rnn.weight_ih, rnn.weight_hh,
+# rnn.bias_ih, rnn.bias_hh}, generator.{weight, bias}. Eval mode (dropout = identity).
+def attn_cell(p, enc, h, c, char, num_classes):
+    """AttentionCell.forward (model/model.py:33-45): additive attention over the encoder
+    sequence, then LSTMCell([context, onehot(char)], (h, c)) (gate order i, f, g, o)."""
+    pre = "attention_cell."
+    proj_H = enc @ p[pre + "i2h.weight"].t()                                   # :35
+    proj_h = (h @ p[pre + "h2h.weight"].t() + p[pre + "h2h.bias"]).unsqueeze(1)  # :36
+    e = torch.tanh(proj_H + proj_h) @ p[pre + "score.weight"].t()             # :37 [B,T,1]
+    alpha = torch.softmax(e, dim=1)                                           # :39
+    context = (alpha.transpose(1, 2) @ enc).squeeze(1)                        # :42
+    onehot = F.one_hot(char, num_classes).to(enc.dtype)                       # :81-85
+    x = torch.cat([context, onehot], 1)                                       # :43
+    gates = x @ p[pre + "rnn.weight_ih"].t() + p[pre + "rnn.bias_ih"] + h @ p[pre + "rnn.weight_hh"].t() \
+        + p[pre + "rnn.bias_hh"]
+    i, f, g, o = gates.chunk(4, 1)
+    c2 = torch.sigmoid(f) * c + torch.sigmoid(i) * torch.tanh(g)
+    h2 = torch.sigmoid(o) * torch.tanh(c2)
+    return h2, c2
+
+
+def attn_greedy(p, enc, steps, sos_id, blank_id, num_classes):
+    """Attention._greedy_decode (model/model.py:91-112): logits per step with the blank column
+    masked to -1e4 (:87-89), next input = argmax. -> [B, steps, V]"""
+    B, H = enc.shape[0], p["attention_cell.h2h.weight"].shape[0]
+    h = torch.zeros(B, H, dtype=enc.dtype)
+    c = torch.zeros(B, H, dtype=enc.dtype)
+    ch = torch.full((B,), sos_id, dtype=torch.long)
+    out = []
+    for _ in range(steps):
+        h, c = attn_cell(p, enc, h, c, ch, num_classes)
+        lg = h @ p["generator.weight"].t() + p["generator.bias"]
+        if blank_id is not None:
+            lg[:, blank_id] = -1e4
+        out.append(lg)
+        ch = lg.argmax(1)
+    return torch.stack(out, 1)
+
+
+def attn_teacher(p, enc, text, steps, blank_id, num_classes):
+    """Attention.forward with teacher forcing (model/model.py:114-148, sampling_prob = 0):
+    input at step t is text[:, t]; logits = generator(all h), blank masked. -> [B, steps, V]"""
+    B, H = enc.shape[0], p["attention_cell.h2h.weight"].shape[0]
+    h = torch.zeros(B, H, dtype=enc.dtype)
+    c = torch.zeros(B, H, dtype=enc.dtype)
+    hs = []
+    for t in range(steps):
+        h, c = attn_cell(p, enc, h, c, text[:, t], num_classes)
+        hs.append(h)
+    lg = torch.stack(hs, 1) @ p["generator.weight"].t() + p["generator.bias"]
+    if blank_id is not None:
+        lg[:, :, blank_id] = -1e4
+    return lg
+
+
 def ctc_loss(logits_btc, targets, lengths, reduction="mean", zero_infinity=True):
     """F.ctc_loss(log_softmax(logits), blank=0) restated (numpy, float64)."""
     return _CTC.apply(logits_btc, targets, lengths, reduction, zero_infinity)

@@ -108,6 +108,9 @@ _SIGS = {
     "crnn_lstm_wgrad_workspace": ([i32, i32, i32, i32], sz),
     "crnn_lstm_wgrad": ([vp, vp, vp, vp, vp, vp, vp, vp, sz, i32, i32, i32, i32, i32, vp], i32),
     "crnn_lstm_dx": ([i32, vp, vp, vp, i32, i32, i32, i32, vp], i32),
+    "crnn_attn_context": ([vp, vp, vp, vp, vp, i32, vp, i32, i32, i32, i32, vp], i32),
+    "crnn_attn_cell": ([vp, vp, vp, vp, i32, vp, i32, vp, vp, vp, i32, vp, i32, i32, i32, i32, vp], i32),
+    "crnn_attn_out": ([vp, i32, i32, i32, i32, vp, i32, vp, vp], i32),
     "crnn_ctc_loss": ([vp, i32, i32, i32, i32, vp, i32, vp, vp, vp, i32, vp], i32),
     "crnn_ctc_reduce_mean": ([vp, vp, i32, vp, vp], i32),
     "crnn_ctc_greedy": ([vp, i32, i32, i32, i32, vp, vp, vp], i32),

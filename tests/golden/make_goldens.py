@@ -15,6 +15,10 @@ Fixtures:
   ctc_cases.npz          F.ctc_loss(blank=0, mean, zero_infinity) values + grads, incl. infeasible labels
   decode.npz/.json       training/utils.py:122-150 ctc_greedy_decoder strings at T < B
   bilstm_stack.npz       4 x BidirectionalLSTM(768) stack (model/model.py:151-163)
+  attn_decoder.npz       the attention decoder (model/model.py:23-148) on a
+                         fixed encoder output: eval greedy decode (incl. blank masking) and
+                         teacher-forced logits, with its (seeded, generator-scaled) weights
+Only some:  python tests/golden/make_goldens.py attn
 """
 from __future__ import annotations
 
@@ -281,7 +285,38 @@ def gen_bilstm_stack():
     print("wrote bilstm_stack", y.shape)
 
 
+def gen_attn():
+    """reference Attention decoder, eval mode (dropout off): greedy decode and teacher forcing.
+    The generator is scaled x30 so the greedy argmax margins survive fp32 reordering."""
+    from model.model import Attention  # noqa (reference, read-only)
+    B, T, H, V, steps = 4, 16, 64, 194, 11
+    torch.manual_seed(41)
+    dec = Attention(input_size=H, hidden_size=H, num_classes=V, sos_id=1, eos_id=2, pad_id=0, blank_id=3,
+                    dropout_p=0.1, sampling_prob=0.0)
+    with torch.no_grad():
+        dec.generator.weight.mul_(30.0)
+        dec.generator.bias.mul_(30.0)
+    dec.eval()
+    g = torch.Generator().manual_seed(42)
+    enc = torch.randn(B, T, H, generator=g)
+    text = torch.randint(4, V, (B, steps), generator=g)
+    text[:, 0] = 1
+    with torch.no_grad():
+        probs = dec(enc, is_train=False, batch_max_length=steps - 1)
+        logits = dec(enc, text=text, is_train=True, batch_max_length=steps - 1)
+    top2 = probs.topk(2, dim=-1).values
+    margin = float((top2[..., 0] - top2[..., 1]).min())
+    out = {k: v.detach().numpy() for k, v in dec.state_dict().items()}
+    out.update(enc=enc.numpy(), text=text.numpy(), probs=probs.numpy(), logits=logits.numpy(),
+               greedy=probs.argmax(-1).numpy(), min_margin=np.float64(margin))
+    np.savez_compressed(os.path.join(HERE, "attn_decoder.npz"), **out)
+    print("wrote attn_decoder", probs.shape, "min greedy margin", margin)
+
+
 def main():
+    if sys.argv[1:] == ["attn"]:
+        gen_attn()
+        return
     itos = load_charset(os.path.join(REF, "configs", "charset.txt"))
     with open(os.path.join(HERE, "charset.txt"), "w", encoding="utf-8") as f:
         for t in itos:
@@ -292,6 +327,7 @@ def main():
     gen_bilstm_stack()
     gen_eval(itos)
     gen_train(itos)
+    gen_attn()
 
 
 if __name__ == "__main__":

@@ -325,3 +325,20 @@ def test_enc_dropout_train():
     model.eval()
     with torch.no_grad():
         model(x)
+
+
+def test_attn_decoder_matches_reference():
+    """HIP attention decoder (crnn_hip/attn.py, csrc/attn.hip) vs the reference's own outputs
+    (attn_decoder.npz, model/model.py:23-148): greedy-decode logits (blank masked) and the greedy
+    sequence, teacher-forced logits; fp32."""
+    from crnn_hip.attn import AttnDecoderHIP
+    z = load("attn_decoder.npz")
+    p = {k: torch.from_numpy(z[k]) for k in z.files if k.startswith(("attention_cell.", "generator."))}
+    steps, V = z["probs"].shape[1], z["probs"].shape[2]
+    dec = AttnDecoderHIP(p, V, sos_id=1, blank_id=3, device=DEV)
+    enc = torch.from_numpy(z["enc"]).to(DEV)
+    probs = dec.run(enc, steps).cpu()
+    np.testing.assert_allclose(probs.numpy(), z["probs"], rtol=1e-4, atol=1e-3)
+    assert np.array_equal(probs.argmax(-1).numpy(), z["greedy"])
+    logits = dec.run(enc, steps, text=torch.from_numpy(z["text"])).cpu()
+    np.testing.assert_allclose(logits.numpy(), z["logits"], rtol=1e-4, atol=1e-3)

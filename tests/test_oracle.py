@@ -120,3 +120,18 @@ def test_forced_decisions_reproduce_own_decisions():
     got = O.maxpool2(O.Ctx(train=True, force={"stem.pool": t}), "stem.pool", x)
     assert torch.equal(got, ref)
     assert torch.equal(O.maxpool2(own, "stem.pool", x), ref)
+
+
+def test_oracle_attn_decoder():
+    """attention decoder restatement vs the reference's own outputs (attn_decoder.npz): greedy
+    decode logits incl. blank masking, the greedy sequence, and teacher-forced logits."""
+    z = load("attn_decoder.npz")
+    p = {k: torch.from_numpy(z[k]) for k in z.files if k.startswith(("attention_cell.", "generator."))}
+    enc = torch.from_numpy(z["enc"])
+    text = torch.from_numpy(z["text"]).long()
+    steps, V = z["probs"].shape[1], z["probs"].shape[2]
+    probs = O.attn_greedy(p, enc, steps, 1, 3, V)
+    np.testing.assert_allclose(probs.numpy(), z["probs"], rtol=1e-5, atol=1e-4)
+    assert np.array_equal(probs.argmax(-1).numpy(), z["greedy"])
+    logits = O.attn_teacher(p, enc, text, steps, 3, V)
+    np.testing.assert_allclose(logits.numpy(), z["logits"], rtol=1e-5, atol=1e-4)
