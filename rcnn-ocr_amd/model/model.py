@@ -64,15 +64,34 @@ class _EncodeFn(torch.autograd.Function):
         return None, None, None, None
 
 
+class _AttentionCellParams(nn.Module):
+    """parameter holder with model/model.py:24-31's names (AttentionCell)."""
+
+    def __init__(self, input_size, hidden_size, num_embeddings):
+        super().__init__()
+        self.i2h = nn.Linear(input_size, hidden_size, bias=False)
+        self.h2h = nn.Linear(hidden_size, hidden_size)
+        self.score = nn.Linear(hidden_size, 1, bias=False)
+        self.rnn = nn.LSTMCell(input_size + num_embeddings, hidden_size)
+
+
+class _AttentionParams(nn.Module):
+    """parameter holder with model/model.py:48-79's names (Attention: attention_cell, generator)."""
+
+    def __init__(self, input_size, hidden_size, num_classes):
+        super().__init__()
+        self.attention_cell = _AttentionCellParams(input_size, hidden_size, num_classes)
+        self.generator = nn.Linear(hidden_size, num_classes)
+
+
 class RCNN(nn.Module):
     def __init__(self, num_classes, hidden_size=256, sos_id: int = 1, eos_id: int = 2, pad_id: int = 0,
                  blank_id: Optional[int] = 3, enc_dropout_p: float = 0.1, dropblock_p: float = 0.0,
                  dropblock_block_size: int = 5, decoder: str = "ctc", num_rnn_layers: int = 2,
                  compute_dtype: torch.dtype = torch.bfloat16):
         super().__init__()
-        if decoder != "ctc":
-            raise NotImplementedError("decoder='attn' (model/model.py:23-148) is outside the MI355X hot path; "
-                                      "SURVEY.md §8(f) next-1")
+        if decoder not in ("ctc", "attn"):
+            raise ValueError(f"decoder must be 'ctc' or 'attn', got {decoder!r}")
         self.num_classes = num_classes
         self.hidden_size = hidden_size
         self.sos_id, self.eos_id, self.pad_id, self.blank_id = sos_id, eos_id, pad_id, blank_id
@@ -88,6 +107,11 @@ class RCNN(nn.Module):
         self.enc_rnn = nn.Sequential(*layers)
         self.enc_dropout = nn.Dropout(enc_dropout_p)
         self.ctc_head = nn.Linear(hidden_size, num_classes)
+        # the reference's attention head (model/model.py:23-79, :203-213): parameter holder with the
+        # reference's state_dict names; compute on the HIP path (crnn_hip/attn.py), forward only
+        self.attn = _AttentionParams(hidden_size, hidden_size, num_classes) if decoder == "attn" else None
+        self._attn_dec = None
+        self._attn_version = None
         self._engine: Optional[CRNNEngine] = None
         self._flat_param: Optional[torch.Tensor] = None
         self._flat_grad: Optional[torch.Tensor] = None
@@ -171,6 +195,25 @@ class RCNN(nn.Module):
         self.mark_params_changed()
         return r
 
+    def _attn_forward(self, x, text, is_train, batch_max_length):
+        from crnn_hip.attn import AttnDecoderHIP
+        if torch.is_grad_enabled() and self.training and any(p.requires_grad for p in self.attn.parameters()):
+            raise NotImplementedError("attention decoder training needs its backward, which is not on the HIP "
+                                      "path yet (SURVEY.md §8(f) next-1: forward only); use torch.no_grad() "
+                                      "or decoder='ctc'")
+        enc = self.encode(x)
+        ver = sum(p._version for p in self.attn.parameters())
+        if self._attn_dec is None or self._attn_version != ver or self._attn_dec.device != enc.device:
+            params = {k: v for k, v in self.attn.state_dict().items()}
+            self._attn_dec = AttnDecoderHIP(params, self.num_classes, self.sos_id, self.blank_id, enc.device)
+            self._attn_version = ver
+        steps = batch_max_length + 1
+        if not is_train:
+            return self._attn_dec.run(enc, steps)
+        if text is None:
+            raise ValueError("For training, `text` with <SOS> at text[:,0] is required")
+        return self._attn_dec.run(enc, steps, text=text)
+
     # ------------------------------------------------------------------ reference API
     def encode(self, x):
         """RCNN.encode (model/model.py:215-221): [B,3,H,W] -> [B, W/8, hidden] (inference)."""
@@ -182,8 +225,13 @@ class RCNN(nn.Module):
         return eng.ws.bufs[key].float().clone()
 
     def forward(self, x, text=None, is_train=True, batch_max_length=25):
-        """CTC logits [B, T, num_classes] (fp32). `text`/`batch_max_length` are accepted for
-        signature compatibility with the attention head and ignored (CTC is alignment-free)."""
+        """decoder='ctc': CTC logits [B, T, num_classes] (fp32); `text` / `batch_max_length` are
+        ignored (CTC is alignment-free). decoder='attn': the reference's RCNN.forward
+        (model/model.py:223-227) — greedy-decode logits [B, batch_max_length+1, num_classes] when
+        is_train is False, teacher-forced logits from `text` (<SOS> at text[:, 0]) otherwise; forward
+        only on the HIP path (the attention decoder's backward is not implemented)."""
+        if self.decoder == "attn":
+            return self._attn_forward(x, text, is_train, batch_max_length)
         self._engine_for(x)
         anchor = next(self.parameters())
         return _EncodeFn.apply(anchor, x, self, torch.is_grad_enabled() and anchor.requires_grad)

@@ -59,10 +59,23 @@ def test_refuses_cpu_tensors():
         m(torch.zeros(1, 3, 32, 64))
 
 
-def test_attention_decoder_is_out_of_scope():
+def test_attention_decoder_surface():
+    """decoder='attn' carries the reference's Attention parameter names (model/model.py:24-79,
+    the keys of tests/golden/attn_decoder.npz under `attn.`) so its checkpoints load; its forward is
+    HIP-only and training (backward) is refused; other decoders are rejected."""
+    import numpy as np
+    from helpers import GOLDEN
     from model.model import RCNN
+    m = RCNN(num_classes=194, hidden_size=64, decoder="attn")
+    z = np.load(os.path.join(GOLDEN, "attn_decoder.npz"))
+    want = {"attn." + k: z[k].shape for k in z.files if k.startswith(("attention_cell.", "generator."))}
+    got = {k: tuple(v.shape) for k, v in m.state_dict().items() if k.startswith("attn.")}
+    assert got == {k: tuple(v) for k, v in want.items()}
+    m.train()
     with pytest.raises(NotImplementedError):
-        RCNN(num_classes=10, decoder="attn")
+        m(torch.zeros(1, 3, 32, 64), text=torch.ones(1, 26, dtype=torch.long))
+    with pytest.raises(ValueError):
+        RCNN(num_classes=10, decoder="transformer")
 
 
 def test_engine_geometry_matches_reference_shapes():

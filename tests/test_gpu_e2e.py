@@ -342,3 +342,34 @@ def test_attn_decoder_matches_reference():
     assert np.array_equal(probs.argmax(-1).numpy(), z["greedy"])
     logits = dec.run(enc, steps, text=torch.from_numpy(z["text"])).cpu()
     np.testing.assert_allclose(logits.numpy(), z["logits"], rtol=1e-4, atol=1e-3)
+
+
+def test_rcnn_attn_model_eval_matches_oracle():
+    """RCNN(decoder='attn') end to end on the HIP path (encode + attention decoder, fp32, eval)
+    vs the oracle (encode + attn_greedy) on the same weights: logits and greedy sequence; the
+    teacher-forced path (is_train=True under no_grad) vs attn_teacher."""
+    from crnn_hip.recipe import recipe_state_dict, synthetic_batch
+    from model.model import RCNN
+    z = load("attn_decoder.npz")
+    sd = recipe_state_dict(O.param_shapes(64, 194), 17)
+    for k in z.files:
+        if k.startswith(("attention_cell.", "generator.")):
+            sd["attn." + k] = torch.from_numpy(z[k])
+    m = RCNN(num_classes=194, hidden_size=64, blank_id=3, decoder="attn", compute_dtype=torch.float32)
+    missing, unexpected = m.load_state_dict(sd, strict=False)
+    assert not unexpected, unexpected
+    m = m.to(DEV).eval()
+    x, _, tg, _ = synthetic_batch(3, 32, 128, 16, 194, seed=18)
+    with torch.no_grad():
+        probs = m(x.to(DEV), is_train=False, batch_max_length=9).cpu()
+        text = torch.randint(4, 194, (3, 10), generator=torch.Generator().manual_seed(5))
+        text[:, 0] = 1
+        tf = m(x.to(DEV), text=text.to(DEV), is_train=True, batch_max_length=9).cpu()
+    p = {k: v.float() for k, v in sd.items()}
+    enc = O.encode(x, p, O.Ctx(train=False))
+    pa = {k[5:]: v for k, v in p.items() if k.startswith("attn.")}
+    ref = O.attn_greedy(pa, enc, 10, 1, 3, 194)
+    assert float((probs - ref).abs().max()) < 1e-2 * float(ref.abs().max())
+    assert torch.equal(probs.argmax(-1), ref.argmax(-1))
+    reft = O.attn_teacher(pa, enc, text, 10, 3, 194)
+    assert float((tf - reft).abs().max()) < 1e-2 * float(reft.abs().max())
