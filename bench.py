@@ -41,9 +41,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=32, help="batch of the CPU baseline sample")
     ap.add_argument("--cpu-steps", type=int, default=6)
-    ap.add_argument("--mode", default="train", choices=["train", "infer"],
+    ap.add_argument("--mode", default="train", choices=["train", "infer", "attn"],
                     help="train: BASELINE configs[2]/[3] (the headline); infer: configs[1] (eval forward + greedy "
-                         "CTC decode on device)")
+                         "CTC decode on device); attn: eval encode + the reference's attention head, 26-step greedy "
+                         "decode (SURVEY 8f next-1)")
     ap.add_argument("--config", default=None, choices=["long"],
                     help="long: BASELINE configs[4] shapes (32x1024 crops, 4x768 BiLSTM, batch 64/GPU)")
     a = ap.parse_args()
@@ -52,8 +53,8 @@ def parse():
     return a
 
 
-def cpu_baseline(args, threads):
-    """oracle (CPU fp32 restatement, 'port') train step on a bounded sample."""
+def cpu_baseline(args, threads, attn_params=None):
+    """oracle (CPU fp32 restatement, 'port') train step / inference on a bounded sample."""
     import crnn_oracle as O
     from crnn_hip.recipe import recipe_state_dict, synthetic_batch
     torch.set_num_threads(threads)
@@ -67,6 +68,10 @@ def cpu_baseline(args, threads):
     x, _, tg, tl = synthetic_batch(args.cpu_sample, args.height, args.width, T, C, seed=99)
 
     def step():
+        if args.mode == "attn":
+            with torch.no_grad():
+                O.attn_greedy(attn_params, O.encode(x, p, O.Ctx(train=False), args.layers), 26, 1, 3, C)
+            return
         if args.mode == "infer":
             with torch.no_grad():
                 O.head(O.encode(x, p, O.Ctx(train=False), args.layers), p).argmax(-1)
@@ -83,7 +88,7 @@ def cpu_baseline(args, threads):
     dt = time.perf_counter() - t0
     return {"value": round(args.cpu_sample * args.cpu_steps / dt, 3), "unit": "text-lines/s",
             "cores": threads, "kind": "port",
-            "sample": f"oracle/crnn_oracle.py fp32 torch-CPU {'eval forward + argmax' if args.mode == 'infer' else 'train step (fwd + numpy CTC + bwd + AdamW)'}, "
+            "sample": f"oracle/crnn_oracle.py fp32 torch-CPU {'eval encode + 26-step greedy attention decode' if args.mode == 'attn' else 'eval forward + argmax' if args.mode == 'infer' else 'train step (fwd + numpy CTC + bwd + AdamW)'}, "
                       f"B={args.cpu_sample} x {args.cpu_steps} steps (+1 warm-up) at {args.height}x{args.width}, "
                       f"hidden {args.hidden}; {dt:.1f} s"}
 
@@ -136,8 +141,9 @@ def main():
     C = 194
     T = args.width // 8
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
-    model = RCNN(num_classes=C, hidden_size=args.hidden, blank_id=None, num_rnn_layers=args.layers,
-                 compute_dtype=dtype)
+    attn = args.mode == "attn"
+    model = RCNN(num_classes=C, hidden_size=args.hidden, blank_id=3 if attn else None, num_rnn_layers=args.layers,
+                 compute_dtype=dtype, decoder="attn" if attn else "ctc")
     model.load_state_dict(recipe_state_dict(O.param_shapes(args.hidden, C, args.layers), 0), strict=False)
     model = model.to(dev).train(args.mode == "train")
     x, _, tg, tl = synthetic_batch(args.batch, args.height, args.width, T, C, seed=1234 + rank)
@@ -167,7 +173,13 @@ def main():
              stream_ptr())
         return lens
 
+    def attn_step():
+        with torch.no_grad():
+            return model(x, is_train=False, batch_max_length=25)
+
     def step():
+        if args.mode == "attn":
+            return attn_step()
         if args.mode == "infer":
             return infer_step()
         eng.forward(x, train=True, save_for_backward=True, dropout_p=model.enc_dropout.p)
@@ -208,7 +220,7 @@ def main():
         divergence = float((cmax - cmin).item())
     lines = args.batch * world * args.steps
     value = lines / elapsed
-    final_loss = float(loss.float().mean().item())
+    final_loss = float(loss.float().mean().item()) if args.mode == "train" else 0.0
 
     if rank == 0:
         lstm = {k: timing.pop(k) for k in ("lstm_fwd", "lstm_bwd") if k in timing}
@@ -231,7 +243,10 @@ def main():
             "metric": (METRIC if args.mode == "train" and args.config is None else
                        "text-lines/sec (train step incl. CTC bwd), long lines: B=64/GPU, 32x1024 crops, 4x768 BiLSTM"
                        if args.mode == "train" else
-                       "text-lines/sec (inference: eval forward + greedy CTC decode), B=256, 32x256 crops, 1 MI355X"),
+                       "text-lines/sec (inference: eval forward + greedy CTC decode), B=256, 32x256 crops, 1 MI355X"
+                       if args.mode == "infer" else
+                       "text-lines/sec (inference with the attention head: eval encode + 26-step greedy attention "
+                       "decode), B=256, 32x256 crops, 1 MI355X"),
             "value": round(value, 2),
             "unit": "text-lines/s",
             "n_gpus": world,
@@ -248,7 +263,10 @@ def main():
                                                                     "configs[2]/[3])")
                                     if args.mode == "train" else
                                     f"inference: SE-ResNet31 + {args.layers}x{args.hidden} BiLSTM + CTC head, eval "
-                                    f"forward + on-device greedy decode (BASELINE configs[1])"),
+                                    f"forward + on-device greedy decode (BASELINE configs[1])"
+                                    if args.mode == "infer" else
+                                    f"inference: SE-ResNet31 + {args.layers}x{args.hidden} BiLSTM encode + the "
+                                    f"reference's attention decoder (fp32), 26 greedy steps (SURVEY 8f next-1)"),
                        "global_batch": args.batch * world, "per_gpu_batch": args.batch,
                        "crop": f"{args.height}x{args.width}", "seq_len": T, "hidden": args.hidden,
                        "rnn_layers": args.layers, "num_classes": C,
@@ -270,7 +288,9 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             try:
                 threads = min(16, os.cpu_count() or 1)
-                out["cpu_baseline"] = cpu_baseline(args, threads)
+                ap_cpu = ({k[5:]: v.detach().float().cpu() for k, v in model.state_dict().items()
+                           if k.startswith("attn.")} if attn else None)
+                out["cpu_baseline"] = cpu_baseline(args, threads, ap_cpu)
             except Exception as e:  # report, never fake
                 out["cpu_baseline"] = {"value": None, "error": repr(e)}
         print(json.dumps(out), flush=True)
