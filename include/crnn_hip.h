@@ -305,17 +305,38 @@ int crnn_lstm_seq_bwd(const void* dhseq, const void* whh_t, const void* gsv, con
  * per call sequence (host loop: crnn_hip/attn.py):
  *   crnn_gemm_nt  proj_h = h W_h2h^T + b_h2h            (proj_H = enc W_i2h^T once per decode)
  *   crnn_attn_context: alpha = softmax_t(score . tanh(proj_H[b,t] + proj_h[b])),
- *                      ctx[b][0..C) (row stride ldc) = sum_t alpha enc[b,t]; alpha optional
+ *                      ctx[b][0..C) (row stride ldc) = sum_t alpha' enc[b,t]; alpha (optional
+ *                      output) = the softmax; alpha' = alpha * mask / (1 - drop_p), the
+ *                      training-mode F.dropout(alpha) of model/model.py:38, mask element (b, t) kept
+ *                      iff splitmix64(seed ^ (b*T + t) * golden) >> 32 >= drop_p * 2^32 (0 = off)
  *   crnn_gemm_nt  gates = hx W_cat^T, hx = [ctx | h] rows, W_cat = [W_ih[:, :C] | W_hh]
  *   crnn_attn_cell: LSTMCell (i, f, g, o) with + b_ih + b_hh + W_ih[:, C + ch[b * ch_stride]]
  *                   (the one-hot input); writes h, c, hx[b][C + j] and hs (optional)
  *   crnn_gemm_nt  logits = h W_gen^T + b_gen
  *   crnn_attn_out: blank column masked to -1e4, logits -> probs_t (optional), argmax -> ch */
 int crnn_attn_context(const float* projH, const float* projh, const float* score, const float* enc, float* ctx,
-                      int ldc, float* alpha, int B, int T, int H, int C, void* stream);
+                      int ldc, float* alpha, int B, int T, int H, int C, float drop_p, unsigned long long seed,
+                      void* stream);
 int crnn_attn_cell(const float* gates, const float* b_ih, const float* b_hh, const float* w_ih, int ldw, const int* ch,
-                   int ch_stride, float* h, float* c, float* hx, int ldx, float* hs, int ld_hs, int B, int H, int C,
-                   void* stream);
+                   int ch_stride, float* h, float* c, float* hx, int ldx, float* hs, int ld_hs, float* gact, float* cs,
+                   int B, int H, int C, void* stream);
+/* backward (teacher forcing; host loop in crnn_hip/attn.py): gact = the activated gates
+ * (i f g o) and cs = c_t the forward saved (crnn_attn_cell's optional outputs), c_prev NULL at
+ * t = 0; dh = dh1 + dh2 (row strides ld1, ld2; either NULL), dc NULL = 0 -> dgates
+ * (pre-activation) and dc_prev */
+int crnn_attn_cell_bwd(const float* gact, const float* c_t, const float* c_prev, const float* dh1, int ld1,
+                       const float* dh2, int ld2, const float* dc, float* dgates, float* dc_prev, int B, int H,
+                       void* stream);
+/* attention backward for one step (block per sample): denc += alpha' dctx; dprojH += du;
+ * dprojh = sum_t du; dscore_part[b] += sum_t de tanh(u) (du, de as in csrc/attn.hip);
+ * drop_p, seed = the forward step's (the mask is regenerated, not stored) */
+int crnn_attn_bwd(const float* dctx, int lddc, const float* alpha, const float* enc, const float* projH,
+                  const float* projh, const float* score, float* denc, float* dprojH, float* dprojh,
+                  float* dscore_part, int B, int T, int H, int C, float drop_p, unsigned long long seed,
+                  void* stream);
+/* dW_ih[r][C + text[b][t]] += dgates[t][b][r] (the one-hot input columns; fp32 atomics) */
+int crnn_attn_onehot_wgrad(const float* dgates, const int* text, int text_ld, int steps, int B, int H4, float* dw_ih,
+                           int ldw, int C, void* stream);
 int crnn_attn_out(const float* logits, int ldl, int B, int V, int blank, float* probs_t, int ldp, int* ch,
                   void* stream);
 

@@ -203,14 +203,17 @@ class _CTC(torch.autograd.Function):
 # Parameters keyed by the reference's Attention state_dict (model/model.py:23-79):
 # attention_cell.{i2h.weight, h2h.weight, h2h.bias, score.weight, rnn.weight_ih, rnn.weight_hh,
 # rnn.bias_ih, rnn.bias_hh}, generator.{weight, bias}. Eval mode (dropout = identity).
-def attn_cell(p, enc, h, c, char, num_classes):
+def attn_cell(p, enc, h, c, char, num_classes, alpha_mask=None):
     """AttentionCell.forward (model/model.py:33-45): additive attention over the encoder
-    sequence, then LSTMCell([context, onehot(char)], (h, c)) (gate order i, f, g, o)."""
+    sequence, then LSTMCell([context, onehot(char)], (h, c)) (gate order i, f, g, o).
+    alpha_mask [B, T]: the training-mode F.dropout(alpha) (:40) as an explicit scaled keep-mask."""
     pre = "attention_cell."
     proj_H = enc @ p[pre + "i2h.weight"].t()                                   # :35
     proj_h = (h @ p[pre + "h2h.weight"].t() + p[pre + "h2h.bias"]).unsqueeze(1)  # :36
     e = torch.tanh(proj_H + proj_h) @ p[pre + "score.weight"].t()             # :37 [B,T,1]
     alpha = torch.softmax(e, dim=1)                                           # :39
+    if alpha_mask is not None:                                                # :40
+        alpha = alpha * alpha_mask.to(alpha.dtype).unsqueeze(2)
     context = (alpha.transpose(1, 2) @ enc).squeeze(1)                        # :42
     onehot = F.one_hot(char, num_classes).to(enc.dtype)                       # :81-85
     x = torch.cat([context, onehot], 1)                                       # :43
@@ -240,20 +243,47 @@ def attn_greedy(p, enc, steps, sos_id, blank_id, num_classes):
     return torch.stack(out, 1)
 
 
-def attn_teacher(p, enc, text, steps, blank_id, num_classes):
+def attn_teacher(p, enc, text, steps, blank_id, num_classes, alpha_masks=None):
     """Attention.forward with teacher forcing (model/model.py:114-148, sampling_prob = 0):
-    input at step t is text[:, t]; logits = generator(all h), blank masked. -> [B, steps, V]"""
+    input at step t is text[:, t]; logits = generator(all h), blank masked. -> [B, steps, V].
+    alpha_masks[t] [B, T]: step t's attention-weight dropout mask (attn_drop_masks), or None."""
     B, H = enc.shape[0], p["attention_cell.h2h.weight"].shape[0]
     h = torch.zeros(B, H, dtype=enc.dtype)
     c = torch.zeros(B, H, dtype=enc.dtype)
     hs = []
     for t in range(steps):
-        h, c = attn_cell(p, enc, h, c, text[:, t], num_classes)
+        h, c = attn_cell(p, enc, h, c, text[:, t], num_classes,
+                         None if alpha_masks is None else alpha_masks[t])
         hs.append(h)
     lg = torch.stack(hs, 1) @ p["generator.weight"].t() + p["generator.bias"]
     if blank_id is not None:
         lg[:, :, blank_id] = -1e4
     return lg
+
+
+def drop_keep_mask(seed: int, n: int, p: float) -> np.ndarray:
+    """The HIP path's counter-based dropout mask (csrc/common.hpp drop_hash): element i kept iff
+    splitmix64-finalizer(seed ^ i * golden) >> 32 >= p * 2^32; -> float64 keep / (1 - p). The
+    reference uses torch's Philox stream, which is not reproduced: masks agree in distribution,
+    so parity with dropout on is checked against this restatement of the mask."""
+    M = np.uint64(0xFFFFFFFFFFFFFFFF)
+    with np.errstate(over="ignore"):
+        i = np.arange(n, dtype=np.uint64)
+        z = np.uint64(seed & 0xFFFFFFFFFFFFFFFF) ^ (i * np.uint64(0x9E3779B97F4A7C15))
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        h = ((z ^ (z >> np.uint64(31))) & M) >> np.uint64(32)
+    t = p * 4294967296.0
+    thr = 0xFFFFFFFF if t >= 4294967295.0 else int(t)
+    return (h >= np.uint64(thr)).astype(np.float64) / (1.0 - p)
+
+
+def attn_drop_masks(seed: int, steps: int, B: int, T: int, p: float):
+    """per-step attention-weight masks of crnn_hip/attn.py run_train (step t uses seed + t,
+    element (b, t') = index b*T + t') -> list of [B, T] tensors (None when p == 0)"""
+    if p == 0.0:
+        return None
+    return [torch.from_numpy(drop_keep_mask(seed + t, B * T, p).reshape(B, T)) for t in range(steps)]
 
 
 def ctc_loss(logits_btc, targets, lengths, reduction="mean", zero_infinity=True):

@@ -23,6 +23,7 @@ vp = C.c_void_p
 i32 = C.c_int
 i64 = C.c_long
 f32 = C.c_float
+u64 = C.c_ulonglong
 sz = C.c_size_t
 
 
@@ -108,8 +109,11 @@ _SIGS = {
     "crnn_lstm_wgrad_workspace": ([i32, i32, i32, i32], sz),
     "crnn_lstm_wgrad": ([vp, vp, vp, vp, vp, vp, vp, vp, sz, i32, i32, i32, i32, i32, vp], i32),
     "crnn_lstm_dx": ([i32, vp, vp, vp, i32, i32, i32, i32, vp], i32),
-    "crnn_attn_context": ([vp, vp, vp, vp, vp, i32, vp, i32, i32, i32, i32, vp], i32),
-    "crnn_attn_cell": ([vp, vp, vp, vp, i32, vp, i32, vp, vp, vp, i32, vp, i32, i32, i32, i32, vp], i32),
+    "crnn_attn_context": ([vp, vp, vp, vp, vp, i32, vp, i32, i32, i32, i32, f32, u64, vp], i32),
+    "crnn_attn_cell": ([vp, vp, vp, vp, i32, vp, i32, vp, vp, vp, i32, vp, i32, vp, vp, i32, i32, i32, vp], i32),
+    "crnn_attn_cell_bwd": ([vp, vp, vp, vp, i32, vp, i32, vp, vp, vp, i32, i32, vp], i32),
+    "crnn_attn_bwd": ([vp, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, f32, u64, vp], i32),
+    "crnn_attn_onehot_wgrad": ([vp, vp, i32, i32, i32, i32, vp, i32, i32, vp], i32),
     "crnn_attn_out": ([vp, i32, i32, i32, i32, vp, i32, vp, vp], i32),
     "crnn_ctc_loss": ([vp, i32, i32, i32, i32, vp, i32, vp, vp, vp, i32, vp], i32),
     "crnn_ctc_reduce_mean": ([vp, vp, i32, vp, vp], i32),

@@ -5,7 +5,10 @@ The host loop runs one decoder step as 3 GEMMs (crnn_gemm_nt) + 3 small kernels
 (csrc/attn.hip): proj_h, attention context, gates (one GEMM over [context | h]), the LSTM cell
 with the one-hot input folded in as a weight column, logits, blank mask + argmax. The encoder
 projection proj_H = enc W_i2h^T is computed once per decode. Forward only (inference and
-teacher-forced logits); the decoder's backward is not on the HIP path yet.
+teacher-forced logits) and the teacher-forced backward (BPTT through the cell and the attention,
+run_train / backward): per step a cell-backward kernel, one GEMM for d[context | h], an attention
+backward kernel and one GEMM for the h2h path; the weight gradients are batched GEMMs over all
+steps afterwards (the one-hot columns of W_ih by an atomic scatter).
 """
 from __future__ import annotations
 
@@ -24,6 +27,7 @@ class AttnDecoderHIP:
     def __init__(self, params: Dict[str, torch.Tensor], num_classes: int, sos_id: int,
                  blank_id: Optional[int], device):
         self.device = torch.device(device)
+        self._saved = None
         self.V = num_classes
         self.Vpad = (num_classes + 7) // 8 * 8
         self.sos_id = sos_id
@@ -52,6 +56,119 @@ class AttnDecoderHIP:
     def _gemm(self, a, lda, w, ldw, out, ldo, bias, M, N, K):
         call("crnn_gemm_nt", L.F32, ptr(a), lda, ptr(w), ldw, ptr(out), ldo, ptr(bias), M, N, K, 1, 0,
              L.stream_ptr())
+
+    def run_train(self, enc: torch.Tensor, steps: int, text: torch.Tensor, drop_p: float = 0.0,
+                  seed: int = 0) -> torch.Tensor:
+        """teacher-forced forward that saves what backward() needs -> logits [B, steps, V].
+        drop_p: the training-mode F.dropout on the attention weights (model/model.py:38; the
+        reference's RCNN uses 0.1); step t's mask comes from the counter hash with seed + t."""
+        enc = enc.to(self.device, torch.float32).contiguous()
+        B, T, C = enc.shape
+        H, V, Vp, dev = self.H, self.V, self.Vpad, self.device
+        s = L.stream_ptr()
+        txt = text.to(dev, torch.int32).contiguous()
+        if txt.shape[1] < steps:
+            raise ValueError("text needs batch_max_length + 1 columns")
+        projH = torch.empty(B * T, H, device=dev)
+        self._gemm(enc, C, self.w_i2h, C, projH, H, None, B * T, H, C)
+        Xs = torch.zeros(steps + 1, B, C + H, device=dev)   # [context_t | h_{t-1}] per step
+        Gs = torch.empty(steps, B, 4 * H, device=dev)       # activated gates
+        Cs = torch.empty(steps, B, H, device=dev)           # cell states
+        Ph = torch.empty(steps, B, H, device=dev)           # proj_h per step
+        As = torch.empty(steps, B, T, device=dev)           # attention weights per step
+        hs = torch.empty(B, steps, H, device=dev)
+        h = torch.zeros(B, H, device=dev)
+        c = torch.zeros(B, H, device=dev)
+        gates = torch.empty(B, 4 * H, device=dev)
+        for t in range(steps):
+            self._gemm(h, H, self.w_h2h, H, Ph[t], H, self.b_h2h, B, H, H)
+            call("crnn_attn_context", ptr(projH), ptr(Ph[t]), ptr(self.score), ptr(enc), ptr(Xs[t]), C + H,
+                 ptr(As[t]), B, T, H, C, drop_p, (seed + t) & (2 ** 64 - 1), s)
+            self._gemm(Xs[t], C + H, self.w_cat, C + H, gates, 4 * H, None, B, 4 * H, C + H)
+            call("crnn_attn_cell", ptr(gates), ptr(self.b_ih), ptr(self.b_hh), ptr(self.w_ih), C + V, ptr(txt[:, t:]),
+                 txt.shape[1], ptr(h), ptr(c), ptr(Xs[t + 1]), C + H, ptr(hs[:, t]), steps * H, ptr(Gs[t]), ptr(Cs[t]),
+                 B, H, C, s)
+        lg = torch.empty(B * steps, Vp, device=dev)
+        self._gemm(hs, H, self.w_gen, H, lg, Vp, self.b_gen, B * steps, Vp, H)
+        out = torch.empty(B, steps, V, device=dev)
+        scratch = torch.empty(B * steps, dtype=torch.int32, device=dev)
+        call("crnn_attn_out", ptr(lg), Vp, B * steps, V, self.blank, ptr(out), V, ptr(scratch), s)
+        self._saved = dict(enc=enc, projH=projH, Xs=Xs, Gs=Gs, Cs=Cs, Ph=Ph, As=As, hs=hs, txt=txt, steps=steps,
+                           drop=(drop_p, seed))
+        return out
+
+    def backward(self, dlogits: torch.Tensor, grads: Dict[str, torch.Tensor], accumulate: bool) -> torch.Tensor:
+        """BPTT of run_train's forward. dlogits [B, steps, V]; grads: fp32 tensors keyed by the
+        reference's Attention parameter names, written (or added to, if accumulate). -> d enc [B, T, C]"""
+        sv = self._saved
+        if sv is None:
+            raise RuntimeError("run_train must precede backward")
+        enc, projH, Xs, Gs, Cs, Ph, As, hs, txt, steps = (sv[k] for k in
+                                                           ("enc", "projH", "Xs", "Gs", "Cs", "Ph", "As", "hs", "txt",
+                                                            "steps"))
+        drop_p, seed = sv["drop"]
+        B, T, C = enc.shape
+        H, V, Vp, dev, s = self.H, self.V, self.Vpad, self.device, L.stream_ptr()
+        F32 = L.F32
+        dL = torch.zeros(B * steps, Vp, device=dev)
+        dL[:, :V] = dlogits.reshape(B * steps, V).to(dev, torch.float32)
+        if self.blank >= 0:
+            dL[:, self.blank] = 0.0   # the masked column is a constant (model/model.py:87-89)
+        dHs = torch.empty(B * steps, H, device=dev)
+        call("crnn_gemm_nn", F32, ptr(dL), Vp, ptr(self.w_gen), H, ptr(dHs), H, B * steps, H, Vp, 1, 0, s)
+        gw = torch.empty(Vp, H, device=dev)
+        call("crnn_gemm_tn", F32, ptr(dL), Vp, ptr(hs), H, ptr(gw), H, Vp, H, B * steps, 0, s)
+        gb = torch.empty(Vp, device=dev)
+        call("crnn_colsum", F32, ptr(dL), Vp, B * steps, Vp, ptr(gb), 0, 1, s)
+        dG = torch.empty(steps, B, 4 * H, device=dev)
+        dPh = torch.empty(steps, B, H, device=dev)
+        denc = torch.zeros(B, T, C, device=dev)
+        dProjH = torch.zeros(B * T, H, device=dev)
+        dscore = torch.zeros(B, H, device=dev)
+        dX = torch.empty(B, C + H, device=dev)
+        dc = [torch.zeros(B, H, device=dev), torch.empty(B, H, device=dev)]
+        dh_rec, ld_rec = None, 0
+        for t in reversed(range(steps)):
+            call("crnn_attn_cell_bwd", ptr(Gs[t]), ptr(Cs[t]), ptr(Cs[t - 1]) if t > 0 else None, ptr(dh_rec), ld_rec,
+                 ptr(dHs.view(B, steps, H)[:, t]), steps * H, ptr(dc[0]), ptr(dG[t]), ptr(dc[1]), B, H, s)
+            dc.reverse()
+            call("crnn_gemm_nn", F32, ptr(dG[t]), 4 * H, ptr(self.w_cat), C + H, ptr(dX), C + H, B, C + H, 4 * H, 1, 0, s)
+            call("crnn_attn_bwd", ptr(dX), C + H, ptr(As[t]), ptr(enc), ptr(projH), ptr(Ph[t]), ptr(self.score),
+                 ptr(denc), ptr(dProjH), ptr(dPh[t]), ptr(dscore), B, T, H, C, drop_p,
+                 (seed + t) & (2 ** 64 - 1), s)
+            # dh_{t-1} = d(h part of [context | h]) + dproj_h W_h2h   (accumulated into dX[:, C:])
+            call("crnn_gemm_nn", F32, ptr(dPh[t]), H, ptr(self.w_h2h), H, ptr(dX[:, C:]), C + H, B, H, H, 1, 1, s)
+            # stream order: step t-1's cell backward reads dh_rec before its GEMM rewrites dX
+            dh_rec, ld_rec = dX[:, C:], C + H
+        # weight gradients, batched over steps
+        wcat = torch.empty(4 * H, C + H, device=dev)
+        call("crnn_gemm_tn", F32, ptr(dG), 4 * H, ptr(Xs), C + H, ptr(wcat), C + H, 4 * H, C + H, steps * B, 0, s)
+        dwih = torch.zeros(4 * H, C + V, device=dev)
+        dwih[:, :C] = wcat[:, :C]
+        call("crnn_attn_onehot_wgrad", ptr(dG), ptr(txt), txt.shape[1], steps, B, 4 * H, ptr(dwih), C + V, C, s)
+        db = torch.empty(4 * H, device=dev)
+        call("crnn_colsum", F32, ptr(dG), 4 * H, steps * B, 4 * H, ptr(db), 0, 1, s)
+        wh2h = torch.empty(H, H, device=dev)
+        call("crnn_gemm_tn", F32, ptr(dPh), H, ptr(Xs[:, :, C:]), C + H, ptr(wh2h), H, H, H, steps * B, 0, s)
+        bh2h = torch.empty(H, device=dev)
+        call("crnn_colsum", F32, ptr(dPh), H, steps * B, H, ptr(bh2h), 0, 1, s)
+        wi2h = torch.empty(H, C, device=dev)
+        call("crnn_gemm_tn", F32, ptr(dProjH), H, ptr(enc), C, ptr(wi2h), C, H, C, B * T, 0, s)
+        call("crnn_gemm_nn", F32, ptr(dProjH), H, ptr(self.w_i2h), C, ptr(denc), C, B * T, C, H, 1, 1, s)
+        dsc = torch.empty(H, device=dev)
+        call("crnn_colsum", F32, ptr(dscore), H, B, H, ptr(dsc), 0, 1, s)
+        pre = "attention_cell."
+        out = {pre + "i2h.weight": wi2h, pre + "h2h.weight": wh2h, pre + "h2h.bias": bh2h,
+               pre + "score.weight": dsc.view(1, H), pre + "rnn.weight_ih": dwih, pre + "rnn.weight_hh": wcat[:, C:],
+               pre + "rnn.bias_ih": db, pre + "rnn.bias_hh": db, "generator.weight": gw[:V], "generator.bias": gb[:V]}
+        for k, v in out.items():
+            g = grads[k]
+            if accumulate:
+                g.add_(v.reshape(g.shape))
+            else:
+                g.copy_(v.reshape(g.shape))
+        self._saved = None
+        return denc
 
     def run(self, enc: torch.Tensor, steps: int, text: Optional[torch.Tensor] = None) -> torch.Tensor:
         """enc [B, T, C] -> logits [B, steps, V] (fp32): greedy decode (text None, model/model.py:91-112)
@@ -95,7 +212,7 @@ class AttnDecoderHIP:
         H, C, s = self.H, self.C, L.stream_ptr()
         self._gemm(h, H, self.w_h2h, H, projh, H, self.b_h2h, B, H, H)
         call("crnn_attn_context", ptr(projH), ptr(projh), ptr(self.score), ptr(enc), ptr(hx), C + H, None,
-             B, T, H, C, s)
+             B, T, H, C, 0.0, 0, s)
         self._gemm(hx, C + H, self.w_cat, C + H, gates, 4 * H, None, B, 4 * H, C + H)
         call("crnn_attn_cell", ptr(gates), ptr(self.b_ih), ptr(self.b_hh), ptr(self.w_ih), C + self.V, ptr(ch),
-             ch_stride, ptr(h), ptr(c), ptr(hx), C + H, ptr(hs), ld_hs, B, H, C, s)
+             ch_stride, ptr(h), ptr(c), ptr(hx), C + H, ptr(hs), ld_hs, None, None, B, H, C, s)

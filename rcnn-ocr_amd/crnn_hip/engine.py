@@ -588,13 +588,16 @@ class CRNNEngine:
         upd(self.co1, h, w)
         return cap
 
-    def backward(self, dlogits: torch.Tensor, grads: Dict[str, torch.Tensor], accumulate: bool = False,
-                 stage_done=None):
+    def backward(self, dlogits: Optional[torch.Tensor], grads: Dict[str, torch.Tensor], accumulate: bool = False,
+                 stage_done=None, denc: Optional[torch.Tensor] = None):
         """Full backward from d loss / d logits [B,T,Cpad] fp32 into `grads` (fp32, reference layouts).
         stage_done(prefixes): called (host side, after the stage's kernels are enqueued) each time the
         gradients of every parameter under the given name prefixes are final — CTC head + BiLSTM, then
         conv_out, each residual block (last to first), the stem — so a data-parallel caller can start
-        their all-reduce while the rest of the backward runs."""
+        their all-reduce while the rest of the backward runs.
+        denc: instead of dlogits, d loss / d encoder output [B,T,hidden] (fp32; the attention
+        decoder's backward, crnn_hip/attn.py) — the CTC head is skipped (its grads are zeroed
+        unless accumulating)."""
         done = stage_done if stage_done is not None else (lambda prefixes: None)
         sv = self._saved
         if sv is None:
@@ -608,18 +611,40 @@ class CRNNEngine:
         self._wg_cap = self._wgrad_capacity(B, st["H"], st["W"])
         acc = 1 if accumulate else 0
         M = B * Tn
+        dx = ws.get("rnn.dx_head", (B, Tn, Hd), T)
+        if denc is not None:   # attention decoder: the gradient enters at the encoder output
+            if tuple(denc.shape) != (B, Tn, Hd) or denc.dtype != torch.float32 or not denc.is_contiguous():
+                raise ValueError("denc must be contiguous fp32 [B, T, hidden]")
+            call("crnn_cast_f32", dt, ptr(denc), ptr(dx), M * Hd, s)
+            if not accumulate:
+                grads["ctc_head.weight"].zero_()
+                grads["ctc_head.bias"].zero_()
+        else:
+            self._head_backward(dlogits, grads, acc, dx)
+        if sv["drop"] is not None:  # enc_dropout backward: the forward's mask, from its seed
+            call("crnn_dropout", dt, ptr(dx), ptr(dx), M * Hd, sv["drop"][0], sv["drop"][1], s)
+        self._backward_encoder(dx, grads, acc, done)
+
+    def _head_backward(self, dlogits, grads, acc, dx):
+        sv, ws, dt, T, s = self._saved, self.ws, self.dt, self.dtype, L.stream_ptr()
+        B, Tn, Hd = sv["B"], sv["T"], self.H
+        M = B * Tn
         # ---- CTC head
         dlT = ws.get("head.dlT", (B, Tn, self.Cpad), T)
         call("crnn_cast_f32", dt, ptr(dlogits), ptr(dlT), M * self.Cpad, s)
         hw_g = ws.get("head.dw", (self.Cpad, Hd), torch.float32)
         self._gemm_tn(dlT, self.Cpad, sv["enc"], Hd, hw_g, Hd, self.Cpad, Hd, M, 0)
-        self._store_grad("ctc_head.weight", hw_g[: self.C], accumulate)
+        self._store_grad("ctc_head.weight", hw_g[: self.C], bool(acc))
         call("crnn_colsum", L.F32, ptr(dlogits), self.Cpad, M, self.C, ptr(grads["ctc_head.bias"]), acc, 1, s)
-        dx = ws.get("rnn.dx_head", (B, Tn, Hd), T)
         call("crnn_gemm_nn", dt, ptr(dlT), self.Cpad, ptr(self.packed["head.w"]), Hd, ptr(dx), Hd, M, Hd,
              self.Cpad, 0, 0, s)
-        if sv["drop"] is not None:  # enc_dropout backward: the forward's mask, from its seed
-            call("crnn_dropout", dt, ptr(dx), ptr(dx), M * Hd, sv["drop"][0], sv["drop"][1], s)
+
+    def _backward_encoder(self, dx, grads, acc, done):
+        sv, ws, dt, T, s = self._saved, self.ws, self.dt, self.dtype, L.stream_ptr()
+        B, Tn, Hd = sv["B"], sv["T"], self.H
+        M = B * Tn
+        accumulate = self.accumulate
+        st = sv["stem"]
         # ---- BiLSTM stack, reverse
         for l in reversed(range(self.nl)):
             pre = f"enc_rnn.{l}"

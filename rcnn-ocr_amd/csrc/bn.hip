@@ -980,14 +980,7 @@ __global__ __launch_bounds__(256) void pack_batch_kernel(const crnn_pack_job* __
 // Counter-based: element i of a call with seed s is kept iff hash(s, i) >= p * 2^32, so the
 // backward regenerates the forward's mask from (seed, index) and nothing is stored. The hash is
 // splitmix64's finalizer on s ^ (i * golden ratio); torch's Philox stream is not reproduced (the
-// masks are equal in distribution, not bit for bit).
-__device__ __forceinline__ uint32_t drop_hash(unsigned long long seed, unsigned long long i) {
-  unsigned long long z = seed ^ (i * 0x9E3779B97F4A7C15ull);
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  return (uint32_t)((z ^ (z >> 31)) >> 32);
-}
-
+// masks are equal in distribution, not bit for bit). drop_hash: common.hpp.
 template <typename T>
 __global__ void dropout_kernel(const T* __restrict__ x, T* __restrict__ y, long n, uint32_t thr, float scale,
                                unsigned long long seed) {
@@ -1666,8 +1659,7 @@ int crnn_nchw_to_nhwc(int dtype, const float* x, void* y, int B, int C, int H, i
 
 int crnn_dropout(int dtype, const void* x, void* y, long n, float p, unsigned long long seed, void* stream) {
   if (!(p >= 0.f && p < 1.f)) return crnn_set_error(hipErrorInvalidValue, "dropout: p must be in [0, 1)");
-  const double t = (double)p * 4294967296.0;
-  const uint32_t thr = t >= 4294967295.0 ? 0xffffffffu : (uint32_t)t;
+  const uint32_t thr = drop_threshold(p);
   DISPATCH(dtype, hipLaunchKernelGGL(dropout_kernel<T>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream,
                                      (const T*)x, (T*)y, n, thr, 1.f / (1.f - p), seed));
   return (int)hipGetLastError();

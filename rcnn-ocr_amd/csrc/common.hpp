@@ -144,6 +144,19 @@ __device__ __forceinline__ int xcd_remap(int b, int nwg) {
 // ---- range-checked buffer loads (CDNA raw buffer addressing)
 // A lane whose byte offset is >= the descriptor's num_records reads zeros in hardware,
 // so masked / out-of-bounds gathers need no exec-mask branches.
+// counter-based dropout hash (enc_dropout in bn.hip, attention-weight dropout in attn.hip):
+// splitmix64's finalizer on seed ^ (i * golden ratio); element i is kept iff hash >= p * 2^32
+__device__ __forceinline__ uint32_t drop_hash(unsigned long long seed, unsigned long long i) {
+  unsigned long long z = seed ^ (i * 0x9E3779B97F4A7C15ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return (uint32_t)((z ^ (z >> 31)) >> 32);
+}
+__host__ inline uint32_t drop_threshold(float p) {
+  const double t = (double)p * 4294967296.0;
+  return t >= 4294967295.0 ? 0xffffffffu : (uint32_t)t;
+}
+
 constexpr uint32_t OOB = 0x80000000u;
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 

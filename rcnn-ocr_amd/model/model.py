@@ -64,6 +64,34 @@ class _EncodeFn(torch.autograd.Function):
         return None, None, None, None
 
 
+class _AttnTrainFn(torch.autograd.Function):
+    """images, text -> teacher-forced attention logits [B, steps, V]; backward: the decoder's BPTT
+    (crnn_hip/attn.py) hands d enc to the engine's encoder backward (model/model.py:223-227)."""
+
+    @staticmethod
+    def forward(ctx, anchor, images, text, model, steps):
+        eng = model._engine_for(images)
+        p = model.enc_dropout.p if model.training else 0.0
+        eng.forward(images, train=model.training, save_for_backward=True, update_running=model.training,
+                    dropout_p=p)
+        key = "enc.drop" if p > 0.0 else f"r{model.num_rnn_layers - 1}.out"
+        enc = eng.ws.bufs[key].float()
+        dec = model._attn_decoder(enc.device)
+        ap = model.attn_dropout_p if model.training else 0.0
+        model._attn_seed = (model._attn_seed + 0x9E3779B97F4A7C15) & (2 ** 64 - 1)
+        ctx.model = model
+        return dec.run_train(enc, steps, text, drop_p=ap, seed=model._attn_seed)
+
+    @staticmethod
+    def backward(ctx, grad_logits):
+        model = ctx.model
+        grads, accumulate = model._grad_views()
+        attn_grads = {k[len("attn."):]: v for k, v in grads.items() if k.startswith("attn.")}
+        denc = model._attn_dec.backward(grad_logits.contiguous(), attn_grads, accumulate)
+        model._engine.backward(None, grads, accumulate=accumulate, denc=denc)
+        return None, None, None, None, None
+
+
 class _AttentionCellParams(nn.Module):
     """parameter holder with model/model.py:24-31's names (AttentionCell)."""
 
@@ -108,10 +136,12 @@ class RCNN(nn.Module):
         self.enc_dropout = nn.Dropout(enc_dropout_p)
         self.ctc_head = nn.Linear(hidden_size, num_classes)
         # the reference's attention head (model/model.py:23-79, :203-213): parameter holder with the
-        # reference's state_dict names; compute on the HIP path (crnn_hip/attn.py), forward only
+        # reference's state_dict names; compute on the HIP path (crnn_hip/attn.py), forward + backward
         self.attn = _AttentionParams(hidden_size, hidden_size, num_classes) if decoder == "attn" else None
         self._attn_dec = None
         self._attn_version = None
+        self.attn_dropout_p = 0.1    # Attention(dropout_p=0.1) in the reference RCNN (model/model.py:203-213)
+        self._attn_seed = 0x5EED
         self._engine: Optional[CRNNEngine] = None
         self._flat_param: Optional[torch.Tensor] = None
         self._flat_grad: Optional[torch.Tensor] = None
@@ -195,24 +225,31 @@ class RCNN(nn.Module):
         self.mark_params_changed()
         return r
 
-    def _attn_forward(self, x, text, is_train, batch_max_length):
+    def _attn_decoder(self, device):
         from crnn_hip.attn import AttnDecoderHIP
-        if torch.is_grad_enabled() and self.training and any(p.requires_grad for p in self.attn.parameters()):
-            raise NotImplementedError("attention decoder training needs its backward, which is not on the HIP "
-                                      "path yet (SURVEY.md §8(f) next-1: forward only); use torch.no_grad() "
-                                      "or decoder='ctc'")
-        enc = self.encode(x)
         ver = sum(p._version for p in self.attn.parameters())
-        if self._attn_dec is None or self._attn_version != ver or self._attn_dec.device != enc.device:
+        if self._attn_dec is None or self._attn_version != ver or self._attn_dec.device != device:
             params = {k: v for k, v in self.attn.state_dict().items()}
-            self._attn_dec = AttnDecoderHIP(params, self.num_classes, self.sos_id, self.blank_id, enc.device)
+            if self._attn_dec is not None and self._attn_dec.device == device:
+                self._attn_dec.refresh(params)
+            else:
+                self._attn_dec = AttnDecoderHIP(params, self.num_classes, self.sos_id, self.blank_id, device)
             self._attn_version = ver
+        return self._attn_dec
+
+    def _attn_forward(self, x, text, is_train, batch_max_length):
         steps = batch_max_length + 1
-        if not is_train:
-            return self._attn_dec.run(enc, steps)
-        if text is None:
+        if is_train and text is None:
             raise ValueError("For training, `text` with <SOS> at text[:,0] is required")
-        return self._attn_dec.run(enc, steps, text=text)
+        anchor = next(self.parameters())
+        if is_train and torch.is_grad_enabled() and anchor.requires_grad:
+            self._engine_for(x)
+            return _AttnTrainFn.apply(anchor, x, text, self, steps)
+        enc = self.encode(x)
+        dec = self._attn_decoder(enc.device)
+        if not is_train:
+            return dec.run(enc, steps)
+        return dec.run(enc, steps, text=text)
 
     # ------------------------------------------------------------------ reference API
     def encode(self, x):
@@ -228,8 +265,9 @@ class RCNN(nn.Module):
         """decoder='ctc': CTC logits [B, T, num_classes] (fp32); `text` / `batch_max_length` are
         ignored (CTC is alignment-free). decoder='attn': the reference's RCNN.forward
         (model/model.py:223-227) — greedy-decode logits [B, batch_max_length+1, num_classes] when
-        is_train is False, teacher-forced logits from `text` (<SOS> at text[:, 0]) otherwise; forward
-        only on the HIP path (the attention decoder's backward is not implemented)."""
+        is_train is False, teacher-forced logits from `text` (<SOS> at text[:, 0]) otherwise; with
+        grad enabled the teacher-forced path is differentiable end to end (decoder BPTT + encoder
+        backward on the HIP path; attention-weight dropout p=attn_dropout_p in training mode)."""
         if self.decoder == "attn":
             return self._attn_forward(x, text, is_train, batch_max_length)
         self._engine_for(x)

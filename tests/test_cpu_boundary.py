@@ -61,8 +61,9 @@ def test_refuses_cpu_tensors():
 
 def test_attention_decoder_surface():
     """decoder='attn' carries the reference's Attention parameter names (model/model.py:24-79,
-    the keys of tests/golden/attn_decoder.npz under `attn.`) so its checkpoints load; its forward is
-    HIP-only and training (backward) is refused; other decoders are rejected."""
+    the keys of tests/golden/attn_decoder.npz under `attn.`) so its checkpoints load; forward and
+    training are HIP-only (a CPU tensor raises, no fallback); a training call without `text` is
+    rejected as in the reference; other decoders are rejected."""
     import numpy as np
     from helpers import GOLDEN
     from model.model import RCNN
@@ -72,8 +73,10 @@ def test_attention_decoder_surface():
     got = {k: tuple(v.shape) for k, v in m.state_dict().items() if k.startswith("attn.")}
     assert got == {k: tuple(v) for k, v in want.items()}
     m.train()
-    with pytest.raises(NotImplementedError):
+    with pytest.raises(RuntimeError, match="HIP device"):
         m(torch.zeros(1, 3, 32, 64), text=torch.ones(1, 26, dtype=torch.long))
+    with pytest.raises(ValueError):
+        m(torch.zeros(1, 3, 32, 64), text=None, is_train=True)
     with pytest.raises(ValueError):
         RCNN(num_classes=10, decoder="transformer")
 

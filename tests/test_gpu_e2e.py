@@ -373,3 +373,88 @@ def test_rcnn_attn_model_eval_matches_oracle():
     assert torch.equal(probs.argmax(-1), ref.argmax(-1))
     reft = O.attn_teacher(pa, enc, text, 10, 3, 194)
     assert float((tf - reft).abs().max()) < 1e-2 * float(reft.abs().max())
+
+
+def _attn_params64(z):
+    return {k: torch.from_numpy(z[k]).double() for k in z.files if k.startswith(("attention_cell.", "generator."))}
+
+
+@pytest.mark.parametrize("drop_p", [0.0, 0.3])
+def test_attn_decoder_backward_matches_oracle(drop_p):
+    """Attention decoder BPTT on the HIP path (AttnDecoderHIP.run_train / backward: cell, attention
+    and one-hot kernels + GEMMs) vs fp64 autograd through the oracle's attn_teacher
+    (model/model.py:33-45, :114-148) on the reference-generated weights (attn_decoder.npz), with
+    the attention-weight dropout off and on (mask = crnn_oracle.attn_drop_masks, the same hash):
+    logits, d enc and every parameter gradient within 1e-4 (relative, fp32 path vs fp64)."""
+    from crnn_hip.attn import AttnDecoderHIP
+    z = load("attn_decoder.npz")
+    p64 = _attn_params64(z)
+    B, T, C, steps, V, seed = 5, 24, p64["attention_cell.i2h.weight"].shape[1], 12, 194, 1234
+    g = torch.Generator().manual_seed(11)
+    enc = torch.randn(B, T, C, generator=g, dtype=torch.float64)
+    text = torch.randint(4, V, (B, steps), generator=g)
+    text[:, 0] = 1
+    gout = torch.randn(B, steps, V, generator=g, dtype=torch.float64)
+    dec = AttnDecoderHIP({k: v.float() for k, v in p64.items()}, V, 1, 3, DEV)
+    lg = dec.run_train(enc.float().to(DEV), steps, text.to(DEV), drop_p=drop_p, seed=seed)
+    grads = {k: torch.zeros(v.shape, device=DEV) for k, v in p64.items()}
+    denc = dec.backward(gout.float().to(DEV), grads, accumulate=False).cpu().double()
+    pr = {k: v.clone().requires_grad_(True) for k, v in p64.items()}
+    e = enc.clone().requires_grad_(True)
+    ref = O.attn_teacher(pr, e, text, steps, 3, V, O.attn_drop_masks(seed, steps, B, T, drop_p))
+    (ref * gout).sum().backward()
+    rel = lambda a, b: float((a - b).norm() / (b.norm() + 1e-30))  # noqa: E731
+    assert rel(lg.cpu().double(), ref.detach()) < 1e-5
+    errs = {k: rel(grads[k].cpu().double(), pr[k].grad) for k in pr}
+    errs["enc"] = rel(denc, e.grad)
+    print("attn backward rel errors:", errs)
+    assert max(errs.values()) < 1e-4, errs
+    # accumulate = True adds
+    lg = dec.run_train(enc.float().to(DEV), steps, text.to(DEV), drop_p=drop_p, seed=seed)
+    dec.backward(gout.float().to(DEV), grads, accumulate=True)
+    for k in pr:
+        assert rel(grads[k].cpu().double(), 2 * pr[k].grad) < 1e-4, k
+
+
+def test_rcnn_attn_train_step_matches_oracle():
+    """RCNN(decoder='attn') training step end to end on the HIP path (fp32): encoder forward
+    (train-mode BN) -> teacher-forced decoder -> cross-entropy -> decoder BPTT -> encoder
+    backward, vs fp64 autograd through the oracle (encode + attn_teacher) taking the HIP
+    forward's ReLU / max-pool decisions (tests/blockcheck.py): every parameter gradient within
+    1e-4; the CTC head (unused by this loss) gets zero gradients."""
+    from blockcheck import hip_decisions
+    from crnn_hip.recipe import recipe_state_dict, synthetic_batch
+    from model.model import RCNN
+    z = load("attn_decoder.npz")
+    sd = recipe_state_dict(O.param_shapes(64, 194), 17)
+    for k in z.files:
+        if k.startswith(("attention_cell.", "generator.")):
+            sd["attn." + k] = torch.from_numpy(z[k])
+    m = RCNN(num_classes=194, hidden_size=64, blank_id=3, decoder="attn", compute_dtype=torch.float32,
+             enc_dropout_p=0.0)
+    m.attn_dropout_p = 0.0
+    missing, unexpected = m.load_state_dict(sd, strict=False)
+    assert not unexpected, unexpected
+    m = m.to(DEV).train()
+    x, _, _, _ = synthetic_batch(3, 32, 128, 16, 194, seed=18)
+    text = torch.randint(4, 194, (3, 10), generator=torch.Generator().manual_seed(5))
+    text[:, 0] = 1
+    logits = m(x.to(DEV), text=text.to(DEV), is_train=True, batch_max_length=9)
+    tgt = torch.roll(text, -1, 1).to(DEV)   # next-token targets; CrossEntropyLoss as training/train.py:289,503
+    loss = torch.nn.functional.cross_entropy(logits.reshape(-1, 194), tgt.reshape(-1))
+    loss.backward()
+    torch.cuda.synchronize()
+    params = dict(m.named_parameters())
+    p = {k: (v.double().clone().requires_grad_(True) if v.is_floating_point() and "running" not in k
+             else (v.double() if v.is_floating_point() else v)) for k, v in sd.items()}
+    enc = O.encode(x.double(), p, O.Ctx(train=True, force=hip_decisions(m._engine)))
+    pa = {k[5:]: v for k, v in p.items() if k.startswith("attn.")}
+    ref = O.attn_teacher(pa, enc, text, 10, 3, 194)
+    rl = torch.nn.functional.cross_entropy(ref.reshape(-1, 194), tgt.cpu().reshape(-1))
+    assert abs(float(loss) - float(rl)) < 1e-5 * abs(float(rl))
+    rl.backward()
+    errs = sorted(((float((params[k].grad.double().cpu() - v.grad).norm() / (v.grad.norm() + 1e-30)), k)
+                   for k, v in p.items() if getattr(v, "grad", None) is not None), reverse=True)
+    print("attn train grad error vs fp64 (HIP decisions): max", errs[0], "median", errs[len(errs) // 2][0])
+    assert errs[0][0] < 1e-4, errs[:5]
+    assert float(params["ctc_head.weight"].grad.abs().max()) == 0.0

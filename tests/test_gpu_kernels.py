@@ -256,6 +256,10 @@ def test_dropout_mask(dtype):
     y0 = torch.empty_like(x)
     L.call("crnn_dropout", dt, x.data_ptr(), y0.data_ptr(), n, 0.0, 7, st)
     assert torch.equal(y0, x)
+    # the mask is exactly the oracle's restatement of the hash (crnn_oracle.drop_keep_mask)
+    import crnn_oracle as O
+    ref = torch.from_numpy(O.drop_keep_mask(7, n, p) != 0).to(DEV)
+    assert torch.equal(k, ref)
 
 
 @pytest.mark.parametrize("BHWC", [(6, 40, 256), (5, 128, 512)])
