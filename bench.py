@@ -41,10 +41,11 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=32, help="batch of the CPU baseline sample")
     ap.add_argument("--cpu-steps", type=int, default=6)
-    ap.add_argument("--mode", default="train", choices=["train", "infer", "attn"],
+    ap.add_argument("--mode", default="train", choices=["train", "infer", "attn", "attn_train"],
                     help="train: BASELINE configs[2]/[3] (the headline); infer: configs[1] (eval forward + greedy "
                          "CTC decode on device); attn: eval encode + the reference's attention head, 26-step greedy "
-                         "decode (SURVEY 8f next-1)")
+                         "decode (SURVEY 8f next-1); attn_train: the reference's own training step (encoder + "
+                         "teacher-forced attention decoder, 26 steps, cross-entropy, backward, AdamW)")
     ap.add_argument("--config", default=None, choices=["long"],
                     help="long: BASELINE configs[4] shapes (32x1024 crops, 4x768 BiLSTM, batch 64/GPU)")
     a = ap.parse_args()
@@ -63,14 +64,25 @@ def cpu_baseline(args, threads, attn_params=None):
     sd = recipe_state_dict(O.param_shapes(args.hidden, C, args.layers), 0)
     p = {k: (v.clone().requires_grad_(True) if v.is_floating_point() and "running" not in k else v)
          for k, v in sd.items()}
+    ap = None
+    if attn_params is not None:
+        ap = {k: v.clone().requires_grad_(args.mode == "attn_train") for k, v in attn_params.items()}
     params = [v for v in p.values() if getattr(v, "requires_grad", False)]
+    params += [v for v in (ap or {}).values() if v.requires_grad]
     opt = torch.optim.AdamW(params, lr=1e-4)
     x, _, tg, tl = synthetic_batch(args.cpu_sample, args.height, args.width, T, C, seed=99)
+    text, ty = attn_text(tg, tl, args.cpu_sample)
 
     def step():
         if args.mode == "attn":
             with torch.no_grad():
                 O.attn_greedy(attn_params, O.encode(x, p, O.Ctx(train=False), args.layers), 26, 1, 3, C)
+            return
+        if args.mode == "attn_train":
+            opt.zero_grad(set_to_none=True)
+            lg = O.attn_teacher(ap, O.encode(x, p, O.Ctx(train=True), args.layers), text, 26, 3, C)
+            torch.nn.functional.cross_entropy(lg.reshape(-1, C), ty.reshape(-1), ignore_index=0).backward()
+            opt.step()
             return
         if args.mode == "infer":
             with torch.no_grad():
@@ -88,9 +100,26 @@ def cpu_baseline(args, threads, attn_params=None):
     dt = time.perf_counter() - t0
     return {"value": round(args.cpu_sample * args.cpu_steps / dt, 3), "unit": "text-lines/s",
             "cores": threads, "kind": "port",
-            "sample": f"oracle/crnn_oracle.py fp32 torch-CPU {'eval encode + 26-step greedy attention decode' if args.mode == 'attn' else 'eval forward + argmax' if args.mode == 'infer' else 'train step (fwd + numpy CTC + bwd + AdamW)'}, "
+            "sample": f"oracle/crnn_oracle.py fp32 torch-CPU {'train step (fwd + teacher-forced attention decode + CE + bwd + AdamW)' if args.mode == 'attn_train' else 'eval encode + 26-step greedy attention decode' if args.mode == 'attn' else 'eval forward + argmax' if args.mode == 'infer' else 'train step (fwd + numpy CTC + bwd + AdamW)'}, "
                       f"B={args.cpu_sample} x {args.cpu_steps} steps (+1 warm-up) at {args.height}x{args.width}, "
                       f"hidden {args.hidden}; {dt:.1f} s"}
+
+
+def attn_text(tg, tl, B, steps=26, sos=1, eos=2):
+    """teacher-forcing inputs / targets from the synthetic labels, as the reference packs them
+    (data/transforms.py:123-157): text_in = [SOS, y[:L], PAD...], target_y = [y[:L], EOS, PAD...],
+    L = min(len, steps - 1); label ids (synthetic_batch: [B, Lmax] zero-padded) are moved past the
+    reserved ids (PAD 0, SOS 1, EOS 2, blank 3)."""
+    text = torch.zeros(B, steps, dtype=torch.long)
+    ty = torch.zeros(B, steps, dtype=torch.long)
+    for b in range(B):
+        n = min(int(tl[b]), steps - 1)
+        y = ((tg[b, :n].long() - 3) % 190) + 4
+        text[b, 0] = sos
+        text[b, 1:n + 1] = y
+        ty[b, :n] = y
+        ty[b, n] = eos
+    return text, ty
 
 
 def pmc_traffic():
@@ -141,11 +170,11 @@ def main():
     C = 194
     T = args.width // 8
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
-    attn = args.mode == "attn"
+    attn = args.mode in ("attn", "attn_train")
     model = RCNN(num_classes=C, hidden_size=args.hidden, blank_id=3 if attn else None, num_rnn_layers=args.layers,
                  compute_dtype=dtype, decoder="attn" if attn else "ctc")
     model.load_state_dict(recipe_state_dict(O.param_shapes(args.hidden, C, args.layers), 0), strict=False)
-    model = model.to(dev).train(args.mode == "train")
+    model = model.to(dev).train(args.mode in ("train", "attn_train"))
     x, _, tg, tl = synthetic_batch(args.batch, args.height, args.width, T, C, seed=1234 + rank)
     x = x.to(dev)
     tg = tg.to(dev, torch.int32)
@@ -177,9 +206,25 @@ def main():
         with torch.no_grad():
             return model(x, is_train=False, batch_max_length=25)
 
+    from crnn_hip.attn import cross_entropy
+    text_in, target_y = attn_text(tg.cpu(), tl.cpu(), args.batch)
+    text_in, target_y = text_in.to(dev), target_y.to(dev)
+
+    def attn_train_step():
+        opt.zero_grad(set_to_none=True)
+        logits = model(x, text=text_in, is_train=True, batch_max_length=25)
+        loss = cross_entropy(logits, target_y, ignore_index=0)
+        loss.backward()
+        opt.step(grad_scale=inv_world)
+        return loss
+
     def step():
         if args.mode == "attn":
             return attn_step()
+        if args.mode == "attn_train":
+            if world > 1:
+                raise NotImplementedError("attn_train is a 1-GPU bench line")
+            return attn_train_step()
         if args.mode == "infer":
             return infer_step()
         eng.forward(x, train=True, save_for_backward=True, dropout_p=model.enc_dropout.p)
@@ -220,7 +265,7 @@ def main():
         divergence = float((cmax - cmin).item())
     lines = args.batch * world * args.steps
     value = lines / elapsed
-    final_loss = float(loss.float().mean().item()) if args.mode == "train" else 0.0
+    final_loss = float(loss.float().mean().item()) if args.mode in ("train", "attn_train") else 0.0
 
     if rank == 0:
         lstm = {k: timing.pop(k) for k in ("lstm_fwd", "lstm_bwd") if k in timing}
@@ -246,7 +291,9 @@ def main():
                        "text-lines/sec (inference: eval forward + greedy CTC decode), B=256, 32x256 crops, 1 MI355X"
                        if args.mode == "infer" else
                        "text-lines/sec (inference with the attention head: eval encode + 26-step greedy attention "
-                       "decode), B=256, 32x256 crops, 1 MI355X"),
+                       "decode), B=256, 32x256 crops, 1 MI355X" if args.mode == "attn" else
+                       "text-lines/sec (the reference's attention training step: encoder + 26-step teacher-forced "
+                       "attention decoder + cross-entropy, bwd, AdamW), B=256, 32x256 crops, 1 MI355X"),
             "value": round(value, 2),
             "unit": "text-lines/s",
             "n_gpus": world,
@@ -266,7 +313,11 @@ def main():
                                     f"forward + on-device greedy decode (BASELINE configs[1])"
                                     if args.mode == "infer" else
                                     f"inference: SE-ResNet31 + {args.layers}x{args.hidden} BiLSTM encode + the "
-                                    f"reference's attention decoder (fp32), 26 greedy steps (SURVEY 8f next-1)"),
+                                    f"reference's attention decoder (fp32), 26 greedy steps (SURVEY 8f next-1)"
+                                    if args.mode == "attn" else
+                                    f"train step: SE-ResNet31 + {args.layers}x{args.hidden} BiLSTM encoder ({args.dtype}) "
+                                    f"+ the reference's attention decoder (fp32), 26 teacher-forced steps, "
+                                    f"cross-entropy (ignore PAD), fwd + bwd + AdamW (SURVEY 8f next-1)"),
                        "global_batch": args.batch * world, "per_gpu_batch": args.batch,
                        "crop": f"{args.height}x{args.width}", "seq_len": T, "hidden": args.hidden,
                        "rnn_layers": args.layers, "num_classes": C,

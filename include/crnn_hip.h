@@ -327,18 +327,34 @@ int crnn_attn_cell(const float* gates, const float* b_ih, const float* b_hh, con
 int crnn_attn_cell_bwd(const float* gact, const float* c_t, const float* c_prev, const float* dh1, int ld1,
                        const float* dh2, int ld2, const float* dc, float* dgates, float* dc_prev, int B, int H,
                        void* stream);
-/* attention backward for one step (block per sample): denc += alpha' dctx; dprojH += du;
- * dprojh = sum_t du; dscore_part[b] += sum_t de tanh(u) (du, de as in csrc/attn.hip);
- * drop_p, seed = the forward step's (the mask is regenerated, not stored) */
+/* attention backward for one step (block per sample): de[b][t'] = alpha (dalpha - sum alpha dalpha)
+ * with dalpha_t' = mask/(1-p) dctx . enc_t'; dprojh[b] = score * sum_t' de (1 - tanh^2 u_t');
+ * dscore_part[b] += sum_t' de tanh(u_t') (u = proj_H + proj_h; csrc/attn.hip). drop_p, seed = the
+ * forward step's (the mask is regenerated, not stored). No [B][T][*] array is written per step: */
 int crnn_attn_bwd(const float* dctx, int lddc, const float* alpha, const float* enc, const float* projH,
-                  const float* projh, const float* score, float* denc, float* dprojH, float* dprojh,
-                  float* dscore_part, int B, int T, int H, int C, float drop_p, unsigned long long seed,
-                  void* stream);
-/* dW_ih[r][C + text[b][t]] += dgates[t][b][r] (the one-hot input columns; fp32 atomics) */
-int crnn_attn_onehot_wgrad(const float* dgates, const int* text, int text_ld, int steps, int B, int H4, float* dw_ih,
-                           int ldw, int C, void* stream);
+                  const float* projh, const float* score, float* de, float* dprojh, float* dscore_part, int B, int T,
+                  int H, int C, float drop_p, unsigned long long seed, void* stream);
+/* after the step loop: denc[b][t'][c] = sum_t alpha'_t[b][t'] dctx_t[b][c] (written; dctx rows
+ * [steps][B] of stride lddc, alpha [steps][B][T], step t's mask from seed + t) */
+int crnn_attn_denc(const float* dctx, int lddc, const float* alpha, int steps, int B, int T, int C, float drop_p,
+                   unsigned long long seed, float* denc, void* stream);
+/* dprojH[b][t'][k] = score_k sum_t de_t[b][t'] (1 - tanh^2(proj_H[b][t'][k] + proj_h_t[b][k]))
+ * (proj_h [steps][B][H], de [steps][B][T]; written) */
+int crnn_attn_dproj_enc(const float* projh, const float* de, const float* projH, const float* score, int steps, int B,
+                     int T, int H, float* dprojH, void* stream);
+/* teacher-forcing one-hot rows: X[t][b][col0 + text[b][t]] = 1 (rows [steps][B] of stride ldx,
+ * zeroed by the caller; ids outside [0, V) leave the row zero) — the saved [context | h | onehot]
+ * rows make dW_ih (both parts) and dW_hh one GEMM in the backward */
+int crnn_attn_onehot_rows(const int* text, int text_ld, int steps, int B, int V, float* X, int ldx, int col0,
+                          void* stream);
 int crnn_attn_out(const float* logits, int ldl, int B, int V, int blank, float* probs_t, int ldp, int* ch,
                   void* stream);
+/* the attention head's training loss, nn.CrossEntropyLoss(ignore_index) (training/train.py:289,503):
+ * logits [M][ldl] (V used), targets [M] -> loss[0] = mean over rows with target != ignore_index of
+ * (logsumexp - logit[target]); dlogits [M][ldd] (may be NULL) = d loss / d logits.
+ * ws: M + 1 floats of scratch. */
+int crnn_attn_xent(const float* logits, int ldl, const int* targets, int M, int V, int ignore_index, float* loss,
+                   float* dlogits, int ldd, float* ws, void* stream);
 
 /* ------------------------------------------------------------------ CTC */
 /* Per-sample log-space CTC over logits [B][T][ldc] (fp32, C classes, blank = 0, input length T).

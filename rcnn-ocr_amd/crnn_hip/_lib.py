@@ -112,9 +112,12 @@ _SIGS = {
     "crnn_attn_context": ([vp, vp, vp, vp, vp, i32, vp, i32, i32, i32, i32, f32, u64, vp], i32),
     "crnn_attn_cell": ([vp, vp, vp, vp, i32, vp, i32, vp, vp, vp, i32, vp, i32, vp, vp, i32, i32, i32, vp], i32),
     "crnn_attn_cell_bwd": ([vp, vp, vp, vp, i32, vp, i32, vp, vp, vp, i32, i32, vp], i32),
-    "crnn_attn_bwd": ([vp, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, f32, u64, vp], i32),
-    "crnn_attn_onehot_wgrad": ([vp, vp, i32, i32, i32, i32, vp, i32, i32, vp], i32),
+    "crnn_attn_bwd": ([vp, i32, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, f32, u64, vp], i32),
+    "crnn_attn_denc": ([vp, i32, vp, i32, i32, i32, i32, f32, u64, vp, vp], i32),
+    "crnn_attn_dproj_enc": ([vp, vp, vp, vp, i32, i32, i32, i32, vp, vp], i32),
+    "crnn_attn_onehot_rows": ([vp, i32, i32, i32, i32, vp, i32, i32, vp], i32),
     "crnn_attn_out": ([vp, i32, i32, i32, i32, vp, i32, vp, vp], i32),
+    "crnn_attn_xent": ([vp, i32, vp, i32, i32, i32, vp, vp, i32, vp, vp], i32),
     "crnn_ctc_loss": ([vp, i32, i32, i32, i32, vp, i32, vp, vp, vp, i32, vp], i32),
     "crnn_ctc_reduce_mean": ([vp, vp, i32, vp, vp], i32),
     "crnn_ctc_greedy": ([vp, i32, i32, i32, i32, vp, vp, vp], i32),

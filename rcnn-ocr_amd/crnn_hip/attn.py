@@ -7,8 +7,10 @@ with the one-hot input folded in as a weight column, logits, blank mask + argmax
 projection proj_H = enc W_i2h^T is computed once per decode. Forward only (inference and
 teacher-forced logits) and the teacher-forced backward (BPTT through the cell and the attention,
 run_train / backward): per step a cell-backward kernel, one GEMM for d[context | h], an attention
-backward kernel and one GEMM for the h2h path; the weight gradients are batched GEMMs over all
-steps afterwards (the one-hot columns of W_ih by an atomic scatter).
+backward kernel (per-sample d attention logits, d proj_h) and one GEMM for the h2h path; d enc,
+d proj_H and the weight gradients are computed once over all steps afterwards (the forward keeps
+the one-hot inputs as extra columns of its saved [context | h] rows, so W_ih and W_hh's gradients
+are one GEMM).
 """
 from __future__ import annotations
 
@@ -71,7 +73,9 @@ class AttnDecoderHIP:
             raise ValueError("text needs batch_max_length + 1 columns")
         projH = torch.empty(B * T, H, device=dev)
         self._gemm(enc, C, self.w_i2h, C, projH, H, None, B * T, H, C)
-        Xs = torch.zeros(steps + 1, B, C + H, device=dev)   # [context_t | h_{t-1}] per step
+        LX = C + H + Vp                                     # [context_t | h_{t-1} | onehot(text_t)] per step
+        Xs = torch.zeros(steps + 1, B, LX, device=dev)
+        call("crnn_attn_onehot_rows", ptr(txt), txt.shape[1], steps, B, V, ptr(Xs), LX, C + H, s)
         Gs = torch.empty(steps, B, 4 * H, device=dev)       # activated gates
         Cs = torch.empty(steps, B, H, device=dev)           # cell states
         Ph = torch.empty(steps, B, H, device=dev)           # proj_h per step
@@ -82,11 +86,11 @@ class AttnDecoderHIP:
         gates = torch.empty(B, 4 * H, device=dev)
         for t in range(steps):
             self._gemm(h, H, self.w_h2h, H, Ph[t], H, self.b_h2h, B, H, H)
-            call("crnn_attn_context", ptr(projH), ptr(Ph[t]), ptr(self.score), ptr(enc), ptr(Xs[t]), C + H,
+            call("crnn_attn_context", ptr(projH), ptr(Ph[t]), ptr(self.score), ptr(enc), ptr(Xs[t]), LX,
                  ptr(As[t]), B, T, H, C, drop_p, (seed + t) & (2 ** 64 - 1), s)
-            self._gemm(Xs[t], C + H, self.w_cat, C + H, gates, 4 * H, None, B, 4 * H, C + H)
+            self._gemm(Xs[t], LX, self.w_cat, C + H, gates, 4 * H, None, B, 4 * H, C + H)
             call("crnn_attn_cell", ptr(gates), ptr(self.b_ih), ptr(self.b_hh), ptr(self.w_ih), C + V, ptr(txt[:, t:]),
-                 txt.shape[1], ptr(h), ptr(c), ptr(Xs[t + 1]), C + H, ptr(hs[:, t]), steps * H, ptr(Gs[t]), ptr(Cs[t]),
+                 txt.shape[1], ptr(h), ptr(c), ptr(Xs[t + 1]), LX, ptr(hs[:, t]), steps * H, ptr(Gs[t]), ptr(Cs[t]),
                  B, H, C, s)
         lg = torch.empty(B * steps, Vp, device=dev)
         self._gemm(hs, H, self.w_gen, H, lg, Vp, self.b_gen, B * steps, Vp, H)
@@ -122,34 +126,37 @@ class AttnDecoderHIP:
         call("crnn_colsum", F32, ptr(dL), Vp, B * steps, Vp, ptr(gb), 0, 1, s)
         dG = torch.empty(steps, B, 4 * H, device=dev)
         dPh = torch.empty(steps, B, H, device=dev)
-        denc = torch.zeros(B, T, C, device=dev)
-        dProjH = torch.zeros(B * T, H, device=dev)
+        De = torch.empty(steps, B, T, device=dev)           # d attention logits per step
         dscore = torch.zeros(B, H, device=dev)
-        dX = torch.empty(B, C + H, device=dev)
+        dX = torch.empty(steps, B, C + H, device=dev)       # d [context | h_{t-1}] per step
         dc = [torch.zeros(B, H, device=dev), torch.empty(B, H, device=dev)]
         dh_rec, ld_rec = None, 0
         for t in reversed(range(steps)):
             call("crnn_attn_cell_bwd", ptr(Gs[t]), ptr(Cs[t]), ptr(Cs[t - 1]) if t > 0 else None, ptr(dh_rec), ld_rec,
                  ptr(dHs.view(B, steps, H)[:, t]), steps * H, ptr(dc[0]), ptr(dG[t]), ptr(dc[1]), B, H, s)
             dc.reverse()
-            call("crnn_gemm_nn", F32, ptr(dG[t]), 4 * H, ptr(self.w_cat), C + H, ptr(dX), C + H, B, C + H, 4 * H, 1, 0, s)
-            call("crnn_attn_bwd", ptr(dX), C + H, ptr(As[t]), ptr(enc), ptr(projH), ptr(Ph[t]), ptr(self.score),
-                 ptr(denc), ptr(dProjH), ptr(dPh[t]), ptr(dscore), B, T, H, C, drop_p,
-                 (seed + t) & (2 ** 64 - 1), s)
-            # dh_{t-1} = d(h part of [context | h]) + dproj_h W_h2h   (accumulated into dX[:, C:])
-            call("crnn_gemm_nn", F32, ptr(dPh[t]), H, ptr(self.w_h2h), H, ptr(dX[:, C:]), C + H, B, H, H, 1, 1, s)
-            # stream order: step t-1's cell backward reads dh_rec before its GEMM rewrites dX
-            dh_rec, ld_rec = dX[:, C:], C + H
+            call("crnn_gemm_nn", F32, ptr(dG[t]), 4 * H, ptr(self.w_cat), C + H, ptr(dX[t]), C + H, B, C + H, 4 * H, 1,
+                 0, s)
+            call("crnn_attn_bwd", ptr(dX[t]), C + H, ptr(As[t]), ptr(enc), ptr(projH), ptr(Ph[t]), ptr(self.score),
+                 ptr(De[t]), ptr(dPh[t]), ptr(dscore), B, T, H, C, drop_p, (seed + t) & (2 ** 64 - 1), s)
+            # dh_{t-1} = d(h part of [context | h]) + dproj_h W_h2h   (accumulated into dX[t][:, C:])
+            call("crnn_gemm_nn", F32, ptr(dPh[t]), H, ptr(self.w_h2h), H, ptr(dX[t][:, C:]), C + H, B, H, H, 1, 1, s)
+            dh_rec, ld_rec = dX[t][:, C:], C + H
+        # encoder-side gradients of the attention, all steps at once
+        denc = torch.empty(B, T, C, device=dev)
+        call("crnn_attn_denc", ptr(dX), C + H, ptr(As), steps, B, T, C, drop_p, seed & (2 ** 64 - 1), ptr(denc), s)
+        dProjH = torch.empty(B * T, H, device=dev)
+        call("crnn_attn_dproj_enc", ptr(Ph), ptr(De), ptr(projH), ptr(self.score), steps, B, T, H, ptr(dProjH), s)
         # weight gradients, batched over steps
-        wcat = torch.empty(4 * H, C + H, device=dev)
-        call("crnn_gemm_tn", F32, ptr(dG), 4 * H, ptr(Xs), C + H, ptr(wcat), C + H, 4 * H, C + H, steps * B, 0, s)
-        dwih = torch.zeros(4 * H, C + V, device=dev)
-        dwih[:, :C] = wcat[:, :C]
-        call("crnn_attn_onehot_wgrad", ptr(dG), ptr(txt), txt.shape[1], steps, B, 4 * H, ptr(dwih), C + V, C, s)
+        # [dW_ih[:, :C] | dW_hh | dW_ih[:, C:]] in one GEMM over the saved [context | h | onehot] rows
+        LX = C + H + Vp
+        wfull = torch.empty(4 * H, LX, device=dev)
+        call("crnn_gemm_tn", F32, ptr(dG), 4 * H, ptr(Xs), LX, ptr(wfull), LX, 4 * H, LX, steps * B, 0, s)
+        dwih = torch.cat([wfull[:, :C], wfull[:, C + H:C + H + V]], 1)
         db = torch.empty(4 * H, device=dev)
         call("crnn_colsum", F32, ptr(dG), 4 * H, steps * B, 4 * H, ptr(db), 0, 1, s)
         wh2h = torch.empty(H, H, device=dev)
-        call("crnn_gemm_tn", F32, ptr(dPh), H, ptr(Xs[:, :, C:]), C + H, ptr(wh2h), H, H, H, steps * B, 0, s)
+        call("crnn_gemm_tn", F32, ptr(dPh), H, ptr(Xs[:, :, C:]), LX, ptr(wh2h), H, H, H, steps * B, 0, s)
         bh2h = torch.empty(H, device=dev)
         call("crnn_colsum", F32, ptr(dPh), H, steps * B, H, ptr(bh2h), 0, 1, s)
         wi2h = torch.empty(H, C, device=dev)
@@ -159,7 +166,7 @@ class AttnDecoderHIP:
         call("crnn_colsum", F32, ptr(dscore), H, B, H, ptr(dsc), 0, 1, s)
         pre = "attention_cell."
         out = {pre + "i2h.weight": wi2h, pre + "h2h.weight": wh2h, pre + "h2h.bias": bh2h,
-               pre + "score.weight": dsc.view(1, H), pre + "rnn.weight_ih": dwih, pre + "rnn.weight_hh": wcat[:, C:],
+               pre + "score.weight": dsc.view(1, H), pre + "rnn.weight_ih": dwih, pre + "rnn.weight_hh": wfull[:, C:C + H],
                pre + "rnn.bias_ih": db, pre + "rnn.bias_hh": db, "generator.weight": gw[:V], "generator.bias": gb[:V]}
         for k, v in out.items():
             g = grads[k]
@@ -216,3 +223,37 @@ class AttnDecoderHIP:
         self._gemm(hx, C + H, self.w_cat, C + H, gates, 4 * H, None, B, 4 * H, C + H)
         call("crnn_attn_cell", ptr(gates), ptr(self.b_ih), ptr(self.b_hh), ptr(self.w_ih), C + self.V, ptr(ch),
              ch_stride, ptr(h), ptr(c), ptr(hx), C + H, ptr(hs), ld_hs, None, None, B, H, C, s)
+
+
+class _XentFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, targets, ignore_index):
+        L.require_device(logits)
+        V = logits.shape[-1]
+        x = logits.detach().reshape(-1, V)
+        if x.dtype != torch.float32 or not x.is_contiguous():
+            raise ValueError("cross_entropy: logits must be contiguous fp32")
+        M = x.shape[0]
+        tg = targets.reshape(-1).to(x.device, torch.int32).contiguous()
+        if tg.numel() != M:
+            raise ValueError("cross_entropy: one target per logits row")
+        loss = torch.empty((), device=x.device)
+        d = torch.empty_like(x)
+        ws = torch.empty(M + 1, device=x.device)
+        call("crnn_attn_xent", ptr(x), V, ptr(tg), M, V, int(ignore_index), ptr(loss), ptr(d), V, ptr(ws),
+             L.stream_ptr())
+        ctx.save_for_backward(d)
+        ctx.shape = logits.shape
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        (d,) = ctx.saved_tensors
+        return d.mul_(g).view(ctx.shape), None, None
+
+
+def cross_entropy(logits: torch.Tensor, targets: torch.Tensor, ignore_index: int = 0) -> torch.Tensor:
+    """nn.CrossEntropyLoss(ignore_index=PAD)(logits.reshape(-1, V), targets.reshape(-1)) — the
+    attention head's training loss (training/train.py:289,503) — on the HIP path (one fused
+    log-softmax / NLL / gradient kernel, csrc/attn.hip)."""
+    return _XentFn.apply(logits, targets, ignore_index)

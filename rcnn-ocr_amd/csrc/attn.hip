@@ -20,18 +20,21 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
-// block per sample: e[t] (wave per t), softmax over t, context over c
-__global__ __launch_bounds__(256) void attn_context_kernel(const float* __restrict__ projH,
-                                                           const float* __restrict__ projh,
-                                                           const float* __restrict__ score,
-                                                           const float* __restrict__ enc, float* __restrict__ ctx,
-                                                           int ldc, float* __restrict__ alpha_out, int T, int H,
-                                                           int C, uint32_t thr, float scale,
-                                                           unsigned long long seed) {
+// block (1024 threads) per sample: e[t] (wave per t), softmax over t, context over c (4 groups of
+// t per channel, combined in LDS in fixed order)
+constexpr int ATT_NT = 1024;
+__global__ __launch_bounds__(ATT_NT) void attn_context_kernel(const float* __restrict__ projH,
+                                                              const float* __restrict__ projh,
+                                                              const float* __restrict__ score,
+                                                              const float* __restrict__ enc, float* __restrict__ ctx,
+                                                              int ldc, float* __restrict__ alpha_out, int T, int H,
+                                                              int C, uint32_t thr, float scale,
+                                                              unsigned long long seed) {
   extern __shared__ float sm[];  // [T] scores -> weights (after the training-mode dropout)
+  __shared__ float red[4][256];
   const int b = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const float* ph = projh + (size_t)b * H;
-  for (int t = w; t < T; t += 4) {
+  for (int t = w; t < T; t += ATT_NT / 64) {
     const float* pH = projH + ((size_t)b * T + t) * H;
     float s = 0.f;
     for (int k = lane; k < H; k += 64) s += score[k] * tanhf(pH[k] + ph[k]);
@@ -57,10 +60,16 @@ __global__ __launch_bounds__(256) void attn_context_kernel(const float* __restri
   }
   __syncthreads();
   const float* eb = enc + (size_t)b * T * C;
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+  const int cq = threadIdx.x & 255, tq = threadIdx.x >> 8;
+  for (int c0 = 0; c0 < C; c0 += 256) {
+    const int c = c0 + cq;
     float s = 0.f;
-    for (int t = 0; t < T; ++t) s += sm[t] * eb[(size_t)t * C + c];
-    ctx[(size_t)b * ldc + c] = s;
+    if (c < C)
+      for (int t = tq; t < T; t += 4) s += sm[t] * eb[(size_t)t * C + c];
+    red[tq][cq] = s;
+    __syncthreads();
+    if (tq == 0 && c < C) ctx[(size_t)b * ldc + c] = ((red[0][cq] + red[1][cq]) + red[2][cq]) + red[3][cq];
+    __syncthreads();
   }
 }
 
@@ -127,81 +136,134 @@ __global__ void attn_cell_bwd_kernel(const float* __restrict__ gact, const float
   }
 }
 
-// attention backward, block per sample: context = sum_t alpha_t enc_t, alpha = softmax(e),
-// e_t = score . tanh(u_t), u_t = proj_H[b,t] + proj_h[b]:
-//   (alpha' = alpha * mask / (1 - p) in training, model/model.py:38)
-//   denc[b,t] += alpha'_t dctx ; dalpha_t = mask_t / (1-p) dctx . enc_t ;
-//   de_t = alpha_t (dalpha_t - sum alpha dalpha)
-//   du_t = de_t score (1 - tanh^2 u_t) -> dprojH[b,t] += du_t, dprojh[b] = sum_t du_t,
-//   dscore_part[b] += sum_t de_t tanh(u_t)
-__global__ __launch_bounds__(256) void attn_bwd_kernel(const float* __restrict__ dctx, int lddc,
-                                                       const float* __restrict__ alpha,
-                                                       const float* __restrict__ enc,
-                                                       const float* __restrict__ projH,
-                                                       const float* __restrict__ projh,
-                                                       const float* __restrict__ score, float* __restrict__ denc,
-                                                       float* __restrict__ dprojH, float* __restrict__ dprojh,
-                                                       float* __restrict__ dscore_part, int T, int H, int C,
-                                                       uint32_t thr, float scale, unsigned long long seed) {
-  extern __shared__ float sm[];  // [3][T]: dalpha, de, dropped alpha
+// attention backward, split so that no step touches a [B][T][*] array read-modify-write:
+//   context = sum_t' alpha'_t' enc_t', alpha = softmax(e), e_t' = score . tanh(u_t'),
+//   u_t' = proj_H[b,t'] + proj_h[b]; alpha' = alpha * mask / (1 - p) (training, model/model.py:40)
+// per decoder step (attn_step_bwd_kernel, block per sample):
+//   dalpha_t' = mask_t'/(1-p) dctx . enc_t' ; de_t' = alpha_t' (dalpha_t' - sum alpha dalpha) -> de
+//   dprojh[b] = sum_t' de_t' score (1 - tanh^2 u_t') ; dscore_part[b] += sum_t' de_t' tanh(u_t')
+// after the step loop (all steps at once):
+//   denc[b,t'] = sum_t alpha'_t[b,t'] dctx_t[b]                              (attn_denc_kernel)
+//   dprojH[b,t',k] = score_k sum_t de_t[b,t'] (1 - tanh^2(proj_H[b,t',k] + proj_h_t[b,k]))
+//                                                                            (attn_dprojH_kernel)
+__device__ __forceinline__ float keep_scale(uint32_t thr, float scale, unsigned long long seed,
+                                            unsigned long long i) {
+  return thr == 0u ? 1.f : (drop_hash(seed, i) >= thr ? scale : 0.f);
+}
+
+__global__ __launch_bounds__(ATT_NT) void attn_step_bwd_kernel(const float* __restrict__ dctx, int lddc,
+                                                               const float* __restrict__ alpha,
+                                                               const float* __restrict__ enc,
+                                                               const float* __restrict__ projH,
+                                                               const float* __restrict__ projh,
+                                                               const float* __restrict__ score,
+                                                               float* __restrict__ de_out, float* __restrict__ dprojh,
+                                                               float* __restrict__ dscore_part, int T, int H, int C,
+                                                               uint32_t thr, float scale, unsigned long long seed) {
+  extern __shared__ float sm[];  // [2][T]: dalpha, de
+  __shared__ float red[2][4][256];
   float* da = sm;
   float* de = sm + T;
-  float* ad = sm + 2 * T;
   const int b = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const float* dc = dctx + (size_t)b * lddc;
   const float* eb = enc + (size_t)b * T * C;
   const float* al = alpha + (size_t)b * T;
-  for (int t = threadIdx.x; t < T; t += blockDim.x)  // the forward's dropout mask, from its seed
-    ad[t] = thr == 0u ? 1.f : (drop_hash(seed, (unsigned long long)b * T + t) >= thr ? scale : 0.f);
-  __syncthreads();
-  for (int t = w; t < T; t += 4) {
+  for (int t = w; t < T; t += ATT_NT / 64) {
     float s = 0.f;
     for (int k = lane; k < C; k += 64) s += dc[k] * eb[(size_t)t * C + k];
     s = wave_sum(s);
-    if (lane == 0) da[t] = s * ad[t];
+    if (lane == 0) da[t] = s * keep_scale(thr, scale, seed, (unsigned long long)b * T + t);
   }
   __syncthreads();
   if (w == 0) {
     float z = 0.f;
     for (int t = lane; t < T; t += 64) z += al[t] * da[t];
     z = wave_sum(z);
-    for (int t = lane; t < T; t += 64) de[t] = al[t] * (da[t] - z);
-  }
-  // denc += alpha'_t dctx (alpha' = the dropped weights the forward used)
-  float* db_ = denc + (size_t)b * T * C;
-  for (int k = threadIdx.x; k < C; k += blockDim.x) {
-    const float dk = dc[k];
-    for (int t = 0; t < T; ++t) db_[(size_t)t * C + k] += al[t] * ad[t] * dk;
+    for (int t = lane; t < T; t += 64) {
+      const float v = al[t] * (da[t] - z);
+      de[t] = v;
+      de_out[(size_t)b * T + t] = v;
+    }
   }
   __syncthreads();
   const float* ph = projh + (size_t)b * H;
-  for (int k = threadIdx.x; k < H; k += blockDim.x) {
+  const float* pH = projH + (size_t)b * T * H;
+  const int kq = threadIdx.x & 255, tq = threadIdx.x >> 8;
+  for (int k0 = 0; k0 < H; k0 += 256) {
+    const int k = k0 + kq;
     float acc_h = 0.f, acc_s = 0.f;
-    const float sk = score[k], pk = ph[k];
-    for (int t = 0; t < T; ++t) {
-      const size_t o = ((size_t)b * T + t) * H + k;
-      const float th = tanhf(projH[o] + pk);
-      const float du = de[t] * sk * (1.f - th * th);
-      dprojH[o] += du;
-      acc_h += du;
-      acc_s += de[t] * th;
+    if (k < H) {
+      const float pk = ph[k];
+      for (int t = tq; t < T; t += 4) {
+        const float th = tanhf(pH[(size_t)t * H + k] + pk);
+        acc_h += de[t] * (1.f - th * th);
+        acc_s += de[t] * th;
+      }
     }
-    dprojh[(size_t)b * H + k] = acc_h;
-    dscore_part[(size_t)b * H + k] += acc_s;
+    red[0][tq][kq] = acc_h;
+    red[1][tq][kq] = acc_s;
+    __syncthreads();
+    if (tq == 0 && k < H) {
+      dprojh[(size_t)b * H + k] = (((red[0][0][kq] + red[0][1][kq]) + red[0][2][kq]) + red[0][3][kq]) * score[k];
+      dscore_part[(size_t)b * H + k] += ((red[1][0][kq] + red[1][1][kq]) + red[1][2][kq]) + red[1][3][kq];
+    }
+    __syncthreads();
   }
 }
 
-// one-hot input columns of W_ih: dW_ih[r][C + char[b][t]] += dgates[t][b][r] (fp32 atomics)
-__global__ void attn_onehot_wgrad_kernel(const float* __restrict__ dgates, const int* __restrict__ text,
-                                         int text_ld, int steps, int B, int H4, float* __restrict__ dw_ih, int ldw,
-                                         int C) {
-  const long n = (long)steps * B * H4;
+// block per (sample, 256 channels): dctx of every step and the step's alpha' staged in LDS
+__global__ __launch_bounds__(256) void attn_denc_kernel(const float* __restrict__ dctx, int lddc,
+                                                        const float* __restrict__ alpha, int steps, int B, int T,
+                                                        int C, uint32_t thr, float scale,
+                                                        unsigned long long seed, float* __restrict__ denc) {
+  extern __shared__ float sm[];  // [steps][256] dctx, [steps][T] alpha'
+  float* dcs = sm;
+  float* as = sm + steps * 256;
+  const int b = blockIdx.x, c0 = blockIdx.y * 256, c = c0 + threadIdx.x;
+  for (int i = threadIdx.x; i < steps * T; i += blockDim.x) {
+    const int t = i / T, tp = i - t * T;
+    as[i] = alpha[((size_t)t * B + b) * T + tp] *
+            keep_scale(thr, scale, seed + (unsigned long long)t, (unsigned long long)b * T + tp);
+  }
+  for (int t = 0; t < steps; ++t) dcs[t * 256 + threadIdx.x] = c < C ? dctx[((size_t)t * B + b) * lddc + c] : 0.f;
+  __syncthreads();
+  if (c >= C) return;
+  float* out = denc + (size_t)b * T * C + c;
+  for (int tp = 0; tp < T; ++tp) {
+    float acc = 0.f;
+    for (int t = 0; t < steps; ++t) acc += as[t * T + tp] * dcs[t * 256 + threadIdx.x];
+    out[(size_t)tp * C] = acc;
+  }
+}
+
+// thread per (b, t', k)
+__global__ void attn_dprojH_kernel(const float* __restrict__ projh, const float* __restrict__ de,
+                                   const float* __restrict__ projH, const float* __restrict__ score, int steps,
+                                   int B, int T, int H, float* __restrict__ dprojH) {
+  const long n = (long)B * T * H;
   for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) {
-    const int r = (int)(e % H4);
-    const long tb = e / H4;
-    const int b = (int)(tb % B), t = (int)(tb / B);
-    const int col = C + text[(size_t)b * text_ld + t];
-    atomicAdd(dw_ih + (size_t)r * ldw + col, dgates[e]);
+    const long bt = e / H;
+    const int k = (int)(e - bt * H);
+    const int b = (int)(bt / T);
+    const float u0 = projH[e];
+    float acc = 0.f;
+    for (int t = 0; t < steps; ++t) {
+      const float th = tanhf(u0 + projh[((size_t)t * B + b) * H + k]);
+      acc += de[(size_t)t * B * T + bt] * (1.f - th * th);
+    }
+    dprojH[e] = acc * score[k];
+  }
+}
+
+// teacher-forcing one-hot rows: X[t][b][col0 + text[b][t]] = 1 (X zeroed by the caller); the
+// backward's gradient of W_ih's one-hot columns is then part of the [context | h | onehot] GEMM
+__global__ void attn_onehot_rows_kernel(const int* __restrict__ text, int text_ld, int steps, int B, int V,
+                                        float* __restrict__ X, int ldx, int col0) {
+  const long n = (long)steps * B;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) {
+    const int t = (int)(e / B), b = (int)(e - (long)t * B);
+    const int v = text[(size_t)b * text_ld + t];
+    if (v >= 0 && v < V) X[(size_t)e * ldx + col0 + v] = 1.f;
   }
 }
 
@@ -240,6 +302,56 @@ __global__ __launch_bounds__(256) void attn_out_kernel(const float* __restrict__
   if (threadIdx.x == 0) ch[b] = bi[0];
 }
 
+// ---- the attention head's loss: nn.CrossEntropyLoss(ignore_index=PAD) over [M = B*steps][V]
+// (training/train.py:289,503), mean over the rows whose target != ignore_index
+__global__ __launch_bounds__(256) void xent_count_kernel(const int* __restrict__ tgt, int M, int ignore,
+                                                         float* __restrict__ inv_n) {
+  __shared__ int part[4];
+  int n = 0;
+  for (int r = threadIdx.x; r < M; r += blockDim.x) n += tgt[r] != ignore;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = n;
+  __syncthreads();
+  if (threadIdx.x == 0) inv_n[0] = 1.f / (float)(part[0] + part[1] + part[2] + part[3]);
+}
+
+// wave per row: log-sum-exp, loss_row = (lse - x[tgt]) / n, d = (softmax - onehot) / n (0 if ignored)
+__global__ __launch_bounds__(256) void xent_rows_kernel(const float* __restrict__ x, int ldx,
+                                                        const int* __restrict__ tgt, int M, int V, int ignore,
+                                                        const float* __restrict__ inv_n, float* __restrict__ lrow,
+                                                        float* __restrict__ d, int ldd) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= M) return;
+  const float* xr = x + (size_t)r * ldx;
+  const int t = tgt[r];
+  const bool on = t != ignore;
+  const float sc = on ? inv_n[0] : 0.f;
+  float m = -INFINITY;
+  for (int v = lane; v < V; v += 64) m = fmaxf(m, xr[v]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  float z = 0.f;
+  for (int v = lane; v < V; v += 64) z += expf(xr[v] - m);
+  z = wave_sum(z);
+  const float lse = m + logf(z), rz = 1.f / z;
+  if (d)
+    for (int v = lane; v < V; v += 64) d[(size_t)r * ldd + v] = (expf(xr[v] - m) * rz - (v == t ? 1.f : 0.f)) * sc;
+  if (lane == 0) lrow[r] = on ? (lse - xr[t]) * sc : 0.f;
+}
+
+__global__ __launch_bounds__(256) void xent_sum_kernel(const float* __restrict__ lrow, int M,
+                                                       float* __restrict__ loss) {
+  __shared__ float part[4];
+  float s = 0.f;
+  for (int r = threadIdx.x; r < M; r += blockDim.x) s += lrow[r];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) loss[0] = part[0] + part[1] + part[2] + part[3];
+}
+
 }  // namespace
 
 extern "C" {
@@ -249,7 +361,7 @@ int crnn_attn_context(const float* projH, const float* projh, const float* score
                       void* stream) {
   if (T <= 0 || T > 4096) return crnn_set_error(hipErrorInvalidValue, "attn_context: T out of range");
   if (!(drop_p >= 0.f && drop_p < 1.f)) return crnn_set_error(hipErrorInvalidValue, "attn_context: p not in [0, 1)");
-  hipLaunchKernelGGL(attn_context_kernel, dim3(B), dim3(256), (size_t)T * sizeof(float), (hipStream_t)stream, projH,
+  hipLaunchKernelGGL(attn_context_kernel, dim3(B), dim3(ATT_NT), (size_t)T * sizeof(float), (hipStream_t)stream, projH,
                      projh, score, enc, ctx, ldc, alpha, T, H, C, drop_threshold(drop_p), 1.f / (1.f - drop_p), seed);
   return (int)hipGetLastError();
 }
@@ -271,21 +383,38 @@ int crnn_attn_cell_bwd(const float* gact, const float* c_t, const float* c_prev,
 }
 
 int crnn_attn_bwd(const float* dctx, int lddc, const float* alpha, const float* enc, const float* projH,
-                  const float* projh, const float* score, float* denc, float* dprojH, float* dprojh,
-                  float* dscore_part, int B, int T, int H, int C, float drop_p, unsigned long long seed,
-                  void* stream) {
+                  const float* projh, const float* score, float* de, float* dprojh, float* dscore_part, int B, int T,
+                  int H, int C, float drop_p, unsigned long long seed, void* stream) {
   if (T <= 0 || T > 4096) return crnn_set_error(hipErrorInvalidValue, "attn_bwd: T out of range");
   if (!(drop_p >= 0.f && drop_p < 1.f)) return crnn_set_error(hipErrorInvalidValue, "attn_bwd: p not in [0, 1)");
-  hipLaunchKernelGGL(attn_bwd_kernel, dim3(B), dim3(256), (size_t)3 * T * sizeof(float), (hipStream_t)stream, dctx,
-                     lddc, alpha, enc, projH, projh, score, denc, dprojH, dprojh, dscore_part, T, H, C,
+  hipLaunchKernelGGL(attn_step_bwd_kernel, dim3(B), dim3(ATT_NT), (size_t)2 * T * sizeof(float), (hipStream_t)stream,
+                     dctx, lddc, alpha, enc, projH, projh, score, de, dprojh, dscore_part, T, H, C,
                      drop_threshold(drop_p), 1.f / (1.f - drop_p), seed);
   return (int)hipGetLastError();
 }
 
-int crnn_attn_onehot_wgrad(const float* dgates, const int* text, int text_ld, int steps, int B, int H4, float* dw_ih,
-                           int ldw, int C, void* stream) {
-  hipLaunchKernelGGL(attn_onehot_wgrad_kernel, dim3(grid_for((long)steps * B * H4)), dim3(256), 0,
-                     (hipStream_t)stream, dgates, text, text_ld, steps, B, H4, dw_ih, ldw, C);
+int crnn_attn_denc(const float* dctx, int lddc, const float* alpha, int steps, int B, int T, int C, float drop_p,
+                   unsigned long long seed, float* denc, void* stream) {
+  const size_t lds = (size_t)steps * (256 + T) * sizeof(float);
+  if (steps <= 0 || T <= 0 || lds > 64 * 1024)
+    return crnn_set_error(hipErrorInvalidValue, "attn_denc: steps * (256 + T) exceeds the LDS stage");
+  if (!(drop_p >= 0.f && drop_p < 1.f)) return crnn_set_error(hipErrorInvalidValue, "attn_denc: p not in [0, 1)");
+  hipLaunchKernelGGL(attn_denc_kernel, dim3(B, (C + 255) / 256), dim3(256), lds, (hipStream_t)stream, dctx, lddc,
+                     alpha, steps, B, T, C, drop_threshold(drop_p), 1.f / (1.f - drop_p), seed, denc);
+  return (int)hipGetLastError();
+}
+
+int crnn_attn_dproj_enc(const float* projh, const float* de, const float* projH, const float* score, int steps, int B,
+                     int T, int H, float* dprojH, void* stream) {
+  hipLaunchKernelGGL(attn_dprojH_kernel, dim3(grid_for((long)B * T * H)), dim3(256), 0, (hipStream_t)stream, projh,
+                     de, projH, score, steps, B, T, H, dprojH);
+  return (int)hipGetLastError();
+}
+
+int crnn_attn_onehot_rows(const int* text, int text_ld, int steps, int B, int V, float* X, int ldx, int col0,
+                          void* stream) {
+  hipLaunchKernelGGL(attn_onehot_rows_kernel, dim3(grid_for((long)steps * B)), dim3(256), 0, (hipStream_t)stream,
+                     text, text_ld, steps, B, V, X, ldx, col0);
   return (int)hipGetLastError();
 }
 
@@ -293,6 +422,17 @@ int crnn_attn_out(const float* logits, int ldl, int B, int V, int blank, float* 
                   void* stream) {
   hipLaunchKernelGGL(attn_out_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, logits, ldl, V, blank, probs_t, ldp,
                      ch);
+  return (int)hipGetLastError();
+}
+
+int crnn_attn_xent(const float* logits, int ldl, const int* targets, int M, int V, int ignore_index, float* loss,
+                   float* dlogits, int ldd, float* ws, void* stream) {
+  if (M <= 0 || V <= 0) return crnn_set_error(hipErrorInvalidValue, "attn_xent: empty input");
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(xent_count_kernel, dim3(1), dim3(256), 0, st, targets, M, ignore_index, ws);
+  hipLaunchKernelGGL(xent_rows_kernel, dim3((M + 3) / 4), dim3(256), 0, st, logits, ldl, targets, M, V, ignore_index,
+                     ws, ws + 1, dlogits, ldd);
+  hipLaunchKernelGGL(xent_sum_kernel, dim3(1), dim3(256), 0, st, ws + 1, M, loss);
   return (int)hipGetLastError();
 }
 

@@ -219,6 +219,7 @@ class RCNN(nn.Module):
         """call after modifying parameters in place (optimizer steps do this via hooks)."""
         if self._engine is not None:
             self._engine.mark_params_changed()
+        self._attn_version = None   # the attention decoder re-reads its weights on next use
 
     def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
         r = super().load_state_dict(state_dict, strict=strict, assign=assign)

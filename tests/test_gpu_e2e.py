@@ -440,8 +440,12 @@ def test_rcnn_attn_train_step_matches_oracle():
     text = torch.randint(4, 194, (3, 10), generator=torch.Generator().manual_seed(5))
     text[:, 0] = 1
     logits = m(x.to(DEV), text=text.to(DEV), is_train=True, batch_max_length=9)
-    tgt = torch.roll(text, -1, 1).to(DEV)   # next-token targets; CrossEntropyLoss as training/train.py:289,503
-    loss = torch.nn.functional.cross_entropy(logits.reshape(-1, 194), tgt.reshape(-1))
+    from crnn_hip.attn import cross_entropy
+    tgt = torch.roll(text, -1, 1)   # next-token targets, PAD (0) tails ignored as training/train.py:289,503
+    tgt[0, 6:] = 0
+    tgt[2, 8:] = 0
+    tgt = tgt.to(DEV)
+    loss = cross_entropy(logits, tgt, ignore_index=0)
     loss.backward()
     torch.cuda.synchronize()
     params = dict(m.named_parameters())
@@ -450,11 +454,31 @@ def test_rcnn_attn_train_step_matches_oracle():
     enc = O.encode(x.double(), p, O.Ctx(train=True, force=hip_decisions(m._engine)))
     pa = {k[5:]: v for k, v in p.items() if k.startswith("attn.")}
     ref = O.attn_teacher(pa, enc, text, 10, 3, 194)
-    rl = torch.nn.functional.cross_entropy(ref.reshape(-1, 194), tgt.cpu().reshape(-1))
-    assert abs(float(loss) - float(rl)) < 1e-5 * abs(float(rl))
+    rl = torch.nn.functional.cross_entropy(ref.reshape(-1, 194), tgt.cpu().reshape(-1), ignore_index=0)
+    assert abs(float(loss.detach()) - float(rl.detach())) < 1e-5 * abs(float(rl.detach()))
     rl.backward()
     errs = sorted(((float((params[k].grad.double().cpu() - v.grad).norm() / (v.grad.norm() + 1e-30)), k)
                    for k, v in p.items() if getattr(v, "grad", None) is not None), reverse=True)
     print("attn train grad error vs fp64 (HIP decisions): max", errs[0], "median", errs[len(errs) // 2][0])
     assert errs[0][0] < 1e-4, errs[:5]
     assert float(params["ctc_head.weight"].grad.abs().max()) == 0.0
+
+
+@pytest.mark.parametrize("MV", [(7, 5), (300, 194), (1000, 37)])
+def test_attn_cross_entropy_matches_torch(MV):
+    """crnn_attn_xent (the attention head's loss, nn.CrossEntropyLoss(ignore_index=PAD),
+    training/train.py:289,503) vs torch fp64: loss and d logits, with ignored rows."""
+    from crnn_hip.attn import cross_entropy
+    M, V = MV
+    g = torch.Generator().manual_seed(M)
+    x = (torch.randn(M, V, generator=g, dtype=torch.float64) * 4)
+    t = torch.randint(0, V, (M,), generator=g)
+    t[::3] = 0
+    xd = x.float().to(DEV).requires_grad_(True)
+    loss = cross_entropy(xd, t.to(DEV), ignore_index=0)
+    (2.5 * loss).backward()
+    xr = x.clone().requires_grad_(True)
+    ref = torch.nn.functional.cross_entropy(xr, t, ignore_index=0)
+    (2.5 * ref).backward()
+    assert abs(float(loss.detach()) - float(ref.detach())) < 1e-5 * abs(float(ref.detach()))
+    assert float((xd.grad.double().cpu() - xr.grad).abs().max()) < 1e-6
