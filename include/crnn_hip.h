@@ -356,6 +356,25 @@ int crnn_attn_out(const float* logits, int ldl, int B, int V, int blank, float* 
 int crnn_attn_xent(const float* logits, int ldl, const int* targets, int M, int V, int ignore_index, float* loss,
                    float* dlogits, int ldd, float* ws, void* stream);
 
+/* ------------------------------------------------------------------ input pipeline
+ * ResizeAndPadA + A.Normalize(0.5, 0.5) + ToTensorV2 (data/transforms.py:62-120, :185-193) for a
+ * ragged batch of uint8 HWC crops packed back to back in `src` (device memory). Per crop the
+ * caller fills the reference's geometry (data/transforms.py:91-118: new size, alignment offsets,
+ * interp 0 = INTER_LINEAR / 1 = INTER_AREA); c = 1 (gray, replicated), 3 (RGB) or 4 (RGBA, alpha
+ * dropped). out_kind 0: fp32 NCHW [B][3][H][W] (the reference's tensor); 1: the encoder input
+ * [B][H][W][8] in dtype (channels 3..7 zero; what crnn_nchw_to_nhwc makes of kind 0);
+ * 2: the uint8 canvas [B][H][W][3] before normalisation. */
+typedef struct {
+  long long offset; /* byte offset of the crop in src */
+  int h, w, c;      /* source size, channels */
+  int new_h, new_w; /* resized size */
+  int y0, x0;       /* placement on the white canvas */
+  int interp;       /* 0 linear, 1 area (the reference's _interp) */
+  int pad;
+} crnn_crop_desc;
+int crnn_preprocess(const unsigned char* src, const crnn_crop_desc* desc, int B, int H, int W, int out_kind,
+                    int dtype, void* out, void* stream);
+
 /* ------------------------------------------------------------------ CTC */
 /* Per-sample log-space CTC over logits [B][T][ldc] (fp32, C classes, blank = 0, input length T).
  * loss[b] = -log p(target_b); dlogits (may be NULL) = grad of the 'mean' reduction

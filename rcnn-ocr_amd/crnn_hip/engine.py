@@ -377,24 +377,33 @@ class CRNNEngine:
     # ------------------------------------------------------------------ forward
     def forward(self, images: torch.Tensor, train: bool, update_running: bool = True,
                 save_for_backward: bool = False, dropout_p: float = 0.0) -> torch.Tensor:
-        """images [B,3,H,W] fp32 (reference NCHW input) -> logits [B,T,C] fp32 (view).
+        """images [B,3,H,W] fp32 (reference NCHW input), or the encoder layout [B,H,W,8] in the
+        compute dtype (crnn_hip.preprocess out="encoder") -> logits [B,T,C] fp32 (view).
         dropout_p: enc_dropout probability applied to the encoder output in training
         (model/model.py:201,220); counter-based mask, regenerated in backward (crnn_dropout)."""
         L.require_device(images)
         self.pack()
         self.update_running = update_running
-        images = images.contiguous().float()
-        B, Cin, H, W = images.shape
-        if Cin != 3:
-            raise ValueError("expected 3-channel crops")
         ws, dt, T = self.ws, self.dt, self.dtype
+        packed = images.dim() == 4 and images.shape[-1] == 8 and images.shape[1] != 3 and images.dtype == T
+        if packed:
+            images = images.contiguous()
+            B, H, W = images.shape[:3]
+        else:
+            images = images.contiguous().float()
+            B, Cin, H, W = images.shape
+            if Cin != 3:
+                raise ValueError("expected 3-channel crops")
         s = L.stream_ptr()
         self._stat_cap = self._stat_capacity(B, H, W) if train else 0
         self._nbt = []
         sv = {}
 
-        x0 = ws.get("in", (B, H, W, 8), T)
-        call("crnn_nchw_to_nhwc", dt, ptr(images), ptr(x0), B, 3, H, W, 8, s)
+        if packed:
+            x0 = images
+        else:
+            x0 = ws.get("in", (B, H, W, 8), T)
+            call("crnn_nchw_to_nhwc", dt, ptr(images), ptr(x0), B, 3, H, W, 8, s)
         # stem (model/seresnet31.py:81-89)
         z0, m0, i0, sc0, sh0, h, w = self._conv_bn(self.stem0, x0, B, H, W, train, "s0")
         a0 = ws.get("s0.a", (B, h, w, 64), T)
