@@ -41,11 +41,13 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=32, help="batch of the CPU baseline sample")
     ap.add_argument("--cpu-steps", type=int, default=6)
-    ap.add_argument("--mode", default="train", choices=["train", "infer", "attn", "attn_train"],
+    ap.add_argument("--mode", default="train", choices=["train", "infer", "attn", "attn_train", "preprocess"],
                     help="train: BASELINE configs[2]/[3] (the headline); infer: configs[1] (eval forward + greedy "
                          "CTC decode on device); attn: eval encode + the reference's attention head, 26-step greedy "
                          "decode (SURVEY 8f next-1); attn_train: the reference's own training step (encoder + "
-                         "teacher-forced attention decoder, 26 steps, cross-entropy, backward, AdamW)")
+                         "teacher-forced attention decoder, 26 steps, cross-entropy, backward, AdamW); preprocess: "
+                         "the input pipeline (ResizeAndPadA + Normalize of ragged uint8 crops into the encoder "
+                         "layout, SURVEY 8f next-2)")
     ap.add_argument("--config", default=None, choices=["long"],
                     help="long: BASELINE configs[4] shapes (32x1024 crops, 4x768 BiLSTM, batch 64/GPU)")
     a = ap.parse_args()
@@ -155,12 +157,96 @@ def lstm_roofline(lstm, args, eng):
     return out
 
 
+def synthetic_crops(n, seed):
+    """ragged uint8 RGB text-line crops: height U{24..96}, aspect U[2, 16] (wider ones are fit by
+    width), random pixels — the shapes ResizeAndPadA sees on real datasets."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(n):
+        h = int(rng.integers(24, 97))
+        w = max(1, int(h * rng.uniform(2.0, 16.0)))
+        out.append(rng.integers(0, 256, (h, w, 3), dtype=np.uint8))
+    return out
+
+
+def bench_preprocess(args, world, rank, dev):
+    """crnn_preprocess over a device-resident ragged batch -> encoder input."""
+    from crnn_hip.preprocess import CropBatch, preprocess
+    dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    crops = synthetic_crops(args.batch, 4321 + rank)
+    batch = CropBatch.upload(crops, dev)
+    H, W = args.height, args.width
+
+    def step():
+        return preprocess(batch, H, W, out="encoder", dtype=dtype)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for e0, e1 in ev:
+        e0.record()
+        step()
+        e1.record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+        torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    kern_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+    src_bytes = int(batch.data.numel())
+    out_bytes = args.batch * H * W * 8 * (2 if dtype == torch.bfloat16 else 4)
+    algo = src_bytes + out_bytes
+    gbs = algo / (kern_ms * 1e-3) / 1e9
+    if rank == 0:
+        out = {
+            "metric": f"text-lines/sec (input pipeline: ResizeAndPadA + Normalize of ragged uint8 crops into the "
+                      f"encoder layout), B={args.batch}, {H}x{W} canvas, 1 MI355X",
+            "value": round(args.batch * world * args.steps / elapsed, 1), "unit": "text-lines/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic ragged uint8 RGB crops (height U{24..96}, aspect U[2,16]), device-resident",
+            "config": {"workload": f"crnn_preprocess -> [B,{H},{W},8] {args.dtype} (SURVEY 8f next-2)",
+                       "global_batch": args.batch * world, "per_gpu_batch": args.batch, "canvas": f"{H}x{W}",
+                       "parallelism": f"dp{world}" if world > 1 else "single"},
+            "roofline": {"bound": "hbm", "kernel": "preprocess_kernel", "achieved": round(gbs, 1),
+                         "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(gbs / PEAK_HBM_GBS, 4), "traffic": None,
+                         "algorithmic_bytes_per_launch": algo, "src_bytes": src_bytes, "out_bytes": out_bytes,
+                         "kernel_us": round(kern_ms * 1e3, 2),
+                         "timing": "HIP events around each launch on the launch stream, timed region"},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            import preprocess_oracle as P
+            sample = crops[: max(1, args.cpu_sample // 4)]
+            t1 = time.perf_counter()
+            for im in sample:
+                P.preprocess(im, H, W)
+            dt = time.perf_counter() - t1
+            out["cpu_baseline"] = {"value": round(len(sample) / dt, 3), "unit": "text-lines/s", "cores": 1,
+                                   "kind": "port", "sample": f"oracle/preprocess_oracle.py (numpy, scalar loops) on "
+                                                             f"{len(sample)} of the crops; {dt:.1f} s"}
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
     from crnn_hip import dist as D
     world, rank, local = D.init_from_env()
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    if args.mode == "preprocess":
+        return bench_preprocess(args, world, rank, dev)
 
     import crnn_oracle as O
     from crnn_hip.optim import FusedAdamW

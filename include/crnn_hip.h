@@ -373,7 +373,9 @@ typedef struct {
   int pad;
 } crnn_crop_desc;
 int crnn_preprocess(const unsigned char* src, const crnn_crop_desc* desc, int B, int H, int W, int out_kind,
-                    int dtype, void* out, void* stream);
+                    int dtype, void* out, void* ws, long ws_bytes, void* stream);
+/* bytes of device workspace crnn_preprocess needs (the per-column / per-row resampling taps) */
+long crnn_preprocess_workspace(int B, int H, int W);
 
 /* ------------------------------------------------------------------ CTC */
 /* Per-sample log-space CTC over logits [B][T][ldc] (fp32, C classes, blank = 0, input length T).

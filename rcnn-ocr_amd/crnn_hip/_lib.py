@@ -117,7 +117,8 @@ _SIGS = {
     "crnn_attn_dproj_enc": ([vp, vp, vp, vp, i32, i32, i32, i32, vp, vp], i32),
     "crnn_attn_onehot_rows": ([vp, i32, i32, i32, i32, vp, i32, i32, vp], i32),
     "crnn_attn_out": ([vp, i32, i32, i32, i32, vp, i32, vp, vp], i32),
-    "crnn_preprocess": ([vp, vp, i32, i32, i32, i32, i32, vp, vp], i32),
+    "crnn_preprocess": ([vp, vp, i32, i32, i32, i32, i32, vp, vp, i64, vp], i32),
+    "crnn_preprocess_workspace": ([i32, i32, i32], i64),
     "crnn_attn_xent": ([vp, i32, vp, i32, i32, i32, vp, vp, i32, vp, vp], i32),
     "crnn_ctc_loss": ([vp, i32, i32, i32, i32, vp, i32, vp, vp, vp, i32, vp], i32),
     "crnn_ctc_reduce_mean": ([vp, vp, i32, vp, vp], i32),

@@ -87,6 +87,24 @@ class CropBatch:
     def __len__(self):
         return len(self.shapes)
 
+    def plan(self, img_h: int, img_w: int, align_h: str = "left", align_v: str = "center"):
+        """device-resident crop descriptors (the reference's geometry per crop) + tap workspace,
+        cached per canvas / alignment."""
+        key = (img_h, img_w, align_h, align_v)
+        cache = self.__dict__.setdefault("_plans", {})
+        if key not in cache:
+            B = len(self)
+            descs = (_CropDesc * B)()
+            for i, ((h, w, c), off) in enumerate(zip(self.shapes, self.offsets)):
+                nh, nw, y0, x0, it = resize_geometry(h, w, img_h, img_w, align_h, align_v)
+                descs[i] = _CropDesc(off, h, w, c, nh, nw, y0, x0, it, 0)
+            raw = torch.frombuffer(bytearray(bytes(descs)), dtype=torch.uint8)
+            d = raw.to(self.data.device)
+            need = int(L.lib().crnn_preprocess_workspace(B, img_h, img_w))
+            ws = torch.empty(need, dtype=torch.uint8, device=self.data.device)
+            cache[key] = (d, ws)
+        return cache[key]
+
 
 def preprocess(batch: CropBatch, img_h: int = 32, img_w: int = 256, align_h: str = "left",
                align_v: str = "center", out: str = "nchw", dtype: torch.dtype = torch.float32) -> torch.Tensor:
@@ -95,12 +113,7 @@ def preprocess(batch: CropBatch, img_h: int = 32, img_w: int = 256, align_h: str
     canvas (before Normalize)."""
     L.require_device(batch.data)
     B = len(batch)
-    descs = (_CropDesc * B)()
-    for i, ((h, w, c), off) in enumerate(zip(batch.shapes, batch.offsets)):
-        nh, nw, y0, x0, it = resize_geometry(h, w, img_h, img_w, align_h, align_v)
-        descs[i] = _CropDesc(off, h, w, c, nh, nw, y0, x0, it, 0)
-    raw = torch.frombuffer(bytearray(bytes(descs)), dtype=torch.uint8)
-    d = raw.pin_memory().to(batch.data.device, non_blocking=True)
+    d, ws = batch.plan(img_h, img_w, align_h, align_v)
     dev = batch.data.device
     if out == "nchw":
         res, kind, dt = torch.empty(B, 3, img_h, img_w, device=dev), 0, L.F32
@@ -110,6 +123,6 @@ def preprocess(batch: CropBatch, img_h: int = 32, img_w: int = 256, align_h: str
         res, kind, dt = torch.empty(B, img_h, img_w, 3, device=dev, dtype=torch.uint8), 2, L.F32
     else:
         raise ValueError("out must be 'nchw', 'encoder' or 'u8'")
-    call("crnn_preprocess", ptr(batch.data), ptr(d), B, img_h, img_w, kind, dt, ptr(res), L.stream_ptr())
-    batch._desc_keepalive = d   # the launch reads it asynchronously
+    call("crnn_preprocess", ptr(batch.data), ptr(d), B, img_h, img_w, kind, dt, ptr(res), ptr(ws), ws.numel(),
+         L.stream_ptr())
     return res

@@ -79,12 +79,6 @@ __device__ __forceinline__ AreaTab area_tab(int d, int ssize, double scale) {
   return t;
 }
 
-__device__ __forceinline__ float area_w(const AreaTab& t, int s, int s1, int s2) {
-  if (t.plo && s == t.lo) return t.wlo;
-  if (t.phi && s == t.hi) return t.whi;
-  return t.wmid;
-}
-
 template <typename T>
 __device__ __forceinline__ void store_px(int kind, void* out, int b, int y, int x, int H, int W, const int v[3]) {
   const float den = 1.f / 127.5f;
@@ -110,10 +104,52 @@ __device__ __forceinline__ void store_px(int kind, void* out, int b, int y, int 
   }
 }
 
+// per destination column / row of a crop: the resampling taps, computed once per launch
+// (tab_kernel) instead of once per output pixel
+struct Tap {
+  int lo, hi;            // linear: s0, s1 ; area: source range [lo, hi]
+  int c0, c1;            // linear: 11-bit coefficients ; area: plo, phi flags
+  float wlo, wmid, whi;  // area weights
+  int pad;
+};
+
+__global__ __launch_bounds__(256) void tab_kernel(const crnn_crop_desc* __restrict__ desc, int H, int W,
+                                                  Tap* __restrict__ tabs) {
+  const int b = blockIdx.y, i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= W + H) return;
+  const crnn_crop_desc d = desc[b];
+  const bool isx = i < W;
+  const int k = isx ? i : i - W;
+  const int dsize = isx ? d.new_w : d.new_h, ssize = isx ? d.w : d.h;
+  if (k >= dsize) return;
+  const double scale = (double)ssize / dsize;
+  Tap t = {};
+  if (d.interp == 0) {
+    linear_tap(k, ssize, scale, isx, t.lo, t.hi, t.c0, t.c1);
+  } else {
+    const AreaTab a = area_tab(k, ssize, scale);
+    t.lo = a.lo;
+    t.hi = a.hi;
+    t.c0 = a.plo;
+    t.c1 = a.phi;
+    t.wlo = a.wlo;
+    t.wmid = a.wmid;
+    t.whi = a.whi;
+  }
+  tabs[(size_t)b * (W + H) + i] = t;
+}
+
+__device__ __forceinline__ float tap_w(const Tap& t, int s) {
+  if (t.c0 && s == t.lo) return t.wlo;
+  if (t.c1 && s == t.hi) return t.whi;
+  return t.wmid;
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void preprocess_kernel(const uint8_t* __restrict__ src,
-                                                         const crnn_crop_desc* __restrict__ desc, int H, int W,
-                                                         int kind, void* __restrict__ out) {
+                                                         const crnn_crop_desc* __restrict__ desc,
+                                                         const Tap* __restrict__ tabs, int H, int W, int kind,
+                                                         void* __restrict__ out) {
   const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y, b = blockIdx.z;
   if (x >= W) return;
   const crnn_crop_desc d = desc[b];
@@ -121,20 +157,29 @@ __global__ __launch_bounds__(256) void preprocess_kernel(const uint8_t* __restri
   const int dy = y - d.y0, dx = x - d.x0;
   if (dy >= 0 && dy < d.new_h && dx >= 0 && dx < d.new_w) {
     const uint8_t* s = src + d.offset;
-    const int cs = d.c, rs = d.w * d.c;  // channel / row strides (GRAY: 1 channel replicated)
-    const int nc = d.c == 1 ? 1 : 3;
+    const int cs = d.c, rs = d.w * d.c;  // channel / row strides
+    const int cm = d.c == 1 ? 0 : 1;     // GRAY: channel 0 read for all three (COLOR_GRAY2RGB)
+    // every load below is unconditional (clamped indices) and issued before its uses: a load under
+    // a runtime condition makes the compiler wait for it on the spot, serializing the taps
+    auto px = [&](int yy, int xx, int c) -> int { return s[(size_t)yy * rs + xx * cs + c * cm]; };
     if (d.new_h == d.h && d.new_w == d.w) {
-      for (int c = 0; c < nc; ++c) v[c] = s[(size_t)dy * rs + dx * cs + c];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) v[c] = px(dy, dx, c);
     } else if (d.interp == 0) {
-      int sx0, sx1, a0, a1, sy0, sy1, b0, b1;
-      linear_tap(dx, d.w, (double)d.w / d.new_w, true, sx0, sx1, a0, a1);
-      linear_tap(dy, d.h, (double)d.h / d.new_h, false, sy0, sy1, b0, b1);
-      const uint8_t* r0 = s + (size_t)sy0 * rs;
-      const uint8_t* r1 = s + (size_t)sy1 * rs;
-      for (int c = 0; c < nc; ++c) {
-        const long h0 = (long)r0[sx0 * cs + c] * a0 + (long)r0[sx1 * cs + c] * a1;
-        const long h1 = (long)r1[sx0 * cs + c] * a0 + (long)r1[sx1 * cs + c] * a1;
-        const long q = (b0 * h0 + b1 * h1 + (1l << (2 * COEF_BITS - 1))) >> (2 * COEF_BITS);
+      const Tap tx = tabs[(size_t)b * (W + H) + dx], ty = tabs[(size_t)b * (W + H) + W + dy];
+      int p[2][2][3];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        p[0][0][c] = px(ty.lo, tx.lo, c);
+        p[0][1][c] = px(ty.lo, tx.hi, c);
+        p[1][0][c] = px(ty.hi, tx.lo, c);
+        p[1][1][c] = px(ty.hi, tx.hi, c);
+      }
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const long h0 = (long)p[0][0][c] * tx.c0 + (long)p[0][1][c] * tx.c1;
+        const long h1 = (long)p[1][0][c] * tx.c0 + (long)p[1][1][c] * tx.c1;
+        const long q = (ty.c0 * h0 + ty.c1 * h1 + (1l << (2 * COEF_BITS - 1))) >> (2 * COEF_BITS);
         v[c] = (int)min(255l, max(0l, q));
       }
     } else {
@@ -142,51 +187,77 @@ __global__ __launch_bounds__(256) void preprocess_kernel(const uint8_t* __restri
       const int ix = (int)rint(scx), iy = (int)rint(scy);
       if (fabs(scx - ix) < 2.220446049250313e-16 && fabs(scy - iy) < 2.220446049250313e-16) {  // resizeAreaFast
         int sum[3] = {0, 0, 0};
+        const int x1 = (dx + 1) * ix - 1;
         for (int yy = dy * iy; yy < (dy + 1) * iy; ++yy)
-          for (int xx = dx * ix; xx < (dx + 1) * ix; ++xx)
-            for (int c = 0; c < nc; ++c) sum[c] += s[(size_t)yy * rs + xx * cs + c];
+          for (int xx = dx * ix; xx <= x1; xx += 4) {
+            int q[4][3];
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+              for (int c = 0; c < 3; ++c) q[k][c] = px(yy, min(xx + k, x1), c);
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+              for (int c = 0; c < 3; ++c) sum[c] += xx + k <= x1 ? q[k][c] : 0;
+          }
         const float inv = 1.f / (float)(ix * iy);
-        for (int c = 0; c < nc; ++c) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
           const int q = (ix == 2 && iy == 2) ? (sum[c] + 2) >> 2 : cv_round(__fmul_rn((float)sum[c], inv));
           v[c] = min(255, max(0, q));
         }
       } else {
-        const AreaTab tx = area_tab(dx, d.w, scx), ty = area_tab(dy, d.h, scy);
+        const Tap tx = tabs[(size_t)b * (W + H) + dx], ty = tabs[(size_t)b * (W + H) + W + dy];
         float acc[3] = {0.f, 0.f, 0.f};
         for (int yy = ty.lo; yy <= ty.hi; ++yy) {
-          const float beta = area_w(ty, yy, ty.lo, ty.hi);
+          const float beta = tap_w(ty, yy);
           float buf[3] = {0.f, 0.f, 0.f};
-          for (int xx = tx.lo; xx <= tx.hi; ++xx) {
-            const float alpha = area_w(tx, xx, tx.lo, tx.hi);
-            for (int c = 0; c < nc; ++c)
-              buf[c] = __fadd_rn(buf[c], __fmul_rn((float)s[(size_t)yy * rs + xx * cs + c], alpha));
+          for (int xx = tx.lo; xx <= tx.hi; xx += 4) {  // OpenCV's order: ascending x, one add at a time
+            int q[4][3];
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+              for (int c = 0; c < 3; ++c) q[k][c] = px(yy, min(xx + k, tx.hi), c);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              if (xx + k > tx.hi) break;
+              const float alpha = tap_w(tx, xx + k);
+#pragma unroll
+              for (int c = 0; c < 3; ++c) buf[c] = __fadd_rn(buf[c], __fmul_rn((float)q[k][c], alpha));
+            }
           }
-          for (int c = 0; c < nc; ++c) {
+#pragma unroll
+          for (int c = 0; c < 3; ++c) {
             const float term = __fmul_rn(beta, buf[c]);
             acc[c] = yy == ty.lo ? term : __fadd_rn(acc[c], term);
           }
         }
-        for (int c = 0; c < nc; ++c) v[c] = min(255, max(0, cv_round(acc[c])));
+#pragma unroll
+        for (int c = 0; c < 3; ++c) v[c] = min(255, max(0, cv_round(acc[c])));
       }
     }
-    if (nc == 1) v[1] = v[2] = v[0];  // COLOR_GRAY2RGB
   }
   store_px<T>(kind, out, b, y, x, H, W, v);
 }
 
 }  // namespace
 
+extern "C" long crnn_preprocess_workspace(int B, int H, int W) { return (long)B * (H + W) * (long)sizeof(Tap); }
+
 extern "C" int crnn_preprocess(const unsigned char* src, const crnn_crop_desc* desc, int B, int H, int W, int out_kind,
-                               int dtype, void* out, void* stream) {
+                               int dtype, void* out, void* ws, long ws_bytes, void* stream) {
   if (B <= 0 || H <= 0 || W <= 0 || B > 65535 || H > 65535)
     return crnn_set_error(hipErrorInvalidValue, "preprocess: bad batch / canvas size");
   if (out_kind < 0 || out_kind > 2) return crnn_set_error(hipErrorInvalidValue, "preprocess: out_kind 0, 1 or 2");
+  if (ws_bytes < crnn_preprocess_workspace(B, H, W))
+    return crnn_set_error(hipErrorInvalidValue, "preprocess: workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  Tap* tabs = (Tap*)ws;
+  hipLaunchKernelGGL(tab_kernel, dim3((W + H + 255) / 256, B), dim3(256), 0, st, desc, H, W, tabs);
   const dim3 grid((W + 255) / 256, H, B);
   if (out_kind == 1 && dtype == CRNN_BF16)
-    hipLaunchKernelGGL(preprocess_kernel<bf16>, grid, dim3(256), 0, (hipStream_t)stream, src, desc, H, W, out_kind,
-                       out);
+    hipLaunchKernelGGL(preprocess_kernel<bf16>, grid, dim3(256), 0, st, src, desc, tabs, H, W, out_kind, out);
   else
-    hipLaunchKernelGGL(preprocess_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, src, desc, H, W, out_kind,
-                       out);
+    hipLaunchKernelGGL(preprocess_kernel<float>, grid, dim3(256), 0, st, src, desc, tabs, H, W, out_kind, out);
   return (int)hipGetLastError();
 }

@@ -1,13 +1,17 @@
-"""Input preprocessing for the CTC path: data/transforms.py of the reference, restated on
-PIL + numpy (cv2 / albumentations are not available in this image).
+"""Input preprocessing: data/transforms.py of the reference on the HIP path (cv2 / albumentations
+are not available in this image; the resampling is restated in csrc/preprocess.hip).
 
   load_charset            data/transforms.py:39-59 (one token per line, blank lines skipped)
-  resize_and_pad          ResizeAndPadA :62-120 (aspect-preserving fit, white canvas, left/center align);
-                          PIL BILINEAR for upscaling (cv2 INTER_LINEAR), BOX for downscaling (INTER_AREA)
-  normalize               A.Normalize(0.5, 0.5) :190 -> (u8/255 - 0.5) / 0.5
-  get_val_transform       :186-193, callable(image=HxWx3 uint8) -> {"image": [3,H,W] float tensor}
+  ResizeAndPadA           :62-120 (aspect-preserving fit, white canvas, alignment; INTER_LINEAR up,
+                          INTER_AREA down, OpenCV 4.x arithmetic) -> crnn_hip.preprocess (HIP)
+  get_val_transform       :185-193, callable(image=HxW[xC] uint8) -> {"image": [3,H,W] float tensor}:
+                          ResizeAndPadA + A.Normalize(0.5, 0.5) ((v - 127.5) * (1/127.5), fp32) + ToTensorV2
+  preprocess_batch        the same for a ragged list of crops in one launch, optionally straight into
+                          the encoder's input layout (what OCRInference.predict uses)
+  pack_attention_targets  :123-157 (text_in = [SOS, ids, PAD...], target_y = [ids, EOS, PAD...])
   ctc_targets             label strings -> padded id tensor + lengths (blank = 0 = <PAD>)
-The resize is not bit-identical to cv2 (different resampling kernels); the rest is exact.
+There is no CPU fallback: the transforms need a HIP device (parity of the kernel with the
+restatement in oracle/preprocess_oracle.py is bit-exact; with cv2 itself it is unpinned).
 """
 from __future__ import annotations
 
@@ -28,35 +32,36 @@ def load_charset(charset_path: str):
     return itos, {s: i for i, s in enumerate(itos)}
 
 
-def _to_rgb(img: np.ndarray) -> np.ndarray:
-    if img.ndim == 2:
-        img = np.repeat(img[:, :, None], 3, axis=2)
-    elif img.shape[2] == 4:
-        img = img[:, :, :3]
-    return img
+def _device(device=None):
+    dev = torch.device(device if device is not None else "cuda")
+    if dev.type != "cuda" or not torch.cuda.is_available():
+        raise RuntimeError("data.transforms runs on the HIP device (crnn_preprocess); no CPU fallback")
+    return dev
+
+
+def preprocess_batch(images: Sequence[np.ndarray], img_h: int = 32, img_w: int = 256, align_h: str = "left",
+                     align_v: str = "center", out: str = "nchw", dtype: torch.dtype = torch.float32, device=None):
+    """ragged list of uint8 crops -> [B, 3, H, W] fp32 ("nchw"), [B, H, W, 8] dtype ("encoder") or
+    [B, H, W, 3] uint8 ("u8"), on the device."""
+    from crnn_hip.preprocess import CropBatch, preprocess
+    batch = CropBatch.upload(list(images), _device(device))
+    return preprocess(batch, img_h, img_w, align_h, align_v, out=out, dtype=dtype)
 
 
 def resize_and_pad(img: np.ndarray, img_h: int = 32, img_w: int = 256, align_h: str = "left",
                    align_v: str = "center") -> np.ndarray:
-    from PIL import Image
-    img = _to_rgb(np.asarray(img))
-    h, w = img.shape[:2]
-    scale = min(img_h / max(h, 1), img_w / max(w, 1))
-    new_w, new_h = max(1, int(round(w * scale))), max(1, int(round(h * scale)))
-    resample = Image.BOX if (new_h < h or new_w < w) else Image.BILINEAR
-    resized = np.asarray(Image.fromarray(img.astype(np.uint8)).resize((new_w, new_h), resample=resample))
-    canvas = np.full((img_h, img_w, 3), 255, dtype=np.uint8)
-    x0 = {"left": 0, "right": img_w - new_w}.get(align_h, (img_w - new_w) // 2)
-    y0 = {"top": 0, "bottom": img_h - new_h}.get(align_v, (img_h - new_h) // 2)
-    x0 = max(0, min(x0, img_w - new_w))
-    y0 = max(0, min(y0, img_h - new_h))
-    canvas[y0:y0 + new_h, x0:x0 + new_w] = resized
-    return canvas
+    """ResizeAndPadA.apply -> [img_h, img_w, 3] uint8 (host array)."""
+    return preprocess_batch([img], img_h, img_w, align_h, align_v, out="u8")[0].cpu().numpy()
 
 
-def normalize(img_u8: np.ndarray) -> torch.Tensor:
-    x = torch.from_numpy(np.ascontiguousarray(img_u8)).float().permute(2, 0, 1)
-    return (x / 255.0 - 0.5) / 0.5
+class ResizeAndPadA:
+    """albumentations-style callable with the reference's constructor (:62-76)."""
+
+    def __init__(self, img_h=32, img_w=256, align_h="left", align_v="center", always_apply=True, p=1.0):
+        self.img_h, self.img_w, self.align_h, self.align_v = int(img_h), int(img_w), align_h, align_v
+
+    def __call__(self, image, **kw) -> Dict[str, np.ndarray]:
+        return {"image": resize_and_pad(image, self.img_h, self.img_w, self.align_h, self.align_v)}
 
 
 class _ValTransform:
@@ -64,11 +69,32 @@ class _ValTransform:
         self.img_h, self.img_w = img_h, img_w
 
     def __call__(self, image) -> Dict[str, torch.Tensor]:
-        return {"image": normalize(resize_and_pad(image, self.img_h, self.img_w))}
+        return {"image": preprocess_batch([image], self.img_h, self.img_w)[0].cpu()}
 
 
 def get_val_transform(img_h: int, img_w: int):
     return _ValTransform(img_h, img_w)
+
+
+def pack_attention_targets(texts, stoi, max_len, drop_blank=True):
+    """data/transforms.py:123-157: text_in [B, max_len+1] = [SOS, ids[:L], PAD...], target_y =
+    [ids[:L], EOS, PAD...], lengths = L + 1; unknown characters (and <BLANK> if drop_blank) skipped."""
+    PAD, SOS, EOS = stoi["<PAD>"], stoi["<SOS>"], stoi["<EOS>"]
+    BLANK = stoi.get("<BLANK>", None)
+    B, T = len(texts), max_len + 1
+    text_in = torch.full((B, T), PAD, dtype=torch.long)
+    text_in[:, 0] = SOS
+    target_y = torch.full((B, T), PAD, dtype=torch.long)
+    lengths = torch.zeros(B, dtype=torch.long)
+    for i, s in enumerate(texts):
+        ids = [stoi[ch] for ch in s if ch in stoi and not (drop_blank and BLANK is not None and stoi[ch] == BLANK)]
+        n = min(len(ids), max_len)
+        if n > 0:
+            text_in[i, 1:1 + n] = torch.tensor(ids[:n], dtype=torch.long)
+            target_y[i, :n] = torch.tensor(ids[:n], dtype=torch.long)
+        target_y[i, n] = EOS
+        lengths[i] = n + 1
+    return text_in, target_y, lengths
 
 
 def ctc_targets(texts: Sequence[str], stoi: Dict[str, int], max_len: int) -> Tuple[torch.Tensor, torch.Tensor]:

@@ -3,8 +3,10 @@
 Same constructor arguments, checkpoint formats and predict() contract (single image -> str,
 list -> list, optional (text, confidence)). The head is CTC, so decoding is the
 greedy CTC collapse (repeats merged, blank = id 0 = <PAD> dropped) done by the HIP greedy
-kernel; confidence = mean max-softmax over the emitted frames. Images go through
-data.transforms.get_val_transform (aspect-preserving resize onto a white canvas, (x-0.5)/0.5).
+kernel; confidence = mean max-softmax over the emitted frames. Each batch of images goes through
+the HIP input pipeline in one launch (data.transforms.preprocess_batch: ResizeAndPadA +
+Normalize, inference.py:93-124 / data/transforms.py:185-193) straight into the encoder's input
+layout.
 """
 from __future__ import annotations
 
@@ -15,7 +17,7 @@ import numpy as np
 import torch
 
 from crnn_hip.ctc import ctc_greedy_decode
-from data.transforms import get_val_transform, load_charset
+from data.transforms import get_val_transform, load_charset, preprocess_batch
 from model.model import RCNN
 
 
@@ -52,19 +54,22 @@ class OCRInference:
         model.load_state_dict(state, strict=any(k.startswith("ctc_head.") for k in state))
         return model.to(self.device).eval()
 
-    def _preprocess_image(self, image) -> torch.Tensor:
+    def _load_image(self, image) -> np.ndarray:
+        """inference.py:104-119: path (read as RGB), PIL image (RGB) or array (gray / RGB / RGBA)."""
         from PIL import Image
         if isinstance(image, str):
             if not os.path.exists(image):
                 raise FileNotFoundError(f"Image file not found: {image}")
-            img = np.asarray(Image.open(image).convert("RGB"))
-        elif isinstance(image, Image.Image):
-            img = np.asarray(image.convert("RGB"))
-        elif isinstance(image, np.ndarray):
-            img = image
-        else:
-            raise ValueError(f"Unsupported image type: {type(image)}")
-        return self.transform(image=img)["image"]
+            return np.asarray(Image.open(image).convert("RGB"))
+        if isinstance(image, Image.Image):
+            return np.asarray(image.convert("RGB"))
+        if isinstance(image, np.ndarray):
+            return image
+        raise ValueError(f"Unsupported image type: {type(image)}")
+
+    def _preprocess_image(self, image) -> torch.Tensor:
+        """inference.py:93-124: one image -> [1, 3, H, W] on the device."""
+        return preprocess_batch([self._load_image(image)], self.img_h, self.img_w, device=self.device)
 
     @torch.no_grad()
     def predict(self, images: Union[np.ndarray, str, "Image.Image", List], max_length: int = 25, batch_size: int = 32,
@@ -73,7 +78,8 @@ class OCRInference:
         items = [images] if single else images
         results = []
         for i in range(0, len(items), batch_size):
-            batch = torch.stack([self._preprocess_image(im) for im in items[i:i + batch_size]]).to(self.device)
+            batch = preprocess_batch([self._load_image(im) for im in items[i:i + batch_size]], self.img_h, self.img_w,
+                                     out="encoder", dtype=self.compute_dtype, device=self.device)
             logits = self.model(batch, is_train=False, batch_max_length=max_length)   # [B, T, C]
             seqs = ctc_greedy_decode(logits)
             if return_confidence:

@@ -10,24 +10,48 @@ import crnn_oracle as O
 from helpers import GOLDEN, case_params, load, pixels_to_images
 
 
+@pytest.mark.gpu
 def test_val_transform_is_identity_resize_plus_normalize():
-    """a crop already at the target size is only normalised (x/255 - 0.5)/0.5, exactly as the
-    goldens' pixels_to_images (data/transforms.py:186-193)."""
+    """a crop already at the target size is only normalised, with albumentations' arithmetic
+    (v - 127.5) * (1/127.5) (data/transforms.py:186-193): exactly the oracle's, and within 1 ulp
+    of the goldens' (x/255 - 0.5)/0.5 (pixels_to_images)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import preprocess_oracle as P
     from data.transforms import get_val_transform
     z = load("encode_eval_b4_32x128_h256.npz")
     pix = np.asarray(z["pixels"])            # [B, 3, H, W] uint8
     tf = get_val_transform(pix.shape[2], pix.shape[3])
     got = torch.stack([tf(image=p.transpose(1, 2, 0))["image"] for p in pix])
-    assert torch.equal(got, pixels_to_images(pix))
+    want = torch.stack([torch.from_numpy(P.normalize(p.transpose(1, 2, 0))) for p in pix])
+    assert torch.equal(got, want)
+    assert float((got - pixels_to_images(pix)).abs().max()) <= 1.2e-7
 
 
+@pytest.mark.gpu
 def test_resize_and_pad_geometry():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
     from data.transforms import resize_and_pad
     img = np.zeros((20, 50, 3), np.uint8)
     out = resize_and_pad(img, 32, 256)
     assert out.shape == (32, 256, 3)
     # 20x50 -> scale min(32/20, 256/50) = 1.6 -> 32x80 at the left, white elsewhere
     assert (out[:, :80] == 0).all() and (out[:, 80:] == 255).all()
+
+
+def test_pack_attention_targets():
+    """data/transforms.py:123-157 semantics: SOS-prefixed inputs, EOS-terminated targets, truncation
+    at max_len, unknown characters and <BLANK> dropped."""
+    from data.transforms import pack_attention_targets, load_charset
+    itos, stoi = load_charset(os.path.join(GOLDEN, "charset.txt"))
+    a, b = itos[5], itos[9]
+    ti, ty, ln = pack_attention_targets([a + b + "\u2603" + a, "", a * 40], stoi, max_len=25)
+    assert ti.shape == (3, 26) and ty.shape == (3, 26)
+    assert ti[0, :4].tolist() == [stoi["<SOS>"], 5, 9, 5] and ti[0, 4:].eq(stoi["<PAD>"]).all()
+    assert ty[0, :4].tolist() == [5, 9, 5, stoi["<EOS>"]] and ln[0] == 4
+    assert ti[1, 0] == stoi["<SOS>"] and ty[1, 0] == stoi["<EOS>"] and ln[1] == 1
+    assert ti[2, 1:].eq(5).all() and ty[2, :25].eq(5).all() and ty[2, 25] == stoi["<EOS>"] and ln[2] == 26
 
 
 def test_metrics():
