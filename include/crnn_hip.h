@@ -96,6 +96,11 @@ typedef struct {
   void* dst;
 } crnn_pack_job;
 int crnn_pack_batch(int dtype, const crnn_pack_job* jobs, int njobs, long total, void* stream);
+/* conv weights only (kind CRNN_PACK_CONV, a..e = Co, Ci, KH, KW, Cip), one block per output channel:
+ * job.start = the job's first output channel in the concatenation (total_rows = sum of Co);
+ * max_slab = the largest Ci*KH*KW (<= 16384). Same output as crnn_pack_batch for these jobs. */
+int crnn_pack_conv_batch(int dtype, const crnn_pack_job* jobs, int njobs, long total_rows, int max_slab,
+                         void* stream);
 
 /* ------------------------------------------------------------------ conv */
 typedef struct {

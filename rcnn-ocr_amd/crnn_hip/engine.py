@@ -175,7 +175,8 @@ class CRNNEngine:
             return
         if self._pack_jobs is None:
             self._build_pack_jobs()
-        jobs, n, total = self._pack_jobs
+        (cjobs, cn, crows, cslab), (jobs, n, total) = self._pack_jobs
+        call("crnn_pack_conv_batch", self.dt, ptr(cjobs), cn, crows, cslab, L.stream_ptr())
         call("crnn_pack_batch", self.dt, ptr(jobs), n, total, L.stream_ptr())
         self.packed_version = ver
 
@@ -189,9 +190,18 @@ class CRNNEngine:
             return dst.numel()
 
         sizes = []
+        # conv weights: their own launch, one block per output channel (crnn_pack_conv_batch)
+        rows, slab = 0, 0
         for cs in self.convs():
             out = self._pbuf(cs.name, (cs.co, cs.kh, cs.kw, cs.ci), T)
-            sizes.append(job(L.PACK_CONV, self.p[cs.name], out, cs.co, cs.ci_real, cs.kh, cs.kw, cs.ci))
+            job(L.PACK_CONV, self.p[cs.name], out, cs.co, cs.ci_real, cs.kh, cs.kw, cs.ci)
+            jobs[-1].start = rows
+            rows += cs.co
+            slab = max(slab, cs.ci_real * cs.kh * cs.kw)
+        carr = (L.PackJob * len(jobs))(*jobs)
+        craw = torch.frombuffer(bytearray(bytes(carr)), dtype=torch.uint8).to(self.device)
+        conv_tab = (craw, len(jobs), rows, slab)
+        jobs.clear()
         for l in range(self.nl):
             pre = f"enc_rnn.{l}"
             ind = self.enc_dim if l == 0 else H
@@ -221,7 +231,7 @@ class CRNNEngine:
             start += n
         arr = (L.PackJob * len(jobs))(*jobs)
         raw = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(self.device)
-        self._pack_jobs = (raw, len(jobs), start)
+        self._pack_jobs = (conv_tab, (raw, len(jobs), start))
 
     # ------------------------------------------------------------------ instrumentation
     def enable_timing(self, on: bool = True):

@@ -976,6 +976,32 @@ __global__ __launch_bounds__(256) void pack_batch_kernel(const crnn_pack_job* __
   }
 }
 
+// conv weights, one block per output channel co: the OIHW source slab [Ci][KH][KW] (contiguous) is
+// staged in LDS with coalesced reads, then written as the OHWI slab [KH][KW][Cip] (contiguous) —
+// both sides coalesced, unlike the per-element gather of pack_batch_kernel (stride KH*KW reads).
+// LDS reads at stride KH*KW words: conflict-free for 3x3 (9 is odd), 4-way at worst for 2x2.
+template <typename T>
+__global__ __launch_bounds__(256) void pack_conv_kernel(const crnn_pack_job* __restrict__ jobs, int njobs) {
+  extern __shared__ float slab[];
+  const long row = blockIdx.x;
+  int lo = 0, hi = njobs - 1;
+  while (lo < hi) {  // last job with start (first output channel) <= row
+    const int mid = (lo + hi + 1) >> 1;
+    if (jobs[mid].start <= row) lo = mid;
+    else hi = mid - 1;
+  }
+  const crnn_pack_job jb = jobs[lo];
+  const int co = (int)(row - jb.start), Ci = jb.b, KHW = jb.c * jb.d, Cip = jb.e;
+  const float* src = jb.src + (size_t)co * Ci * KHW;
+  for (int i = threadIdx.x; i < Ci * KHW; i += blockDim.x) slab[i] = src[i];
+  __syncthreads();
+  T* dst = (T*)jb.dst + (size_t)co * KHW * Cip;
+  for (int i = threadIdx.x; i < KHW * Cip; i += blockDim.x) {
+    const int t = i / Cip, ci = i - t * Cip;
+    dst[i] = fromf<T>(ci < Ci ? slab[ci * KHW + t] : 0.f);
+  }
+}
+
 // ------------------------------------------------------------ dropout (enc_dropout, model/model.py:201,220)
 // Counter-based: element i of a call with seed s is kept iff hash(s, i) >= p * 2^32, so the
 // backward regenerates the forward's mask from (seed, index) and nothing is stored. The hash is
@@ -1687,6 +1713,15 @@ int crnn_pack_batch(int dtype, const crnn_pack_job* jobs, int njobs, long total,
   const long chunk = (total + blocks - 1) / blocks;
   DISPATCH(dtype, hipLaunchKernelGGL(pack_batch_kernel<T>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
                                      jobs, njobs, total, chunk));
+  return (int)hipGetLastError();
+}
+
+int crnn_pack_conv_batch(int dtype, const crnn_pack_job* jobs, int njobs, long total_rows, int max_slab,
+                         void* stream) {
+  if (njobs <= 0 || total_rows <= 0 || max_slab <= 0 || max_slab > 16384)
+    return crnn_set_error(hipErrorInvalidValue, "pack_conv_batch: bad job table / slab size");
+  DISPATCH(dtype, hipLaunchKernelGGL(pack_conv_kernel<T>, dim3((unsigned)total_rows), dim3(256),
+                                     (size_t)max_slab * sizeof(float), (hipStream_t)stream, jobs, njobs));
   return (int)hipGetLastError();
 }
 

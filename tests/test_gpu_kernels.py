@@ -895,3 +895,27 @@ def test_bn_bwd_pool_mode_matches_maxpool_then_relu_mode(dtype, shape):
     tol = 1e-4 if dtype == torch.float32 else 3e-2
     assert relerr(dz_p.permute(0, 3, 1, 2), zr.grad) < tol
     assert relerr(dgam_p, pr[0].grad) < tol and relerr(dbet_p, pr[1].grad) < tol
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_weight_pack_layouts(dtype):
+    """CRNNEngine.pack (crnn_pack_conv_batch for the 28 convs, crnn_pack_batch for the rest): every
+    conv weight is the OIHW fp32 parameter as OHWI with Ci zero-padded to Cip, cast to the
+    compute dtype (exact)."""
+    import crnn_oracle as O
+    from crnn_hip.recipe import recipe_state_dict
+    from model.model import RCNN
+    m = RCNN(num_classes=194, hidden_size=256, blank_id=None, compute_dtype=dtype)
+    m.load_state_dict(recipe_state_dict(O.param_shapes(256, 194), 3), strict=False)
+    m = m.to(DEV).eval()
+    eng = m._engine_for(torch.zeros(2, 3, 32, 128, device=DEV))
+    eng.pack()
+    torch.cuda.synchronize()
+    n = 0
+    for cs in eng.convs():
+        w = eng.p[cs.name].detach().float()
+        want = torch.zeros(cs.co, cs.kh, cs.kw, cs.ci, device=DEV)
+        want[..., :cs.ci_real] = w.permute(0, 2, 3, 1)
+        assert torch.equal(eng.packed[cs.name], want.to(dtype)), cs.name
+        n += 1
+    assert n == 28
