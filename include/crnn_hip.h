@@ -57,7 +57,9 @@ enum { CRNN_OPT_GEMM_STAGGER = 0,    /* 256-row conv GEMM: waves 4-7 one barrier
        CRNN_OPT_HALO_CONV = 5,       /* full-resolution 3x3 stride-1 convs (the stem's 64 -> 128) on the
                                         halo-tiled direct kernel (conv_halo.hip): 1 = on (default), 0 = GEMM,
                                         n >= 2: on, with n-row bands for the MFMA-bound instances */
-       CRNN_OPT_COUNT = 6 };
+       CRNN_OPT_LSTM_HANDOFF = 6,    /* persistent BiLSTM forward: 1 = data-tagged granule ring (default),
+                                        0 = write-through payload + step counter */
+       CRNN_OPT_COUNT = 7 };
 int crnn_set_option(int key, int value);
 
 /* ------------------------------------------------------------------ layout */
@@ -287,10 +289,11 @@ int crnn_lstm_wgrad(const void* dgates, const void* x, const void* hseq, float* 
  * buffers and results). One workgroup per (direction, S samples, U units), S x U chosen per
  * sweep by crnn_lstm_seq_config() among 16 x 32, 32 x 32 and 16 x 64 (H <= 512) such that the
  * grid 2*(B/S)*(H/U) fits the device's CU count (all resident); H in {256, 512, 768}.
- * ws: crnn_lstm_seq_workspace(B) bytes of device memory, zeroed by the call itself:
+ * ws: crnn_lstm_seq_workspace(B) bytes of device memory, the used part zeroed by the call itself:
  * [2*(B/16+1)] step counters (the first 2*B/S used; counter of slice (d, bs) = d*(B/S)+bs reaches
  * (H/U)*T) then one error word (non-zero after a bounded wait timed out, in which case the outputs
- * carry NaN). */
+ * carry NaN), then (256-B aligned) the forward's hand-off ring of 2*B*H 8-byte granules
+ * {2 bf16 of h_t, u32 tag}. */
 int crnn_lstm_seq_supported(int dtype, int B, int H);
 /* the (samples, units) workgroup tile the forward (bwd = 0) or BPTT (bwd = 1) sweep uses for
  * (B, H); 0 if unsupported */

@@ -307,12 +307,13 @@ class CRNNEngine:
 
     def _seq_ws(self, B):
         n = (L.lib().crnn_lstm_seq_workspace(B) + 3) // 4
+        self._seq_err_index = 2 * (B // 16 + 1)   # include/crnn_hip.h: counters, then the error word
         return self.ws.get("rnn.seq_ws", (n,), torch.int32)
 
     def seq_status(self) -> int:
         """error word of the last persistent BiLSTM launch (0 = ok; non-zero: a bounded wait timed out)."""
         t = self.ws.bufs.get("rnn.seq_ws")
-        return 0 if t is None else int(t[-1].item() if t.numel() else 0)
+        return 0 if t is None else int(t[self._seq_err_index].item())
 
     def _bn_finalize(self, prefix, psum, psq, rows, count, train, tag, rpp=1):
         C = psum.shape[-1] if psum is not None else self.p[prefix + ".weight"].numel()

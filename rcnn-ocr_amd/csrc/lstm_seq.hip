@@ -84,17 +84,26 @@ __device__ __forceinline__ void seq_coords(int nsl, int nbs, int& d, int& bs, in
 // [w*H/4, (w+1)*H/4) of the W_hh' slice (NJ = 4U/16 row fragments x KK k-steps) in VGPRs and
 // computes an S x 4U partial tile; the partials are summed through LDS and wave w finalises the
 // fragment blocks bi = w*QB .. w*QB+QB-1 (QB = MI*NJ/4), bi -> (i = bi / NJ, j = bi % NJ).
-template <int H, int S, int U>
+//
+// TAG = true (the default, CRNN_OPT_LSTM_HANDOFF = 1): h_t travels as data-tagged 8-byte granules
+// {2 bf16 of h, u32 tag = step + 1} in a 2-slot ring (slot = step & 1, zeroed per launch), written
+// by 16-B sc1 stores (two granules each) and read by 16-B sc1 loads that each wave re-issues until
+// every tag it loaded matches (MI355X_MICROARCH.md price list, handoff-1to1 vs handoff-flag: no
+// vmcnt drain, barrier, counter add or poll on the critical path). Two slots suffice: a producer
+// writes slot s & 1 again at step s + 2 only after it has read h_{s+1} of every workgroup of its
+// group, each of which was computed after that workgroup's loads of h_s had returned.
+// TAG = false: the write-through payload + drained counter hand-off described at the top.
+template <int H, int S, int U, bool TAG>
 __global__ __launch_bounds__(256) void lstm_seq_fwd_kernel(const bf16* __restrict__ xg, const bf16* __restrict__ whh,
                                                            bf16* hseq, bf16* __restrict__ gsv, float* __restrict__ csv,
-                                                           unsigned* cnt, unsigned* err, int B, int Tn,
+                                                           unsigned* cnt, unsigned* err, uint2* ring, int B, int Tn,
                                                            unsigned long long* stamps) {
   constexpr int KW = H / 4, KK = KW / 32;
   constexpr int GR = 4 * U, NJ = GR / 16, MI = S / 16;
   constexpr int QB = MI * NJ / 4;   // blocks finalised per wave
   constexpr int H4 = 4 * H;
   static_assert(H % 128 == 0 && S % 16 == 0 && U % 16 == 0 && (MI * NJ) % 4 == 0, "shape");
-  static_assert(S * U / 8 <= 256, "publish: one 16-B store per thread");
+  static_assert(S * U / 8 <= 256 && S * U / 4 <= 256, "publish: one 16-B store per thread");
   __shared__ __attribute__((aligned(16))) f32x4 part[4][MI][NJ][64];
   __shared__ __attribute__((aligned(16))) bf16 htile[S][U];
 
@@ -122,6 +131,7 @@ __global__ __launch_bounds__(256) void lstm_seq_fwd_kernel(const bf16* __restric
       }
   }
   const __amdgpu_buffer_rsrc_t rh = rsrc_of(hseq);
+  const __amdgpu_buffer_rsrc_t rr = rsrc_of(ring);
   float cst[QB];
 #pragma unroll
   for (int q = 0; q < QB; ++q) cst[q] = 0.f;
@@ -146,24 +156,67 @@ __global__ __launch_bounds__(256) void lstm_seq_fwd_kernel(const bf16* __restric
     bool ok = true;
     SEQ_STAMP(0);
     if (s > 0) {
-      __shared__ int okflag;
-      if (threadIdx.x == 0) okflag = seq_wait(mycnt, (unsigned)(nsl * s), err) ? 1 : 0;
-      __syncthreads();
-      SEQ_STAMP(1);
-      ok = okflag != 0;
-      // A fragments: h_{tp}[b0 + 16i + c][w*KW + 32kc + 8g] (sc1: handed-off bytes)
       bf16x8 af[MI][KK];
-      const uint32_t abase = (uint32_t)((((size_t)b0 + c) * Tn + tp) * 2 * H + d * H + w * KW + 8 * g) * 2u;
+      if constexpr (TAG) {
+        // granules of h_{s-1}: row b0 + 16i + c, k = w*KW + 32kc + 8g .. +7 -> 4 granules (32 B)
+        const uint32_t want = (uint32_t)s;
+        const uint32_t gbase =
+            (uint32_t)((((size_t)((s - 1) & 1) * B + b0 + c) * H + (d * H + w * KW + 8 * g) / 2) * 8u);
+        unsigned long long t0 = 0;
+        u32x4 gv[MI][KK][2];
+        for (;;) {
 #pragma unroll
-      for (int kk = 0; kk < KK; ++kk)
+          for (int kk = 0; kk < KK; ++kk)
 #pragma unroll
-        for (int i = 0; i < MI; ++i) {
-          const int kc = kk + rot < KK ? kk + rot : kk + rot - KK;
-          af[i][kk] = ld_sc1(rh, abase + (uint32_t)(i * 16 * Tn * 2 * H * 2 + kc * 64));
+            for (int i = 0; i < MI; ++i) {
+              const int kc = kk + rot < KK ? kk + rot : kk + rot - KK;
+              const uint32_t off = gbase + (uint32_t)(i * 16 * H * 8 + kc * 128);
+              gv[i][kk][0] = __builtin_amdgcn_raw_buffer_load_b128(rr, off, 0, 16);
+              gv[i][kk][1] = __builtin_amdgcn_raw_buffer_load_b128(rr, off + 16, 0, 16);
+            }
+          bool mine = true;
+#pragma unroll
+          for (int kk = 0; kk < KK; ++kk)
+#pragma unroll
+            for (int i = 0; i < MI; ++i)
+#pragma unroll
+              for (int h2 = 0; h2 < 2; ++h2) mine &= (gv[i][kk][h2][1] == want) & (gv[i][kk][h2][3] == want);
+          if (__all(mine)) break;
+          const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+          if (t0 == 0) t0 = now;
+          if (now - t0 > SEQ_TIMEOUT_TICKS || __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+            __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            ok = false;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
         }
-      // every hand-off load in flight before the first MFMA (else the scheduler interleaves them
-      // with the MFMAs one load at a time, each behind a vmcnt(0))
-      __builtin_amdgcn_sched_barrier(0);
+        SEQ_STAMP(1);
+#pragma unroll
+        for (int kk = 0; kk < KK; ++kk)
+#pragma unroll
+          for (int i = 0; i < MI; ++i)
+            af[i][kk] = __builtin_bit_cast(bf16x8, u32x4{gv[i][kk][0][0], gv[i][kk][0][2], gv[i][kk][1][0],
+                                                         gv[i][kk][1][2]});
+      } else {
+        __shared__ int okflag;
+        if (threadIdx.x == 0) okflag = seq_wait(mycnt, (unsigned)(nsl * s), err) ? 1 : 0;
+        __syncthreads();
+        SEQ_STAMP(1);
+        ok = okflag != 0;
+        // A fragments: h_{tp}[b0 + 16i + c][w*KW + 32kc + 8g] (sc1: handed-off bytes)
+        const uint32_t abase = (uint32_t)((((size_t)b0 + c) * Tn + tp) * 2 * H + d * H + w * KW + 8 * g) * 2u;
+#pragma unroll
+        for (int kk = 0; kk < KK; ++kk)
+#pragma unroll
+          for (int i = 0; i < MI; ++i) {
+            const int kc = kk + rot < KK ? kk + rot : kk + rot - KK;
+            af[i][kk] = ld_sc1(rh, abase + (uint32_t)(i * 16 * Tn * 2 * H * 2 + kc * 64));
+          }
+        // every hand-off load in flight before the first MFMA (else the scheduler interleaves them
+        // with the MFMAs one load at a time, each behind a vmcnt(0))
+        __builtin_amdgcn_sched_barrier(0);
+      }
       f32x4 acc[MI][NJ];
 #pragma unroll
       for (int i = 0; i < MI; ++i)
@@ -205,15 +258,35 @@ __global__ __launch_bounds__(256) void lstm_seq_fwd_kernel(const bf16* __restric
     }
     SEQ_STAMP(4);
     __syncthreads();
-    // publish h_t of this (samples, units) tile: S rows x 2U bytes, one 16-B sc1 store per thread
-    if (threadIdx.x < S * U / 8) {
-      const int row = threadIdx.x / (U / 8), ch = threadIdx.x % (U / 8);
-      const bf16x8 hv = *reinterpret_cast<const bf16x8*>(&htile[row][8 * ch]);
-      st_sc1(rh, (uint32_t)((((size_t)(b0 + row) * Tn + t) * 2 * H + d * H + ns * U + 8 * ch) * sizeof(bf16)), hv);
+    if constexpr (TAG) {
+      // publish: S rows x U/2 granules into slot s & 1, two granules per 16-B sc1 store
+      if (threadIdx.x < S * U / 4) {
+        const int row = threadIdx.x / (U / 4), gp = threadIdx.x % (U / 4);
+        const u32x4 hv = __builtin_bit_cast(u32x4, *reinterpret_cast<const bf16x8*>(&htile[row][8 * (gp >> 1)]));
+        const uint32_t tag = (uint32_t)(s + 1);
+        const u32x4 v = (gp & 1) ? u32x4{hv[2], tag, hv[3], tag} : u32x4{hv[0], tag, hv[1], tag};
+        __builtin_amdgcn_raw_buffer_store_b128(
+            v, rr, (uint32_t)((((size_t)(s & 1) * B + b0 + row) * H + (d * H + ns * U + 4 * gp) / 2) * 8u), 0, 16);
+      }
+      SEQ_STAMP(5);
+      // h_t for the next layer / BPTT: plain stores, off the critical path
+      if (threadIdx.x < S * U / 8) {
+        const int row = threadIdx.x / (U / 8), ch = threadIdx.x % (U / 8);
+        *reinterpret_cast<bf16x8*>(hseq + ((size_t)(b0 + row) * Tn + t) * 2 * H + d * H + ns * U + 8 * ch) =
+            *reinterpret_cast<const bf16x8*>(&htile[row][8 * ch]);
+      }
+      SEQ_STAMP(6);
+    } else {
+      // publish h_t of this (samples, units) tile: S rows x 2U bytes, one 16-B sc1 store per thread
+      if (threadIdx.x < S * U / 8) {
+        const int row = threadIdx.x / (U / 8), ch = threadIdx.x % (U / 8);
+        const bf16x8 hv = *reinterpret_cast<const bf16x8*>(&htile[row][8 * ch]);
+        st_sc1(rh, (uint32_t)((((size_t)(b0 + row) * Tn + t) * 2 * H + d * H + ns * U + 8 * ch) * sizeof(bf16)), hv);
+      }
+      SEQ_STAMP(5);
+      seq_publish(mycnt);
+      SEQ_STAMP(6);
     }
-    SEQ_STAMP(5);
-    seq_publish(mycnt);
-    SEQ_STAMP(6);
     // saved-forward stores for BPTT, off the hand-off's critical path (issued after the signal;
     // the next step's vmcnt(0) drains them long after they completed)
 #pragma unroll
@@ -227,6 +300,9 @@ __global__ __launch_bounds__(256) void lstm_seq_fwd_kernel(const bf16* __restric
     // next step's input rows, unconditionally (a load under a runtime branch gets a vmcnt(0) at
     // the join, which would stall on the stores above): the last step re-reads its own row
     load_xg(s + 1 < Tn ? (d == 0 ? t + 1 : t - 1) : t);
+  }
+  if constexpr (TAG) {  // steps completed (the counter-mode invariant: (H/U)*T per slice at the end)
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(mycnt, (unsigned)Tn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -402,19 +478,31 @@ bool seq_config(int B, int H, bool bwd, int& S, int& U) {
   return false;
 }
 
+template <int H, int S, int U>
+void launch_fwd_tile(bool tag, dim3 grid, hipStream_t st, const bf16* xg, const bf16* whh, bf16* hseq, bf16* gsv,
+                     float* csv, unsigned* cnt, unsigned* err, uint2* ring, int B, int T) {
+  if (tag)
+    hipLaunchKernelGGL((lstm_seq_fwd_kernel<H, S, U, true>), grid, dim3(256), 0, st, xg, whh, hseq, gsv, csv, cnt, err,
+                       ring, B, T, g_stamps);
+  else
+    hipLaunchKernelGGL((lstm_seq_fwd_kernel<H, S, U, false>), grid, dim3(256), 0, st, xg, whh, hseq, gsv, csv, cnt,
+                       err, ring, B, T, g_stamps);
+}
+
 template <int H>
 int launch_fwd(int S, int U, dim3 grid, hipStream_t st, const bf16* xg, const bf16* whh, bf16* hseq, bf16* gsv,
-               float* csv, unsigned* cnt, unsigned* err, int B, int T) {
+               float* csv, unsigned* cnt, unsigned* err, uint2* ring, int B, int T) {
+  const bool tag = crnn_option(CRNN_OPT_LSTM_HANDOFF) != 0;
   if constexpr (H <= 512) {  // 16 x 64 would spill at H = 768 (seq_config never picks it)
     if (S == 16 && U == 64) {
-      hipLaunchKernelGGL((lstm_seq_fwd_kernel<H, 16, 64>), grid, dim3(256), 0, st, xg, whh, hseq, gsv, csv, cnt, err, B, T, g_stamps);
+      launch_fwd_tile<H, 16, 64>(tag, grid, st, xg, whh, hseq, gsv, csv, cnt, err, ring, B, T);
       return (int)hipGetLastError();
     }
   }
   if (S == 16)
-    hipLaunchKernelGGL((lstm_seq_fwd_kernel<H, 16, 32>), grid, dim3(256), 0, st, xg, whh, hseq, gsv, csv, cnt, err, B, T, g_stamps);
+    launch_fwd_tile<H, 16, 32>(tag, grid, st, xg, whh, hseq, gsv, csv, cnt, err, ring, B, T);
   else
-    hipLaunchKernelGGL((lstm_seq_fwd_kernel<H, 32, 32>), grid, dim3(256), 0, st, xg, whh, hseq, gsv, csv, cnt, err, B, T, g_stamps);
+    launch_fwd_tile<H, 32, 32>(tag, grid, st, xg, whh, hseq, gsv, csv, cnt, err, ring, B, T);
   return (int)hipGetLastError();
 }
 
@@ -458,23 +546,29 @@ int crnn_lstm_seq_debug_stamps(unsigned long long* buf) {
   return 0;
 }
 
-// counters: one per (direction, batch slice) of the smallest slice (16 samples), then the error word
-size_t crnn_lstm_seq_workspace(int B) { return (size_t)((2 * (B / 16 + 1) + 1 + 3) / 4 * 16); }
+// counters: one per (direction, batch slice) of the smallest slice (16 samples), then the error word;
+// then (from byte seq_ring_offset) the forward's 2-slot granule ring: 2 x B x H 8-byte granules
+// (sized for H = 768, the largest supported)
+static size_t seq_ring_offset(int B) { return (size_t)((2 * (B / 16 + 1) + 1 + 63) / 64 * 256); }
+size_t crnn_lstm_seq_workspace(int B) { return seq_ring_offset(B) + (size_t)2 * B * 768 * 8; }
 
 int crnn_lstm_seq_fwd(const void* xg, const void* whh, void* hseq, void* gsv, float* csv, unsigned* ws, int B, int T,
                       int H, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   int S, U;
   if (!seq_config(B, H, false, S, U)) return crnn_set_error(hipErrorInvalidValue, "lstm_seq: unsupported shape");
-  hipError_t e = hipMemsetAsync(ws, 0, crnn_lstm_seq_workspace(B), st);
+  // counters + error word, and the ring slots this (B, H) uses (tag 0 = not yet written)
+  const size_t zero = seq_ring_offset(B) + (crnn_option(CRNN_OPT_LSTM_HANDOFF) ? (size_t)2 * B * H * 8 : 0);
+  hipError_t e = hipMemsetAsync(ws, 0, zero, st);
   if (e != hipSuccess) return (int)e;
   unsigned* cnt = ws;
   unsigned* err = ws + 2 * (B / 16 + 1);
+  uint2* ring = (uint2*)((char*)ws + seq_ring_offset(B));
   const dim3 grid(2 * (B / S) * (H / U));
   const bf16 *x = (const bf16*)xg, *w = (const bf16*)whh;
-  if (H == 256) return launch_fwd<256>(S, U, grid, st, x, w, (bf16*)hseq, (bf16*)gsv, csv, cnt, err, B, T);
-  if (H == 512) return launch_fwd<512>(S, U, grid, st, x, w, (bf16*)hseq, (bf16*)gsv, csv, cnt, err, B, T);
-  return launch_fwd<768>(S, U, grid, st, x, w, (bf16*)hseq, (bf16*)gsv, csv, cnt, err, B, T);
+  if (H == 256) return launch_fwd<256>(S, U, grid, st, x, w, (bf16*)hseq, (bf16*)gsv, csv, cnt, err, ring, B, T);
+  if (H == 512) return launch_fwd<512>(S, U, grid, st, x, w, (bf16*)hseq, (bf16*)gsv, csv, cnt, err, ring, B, T);
+  return launch_fwd<768>(S, U, grid, st, x, w, (bf16*)hseq, (bf16*)gsv, csv, cnt, err, ring, B, T);
 }
 
 int crnn_lstm_seq_bwd(const void* dhseq, const void* whh_t, const void* gsv, const float* csv, void* dgates,
@@ -482,7 +576,7 @@ int crnn_lstm_seq_bwd(const void* dhseq, const void* whh_t, const void* gsv, con
   hipStream_t st = (hipStream_t)stream;
   int S, U;
   if (!seq_config(B, H, true, S, U)) return crnn_set_error(hipErrorInvalidValue, "lstm_seq: unsupported shape");
-  hipError_t e = hipMemsetAsync(ws, 0, crnn_lstm_seq_workspace(B), st);
+  hipError_t e = hipMemsetAsync(ws, 0, seq_ring_offset(B), st);  // counters + error word
   if (e != hipSuccess) return (int)e;
   unsigned* cnt = ws;
   unsigned* err = ws + 2 * (B / 16 + 1);

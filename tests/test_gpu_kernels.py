@@ -462,7 +462,7 @@ def _bilstm_case(L, BTHI, dtype, oneshot):
         sws = torch.full((L.lib().crnn_lstm_seq_workspace(B) // 4,), 7, dtype=torch.int32, device=DEV)
         L.call("crnn_lstm_seq_fwd", xg.data_ptr(), whh.data_ptr(), hseq.data_ptr(), gsv.data_ptr(), csv.data_ptr(),
                sws.data_ptr(), B, T, H, st)
-        assert int(sws[-1].item()) == 0   # no timed-out wait
+        assert int(sws[2 * (B // 16 + 1)].item()) == 0   # error word: no timed-out wait
         S, U = seq_tile(B, H)
         assert int(sws[: 2 * (B // S)].min().item()) == H // U * T   # every slice published every step
     else:
@@ -479,7 +479,7 @@ def _bilstm_case(L, BTHI, dtype, oneshot):
     if seq:
         L.call("crnn_lstm_seq_bwd", dh.data_ptr(), whh_t.data_ptr(), gsv.data_ptr(), csv.data_ptr(), dg.data_ptr(),
                sws.data_ptr(), B, T, H, st)
-        assert int(sws[-1].item()) == 0
+        assert int(sws[2 * (B // 16 + 1)].item()) == 0
         S, U = seq_tile(B, H, 1)
         assert int(sws[: 2 * (B // S)].min().item()) == H // U * T
         # the per-step path on the same saved forward agrees to bf16 rounding of dgates
@@ -919,3 +919,43 @@ def test_weight_pack_layouts(dtype):
         assert torch.equal(eng.packed[cs.name], want.to(dtype)), cs.name
         n += 1
     assert n == 28
+
+
+@pytest.mark.parametrize("BTH", [(256, 32, 512), (64, 20, 768), (32, 7, 256), (128, 9, 512)])
+def test_lstm_seq_fwd_handoff_forms_agree(BTH):
+    """Persistent BiLSTM forward: the tagged-granule hand-off (CRNN_OPT_LSTM_HANDOFF = 1, default)
+    and the write-through payload + counter hand-off (0) compute the same arithmetic, so h, the
+    saved gates and the cell states are bit-identical, for every tile the shape supports."""
+    L = _L()
+    B, T, H = BTH
+    g = torch.Generator().manual_seed(11)
+    xg = (torch.randn(B, T, 2, 4 * H, generator=g) * 0.7).to(DEV, torch.bfloat16)
+    whh = (torch.randn(2, 4 * H, H, generator=g) / H ** 0.5).to(DEV, torch.bfloat16)
+    st = L.stream_ptr()
+    outs = {}
+    try:
+        for force in (1, 2, 3):
+            L.call("crnn_set_option", L.OPT_LSTM_TILE, force)
+            if not L.lib().crnn_lstm_seq_supported(L.dtype_code(torch.bfloat16), B, H):
+                continue
+            for ho in (1, 0):
+                L.call("crnn_set_option", L.OPT_LSTM_HANDOFF, ho)
+                hseq = torch.full((B, T, 2 * H), 3.0, dtype=torch.bfloat16, device=DEV)
+                gsv = torch.full((2, T, B, 4 * H), 3.0, dtype=torch.bfloat16, device=DEV)
+                csv = torch.full((2, T, B, H), 3.0, device=DEV)
+                ws = torch.full((L.lib().crnn_lstm_seq_workspace(B) // 4,), 7, dtype=torch.int32, device=DEV)
+                L.call("crnn_lstm_seq_fwd", xg.data_ptr(), whh.data_ptr(), hseq.data_ptr(), gsv.data_ptr(),
+                       csv.data_ptr(), ws.data_ptr(), B, T, H, st)
+                torch.cuda.synchronize()
+                S, U = seq_tile(B, H)
+                assert int(ws[2 * (B // 16 + 1)].item()) == 0      # error word: no timed-out wait
+                assert int(ws[: 2 * (B // S)].min().item()) == H // U * T
+                outs[(force, ho)] = (hseq, gsv, csv)
+            a, b = outs[(force, 1)], outs[(force, 0)]
+            for x, y in zip(a, b):
+                assert torch.isfinite(x.float()).all()
+                assert torch.equal(x, y), (BTH, force)
+    finally:
+        L.call("crnn_set_option", L.OPT_LSTM_TILE, 0)
+        L.call("crnn_set_option", L.OPT_LSTM_HANDOFF, 1)
+    assert outs

@@ -59,7 +59,9 @@ def run(kind, B, T, H):
     torch.cuda.synchronize()
     L.call("crnn_lstm_seq_debug_stamps", None)
     s = stamps.view(grid, T, 8).cpu().numpy().astype(np.int64)
-    print(f"{kind}: B={B} T={T} H={H} tile {S}x{U} grid={grid}: {us:.1f} us/sweep = {us / T:.2f} us/step (no stamps)")
+    ho = "granule" if HANDOFF else "counter"
+    print(f"{kind}: B={B} T={T} H={H} tile {S}x{U} grid={grid} hand-off {ho if kind == 'fwd' else 'counter'}: "
+          f"{us:.1f} us/sweep = {us / T:.2f} us/step (no stamps)")
     steps = slice(2, T - 1)
     d = s[:, steps, :]
     for p in range(1, 7):
@@ -78,10 +80,16 @@ def run(kind, B, T, H):
     print(f"  last publish (any block, step s-1) -> waited (step s): median {np.median(lat):.3f} us")
 
 
+HANDOFF = 1
+
 if __name__ == "__main__":
+    # forward under both hand-off forms (CRNN_OPT_LSTM_HANDOFF), each tile, in one process
     B, T, H = (int(a) for a in sys.argv[1:4]) if len(sys.argv) > 3 else (256, 32, 512)
     for force in (1, 2, 3):
         L.call("crnn_set_option", L.OPT_LSTM_TILE, force)
-        run("fwd", B, T, H)
+        for HANDOFF in (1, 0, 1):
+            L.call("crnn_set_option", L.OPT_LSTM_HANDOFF, HANDOFF)
+            run("fwd", B, T, H)
         run("bwd", B, T, H)
     L.call("crnn_set_option", L.OPT_LSTM_TILE, 0)
+    L.call("crnn_set_option", L.OPT_LSTM_HANDOFF, 1)
