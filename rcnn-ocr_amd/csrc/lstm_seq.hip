@@ -149,10 +149,8 @@ __global__ __launch_bounds__(256) void lstm_seq_fwd_kernel(const bf16* __restric
   for (int s = 0; s < Tn; ++s) {
     const int t = d == 0 ? s : Tn - 1 - s;
     const int tp = d == 0 ? t - 1 : t + 1;
+    // the input rows xv are added after the hand-off (their load's latency hides under it)
     f32x4 sum[QB];
-#pragma unroll
-    for (int q = 0; q < QB; ++q)
-      sum[q] = f32x4{(float)xv[q][0], (float)xv[q][1], (float)xv[q][2], (float)xv[q][3]};
     bool ok = true;
     SEQ_STAMP(0);
     if (s > 0) {
@@ -238,10 +236,20 @@ __global__ __launch_bounds__(256) void lstm_seq_fwd_kernel(const bf16* __restric
 #pragma unroll
       for (int q = 0; q < QB; ++q) {
         const int bi = w * QB + q, i = bi / NJ, j = bi % NJ;
+        sum[q] = f32x4{(float)xv[q][0], (float)xv[q][1], (float)xv[q][2], (float)xv[q][3]};
 #pragma unroll
         for (int ww = 0; ww < 4; ++ww) sum[q] += part[ww][i][j][lane];
       }
+    } else {
+#pragma unroll
+      for (int q = 0; q < QB; ++q) sum[q] = f32x4{(float)xv[q][0], (float)xv[q][1], (float)xv[q][2], (float)xv[q][3]};
     }
+    // next step's input rows, unconditionally (a load under a runtime branch gets a vmcnt(0) at
+    // the join); the last step re-reads its own row. Granule form: issued as soon as xv is
+    // consumed, a whole step ahead of its use (nothing drains vmcnt before the next poll); counter
+    // form: after the publish's vmcnt(0) drain
+    const int tn = s + 1 < Tn ? (d == 0 ? t + 1 : t - 1) : t;
+    if constexpr (TAG) load_xg(tn);
     // cell update: lane holds gates (i,f,g,o) of unit n/4 for one sample, per block
     f32x4 gq[QB];
 #pragma unroll
@@ -297,9 +305,7 @@ __global__ __launch_bounds__(256) void lstm_seq_fwd_kernel(const bf16* __restric
       csv[((size_t)(d * Tn + t) * B + b) * H + u] = cst[q];
       st4<bf16>(gsv + ((size_t)(d * Tn + t) * B + b) * H4 + n, gq[q]);
     }
-    // next step's input rows, unconditionally (a load under a runtime branch gets a vmcnt(0) at
-    // the join, which would stall on the stores above): the last step re-reads its own row
-    load_xg(s + 1 < Tn ? (d == 0 ? t + 1 : t - 1) : t);
+    if constexpr (!TAG) load_xg(tn);
   }
   if constexpr (TAG) {  // steps completed (the counter-mode invariant: (H/U)*T per slice at the end)
     if (threadIdx.x == 0) __hip_atomic_fetch_add(mycnt, (unsigned)Tn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
