@@ -921,7 +921,8 @@ def test_weight_pack_layouts(dtype):
     assert n == 28
 
 
-@pytest.mark.parametrize("BTH", [(256, 32, 512), (64, 20, 768), (32, 7, 256), (128, 9, 512)])
+@pytest.mark.parametrize("BTH", [(256, 32, 512), (64, 20, 768), (32, 7, 256), (128, 9, 512), (16, 1, 256),
+                                 (48, 2, 768)])
 def test_lstm_seq_fwd_handoff_forms_agree(BTH):
     """Persistent BiLSTM forward: the tagged-granule hand-off (CRNN_OPT_LSTM_HANDOFF = 1, default)
     and the write-through payload + counter hand-off (0) compute the same arithmetic, so h, the
