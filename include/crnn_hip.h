@@ -59,7 +59,9 @@ enum { CRNN_OPT_GEMM_STAGGER = 0,    /* 256-row conv GEMM: waves 4-7 one barrier
                                         n >= 2: on, with n-row bands for the MFMA-bound instances */
        CRNN_OPT_LSTM_HANDOFF = 6,    /* persistent BiLSTM forward: 1 = data-tagged granule ring (default),
                                         0 = write-through payload + step counter */
-       CRNN_OPT_COUNT = 7 };
+       CRNN_OPT_WGRAD_REDUCE = 7,    /* conv wgrad split-K slab reduce: 1 = (co, 64-channel) tiles transposed
+                                        through LDS, coalesced OIHW stores (default), 0 = flat, scattered stores */
+       CRNN_OPT_COUNT = 8 };
 int crnn_set_option(int key, int value);
 
 /* ------------------------------------------------------------------ layout */

@@ -497,6 +497,49 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
   }
 }
 
+// the same sum, tiled: one workgroup per (co, 64-channel chunk of Cip). Slab loads as above (16 B,
+// coalesced along ci; T * 16 vectors per slab, the slabs split over G = 256 / (T * 16) thread groups
+// when the tile is narrow), partial sums transposed through LDS (pitch cc + 1: taps of one channel
+// on different banks), then the OIHW rows [ci][kh][kw] of the chunk written contiguously. The
+// flat kernel's 4-B stores land KH*KW floats apart; here every store is a coalesced run.
+__global__ __launch_bounds__(256) void wgrad_reduce_tiled_kernel(const float* __restrict__ ws, int S,
+                                                                 float* __restrict__ dw, int Ci, int Cip, int T,
+                                                                 float beta) {
+  __shared__ float red[2112];
+  const int nchunk = (Cip + 63) / 64;
+  const int co = blockIdx.x / nchunk, c0 = (blockIdx.x - co * nchunk) * 64;
+  const int cc = min(64, Cip - c0), cv = cc / 4, nv = T * cv, P = cc + 1;
+  const int G = max(1, 256 / nv);
+  const long Kp = (long)T * Cip, total = Kp * (long)gridDim.x / nchunk;
+  const int t = threadIdx.x, g = t / nv, v = t - g * nv;
+  if (g < G) {
+    const int tap = v / cv, c = 4 * (v - tap * cv);
+    const float* src = ws + (long)co * Kp + (long)tap * Cip + c0 + c;
+    f32x4 s = {0.f, 0.f, 0.f, 0.f};
+    int z = g;
+    for (; z + 7 * G < S; z += 8 * G) {
+      f32x4 r[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) r[q] = *reinterpret_cast<const f32x4*>(src + (size_t)(z + q * G) * total);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) s += r[q];
+    }
+    for (; z < S; z += G) s += *reinterpret_cast<const f32x4*>(src + (size_t)z * total);
+    float* d = red + (g * T + tap) * P + c;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) d[e] = s[e];
+  }
+  __syncthreads();
+  const int cr = min(cc, Ci - c0);  // real (unpadded) channels of the chunk
+  float* out = dw + ((size_t)co * Ci + c0) * T;
+  for (int o = t; o < cr * T; o += 256) {
+    const int ci = o / T, tap = o - ci * T;
+    float a = 0.f;
+    for (int q = 0; q < G; ++q) a += red[(q * T + tap) * P + ci];
+    out[o] = beta != 0.f ? beta * out[o] + a : a;
+  }
+}
+
 inline uint32_t nbytes(long elems, size_t es) { return (uint32_t)((size_t)elems * es); }
 
 template <typename T, bool UT>
@@ -649,6 +692,11 @@ template <typename T> int conv_wgrad_t(const crnn_conv_desc* d, const void* dy, 
   if (rc) return rc;
   int ci_real = d->Ci_real > 0 ? d->Ci_real : g.Ci;
   long total = (long)g.Co * Kp;
+  if (crnn_option(CRNN_OPT_WGRAD_REDUCE) != 0 && g.KH * g.KW <= 16 && g.Ci % 8 == 0) {
+    hipLaunchKernelGGL(wgrad_reduce_tiled_kernel, dim3(g.Co * ((g.Ci + 63) / 64)), dim3(256), 0, st, ws, splits,
+                       dw, ci_real, g.Ci, g.KH * g.KW, beta);
+    return (int)hipGetLastError();
+  }
   int blocks = (int)((total / 4 + 255) / 256);
   if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, ws, splits, dw, g.Co, ci_real,

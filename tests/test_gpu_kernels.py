@@ -131,6 +131,17 @@ def test_conv_fwd_dgrad_wgrad(cfg, dtype):
     dw = torch.full((Co, Ci, k[0], k[1]), 7.0, device=DEV)
     L.call("crnn_conv_wgrad", dt, d, dyd.data_ptr(), xd.data_ptr(), dw.data_ptr(), ws.data_ptr(), need, 0.0, st)
     assert relerr(dw.cpu(), wr.grad) < (1e-5 if dtype == torch.float32 else 1e-2)
+    # the split-K slab reduce: LDS-tiled (default) vs flat (CRNN_OPT_WGRAD_REDUCE = 0) agree to fp32
+    # summation order; accumulate mode (beta = 1) doubles the gradient
+    dw_flat = torch.empty_like(dw)
+    try:
+        L.call("crnn_set_option", L.OPT_WGRAD_REDUCE, 0)
+        L.call("crnn_conv_wgrad", dt, d, dyd.data_ptr(), xd.data_ptr(), dw_flat.data_ptr(), ws.data_ptr(), need, 0.0, st)
+    finally:
+        L.call("crnn_set_option", L.OPT_WGRAD_REDUCE, 1)
+    assert relerr(dw_flat.cpu(), dw.cpu()) < 1e-6
+    L.call("crnn_conv_wgrad", dt, d, dyd.data_ptr(), xd.data_ptr(), dw.data_ptr(), ws.data_ptr(), need, 1.0, st)
+    assert relerr(dw.cpu(), 2 * dw_flat.cpu()) < 1e-6
 
 
 def test_conv_halo_vs_gemm():
