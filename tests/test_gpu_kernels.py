@@ -65,6 +65,7 @@ CONVS_DEEP = [
     (4, 64, 6, 256, 128, (3, 3), (1, 1), (1, 1)),
     (3, 64, 5, 128, 128, (3, 3), (1, 1), (1, 1)),
     (4, 3, 5, 256, 64, (3, 3), (1, 1), (1, 1)),   # the input conv (3 -> 8 padded channels, taps along k)
+    (256, 512, 2, 33, 512, (2, 2), (1, 1), (0, 0)),  # conv_out[1]: Mp = 8192, the deep wgrad's smallest K
 ]
 
 
