@@ -295,8 +295,11 @@ int crnn_lstm_wgrad(const void* dgates, const void* x, const void* hseq, float* 
  * [2*(B/16+1)] step counters (the first 2*B/S used; counter of slice (d, bs) = d*(B/S)+bs reaches
  * (H/U)*T) then one error word (non-zero after a bounded wait timed out, in which case the outputs
  * carry NaN), then (256-B aligned) the forward's hand-off ring of 2*B*H 8-byte granules
- * {2 bf16 of h_t, u32 tag}. */
+ * {2 bf16 of h_t, u32 tag}, then at crnn_lstm_seq_status_offset(B) a sticky status word that no
+ * call zeroes (the caller zeroes it once, at allocation): every call ORs its error word into it,
+ * so the host can poll one word for "any persistent sweep since allocation timed out". */
 int crnn_lstm_seq_supported(int dtype, int B, int H);
+size_t crnn_lstm_seq_status_offset(int B);
 /* the (samples, units) workgroup tile the forward (bwd = 0) or BPTT (bwd = 1) sweep uses for
  * (B, H); 0 if unsupported */
 int crnn_lstm_seq_config(int B, int H, int bwd, int* S, int* U);

@@ -100,11 +100,10 @@ def ctc_loss_and_grad(logits_btc, targets, lengths, reduction="mean", zero_infin
         label = [int(v) for v in np.asarray(targets[b])[:L]]
         nll, post = ctc_single(lp[b], label)
         g = sm[b] - post
-        if not np.isfinite(nll):
-            if zero_infinity:
-                nll, g = 0.0, np.zeros_like(g)
-            else:
-                g = np.full_like(g, np.nan)
+        if np.isinf(nll) and zero_infinity:    # torch zeroes only +inf (infeasible); NaN stays NaN
+            nll, g = 0.0, np.zeros_like(g)
+        elif not np.isfinite(nll):
+            g = np.full_like(g, np.nan)
         losses[b] = nll
         grads[b] = g
     if reduction == "mean":

@@ -118,6 +118,10 @@ class Workspace:
         return sum(t.numel() * t.element_size() for t in self.bufs.values())
 
 
+_SEQ_TIMEOUT_MSG = ("persistent BiLSTM sweep timed out waiting for a co-resident workgroup (error word set; "
+                    "its outputs are NaN): the grid was not fully resident on the device")
+
+
 class CRNNEngine:
     def __init__(self, params: Dict[str, torch.Tensor], buffers: Dict[str, torch.Tensor], hidden: int,
                  num_classes: int, num_rnn_layers: int = 2, dtype: torch.dtype = torch.bfloat16,
@@ -127,6 +131,9 @@ class CRNNEngine:
         self.H = hidden
         self.C = num_classes
         self.Cpad = round8(num_classes)
+        # RCNN(decoder="attn") has no CTC head (the reference's parameter set): the encoder ends at
+        # enc_dropout and forward() returns None
+        self.has_head = "ctc_head.weight" in params
         self.nl = num_rnn_layers
         self.enc_dim = enc_dim
         self.dtype = dtype
@@ -146,6 +153,14 @@ class CRNNEngine:
         # flat buffer's version counter; kernel-side updates call mark_params_changed()
         self.version_source = version_source
         self._saved = None
+        # forward generation: the engine keeps ONE set of saved activations, so a backward must
+        # belong to the latest grad-enabled forward (checked by saved_generation())
+        self.fwd_gen = 0
+        # persistent BiLSTM status (see poll_status)
+        self._seq_used = False
+        self._sticky_carry = 0
+        self._status_host = None
+        self._status_evt = None
         self.debug = False      # when set, backward keeps copies of block-boundary gradients
         self._last_partials = None  # (psum, rows, rows_per_partial) of the latest training-mode conv
         self._drop_seed = int(torch.initial_seed()) & 0xFFFFFFFFFFFFFFFF  # enc_dropout mask stream
@@ -221,10 +236,11 @@ class CRNNEngine:
                                  out_f32=True, perm=self.perm, src2=self.p[r + "bias_hh_l0" + sfx]))
             lw = self._pbuf(pre + ".lin", (H, 2 * H), T)
             sizes.append(job(L.PACK_ROWS, self.p[pre + ".linear.weight"], lw, H, H, 2 * H))
-        hw = self._pbuf("head.w", (self.Cpad, H), T)
-        sizes.append(job(L.PACK_ROWS, self.p["ctc_head.weight"], hw, self.Cpad, self.C, H))
-        hb = self._pbuf("head.b", (self.Cpad,), torch.float32)
-        sizes.append(job(L.PACK_ROWS, self.p["ctc_head.bias"], hb, self.Cpad, self.C, 1, out_f32=True))
+        if self.has_head:
+            hw = self._pbuf("head.w", (self.Cpad, H), T)
+            sizes.append(job(L.PACK_ROWS, self.p["ctc_head.weight"], hw, self.Cpad, self.C, H))
+            hb = self._pbuf("head.b", (self.Cpad,), torch.float32)
+            sizes.append(job(L.PACK_ROWS, self.p["ctc_head.bias"], hb, self.Cpad, self.C, 1, out_f32=True))
         start = 0
         for jb, n in zip(jobs, sizes):
             jb.start = start
@@ -308,12 +324,50 @@ class CRNNEngine:
     def _seq_ws(self, B):
         n = (L.lib().crnn_lstm_seq_workspace(B) + 3) // 4
         self._seq_err_index = 2 * (B // 16 + 1)   # include/crnn_hip.h: counters, then the error word
-        return self.ws.get("rnn.seq_ws", (n,), torch.int32)
+        t = self.ws.bufs.get("rnn.seq_ws")
+        if t is None or t.numel() != n:
+            if t is not None:
+                self._fold_sticky(t)
+            # zeroed at allocation: the sticky status word (after the ring) is never zeroed again
+            t = self.ws.bufs["rnn.seq_ws"] = torch.zeros(n, dtype=torch.int32, device=self.device)
+        self._seq_used = True
+        return t
+
+    def _fold_sticky(self, old):
+        self._sticky_carry |= int(old[self._sticky_idx_of(old)].item())
+
+    def _sticky_idx_of(self, t):
+        return t.numel() - 64   # crnn_lstm_seq_workspace = status offset + 256 bytes
 
     def seq_status(self) -> int:
-        """error word of the last persistent BiLSTM launch (0 = ok; non-zero: a bounded wait timed out)."""
+        """OR of the error words of every persistent BiLSTM launch so far (0 = ok; non-zero: a
+        bounded wait timed out and that sweep's outputs are NaN). Synchronises."""
         t = self.ws.bufs.get("rnn.seq_ws")
-        return 0 if t is None else int(t[self._seq_err_index].item())
+        return self._sticky_carry | (0 if t is None else int(t[self._sticky_idx_of(t)].item()))
+
+    def check_status(self):
+        """raise if any persistent BiLSTM sweep has timed out (synchronises)"""
+        if self.seq_status():
+            raise RuntimeError(_SEQ_TIMEOUT_MSG)
+
+    def poll_status(self):
+        """non-blocking check, called once per forward / backward: raise if a status copy enqueued
+        by an earlier call has landed and shows a timed-out sweep; enqueue the next copy (4 bytes
+        into pinned host memory, ordered after this call's kernels on the current stream)."""
+        if not self._seq_used:
+            return
+        if self._status_evt is not None and self._status_evt.query():
+            if int(self._status_host[0]) or self._sticky_carry:
+                raise RuntimeError(_SEQ_TIMEOUT_MSG)
+            self._status_evt = None
+        if self._status_evt is None:
+            t = self.ws.bufs["rnn.seq_ws"]
+            if self._status_host is None:
+                self._status_host = torch.zeros(1, dtype=torch.int32).pin_memory()
+            i = self._sticky_idx_of(t)
+            self._status_host.copy_(t[i:i + 1], non_blocking=True)
+            self._status_evt = torch.cuda.Event()
+            self._status_evt.record()
 
     def _bn_finalize(self, prefix, psum, psq, rows, count, train, tag, rpp=1):
         C = psum.shape[-1] if psum is not None else self.p[prefix + ".weight"].numel()
@@ -514,14 +568,31 @@ class CRNNEngine:
             call("crnn_dropout", dt, ptr(xin), ptr(xdr), B * Tn * Hd, float(dropout_p), seed, s)
             sv["drop"] = (float(dropout_p), seed)
             xin = xdr
-        # CTC head
-        logits = ws.get("logits", (B, Tn, self.Cpad), torch.float32)
-        call("crnn_gemm_nt", dt, ptr(xin), Hd, ptr(self.packed["head.w"]), Hd, ptr(logits), self.Cpad,
-             ptr(self.packed["head.b"]), B * Tn, self.Cpad, Hd, 1, 0, s)
         sv["enc"] = xin
         sv["B"], sv["T"] = B, Tn
+        logits = None
+        if self.has_head:   # CTC head
+            logits = ws.get("logits", (B, Tn, self.Cpad), torch.float32)
+            call("crnn_gemm_nt", dt, ptr(xin), Hd, ptr(self.packed["head.w"]), Hd, ptr(logits), self.Cpad,
+                 ptr(self.packed["head.b"]), B * Tn, self.Cpad, Hd, 1, 0, s)
+        self.poll_status()
+        if save_for_backward:
+            self.fwd_gen += 1
+            sv["gen"] = self.fwd_gen
         self._saved = sv if save_for_backward else None
-        return logits[:, :, : self.C]
+        return logits[:, :, : self.C] if logits is not None else None
+
+    def check_generation(self, gen: int):
+        """raise unless the saved activations are those of forward generation `gen`: a second
+        grad-enabled forward (loss = f(m(x1)) + f(m(x2)), activation checkpointing) before the
+        first one's backward would otherwise silently differentiate the wrong batch."""
+        cur = self._saved["gen"] if self._saved is not None else None
+        if cur != gen:
+            raise RuntimeError(
+                "RCNN HIP engine: this backward belongs to forward #%d, but the engine holds the saved "
+                "activations of %s; it keeps one forward's activations, so run backward before the next "
+                "grad-enabled forward (or run the other forwards under torch.no_grad())"
+                % (gen, "forward #%d" % cur if cur is not None else "no forward"))
 
     # ------------------------------------------------------------------ CTC
     def ctc(self, logits_padded: torch.Tensor, targets: torch.Tensor, lengths: torch.Tensor,
@@ -636,7 +707,7 @@ class CRNNEngine:
             if tuple(denc.shape) != (B, Tn, Hd) or denc.dtype != torch.float32 or not denc.is_contiguous():
                 raise ValueError("denc must be contiguous fp32 [B, T, hidden]")
             call("crnn_cast_f32", dt, ptr(denc), ptr(dx), M * Hd, s)
-            if not accumulate:
+            if not accumulate and self.has_head:
                 grads["ctc_head.weight"].zero_()
                 grads["ctc_head.bias"].zero_()
         else:
@@ -644,6 +715,7 @@ class CRNNEngine:
         if sv["drop"] is not None:  # enc_dropout backward: the forward's mask, from its seed
             call("crnn_dropout", dt, ptr(dx), ptr(dx), M * Hd, sv["drop"][0], sv["drop"][1], s)
         self._backward_encoder(dx, grads, acc, done)
+        self.poll_status()
 
     def _head_backward(self, dlogits, grads, acc, dx):
         sv, ws, dt, T, s = self._saved, self.ws, self.dt, self.dtype, L.stream_ptr()

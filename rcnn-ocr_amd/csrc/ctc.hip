@@ -64,13 +64,16 @@ __global__ __launch_bounds__(256) void ctc_kernel(const float* __restrict__ logi
   float ll = alpha[(size_t)(T - 1) * S + S - 1];
   if (S > 1) ll = lse2(ll, alpha[(size_t)(T - 1) * S + S - 2]);
   const float nll = -ll;
-  const bool bad = !(nll < INFINITY);
-  if (tid == 0) loss[b] = (bad && zero_inf) ? 0.f : nll;
+  // torch's zero_infinity replaces only an infinite loss (an infeasible alignment); a NaN loss
+  // (NaN logits, or NaN outputs of a failed persistent BiLSTM launch) stays NaN with NaN gradients
+  const bool inf = nll == INFINITY;
+  const bool bad = inf || nll != nll;
+  if (tid == 0) loss[b] = (inf && zero_inf) ? 0.f : nll;
   if (dlogits == nullptr) return;
   float* dl = dlogits + (size_t)b * T * ldc;
   const float scale = inv_B / (float)(L > 0 ? L : 1);
   if (bad) {
-    const float fill = zero_inf ? 0.f : NAN;
+    const float fill = (inf && zero_inf) ? 0.f : NAN;
     for (int i = tid; i < T * ldc; i += blockDim.x) dl[i] = (i % ldc) < C ? fill : 0.f;
     return;
   }

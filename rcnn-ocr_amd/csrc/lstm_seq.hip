@@ -528,6 +528,13 @@ int launch_bwd(int S, int U, dim3 grid, hipStream_t st, const bf16* dhseq, const
   return (int)hipGetLastError();
 }
 
+// sticky status: OR the launch's error word into a word no launch zeroes (read by the host
+// asynchronously, crnn_hip/engine.py poll_status), so a timed-out wait cannot pass unnoticed
+__global__ void seq_status_accum_kernel(const unsigned* err, unsigned* sticky) {
+  const unsigned e = err[0];
+  if (e) sticky[0] |= e;
+}
+
 }  // namespace
 
 extern "C" {
@@ -556,7 +563,16 @@ int crnn_lstm_seq_debug_stamps(unsigned long long* buf) {
 // then (from byte seq_ring_offset) the forward's 2-slot granule ring: 2 x B x H 8-byte granules
 // (sized for H = 768, the largest supported)
 static size_t seq_ring_offset(int B) { return (size_t)((2 * (B / 16 + 1) + 1 + 63) / 64 * 256); }
-size_t crnn_lstm_seq_workspace(int B) { return seq_ring_offset(B) + (size_t)2 * B * 768 * 8; }
+// after the ring: the sticky status word (zeroed once by the caller when it allocates ws)
+size_t crnn_lstm_seq_status_offset(int B) { return seq_ring_offset(B) + (size_t)2 * B * 768 * 8; }
+size_t crnn_lstm_seq_workspace(int B) { return crnn_lstm_seq_status_offset(B) + 256; }
+
+static int seq_accum_status(unsigned* ws, int B, hipStream_t st, int rc) {
+  if (rc != 0) return rc;
+  hipLaunchKernelGGL(seq_status_accum_kernel, dim3(1), dim3(64), 0, st, ws + 2 * (B / 16 + 1),
+                     (unsigned*)((char*)ws + crnn_lstm_seq_status_offset(B)));
+  return (int)hipGetLastError();
+}
 
 int crnn_lstm_seq_fwd(const void* xg, const void* whh, void* hseq, void* gsv, float* csv, unsigned* ws, int B, int T,
                       int H, void* stream) {
@@ -572,9 +588,11 @@ int crnn_lstm_seq_fwd(const void* xg, const void* whh, void* hseq, void* gsv, fl
   uint2* ring = (uint2*)((char*)ws + seq_ring_offset(B));
   const dim3 grid(2 * (B / S) * (H / U));
   const bf16 *x = (const bf16*)xg, *w = (const bf16*)whh;
-  if (H == 256) return launch_fwd<256>(S, U, grid, st, x, w, (bf16*)hseq, (bf16*)gsv, csv, cnt, err, ring, B, T);
-  if (H == 512) return launch_fwd<512>(S, U, grid, st, x, w, (bf16*)hseq, (bf16*)gsv, csv, cnt, err, ring, B, T);
-  return launch_fwd<768>(S, U, grid, st, x, w, (bf16*)hseq, (bf16*)gsv, csv, cnt, err, ring, B, T);
+  int rc;
+  if (H == 256) rc = launch_fwd<256>(S, U, grid, st, x, w, (bf16*)hseq, (bf16*)gsv, csv, cnt, err, ring, B, T);
+  else if (H == 512) rc = launch_fwd<512>(S, U, grid, st, x, w, (bf16*)hseq, (bf16*)gsv, csv, cnt, err, ring, B, T);
+  else rc = launch_fwd<768>(S, U, grid, st, x, w, (bf16*)hseq, (bf16*)gsv, csv, cnt, err, ring, B, T);
+  return seq_accum_status(ws, B, st, rc);
 }
 
 int crnn_lstm_seq_bwd(const void* dhseq, const void* whh_t, const void* gsv, const float* csv, void* dgates,
@@ -588,9 +606,11 @@ int crnn_lstm_seq_bwd(const void* dhseq, const void* whh_t, const void* gsv, con
   unsigned* err = ws + 2 * (B / 16 + 1);
   const dim3 grid(2 * (B / S) * (H / U));
   const bf16 *dh = (const bf16*)dhseq, *wt = (const bf16*)whh_t, *gv = (const bf16*)gsv;
-  if (H == 256) return launch_bwd<256>(S, U, grid, st, dh, wt, gv, csv, (bf16*)dgates, cnt, err, B, T);
-  if (H == 512) return launch_bwd<512>(S, U, grid, st, dh, wt, gv, csv, (bf16*)dgates, cnt, err, B, T);
-  return launch_bwd<768>(S, U, grid, st, dh, wt, gv, csv, (bf16*)dgates, cnt, err, B, T);
+  int rc;
+  if (H == 256) rc = launch_bwd<256>(S, U, grid, st, dh, wt, gv, csv, (bf16*)dgates, cnt, err, B, T);
+  else if (H == 512) rc = launch_bwd<512>(S, U, grid, st, dh, wt, gv, csv, (bf16*)dgates, cnt, err, B, T);
+  else rc = launch_bwd<768>(S, U, grid, st, dh, wt, gv, csv, (bf16*)dgates, cnt, err, B, T);
+  return seq_accum_status(ws, B, st, rc);
 }
 
 }  // extern "C"

@@ -1,9 +1,11 @@
 """OCRInference — the reference's inference.py:12-195 API on the MI355X CTC path.
 
 Same constructor arguments, checkpoint formats and predict() contract (single image -> str,
-list -> list, optional (text, confidence)). The head is CTC, so decoding is the
-greedy CTC collapse (repeats merged, blank = id 0 = <PAD> dropped) done by the HIP greedy
-kernel; confidence = mean max-softmax over the emitted frames. Each batch of images goes through
+list -> list, optional (text, confidence)). The checkpoint picks the decoder (strict load): a
+CTC checkpoint (ctc_head.*) decodes by the greedy CTC collapse (repeats merged,
+blank = id 0 = <PAD> dropped) in the HIP greedy kernel, confidence = mean max-softmax over the
+emitted frames; a reference checkpoint (attn.*) runs the HIP attention decoder and the
+reference's decode_tokens / confidence rule (inference.py:166-190). Each batch of images goes through
 the HIP input pipeline in one launch (data.transforms.preprocess_batch: ResizeAndPadA +
 Normalize, inference.py:93-124 / data/transforms.py:185-193) straight into the encoder's input
 layout.
@@ -17,8 +19,9 @@ import numpy as np
 import torch
 
 from crnn_hip.ctc import ctc_greedy_decode
-from data.transforms import get_val_transform, load_charset, preprocess_batch
+from data.transforms import decode_tokens, get_val_transform, load_charset, preprocess_batch
 from model.model import RCNN
+from training.utils import rcnn_from_state
 
 
 class OCRInference:
@@ -48,10 +51,8 @@ class OCRInference:
             state = ckpt["model_state_dict"]
         else:
             hidden, state = 256, ckpt
-        model = RCNN(num_classes=len(self.itos), hidden_size=hidden, sos_id=self.sos_id, eos_id=self.eos_id,
-                     pad_id=self.pad_id, blank_id=self.blank_id, compute_dtype=self.compute_dtype)
-        state = {k: v for k, v in state.items() if not k.startswith("attn.")}
-        model.load_state_dict(state, strict=any(k.startswith("ctc_head.") for k in state))
+        model = rcnn_from_state(state, len(self.itos), hidden, self.sos_id, self.eos_id, self.pad_id,
+                                self.blank_id, self.compute_dtype)
         return model.to(self.device).eval()
 
     def _load_image(self, image) -> np.ndarray:
@@ -81,6 +82,9 @@ class OCRInference:
             batch = preprocess_batch([self._load_image(im) for im in items[i:i + batch_size]], self.img_h, self.img_w,
                                      out="encoder", dtype=self.compute_dtype, device=self.device)
             logits = self.model(batch, is_train=False, batch_max_length=max_length)   # [B, T, C]
+            if self.model.decoder == "attn":
+                results.extend(self._attn_texts(logits, return_confidence))
+                continue
             seqs = ctc_greedy_decode(logits)
             if return_confidence:
                 probs = torch.softmax(logits.float(), dim=-1).max(dim=-1)
@@ -95,3 +99,20 @@ class OCRInference:
                 else:
                     results.append(text)
         return results[0] if single else results
+
+    def _attn_texts(self, logits, return_confidence):
+        """inference.py:166-190 for the reference's attention decoder: argmax per step ->
+        decode_tokens (stop at <EOS>, skip <PAD> / <BLANK>); confidence = mean max-softmax over the
+        steps that are neither <PAD> nor <EOS>."""
+        pred = logits.argmax(dim=-1).cpu()
+        if return_confidence:
+            best = torch.softmax(logits.float(), dim=-1).max(dim=-1).values.cpu()
+        out = []
+        for j, row in enumerate(pred):
+            text = decode_tokens(row, self.itos, pad_id=self.pad_id, eos_id=self.eos_id, blank_id=self.blank_id)
+            if return_confidence:
+                keep = (row != self.pad_id) & (row != self.eos_id)
+                out.append((text, float(best[j][keep].mean()) if bool(keep.any()) else 0.0))
+            else:
+                out.append(text)
+        return out

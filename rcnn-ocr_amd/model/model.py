@@ -7,8 +7,10 @@ running SE-ResNet31 -> BiLSTM -> CTC head on the MI355X HIP engine.
     .encode(x [B,3,H,W]) -> [B, T=W/8, hidden]        (model/model.py:215-221)
     .forward(x, text=None, is_train=True, batch_max_length=25) -> CTC logits [B, T, C]
 
-State-dict keys are the reference's (cnn.*, enc_rnn.*) plus ctc_head.{weight,bias}
-(the reference's training head is an attention decoder; this path is CTC).
+State-dict keys are the reference's (cnn.*, enc_rnn.*) plus ctc_head.{weight,bias} for
+decoder="ctc" (the reference's training head is an attention decoder; this path is
+CTC), or plus the reference's attn.* for decoder="attn" — exactly the reference's key set, so its
+checkpoints load strictly.
 Every forward/backward runs in libcrnn_hip.so; there is no CPU path — on a CPU
 tensor the module raises.
 """
@@ -49,12 +51,14 @@ class _EncodeFn(torch.autograd.Function):
                              update_running=model.training,
                              dropout_p=model.enc_dropout.p if model.training else 0.0)
         ctx.model = model
+        ctx.gen = eng.fwd_gen
         return logits.clone()
 
     @staticmethod
     def backward(ctx, grad_logits):
         model = ctx.model
         eng = model._engine
+        eng.check_generation(ctx.gen)
         B, T, C = grad_logits.shape
         dl = eng.ws.get("autograd.dlogits", (B, T, eng.Cpad), torch.float32)
         dl[:, :, C:].zero_()
@@ -80,11 +84,13 @@ class _AttnTrainFn(torch.autograd.Function):
         ap = model.attn_dropout_p if model.training else 0.0
         model._attn_seed = (model._attn_seed + 0x9E3779B97F4A7C15) & (2 ** 64 - 1)
         ctx.model = model
+        ctx.gen = eng.fwd_gen     # the decoder's saved state is replaced together with the engine's
         return dec.run_train(enc, steps, text, drop_p=ap, seed=model._attn_seed)
 
     @staticmethod
     def backward(ctx, grad_logits):
         model = ctx.model
+        model._engine.check_generation(ctx.gen)
         grads, accumulate = model._grad_views()
         attn_grads = {k[len("attn."):]: v for k, v in grads.items() if k.startswith("attn.")}
         denc = model._attn_dec.backward(grad_logits.contiguous(), attn_grads, accumulate)
@@ -134,7 +140,7 @@ class RCNN(nn.Module):
         layers += [BidirectionalLSTM(hidden_size, hidden_size, hidden_size) for _ in range(1, num_rnn_layers)]
         self.enc_rnn = nn.Sequential(*layers)
         self.enc_dropout = nn.Dropout(enc_dropout_p)
-        self.ctc_head = nn.Linear(hidden_size, num_classes)
+        self.ctc_head = nn.Linear(hidden_size, num_classes) if decoder == "ctc" else None
         # the reference's attention head (model/model.py:23-79, :203-213): parameter holder with the
         # reference's state_dict names; compute on the HIP path (crnn_hip/attn.py), forward + backward
         self.attn = _AttentionParams(hidden_size, hidden_size, num_classes) if decoder == "attn" else None

@@ -1,7 +1,7 @@
 """training/utils.py API of sherstpasha/RCNN-OCR (training/utils.py:9-162) for the CTC path.
 
 Checkpoint dict keys are the reference's (training/utils.py:24-37), so `model_state` holds
-reference-named encoder weights (+ ctc_head.*). Loading uses torch.load(weights_only=True):
+reference-named encoder weights plus ctc_head.* (CTC) or the reference's attn.* (attention). Loading uses torch.load(weights_only=True):
 the dict holds only tensors, numbers, strings, lists and dicts.
 """
 from __future__ import annotations
@@ -56,11 +56,29 @@ def set_seed(seed: int = 42):
     torch.manual_seed(seed)
 
 
+def rcnn_from_state(model_state, num_classes, hidden_size, sos_id, eos_id, pad_id, blank_id,
+                    compute_dtype=torch.bfloat16) -> RCNN:
+    """An RCNN whose decoder matches the checkpoint, loaded strictly: ctc_head.* -> the CTC model;
+    attn.* (every checkpoint the reference trains, model/model.py:203-213) -> decoder="attn" (the
+    reference's exact key set); neither -> ValueError (no head to decode with)."""
+    if any(k.startswith("ctc_head.") for k in model_state):
+        decoder = "ctc"
+    elif any(k.startswith("attn.") for k in model_state):
+        decoder = "attn"
+    else:
+        raise ValueError("checkpoint has neither ctc_head.* nor attn.* weights: no decoder to load")
+    n_rnn = len({k.split(".")[1] for k in model_state if k.startswith("enc_rnn.") and k.endswith("linear.bias")})
+    model = RCNN(num_classes=num_classes, hidden_size=hidden_size, sos_id=sos_id, eos_id=eos_id, pad_id=pad_id,
+                 blank_id=blank_id, decoder=decoder, num_rnn_layers=max(1, n_rnn), compute_dtype=compute_dtype)
+    model.load_state_dict(model_state, strict=True)
+    return model
+
+
 def load_crnn(checkpoint_path, itos=None, stoi=None, hidden_size=256, sos_token="<SOS>", eos_token="<EOS>",
               pad_token="<PAD>", blank_token="<BLANK>", device=None, eval_mode=True,
               compute_dtype=torch.bfloat16) -> RCNN:
-    """training/utils.py:70-119 for the CTC model. Reference checkpoints without ctc_head.* load
-    their encoder with strict=False (the head then keeps its initialisation)."""
+    """training/utils.py:70-119: strict load (the reference's own contract) into the decoder the
+    checkpoint holds — CTC (ctc_head.*) or the reference's attention decoder (attn.*)."""
     if device is None:
         device = torch.device("cuda" if torch.cuda.is_available() else "cpu")
     state = torch.load(checkpoint_path, map_location="cpu", weights_only=True)
@@ -72,11 +90,8 @@ def load_crnn(checkpoint_path, itos=None, stoi=None, hidden_size=256, sos_token=
         model_state = state
     assert itos is not None and stoi is not None, "itos/stoi required (pass them or use a full checkpoint)"
     blank = stoi.get(blank_token, None) if blank_token is not None else None
-    model = RCNN(num_classes=len(itos), hidden_size=hidden_size, sos_id=stoi[sos_token], eos_id=stoi[eos_token],
-                 pad_id=stoi[pad_token], blank_id=blank, compute_dtype=compute_dtype)
-    enc_only = {k: v for k, v in model_state.items() if not k.startswith("attn.")}
-    strict = any(k.startswith("ctc_head.") for k in enc_only)
-    model.load_state_dict(enc_only, strict=strict)
+    model = rcnn_from_state(model_state, len(itos), hidden_size, stoi[sos_token], stoi[eos_token], stoi[pad_token],
+                            blank, compute_dtype)
     model = model.to(device)
     if eval_mode:
         model.eval()

@@ -573,6 +573,34 @@ def test_ctc_long_sequence_vs_oracle():
     np.testing.assert_allclose(xd.grad.cpu().numpy(), ref_grad, rtol=2e-3, atol=1e-6)
 
 
+def test_ctc_zero_infinity_keeps_nan():
+    """zero_infinity zeroes an infeasible (+inf) sample only; a NaN logit gives a NaN loss and
+    NaN gradients for its sample, as torch.nn.functional.ctc_loss does."""
+    _L()
+    import torch.nn.functional as F
+    from crnn_hip.ctc import ctc_loss
+    g = torch.Generator().manual_seed(11)
+    B, T, C = 3, 6, 12
+    x = torch.randn(B, T, C, generator=g)
+    tg = torch.tensor([[1, 2, 0, 0], [3, 3, 3, 3], [4, 5, 6, 0]])
+    tl = torch.tensor([2, 4, 3])            # sample 1: 4 repeats need 7 frames > T = 6 -> +inf
+    x[2, 3, 5] = float("nan")               # sample 2: NaN
+    for zi in (True, False):
+        ref = F.ctc_loss(x.log_softmax(-1).transpose(0, 1), tg, torch.full((B,), T), tl, zero_infinity=zi,
+                         reduction="none")
+        xd = x.to(DEV).requires_grad_(True)
+        loss = ctc_loss(xd, tg, tl, zero_infinity=zi)
+        loss.backward()
+        gr = xd.grad.cpu()
+        assert bool(torch.isnan(loss).item())           # the NaN sample poisons the mean
+        assert torch.isnan(ref[2]) and torch.isnan(gr[2]).all()
+        assert torch.isfinite(gr[0]).all()
+        if zi:
+            assert float(ref[1]) == 0.0 and bool((gr[1] == 0).all())
+        else:
+            assert torch.isinf(ref[1]) and torch.isnan(gr[1]).all()
+
+
 def test_greedy_decode_golden(itos):
     _L()
     import json
