@@ -61,7 +61,9 @@ enum { CRNN_OPT_GEMM_STAGGER = 0,    /* 256-row conv GEMM: waves 4-7 one barrier
                                         0 = write-through payload + step counter */
        CRNN_OPT_WGRAD_REDUCE = 7,    /* conv wgrad split-K slab reduce: 1 = (co, 64-channel) tiles transposed
                                         through LDS, coalesced OIHW stores (default), 0 = flat, scattered stores */
-       CRNN_OPT_COUNT = 8 };
+       CRNN_OPT_WGRAD_FAST = 8,      /* conv wgrad on the 256-row kernel: 1 = per-tile scalar pixel decode for
+                                        64-aligned pixel tiles (default), 0 = per-lane decode */
+       CRNN_OPT_COUNT = 9 };
 int crnn_set_option(int key, int value);
 
 /* ------------------------------------------------------------------ layout */

@@ -359,6 +359,84 @@ template <typename T> struct WgradB {
   }
 };
 
+// ---- wgrad loaders for 64-aligned pixel tiles (the 256-row kernel's common case): every K-tile
+// (64 output pixels, k0 % 64 == 0) lies inside one image (Ho*Wo % 64 == 0) and starts at a row
+// start (Wo | 64) or inside one row (64 | Wo), so a pixel k0 + kr splits into per-tile scalars
+// (image, first row, first column: SALU, once per K-tile) plus per-lane constants of the lane's
+// k-row kr (hoisted out of the K-loop). The generic loaders above re-derive (b, ho, wo) per lane
+// and per K-tile with 64-bit multiply-adds: 3x the VALU of the fwd loop.
+template <typename T> struct WgradAF {
+  static constexpr bool kRowVec = true;
+  const T* dy;
+  int Co;
+  uint32_t bytes;
+  struct Ctx { int co; bool ok; };
+  typedef int Prep;   // k0 * Co
+  __device__ __forceinline__ Ctx row_ctx(int r8) const { return Ctx{r8, r8 < Co}; }
+  __device__ __forceinline__ Prep prep(int k0) const { return k0 * Co; }
+  __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc() const { return mk_rsrc(dy, bytes); }
+  __device__ __forceinline__ uint32_t offs(const Ctx& c, Prep base, int kr) const {
+    return c.ok ? (uint32_t)(base + kr * Co + c.co) * (uint32_t)sizeof(T) : OOB;
+  }
+  __device__ __forceinline__ typename VT<T>::v8 load(const Ctx& c, Prep p, int kofs) const {
+    return bld8<T>(rsrc(), offs(c, p, kofs));
+  }
+};
+
+template <typename T, bool WIDE> struct WgradBF {   // WIDE: Wo % 64 == 0, else 64 % Wo == 0
+  static constexpr bool kRowVec = true;
+  const T* x;
+  Geo g;
+  int Kp, lwo;        // lwo = log2(Wo) (narrow rows)
+  uint32_t bytes;
+  struct Ctx { int kh, kw, ci; bool ok; };
+  struct Prep { int base, hs, ws; };   // element offset of (b, ho0*sh, wo0*sw, 0); row / column bases
+  __device__ __forceinline__ Ctx row_ctx(int r8) const {
+    Ctx c;
+    c.ok = r8 < Kp;
+    uint32_t ci, kw;
+    uint32_t tap = g.dCi.divmod(c.ok ? r8 : 0, ci);
+    uint32_t kh = g.dKW.divmod(tap, kw);
+    c.ci = (int)ci;
+    c.kh = (int)kh - g.ph;
+    c.kw = (int)kw - g.pw;
+    return c;
+  }
+  __device__ __forceinline__ Prep prep(int k0) const {
+    uint32_t r, wo0;
+    const uint32_t b = g.dHoWo.divmod((uint32_t)k0, r);
+    const uint32_t ho0 = g.dWo.divmod(r, wo0);
+    Prep p;
+    p.hs = (int)ho0 * g.sh;
+    p.ws = WIDE ? (int)wo0 * g.sw : 0;
+    p.base = (((int)b * g.Hi + p.hs) * g.Wi + p.ws) * g.Ci;
+    return p;
+  }
+  __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc() const { return mk_rsrc(x, bytes); }
+  __device__ __forceinline__ uint32_t offs(const Ctx& c, const Prep& p, int kr) const {
+    // lane constants (loop-invariant): row / column offsets of this lane's pixel and tap
+    const int dho = WIDE ? 0 : kr >> lwo;
+    const int dwo = WIDE ? kr : kr & ((1 << lwo) - 1);
+    const int lh = dho * g.sh + c.kh, lw = dwo * g.sw + c.kw;
+    const int lc = (lh * g.Wi + lw) * g.Ci + c.ci;
+    const bool okw = c.ok && (WIDE || (unsigned)lw < (unsigned)g.Wi);
+    const bool ok = okw && (unsigned)(p.hs + lh) < (unsigned)g.Hi && (!WIDE || (unsigned)(p.ws + lw) < (unsigned)g.Wi);
+    return ok ? (uint32_t)(p.base + lc) * (uint32_t)sizeof(T) : OOB;
+  }
+  __device__ __forceinline__ typename VT<T>::v8 load(const Ctx& c, const Prep& p, int kofs) const {
+    return bld8<T>(rsrc(), offs(c, p, kofs));
+  }
+};
+
+// the fast loaders' geometry condition (see WgradAF); 0 = generic, 1 = narrow rows, 2 = wide rows
+inline int wgrad_fast_kind(const Geo& g) {
+  const int HoWo = g.Ho * g.Wo;
+  if (crnn_option(CRNN_OPT_WGRAD_FAST) == 0 || HoWo % 64) return 0;
+  if (g.Wo % 64 == 0) return 2;
+  if (64 % g.Wo == 0) return 1;
+  return 0;
+}
+
 // ---- epilogues
 template <typename T> struct FwdEpi {
   static constexpr bool kStats = true;
@@ -682,7 +760,18 @@ template <typename T> int conv_wgrad_t(const crnn_conv_desc* d, const void* dy, 
   WgradB<T> lb{(const T*)x, g, Kp, Mp, nbytes((long)g.B * g.Hi * g.Wi * g.Ci, sizeof(T))};
   SlabEpi ep{ws, g.Co, Kp};
   if constexpr (sizeof(T) == 2) {
-    if (bm == 256 && bn == 256) rc = launch256<256, 256>(la, lb, ep, g.Co, Kp, Mp, st, splits);
+    const int fk = bm == 256 ? wgrad_fast_kind(g) : 0;
+    if (fk) {
+      WgradAF<T> fa{(const T*)dy, g.Co, la.bytes};
+      int lwo = 0;
+      while ((1 << lwo) < g.Wo) ++lwo;
+      WgradBF<T, true> fbw{(const T*)x, g, Kp, lwo, lb.bytes};
+      WgradBF<T, false> fbn{(const T*)x, g, Kp, lwo, lb.bytes};
+      if (bn == 256) rc = fk == 2 ? launch256<256, 256>(fa, fbw, ep, g.Co, Kp, Mp, st, splits)
+                                  : launch256<256, 256>(fa, fbn, ep, g.Co, Kp, Mp, st, splits);
+      else rc = fk == 2 ? launch256<256, 128>(fa, fbw, ep, g.Co, Kp, Mp, st, splits)
+                        : launch256<256, 128>(fa, fbn, ep, g.Co, Kp, Mp, st, splits);
+    } else if (bm == 256 && bn == 256) rc = launch256<256, 256>(la, lb, ep, g.Co, Kp, Mp, st, splits);
     else if (bm == 256 && bn == 128) rc = launch256<256, 128>(la, lb, ep, g.Co, Kp, Mp, st, splits);
   }
   if (bm == 256) {

@@ -141,6 +141,15 @@ def test_conv_fwd_dgrad_wgrad(cfg, dtype):
     finally:
         L.call("crnn_set_option", L.OPT_WGRAD_REDUCE, 1)
     assert relerr(dw_flat.cpu(), dw.cpu()) < 1e-6
+    # the per-tile pixel decode of 64-aligned tiles (CRNN_OPT_WGRAD_FAST, default) vs the per-lane
+    # decode: the same bytes in the same order, so bit-identical
+    dw_gen = torch.empty_like(dw)
+    try:
+        L.call("crnn_set_option", L.OPT_WGRAD_FAST, 0)
+        L.call("crnn_conv_wgrad", dt, d, dyd.data_ptr(), xd.data_ptr(), dw_gen.data_ptr(), ws.data_ptr(), need, 0.0, st)
+    finally:
+        L.call("crnn_set_option", L.OPT_WGRAD_FAST, 1)
+    assert torch.equal(dw_gen.cpu(), dw.cpu())
     L.call("crnn_conv_wgrad", dt, d, dyd.data_ptr(), xd.data_ptr(), dw.data_ptr(), ws.data_ptr(), need, 1.0, st)
     assert relerr(dw.cpu(), 2 * dw_flat.cpu()) < 1e-6
 
