@@ -63,7 +63,9 @@ enum { CRNN_OPT_GEMM_STAGGER = 0,    /* 256-row conv GEMM: waves 4-7 one barrier
                                         through LDS, coalesced OIHW stores (default), 0 = flat, scattered stores */
        CRNN_OPT_WGRAD_FAST = 8,      /* conv wgrad on the 256-row kernel: 1 = per-tile scalar pixel decode for
                                         64-aligned pixel tiles (default), 0 = per-lane decode */
-       CRNN_OPT_COUNT = 9 };
+       CRNN_OPT_ROW_SKIP = 9,        /* 256-row conv fwd / stride-1 dgrad: 1 = skip the MFMAs of 16-row fragments
+                                        whose input row for the K-tile's tap is zero padding (default) */
+       CRNN_OPT_COUNT = 10 };
 int crnn_set_option(int key, int value);
 
 /* ------------------------------------------------------------------ layout */
