@@ -280,6 +280,10 @@ def main():
     ids = torch.empty(args.batch, T, dtype=torch.int32, device=dev)
     lens = torch.empty(args.batch, dtype=torch.int32, device=dev)
     from crnn_hip._lib import call, stream_ptr
+    # A/B switches (include/crnn_hip.h CRNN_OPT_*): CRNN_OPTS="key=value,key=value"
+    opts = {int(k): int(v) for k, v in (kv.split("=") for kv in os.environ.get("CRNN_OPTS", "").split(",") if kv)}
+    for k, v in opts.items():
+        call("crnn_set_option", k, v)
 
     def infer_step():
         eng.forward(x, train=False, save_for_backward=False)
@@ -419,6 +423,7 @@ def main():
             "kernels": per_kind,
             "roofline_lstm": lstm_roofline(lstm, args, eng),
             "final_loss": round(final_loss, 4),
+            **({"options": opts} if opts else {}),
             "dp": ({"allreduce": "RCCL sum of the flat fp32 gradient, bucketed and overlapped with the backward",
                     "param_checksum_spread": divergence} if world > 1 else None),
         }
