@@ -704,16 +704,30 @@ template <typename T> int deep_dgrad_bn(long M, int N, int Co, long min_tiles) {
   return 0;
 }
 
+// the 256-row kernel's share of the CUs in its last round of tiles (1 block per CU): a grid of
+// 264 tiles runs two rounds, the second nearly empty
+inline double round_eff(long tiles) {
+  const long ncu = crnn_cu_count();
+  return (double)tiles / (double)(((tiles + ncu - 1) / ncu) * ncu);
+}
+// CRNN_OPT_QUANT_TILE: a deep-kernel grid that fills its rounds this badly runs on the 128x128
+// kernel (two blocks per CU, 4x the tiles) instead
+constexpr double kQuantEff = 0.7;
+
+// rows: row classes (each input row its own class, Hc = 1) instead of parity classes in height —
+// for maps of 1-2 output rows (conv_out[1]: Ho = 1), where half of a generic dgrad's taps read
+// nothing but padding rows; the stride may then be 1
 template <typename T>
 int conv_dgrad_strided(const Geo& g, const void* dy, const void* w, void* dx, const void* dres, const void* yres,
-                       int accumulate, hipStream_t st) {
+                       int accumulate, hipStream_t st, bool rows = false) {
   const uint32_t dyb = nbytes((long)g.B * g.Ho * g.Wo * g.Co, sizeof(T));
   const uint32_t wb = nbytes((long)g.Co * g.KH * g.KW * g.Ci, sizeof(T));
-  for (int pch = 0; pch < g.sh; ++pch)
+  for (int pch = 0; pch < (rows ? g.Hi : g.sh); ++pch)
     for (int pcw = 0; pcw < g.sw; ++pcw) {
       TapTable tt{};
       for (int kh = 0; kh < g.KH; ++kh) {
         if (((pch + g.ph - kh) % g.sh + g.sh) % g.sh) continue;
+        if (rows && (pch + g.ph - kh < 0 || (pch + g.ph - kh) / g.sh >= g.Ho)) continue;
         for (int kw = 0; kw < g.KW; ++kw) {
           if (((pcw + g.pw - kw) % g.sw + g.sw) % g.sw) continue;
           if (tt.n >= 4) return crnn_set_error(hipErrorInvalidValue, "conv_dgrad: > 4 taps per parity class");
@@ -723,7 +737,7 @@ int conv_dgrad_strided(const Geo& g, const void* dy, const void* w, void* dx, co
           ++tt.n;
         }
       }
-      const int Hc = (g.Hi - pch + g.sh - 1) / g.sh, Wc = (g.Wi - pcw + g.sw - 1) / g.sw;
+      const int Hc = rows ? 1 : (g.Hi - pch + g.sh - 1) / g.sh, Wc = (g.Wi - pcw + g.sw - 1) / g.sw;
       if (Hc <= 0 || Wc <= 0) continue;
       // a class no tap reaches contributes 0: with accumulate and no residual term it leaves dx
       // as it is (the 1x1 stride-2 downsample: 3 of 4 classes), so skip its read + write pass
@@ -734,7 +748,8 @@ int conv_dgrad_strided(const Geo& g, const void* dy, const void* w, void* dx, co
       DgradClsB<T> lb{(const T*)w, g, tt, K, wb};
       DgradClsEpi<T> ep{(T*)dx, (const T*)dres, (const T*)yres, g, M, N, accumulate, pch, pcw, dWc, dHcWc};
       int rc = 0;
-      const int deep = deep_dgrad_bn<T>(M, N, g.Co, 256);
+      int deep = deep_dgrad_bn<T>(M, N, g.Co, 256);
+      if (deep && crnn_option(CRNN_OPT_QUANT_TILE) && round_eff((M + 255) / 256 * (N / deep)) < kQuantEff) deep = 0;
       if constexpr (sizeof(T) == 2) {
         if (deep == 256) rc = launch256<256, 256>(la, lb, ep, M, N, K, st);
         else if (deep == 128) rc = launch256<256, 128>(la, lb, ep, M, N, K, st);
@@ -752,6 +767,8 @@ template <typename T> int conv_dgrad_t(const crnn_conv_desc* d, const void* dy, 
   Geo g = geo(d);
   if ((g.sh > 1 || g.sw > 1) && g.Co % kstage<T>() == 0)
     return conv_dgrad_strided<T>(g, dy, w, dx, dres, yres, accumulate, st);
+  if (g.Hi <= 2 && g.KH > 1 && g.Co % kstage<T>() == 0 && crnn_option(CRNN_OPT_ROW_CLASS))
+    return conv_dgrad_strided<T>(g, dy, w, dx, dres, yres, accumulate, st, true);
   int M = g.B * g.Hi * g.Wi, N = g.Ci, K = g.KH * g.KW * g.Co;
   int lsh = ilog2s(g.sh), lsw = ilog2s(g.sw);
   if (lsh < 0 || lsw < 0 || g.Co % kstage<T>())
@@ -760,7 +777,8 @@ template <typename T> int conv_dgrad_t(const crnn_conv_desc* d, const void* dy, 
   DgradB<T> lb{(const T*)w, g, K, nbytes((long)g.Co * g.KH * g.KW * g.Ci, sizeof(T))};
   DgradEpi<T> ep{(T*)dx, (const T*)dres, (const T*)yres, M, N, accumulate};
   if constexpr (sizeof(T) == 2) {
-    const int deep = deep_dgrad_bn<T>(M, N, g.Co, 128);
+    int deep = deep_dgrad_bn<T>(M, N, g.Co, 128);
+    if (deep && crnn_option(CRNN_OPT_QUANT_TILE) && round_eff(((long)M + 255) / 256 * (N / deep)) < kQuantEff) deep = 0;
     la.rskip = row_skip_ok(g, g.Wi, deep ? 256 : 0);
     if (deep == 256) return launch256<256, 256>(la, lb, ep, M, N, K, st);
     if (deep == 128) return launch256<256, 128>(la, lb, ep, M, N, K, st);
@@ -853,7 +871,11 @@ void crnn_conv_fwd_tile(int dtype, const crnn_conv_desc* d, int* bm, int* bn) {
   const bool deep = dtype == CRNN_BF16 && d->Ci % 64 == 0 && d->Co % 128 == 0 && d->Co >= CRNN_DEEP_MIN_CO;
   if (deep && d->Co >= 256 && M * d->Co >= 256L * 256 * 128) { *bm = 256; *bn = 256; }
   else if (deep && M * d->Co >= 256L * 128 * 128) { *bm = 256; *bn = 128; }
-  else if (d->Co <= 64) { *bm = 128; *bn = 64; }
+  else { *bm = 0; }
+  if (*bm == 256 && crnn_option(CRNN_OPT_QUANT_TILE) && round_eff((M + 255) / 256 * (d->Co / *bn)) < kQuantEff)
+    *bm = 0;
+  if (*bm == 256) return;
+  if (d->Co <= 64) { *bm = 128; *bn = 64; }
   else if (M * d->Co >= 128L * 128 * 192) { *bm = 128; *bn = 128; }
   else { *bm = 64; *bn = 64; }
 }

@@ -173,6 +173,35 @@ def test_conv_fwd_dgrad_wgrad(cfg, dtype):
                 L.call("crnn_set_option", L.OPT_ROW_SKIP, 1)
         for a, b in zip(*outs):
             assert torch.equal(a, b)
+        # row classes for 1-2-row maps (CRNN_OPT_ROW_CLASS) and the round-quantization tile rule
+        # (CRNN_OPT_QUANT_TILE): only exact-zero products and the kernel choice change. Row classes
+        # and the fwd on either kernel accumulate the same K order (bit-identical); a dgrad moved to
+        # the 128x128 kernel sums each 32-deep MFMA step in its permuted k order (gemm.hpp kmap), so
+        # it agrees to fp32 summation order (bf16 outputs within one rounding step)
+        for key in (L.OPT_ROW_CLASS, L.OPT_QUANT_TILE):
+            outs = []
+            for v in (1, 0):
+                L.call("crnn_set_option", key, v)
+                try:
+                    y2 = torch.empty_like(yd)
+                    ps2, pq2 = torch.zeros_like(ps), torch.zeros_like(pq)
+                    L.call("crnn_conv_fwd", dt, d, xd.data_ptr(), wd.data_ptr(), y2.data_ptr(), ps2.data_ptr(),
+                           pq2.data_ptr(), st)
+                    dx2 = torch.zeros(B, H, W, Cip, dtype=dtype, device=DEV)
+                    if Ci % 8 == 0:
+                        L.call("crnn_conv_dgrad", dt, d, dyd.data_ptr(), wd.data_ptr(), dx2.data_ptr(), None, None, 0, st)
+                    torch.cuda.synchronize()
+                    outs.append((y2, dx2, ps2.sum(0), pq2.sum(0)))
+                finally:
+                    L.call("crnn_set_option", key, 1)
+            assert torch.equal(outs[0][0], outs[1][0])
+            if key == L.OPT_ROW_CLASS:
+                assert torch.equal(outs[0][1], outs[1][1])
+            else:
+                a, b = outs[0][1].float(), outs[1][1].float()
+                assert float((a - b).abs().max()) <= 2 ** -7 * float(b.abs().max()) and relerr(a, b) < 2e-3
+            # BN partials: the partial grouping may change with the tile (sums agree to fp32 order)
+            assert relerr(outs[0][2], outs[1][2]) < 1e-5
 
 
 def test_conv_halo_vs_gemm():
