@@ -793,7 +793,11 @@ template <typename T> int conv_dgrad_t(const crnn_conv_desc* d, const void* dy, 
 inline int dgrad_bnrelu_rows(const crnn_conv_desc* d) {
   if (d->sh != 1 || d->sw != 1 || d->Co % 64 || d->Ci % 8) return 0;
   const long M = (long)d->B * d->Hi * d->Wi;
-  if (!deep_dgrad_bn<bf16>(M, d->Ci, d->Co, 128)) return 0;
+  const int deep = deep_dgrad_bn<bf16>(M, d->Ci, d->Co, 128);
+  if (!deep) return 0;
+  // the plain dgrad of this geometry would leave the 256-row kernel (CRNN_OPT_QUANT_TILE): so does
+  // the fused one (callers then run the unfused pair)
+  if (crnn_option(CRNN_OPT_QUANT_TILE) && round_eff((M + 255) / 256 * (d->Ci / deep)) < kQuantEff) return 0;
   return (int)((M + 255) / 256 * 2);
 }
 

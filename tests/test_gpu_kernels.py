@@ -252,7 +252,7 @@ def test_conv_halo_vs_gemm():
     assert relerr(w1, w0) < 1e-5   # fp32 accumulation both ways (beta = 1 keeps the 0.25 start)
 
 
-@pytest.mark.parametrize("geo", [(64, 256, 8, 64, 256), (128, 512, 4, 32, 512), (70, 256, 8, 60, 256)])
+@pytest.mark.parametrize("geo", [(128, 256, 8, 64, 256), (256, 512, 4, 32, 512), (131, 256, 8, 62, 256)])
 def test_dgrad_bnrelu_fused(geo):
     """crnn_conv_dgrad_bnrelu == crnn_conv_dgrad + crnn_bn_bwd_reduce (CRNN_BNG_RELU) through
     crnn_bn_bwd_finalize (incl. a ragged last tile)."""
