@@ -63,13 +63,11 @@ enum { CRNN_OPT_GEMM_STAGGER = 0,    /* 256-row conv GEMM: waves 4-7 one barrier
                                         through LDS, coalesced OIHW stores (default), 0 = flat, scattered stores */
        CRNN_OPT_WGRAD_FAST = 8,      /* conv wgrad on the 256-row kernel: 1 = per-tile scalar pixel decode for
                                         64-aligned pixel tiles (default), 0 = per-lane decode */
-       CRNN_OPT_ROW_SKIP = 9,        /* 256-row conv fwd / stride-1 dgrad: 1 = skip the MFMAs of 16-row fragments
-                                        whose input row for the K-tile's tap is zero padding (default) */
-       CRNN_OPT_ROW_CLASS = 10,      /* conv dgrad of 1-2-row maps (conv_out[1]): 1 = one class per input row (only
+       CRNN_OPT_ROW_CLASS = 9,       /* conv dgrad of 1-2-row maps (conv_out[1]): 1 = one class per input row (only
                                         the taps that reach a real output row; default), 0 = generic */
-       CRNN_OPT_QUANT_TILE = 11,     /* conv fwd / dgrad: 1 = a 256-row grid that fills its last round of tiles to
+       CRNN_OPT_QUANT_TILE = 10,     /* conv fwd / dgrad: 1 = a 256-row grid that fills its last round of tiles to
                                         < 70 % runs on the 128x128 kernel (default), 0 = off */
-       CRNN_OPT_COUNT = 12 };
+       CRNN_OPT_COUNT = 11 };
 int crnn_set_option(int key, int value);
 
 /* ------------------------------------------------------------------ layout */

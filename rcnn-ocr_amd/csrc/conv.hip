@@ -83,12 +83,10 @@ __device__ __forceinline__ TapPrep tap_prep(const FastDiv& dC, const FastDiv& dK
 // UT: the stage never straddles a tap (Ci % stage depth == 0)
 template <typename T, bool UT> struct FwdA {
   static constexpr bool kRowVec = false;
-  static constexpr bool kRowSkip = UT;  // gemm256.hpp has_row_skip
   const T* x;
   Geo g;
   int M, K;
   uint32_t bytes;
-  int rskip;   // row skip on (host: 256-row kernel, 16 | Wo, KH <= 4)
   struct Ctx { int off; uint32_t mask; int hb, wb; };  // off = element offset of (b, hb, wb, 0)
   typedef TapPrep Prep;
   __device__ __forceinline__ Ctx row_ctx(int m) const {
@@ -113,23 +111,6 @@ template <typename T, bool UT> struct FwdA {
     p.tap = k0;
     return p;
   }
-  // row skip: fragment i = output rows rbase + 16i..+15 (one output row ho), input row ho*sh - ph + kh
-  __device__ __forceinline__ uint32_t frag_mask(int rbase) const {
-    if (!rskip) return ~0u;
-    uint32_t msk = 0;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int m = rbase + 16 * i;
-      if (m >= M) continue;
-      uint32_t r, wo;
-      g.dHoWo.divmod((uint32_t)m, r);
-      const int hb = (int)g.dWo.divmod(r, wo) * g.sh - g.ph;
-      for (int kh = 0; kh < g.KH; ++kh)
-        if ((unsigned)(hb + kh) < (unsigned)g.Hi) msk |= 1u << (8 * kh + i);
-    }
-    return msk;
-  }
-  __device__ __forceinline__ int prep_kh(const Prep& p) const { return p.kh < 3 ? p.kh : 3; }
   __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc() const { return mk_rsrc(x, bytes); }
   // byte offset of elements (row, k0+kofs .. +7), or OOB (reads zeros) — UT only
   __device__ __forceinline__ uint32_t offs(const Ctx& c, const Prep& p, int kofs) const {
@@ -158,12 +139,10 @@ template <typename T, bool UT> struct FwdA {
 // plus a per-stage scalar.
 template <typename T> struct DgradA {
   static constexpr bool kRowVec = false;
-  static constexpr bool kRowSkip = true;  // gemm256.hpp has_row_skip
   const T* dy;
   Geo g;
   int M, K, lsh, lsw;
   uint32_t bytes;
-  int rskip;   // row skip on (host: 256-row kernel, 16 | Wi, KH <= 4)
   struct Ctx { int off; uint32_t mask; };
   typedef TapPrep Prep;
   __device__ __forceinline__ Ctx row_ctx(int m) const {
@@ -186,25 +165,6 @@ template <typename T> struct DgradA {
     return c;
   }
   __device__ __forceinline__ Prep prep(int k0) const { return tap_prep(g.dCo, g.dKW, k0); }
-  // row skip: fragment i = input rows rbase + 16i..+15 (one input row hi); output row (hi+ph-kh)/sh
-  __device__ __forceinline__ uint32_t frag_mask(int rbase) const {
-    if (!rskip) return ~0u;
-    uint32_t msk = 0;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int m = rbase + 16 * i;
-      if (m >= M) continue;
-      uint32_t r, wi;
-      g.dHiWi.divmod((uint32_t)m, r);
-      const int hp = (int)g.dWi.divmod(r, wi) + g.ph;
-      for (int kh = 0; kh < g.KH; ++kh) {
-        const int th = hp - kh;
-        if (th >= 0 && !(th & ((1 << lsh) - 1)) && (th >> lsh) < g.Ho) msk |= 1u << (8 * kh + i);
-      }
-    }
-    return msk;
-  }
-  __device__ __forceinline__ int prep_kh(const Prep& p) const { return p.kh < 3 ? p.kh : 3; }
   __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc() const { return mk_rsrc(dy, bytes); }
   __device__ __forceinline__ uint32_t offs(const Ctx& c, const Prep& p, int kofs) const {
     const bool ok = (c.mask >> p.tap) & 1u;
@@ -661,11 +621,6 @@ __global__ __launch_bounds__(256) void wgrad_reduce_tiled_kernel(const float* __
 
 inline uint32_t nbytes(long elems, size_t es) { return (uint32_t)((size_t)elems * es); }
 
-// fragment row skip (gemm256.hpp has_row_skip): 256-row kernel, 16-row fragments inside one
-// image row (16 | row width), kernel rows in the mask's 4 bytes
-inline int row_skip_ok(const Geo& g, int width, int bm) {
-  return crnn_option(CRNN_OPT_ROW_SKIP) != 0 && bm == 256 && width % 16 == 0 && g.KH <= 4;
-}
 
 template <typename T, bool UT>
 int conv_fwd_tt(const Geo& g, const crnn_conv_desc* d, const void* x, const void* w, void* y, float* psum,
@@ -676,7 +631,6 @@ int conv_fwd_tt(const Geo& g, const crnn_conv_desc* d, const void* x, const void
   FwdEpi<T> ep{(T*)y, psum, psq, M, N};
   int bm, bn;
   crnn_conv_fwd_tile(sizeof(T) == 2 ? CRNN_BF16 : CRNN_F32, d, &bm, &bn);
-  la.rskip = row_skip_ok(g, g.Wo, bm);
   if constexpr (sizeof(T) == 2 && UT) {
     if (bm == 256 && bn == 256) return launch256<256, 256>(la, lb, ep, M, N, K, st);
     if (bm == 256 && bn == 128) return launch256<256, 128>(la, lb, ep, M, N, K, st);
@@ -779,7 +733,6 @@ template <typename T> int conv_dgrad_t(const crnn_conv_desc* d, const void* dy, 
   if constexpr (sizeof(T) == 2) {
     int deep = deep_dgrad_bn<T>(M, N, g.Co, 128);
     if (deep && crnn_option(CRNN_OPT_QUANT_TILE) && round_eff(((long)M + 255) / 256 * (N / deep)) < kQuantEff) deep = 0;
-    la.rskip = row_skip_ok(g, g.Wi, deep ? 256 : 0);
     if (deep == 256) return launch256<256, 256>(la, lb, ep, M, N, K, st);
     if (deep == 128) return launch256<256, 128>(la, lb, ep, M, N, K, st);
   }
@@ -811,7 +764,6 @@ int conv_dgrad_bnrelu(const crnn_conv_desc* d, const void* dy, const void* w, vo
   DgradB<T> lb{(const T*)w, g, K, nbytes((long)g.Co * g.KH * g.KW * g.Ci, sizeof(T))};
   DgradBnEpi<T> ep{(T*)dx, M, N, (const T*)z, mean, inv, scale, shift, pg, pgx};
   const int deep = deep_dgrad_bn<T>(M, N, g.Co, 128);
-  la.rskip = row_skip_ok(g, g.Wi, 256);
   if (deep == 256) return launch256<256, 256>(la, lb, ep, M, N, K, st);
   return launch256<256, 128>(la, lb, ep, M, N, K, st);
 }

@@ -61,18 +61,6 @@ __device__ __forceinline__ void raw_barrier() {
 template <class E, class = void> struct has_tile_hook : std::false_type {};
 template <class E> struct has_tile_hook<E, std::void_t<decltype(E::kTileHook)>> : std::bool_constant<E::kTileHook> {};
 
-// optional A-loader hook (conv fwd / stride-1 dgrad): skip the MFMAs of 16-row fragments whose
-// rows read only zero padding for the K-tile's kernel row. An LA with `kRowSkip` provides
-//   uint32_t frag_mask(int rbase): bit 8*kh + i set when fragment i (rows rbase + 16i .. +15, one
-//                                  input row since 16 | W) has a real input row for kernel row kh;
-//   int prep_kh(const Prep&):      the K-tile's kernel row (a stage never straddles a tap), <= 3.
-// A skipped MFMA would add exact zeros: results are bit-identical with and without the skip.
-// In a conv over 4-row feature maps (layer3/4 of the backbone) 1/6 of the fwd / dgrad MFMAs are
-// such zero products, 1/12 over 8-row maps; every wave holds whole image rows, so the saving is
-// spread evenly over the waves of every tile.
-template <class L, class = void> struct has_row_skip : std::false_type {};
-template <class L> struct has_row_skip<L, std::void_t<decltype(L::kRowSkip)>> : std::bool_constant<L::kRowSkip> {};
-
 // per-wave, per-column partial statistics (sum, sum of squared deviations from the partial
 // mean) over this wave's WM accumulator rows — the BN two-pass-in-registers epilogue
 template <int MI, int NI, class EPI>
@@ -176,17 +164,14 @@ template <class L, int R, int Q> struct Op256 {
   }
   // N fragments (rows rb0 + H*Q + 16f) x both 32-deep k sub-steps, from the operand tile at `tile`
   // (LDS address `lds` of the same tile for the row-contiguous asm reads)
-  // fm: fragments to read (bit H*N + f; the row-skip mask of the A operand, all ones otherwise)
   template <int H, int N>
-  __device__ __forceinline__ void load(bf16x8 (&fr)[N][2], const char* tile, uint32_t lds, int rb0, int lane,
-                                       uint32_t fm = ~0u) const {
+  __device__ __forceinline__ void load(bf16x8 (&fr)[N][2], const char* tile, uint32_t lds, int rb0, int lane) const {
     if constexpr (!RV) {
 #pragma unroll
       for (int f = 0; f < N; ++f)
-        if (fm & (1u << (H * N + f)))
 #pragma unroll
-          for (int kk = 0; kk < 2; ++kk)
-            fr[f][kk] = gemm::frag<bf16, R, false, false, 64>(reinterpret_cast<const bf16*>(tile), rb0 + H * Q + f * 16, kk, lane);
+        for (int kk = 0; kk < 2; ++kk)
+          fr[f][kk] = gemm::frag<bf16, R, false, false, 64>(reinterpret_cast<const bf16*>(tile), rb0 + H * Q + f * 16, kk, lane);
     } else {
       const uint32_t bl = lds + plo, bh = lds + phi;
 #pragma unroll
@@ -233,9 +218,6 @@ __device__ __forceinline__ void gemm256_item(LA la, LB lb, EPI epi, int M, int K
   oa.init(la, m0, wid, lane, wr);
   ob.init(lb, n0, wid, lane, wc);
   const __amdgpu_buffer_rsrc_t ra = la.rsrc(), rb = lb.rsrc();
-  constexpr bool RS = has_row_skip<LA>::value;
-  uint32_t rvm = ~0u;                      // row-skip mask of this wave's fragments (scalar)
-  if constexpr (RS) rvm = __builtin_amdgcn_readfirstlane(la.frag_mask(m0 + wr * WM));
   char* const sA0 = smem;
   char* const sB0 = smem + OA::TB;
 
@@ -255,11 +237,8 @@ __device__ __forceinline__ void gemm256_item(LA la, LB lb, EPI epi, int M, int K
     oa.issue(la, ra, sA0, 1, pa2);
   }
   typename LA::Prep pa1 = pa2;  // prep of tile t+1 (for its A-half1)
-  int kh0 = 0, kh1 = 0;          // row skip: kernel rows of tiles t, t+1
-  if constexpr (RS) kh0 = la.prep_kh(pa2);
   if (nk > 1) {
     pa1 = la.prep(kbeg + KS);
-    if constexpr (RS) kh1 = la.prep_kh(pa1);
     const typename LB::Prep pb1 = lb.prep(kbeg + KS);
     oa.issue(la, ra, sA0 + STAGE, 0, pa1);
     ob.issue(lb, rb, sB0 + STAGE, 0, pb1);
@@ -280,16 +259,12 @@ __device__ __forceinline__ void gemm256_item(LA la, LB lb, EPI epi, int M, int K
     const char* Bs = As + OA::TB;
     const uint32_t lA = lds_addr(As), lB = lds_addr(Bs);
     const bool n1 = t + 1 < nk, n2 = t + 2 < nk;
-    int kh2 = 0;
     if (n2) {
       pa2 = la.prep(kbeg + (t + 2) * KS);
       pb2 = lb.prep(kbeg + (t + 2) * KS);
-      if constexpr (RS) kh2 = la.prep_kh(pa2);
     }
-    // fragments of this K-tile with a real input row (all of them without the row-skip hook)
-    const uint32_t fm = RS ? (rvm >> (8 * kh0)) & 0xffu : 0xffu;
     // ---- P1: quadrant (0,0)
-    oa.template load<0, MQ>(af, As, lA, wr * WM, lane, fm);
+    oa.template load<0, MQ>(af, As, lA, wr * WM, lane);
     ob.template load<0, NQ>(*reinterpret_cast<bf16x8(*)[NQ][2]>(&bfr[0]), Bs, lB, wc * WN, lane);
     if (n1) oa.issue(la, ra, sA0 + (b ^ 1) * STAGE, 1, pa1);
     lds_wait_all();
@@ -299,7 +274,6 @@ __device__ __forceinline__ void gemm256_item(LA la, LB lb, EPI epi, int M, int K
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
       for (int i = 0; i < MQ; ++i)
-        if (fm & (1u << i))
 #pragma unroll
           for (int j = 0; j < NQ; ++j) mma<T>(acc[i][j], bfr[j][kk], af[i][kk]);
     __builtin_amdgcn_s_setprio(0);
@@ -314,13 +288,12 @@ __device__ __forceinline__ void gemm256_item(LA la, LB lb, EPI epi, int M, int K
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
       for (int i = 0; i < MQ; ++i)
-        if (fm & (1u << i))
 #pragma unroll
           for (int j = NQ; j < NI; ++j) mma<T>(acc[i][j], bfr[j][kk], af[i][kk]);
     __builtin_amdgcn_s_setprio(0);
     raw_barrier();
     // ---- P3: quadrant (1,1)
-    oa.template load<1, MQ>(af, As, lA, wr * WM, lane, fm);
+    oa.template load<1, MQ>(af, As, lA, wr * WM, lane);
     if (n2) ob.issue(lb, rb, sB0 + b * STAGE, 0, pb2);
     lds_wait_all();
     raw_barrier();
@@ -329,7 +302,6 @@ __device__ __forceinline__ void gemm256_item(LA la, LB lb, EPI epi, int M, int K
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
       for (int i = 0; i < MQ; ++i)
-        if (fm & (1u << (MQ + i)))
 #pragma unroll
           for (int j = NQ; j < NI; ++j) mma<T>(acc[MQ + i][j], bfr[j][kk], af[i][kk]);
     __builtin_amdgcn_s_setprio(0);
@@ -342,15 +314,12 @@ __device__ __forceinline__ void gemm256_item(LA la, LB lb, EPI epi, int M, int K
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     pa1 = pa2;
-    kh0 = kh1;
-    kh1 = kh2;
     raw_barrier();
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
       for (int i = 0; i < MQ; ++i)
-        if (fm & (1u << (MQ + i)))
 #pragma unroll
           for (int j = 0; j < NQ; ++j) mma<T>(acc[MQ + i][j], bfr[j][kk], af[i][kk]);
     __builtin_amdgcn_s_setprio(0);
