@@ -67,7 +67,9 @@ enum { CRNN_OPT_GEMM_STAGGER = 0,    /* 256-row conv GEMM: waves 4-7 one barrier
                                         the taps that reach a real output row; default), 0 = generic */
        CRNN_OPT_QUANT_TILE = 10,     /* conv fwd / dgrad: 1 = a 256-row grid that fills its last round of tiles to
                                         < 70 % runs on the 128x128 kernel (default), 0 = off */
-       CRNN_OPT_COUNT = 11 };
+       CRNN_OPT_PAD_SKIP = 11,       /* 3x3 conv fwd / dgrad over 4-row maps on the 256-row kernel: 1 = skip the MFMAs
+                                        of the fragment rows that read only zero padding (default) */
+       CRNN_OPT_COUNT = 12 };
 int crnn_set_option(int key, int value);
 
 /* ------------------------------------------------------------------ layout */

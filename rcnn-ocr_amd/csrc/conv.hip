@@ -621,6 +621,14 @@ __global__ __launch_bounds__(256) void wgrad_reduce_tiled_kernel(const float* __
 
 inline uint32_t nbytes(long elems, size_t es) { return (uint32_t)((size_t)elems * es); }
 
+// the 256-row kernel's padding-row fragment skip (gemm256.hpp SKIP): a 3x3 / stride-1 / pad-1 conv
+// over 4-row maps of 128 pixels (layer3 / layer4: 4 x 32), so each wave's 128 rows are one image
+// and the rows reading only padding are the same two fragment rows in every wave
+inline bool pad_skip_ok(const Geo& g, int rows, int cols) {
+  return crnn_option(CRNN_OPT_PAD_SKIP) != 0 && g.KH == 3 && g.KW == 3 && g.sh == 1 && g.sw == 1 && g.ph == 1 &&
+         g.pw == 1 && rows == 4 && rows * cols == 128;
+}
+
 
 template <typename T, bool UT>
 int conv_fwd_tt(const Geo& g, const crnn_conv_desc* d, const void* x, const void* w, void* y, float* psum,
@@ -632,6 +640,11 @@ int conv_fwd_tt(const Geo& g, const crnn_conv_desc* d, const void* x, const void
   int bm, bn;
   crnn_conv_fwd_tile(sizeof(T) == 2 ? CRNN_BF16 : CRNN_F32, d, &bm, &bn);
   if constexpr (sizeof(T) == 2 && UT) {
+    if (bm == 256 && pad_skip_ok(g, g.Ho, g.Wo)) {
+      const int ktk = g.KW * g.Ci / 64;
+      if (bn == 256) return launch256<256, 256, 1>(la, lb, ep, M, N, K, st, 1, 1, ktk);
+      return launch256<256, 128, 1>(la, lb, ep, M, N, K, st, 1, 1, ktk);
+    }
     if (bm == 256 && bn == 256) return launch256<256, 256>(la, lb, ep, M, N, K, st);
     if (bm == 256 && bn == 128) return launch256<256, 128>(la, lb, ep, M, N, K, st);
   }
@@ -664,9 +677,11 @@ inline double round_eff(long tiles) {
   const long ncu = crnn_cu_count();
   return (double)tiles / (double)(((tiles + ncu - 1) / ncu) * ncu);
 }
-// CRNN_OPT_QUANT_TILE: a deep-kernel grid that fills its rounds this badly runs on the 128x128
-// kernel (two blocks per CU, 4x the tiles) instead
-constexpr double kQuantEff = 0.7;
+// CRNN_OPT_QUANT_TILE: a deep-kernel grid that fills its last round this badly runs on the 128x128
+// kernel (two blocks per CU, 4x the tiles, balanced) instead. The 128x128 kernel's rate relative to
+// the 256-row kernel (measured on conv_out: ~0.4 of the 256 x 256 tile, ~0.6 of the 256 x 128
+// tile) is the break-even share of the CUs: below it the smaller tiles finish first
+inline double quant_eff(int bn) { return bn == 256 ? 0.4 : 0.6; }
 
 // rows: row classes (each input row its own class, Hc = 1) instead of parity classes in height —
 // for maps of 1-2 output rows (conv_out[1]: Ho = 1), where half of a generic dgrad's taps read
@@ -703,7 +718,7 @@ int conv_dgrad_strided(const Geo& g, const void* dy, const void* w, void* dx, co
       DgradClsEpi<T> ep{(T*)dx, (const T*)dres, (const T*)yres, g, M, N, accumulate, pch, pcw, dWc, dHcWc};
       int rc = 0;
       int deep = deep_dgrad_bn<T>(M, N, g.Co, 256);
-      if (deep && crnn_option(CRNN_OPT_QUANT_TILE) && round_eff((M + 255) / 256 * (N / deep)) < kQuantEff) deep = 0;
+      if (deep && crnn_option(CRNN_OPT_QUANT_TILE) && round_eff((M + 255) / 256 * (N / deep)) < quant_eff(deep)) deep = 0;
       if constexpr (sizeof(T) == 2) {
         if (deep == 256) rc = launch256<256, 256>(la, lb, ep, M, N, K, st);
         else if (deep == 128) rc = launch256<256, 128>(la, lb, ep, M, N, K, st);
@@ -732,7 +747,12 @@ template <typename T> int conv_dgrad_t(const crnn_conv_desc* d, const void* dy, 
   DgradEpi<T> ep{(T*)dx, (const T*)dres, (const T*)yres, M, N, accumulate};
   if constexpr (sizeof(T) == 2) {
     int deep = deep_dgrad_bn<T>(M, N, g.Co, 128);
-    if (deep && crnn_option(CRNN_OPT_QUANT_TILE) && round_eff(((long)M + 255) / 256 * (N / deep)) < kQuantEff) deep = 0;
+    if (deep && crnn_option(CRNN_OPT_QUANT_TILE) && round_eff(((long)M + 255) / 256 * (N / deep)) < quant_eff(deep)) deep = 0;
+    if (deep && pad_skip_ok(g, g.Hi, g.Wi)) {
+      const int ktk = g.KW * g.Co / 64;
+      if (deep == 256) return launch256<256, 256, 2>(la, lb, ep, M, N, K, st, 1, 1, ktk);
+      return launch256<256, 128, 2>(la, lb, ep, M, N, K, st, 1, 1, ktk);
+    }
     if (deep == 256) return launch256<256, 256>(la, lb, ep, M, N, K, st);
     if (deep == 128) return launch256<256, 128>(la, lb, ep, M, N, K, st);
   }
@@ -750,7 +770,7 @@ inline int dgrad_bnrelu_rows(const crnn_conv_desc* d) {
   if (!deep) return 0;
   // the plain dgrad of this geometry would leave the 256-row kernel (CRNN_OPT_QUANT_TILE): so does
   // the fused one (callers then run the unfused pair)
-  if (crnn_option(CRNN_OPT_QUANT_TILE) && round_eff((M + 255) / 256 * (d->Ci / deep)) < kQuantEff) return 0;
+  if (crnn_option(CRNN_OPT_QUANT_TILE) && round_eff((M + 255) / 256 * (d->Ci / deep)) < quant_eff(deep)) return 0;
   return (int)((M + 255) / 256 * 2);
 }
 
@@ -764,6 +784,11 @@ int conv_dgrad_bnrelu(const crnn_conv_desc* d, const void* dy, const void* w, vo
   DgradB<T> lb{(const T*)w, g, K, nbytes((long)g.Co * g.KH * g.KW * g.Ci, sizeof(T))};
   DgradBnEpi<T> ep{(T*)dx, M, N, (const T*)z, mean, inv, scale, shift, pg, pgx};
   const int deep = deep_dgrad_bn<T>(M, N, g.Co, 128);
+  if (pad_skip_ok(g, g.Hi, g.Wi)) {
+    const int ktk = g.KW * g.Co / 64;
+    if (deep == 256) return launch256<256, 256, 2>(la, lb, ep, M, N, K, st, 1, 1, ktk);
+    return launch256<256, 128, 2>(la, lb, ep, M, N, K, st, 1, 1, ktk);
+  }
   if (deep == 256) return launch256<256, 256>(la, lb, ep, M, N, K, st);
   return launch256<256, 128>(la, lb, ep, M, N, K, st);
 }
@@ -828,7 +853,7 @@ void crnn_conv_fwd_tile(int dtype, const crnn_conv_desc* d, int* bm, int* bn) {
   if (deep && d->Co >= 256 && M * d->Co >= 256L * 256 * 128) { *bm = 256; *bn = 256; }
   else if (deep && M * d->Co >= 256L * 128 * 128) { *bm = 256; *bn = 128; }
   else { *bm = 0; }
-  if (*bm == 256 && crnn_option(CRNN_OPT_QUANT_TILE) && round_eff((M + 255) / 256 * (d->Co / *bn)) < kQuantEff)
+  if (*bm == 256 && crnn_option(CRNN_OPT_QUANT_TILE) && round_eff((M + 255) / 256 * (d->Co / *bn)) < quant_eff(*bn))
     *bm = 0;
   if (*bm == 256) return;
   if (d->Co <= 64) { *bm = 128; *bn = 64; }

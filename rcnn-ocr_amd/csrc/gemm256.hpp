@@ -164,14 +164,16 @@ template <class L, int R, int Q> struct Op256 {
   }
   // N fragments (rows rb0 + H*Q + 16f) x both 32-deep k sub-steps, from the operand tile at `tile`
   // (LDS address `lds` of the same tile for the row-contiguous asm reads)
-  template <int H, int N>
+  // FM (compile time): fragments to read, bit H * N + f (the A operand's padding-row skip)
+  template <int H, int N, uint32_t FM = 0xffu>
   __device__ __forceinline__ void load(bf16x8 (&fr)[N][2], const char* tile, uint32_t lds, int rb0, int lane) const {
     if constexpr (!RV) {
 #pragma unroll
       for (int f = 0; f < N; ++f)
+        if ((FM >> (H * N + f)) & 1u)
 #pragma unroll
-        for (int kk = 0; kk < 2; ++kk)
-          fr[f][kk] = gemm::frag<bf16, R, false, false, 64>(reinterpret_cast<const bf16*>(tile), rb0 + H * Q + f * 16, kk, lane);
+          for (int kk = 0; kk < 2; ++kk)
+            fr[f][kk] = gemm::frag<bf16, R, false, false, 64>(reinterpret_cast<const bf16*>(tile), rb0 + H * Q + f * 16, kk, lane);
     } else {
       const uint32_t bl = lds + plo, bh = lds + phi;
 #pragma unroll
@@ -189,9 +191,9 @@ __device__ __forceinline__ uint32_t lds_addr(const char* p) {
 }
 
 // One work item of the grid kernel: tile (m_tile, n_tile), K range [kz*klen, min(K, (kz+1)*klen)).
-template <int BM, int BN, class LA, class LB, class EPI>
+template <int BM, int BN, int SKIP, class LA, class LB, class EPI>
 __device__ __forceinline__ void gemm256_item(LA la, LB lb, EPI epi, int M, int K, int klen, int m_tile, int n_tile,
-                                             int kz, int stagger) {
+                                             int kz, int stagger, int ktk) {
   using T = bf16;
   static_assert(BM == 256 && (BN == 256 || BN == 128), "tile");
   constexpr int KS = 64;
@@ -253,7 +255,11 @@ __device__ __forceinline__ void gemm256_item(LA la, LB lb, EPI epi, int M, int K
   if (stagger && wr == 1) raw_barrier();
 
   bf16x8 af[MQ][2], bfr[NI][2];
-  for (int t = 0; t < nk; ++t) {
+  // one K-tile; FM (compile time): the fragment rows i whose MFMAs run (bit i). Fragment skipping
+  // is only ever a compile-time property of a loop segment: a runtime mask test between the MFMAs
+  // breaks the phase's MFMA cluster (measured 20-25 % slower, profiles/r02h_rowskip_regression.log)
+  auto ktile = [&](auto fmc, int t) {
+    constexpr uint32_t FM = decltype(fmc)::value;
     const int b = t & 1;
     const char* As = smem + b * STAGE;
     const char* Bs = As + OA::TB;
@@ -264,7 +270,7 @@ __device__ __forceinline__ void gemm256_item(LA la, LB lb, EPI epi, int M, int K
       pb2 = lb.prep(kbeg + (t + 2) * KS);
     }
     // ---- P1: quadrant (0,0)
-    oa.template load<0, MQ>(af, As, lA, wr * WM, lane);
+    oa.template load<0, MQ, FM>(af, As, lA, wr * WM, lane);
     ob.template load<0, NQ>(*reinterpret_cast<bf16x8(*)[NQ][2]>(&bfr[0]), Bs, lB, wc * WN, lane);
     if (n1) oa.issue(la, ra, sA0 + (b ^ 1) * STAGE, 1, pa1);
     lds_wait_all();
@@ -274,6 +280,7 @@ __device__ __forceinline__ void gemm256_item(LA la, LB lb, EPI epi, int M, int K
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
       for (int i = 0; i < MQ; ++i)
+        if ((FM >> i) & 1u)
 #pragma unroll
           for (int j = 0; j < NQ; ++j) mma<T>(acc[i][j], bfr[j][kk], af[i][kk]);
     __builtin_amdgcn_s_setprio(0);
@@ -288,12 +295,13 @@ __device__ __forceinline__ void gemm256_item(LA la, LB lb, EPI epi, int M, int K
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
       for (int i = 0; i < MQ; ++i)
+        if ((FM >> i) & 1u)
 #pragma unroll
           for (int j = NQ; j < NI; ++j) mma<T>(acc[i][j], bfr[j][kk], af[i][kk]);
     __builtin_amdgcn_s_setprio(0);
     raw_barrier();
     // ---- P3: quadrant (1,1)
-    oa.template load<1, MQ>(af, As, lA, wr * WM, lane);
+    oa.template load<1, MQ, FM>(af, As, lA, wr * WM, lane);
     if (n2) ob.issue(lb, rb, sB0 + b * STAGE, 0, pb2);
     lds_wait_all();
     raw_barrier();
@@ -302,6 +310,7 @@ __device__ __forceinline__ void gemm256_item(LA la, LB lb, EPI epi, int M, int K
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
       for (int i = 0; i < MQ; ++i)
+        if ((FM >> (MQ + i)) & 1u)
 #pragma unroll
           for (int j = NQ; j < NI; ++j) mma<T>(acc[MQ + i][j], bfr[j][kk], af[i][kk]);
     __builtin_amdgcn_s_setprio(0);
@@ -320,10 +329,25 @@ __device__ __forceinline__ void gemm256_item(LA la, LB lb, EPI epi, int M, int K
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
       for (int i = 0; i < MQ; ++i)
+        if ((FM >> (MQ + i)) & 1u)
 #pragma unroll
           for (int j = 0; j < NQ; ++j) mma<T>(acc[MQ + i][j], bfr[j][kk], af[i][kk]);
     __builtin_amdgcn_s_setprio(0);
     raw_barrier();
+    };
+  if constexpr (SKIP == 0) {
+    for (int t = 0; t < nk; ++t) ktile(std::integral_constant<uint32_t, 0xffu>{}, t);
+  } else {
+    // 3x3 conv over 4-row maps, one image per wave (128 rows = 4 rows x 32 columns): the K-tiles run
+    // in tap order, kernel row kh owning [kh * ktk, (kh + 1) * ktk); for kh = 0 and kh = 2 one
+    // image row (two fragment rows) reads only zero padding (SKIP 1: conv fwd, output row 0 / 3;
+    // SKIP 2: dgrad, input row 3 / 0) — 1/6 of the MFMAs, skipped per segment at compile time
+    constexpr uint32_t M0 = SKIP == 1 ? 0xfcu : 0x3fu, M2 = SKIP == 1 ? 0x3fu : 0xfcu;
+    const int e0 = min(nk, ktk), e1 = min(nk, 2 * ktk);
+    int t = 0;
+    for (; t < e0; ++t) ktile(std::integral_constant<uint32_t, M0>{}, t);
+    for (; t < e1; ++t) ktile(std::integral_constant<uint32_t, 0xffu>{}, t);
+    for (; t < nk; ++t) ktile(std::integral_constant<uint32_t, M2>{}, t);
   }
   if (stagger && wr == 0) raw_barrier();
 
@@ -337,10 +361,10 @@ __device__ __forceinline__ void gemm256_item(LA la, LB lb, EPI epi, int M, int K
 }
 
 // One block per work item (the default): the K-loop above, block-level.
-template <int BM, int BN, class LA, class LB, class EPI>
+template <int BM, int BN, int SKIP, class LA, class LB, class EPI>
 __global__ __launch_bounds__(512) void gemm256_kernel(LA la, LB lb, EPI epi, int M, int N, int K, int klen,
                                                       int tiles_m, int tiles_n, int nsplit, int stagger,
-                                                      int nbatch) {
+                                                      int nbatch, int ktk) {
   // one work item per block: ((batch * nsplit + split) * tiles_m + m_tile) * tiles_n + n_tile
   const int nwg = tiles_m * tiles_n * nsplit * nbatch;
   const int wg = xcd_remap(blockIdx.x, nwg);
@@ -351,7 +375,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(LA la, LB lb, EPI epi, int
     if constexpr (has_set_batch<LB>::value) lb.set_batch(bz);
     if constexpr (has_set_batch<EPI>::value) epi.set_batch(bz);
   }
-  gemm256_item<BM, BN>(la, lb, epi, M, K, klen, m_tile, n_tile, kz, stagger);
+  gemm256_item<BM, BN, SKIP>(la, lb, epi, M, K, klen, m_tile, n_tile, kz, stagger, ktk);
 }
 
 // Persistent variant (crnn_set_option CRNN_OPT_GEMM_PERSISTENT): grid <= CU count, every block
@@ -588,9 +612,11 @@ __global__ __launch_bounds__(512) void gemm256p_kernel(LA la, LB lb, EPI epi, in
 
 // nsplit: split-K factor (K ranges of split_len(K, nsplit), multiples of 64)
 // nbatch: independent GEMMs of one shape in one launch (loaders / epilogue with set_batch(int))
-template <int BM, int BN, class LA, class LB, class EPI>
+// SKIP (1: conv fwd, 2: stride-1 dgrad, 3x3 over 4-row maps of 128 pixels; nsplit 1): the
+// padding-row fragment skip of gemm256_item, ktk = K-tiles per kernel row
+template <int BM, int BN, int SKIP = 0, class LA, class LB, class EPI>
 inline int launch256(const LA& la, const LB& lb, const EPI& epi, int M, int N, int K, hipStream_t st,
-                     int nsplit = 1, int nbatch = 1) {
+                     int nsplit = 1, int nbatch = 1, int ktk = 0) {
   if (M <= 0 || N <= 0) return 0;
   const int tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN;
   const int klen = split_len(K, nsplit);
@@ -598,13 +624,13 @@ inline int launch256(const LA& la, const LB& lb, const EPI& epi, int M, int N, i
   const int items = tm * tn * nsplit * nbatch;
   const int ncu = crnn_cu_count();
   const int popt = crnn_option(CRNN_OPT_GEMM_PERSISTENT);   // 1: when items > CUs, 2: always
-  if ((popt == 1 && items > ncu) || popt == 2) {
+  if (SKIP == 0 && ((popt == 1 && items > ncu) || popt == 2)) {
     hipLaunchKernelGGL((gemm256p_kernel<BM, BN, LA, LB, EPI>), dim3(items < ncu ? items : ncu), dim3(512), 0, st, la,
                        lb, epi, M, N, K, klen, tm, tn, nsplit, crnn_option(CRNN_OPT_GEMM_STAGGER), nbatch);
     return (int)hipGetLastError();
   }
-    hipLaunchKernelGGL((gemm256_kernel<BM, BN, LA, LB, EPI>), dim3(items), dim3(512), 0, st, la, lb, epi,
-                       M, N, K, klen, tm, tn, nsplit, crnn_option(CRNN_OPT_GEMM_STAGGER), nbatch);
+    hipLaunchKernelGGL((gemm256_kernel<BM, BN, SKIP, LA, LB, EPI>), dim3(items), dim3(512), 0, st, la, lb, epi,
+                       M, N, K, klen, tm, tn, nsplit, crnn_option(CRNN_OPT_GEMM_STAGGER), nbatch, ktk);
   return (int)hipGetLastError();
 }
 

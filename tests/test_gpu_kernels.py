@@ -154,12 +154,13 @@ def test_conv_fwd_dgrad_wgrad(cfg, dtype):
     L.call("crnn_conv_wgrad", dt, d, dyd.data_ptr(), xd.data_ptr(), dw.data_ptr(), ws.data_ptr(), need, 1.0, st)
     assert relerr(dw.cpu(), 2 * dw_flat.cpu()) < 1e-6
     if dtype == torch.bfloat16:
-        # row classes for 1-2-row maps (CRNN_OPT_ROW_CLASS) and the round-quantization tile rule
-        # (CRNN_OPT_QUANT_TILE): only exact-zero products and the kernel choice change. Row classes
-        # and the fwd on either kernel accumulate the same K order (bit-identical); a dgrad moved to
-        # the 128x128 kernel sums each 32-deep MFMA step in its permuted k order (gemm.hpp kmap), so
-        # it agrees to fp32 summation order (bf16 outputs within one rounding step)
-        for key in (L.OPT_ROW_CLASS, L.OPT_QUANT_TILE):
+        # row classes for 1-2-row maps (CRNN_OPT_ROW_CLASS), the padding-row fragment skip of 4-row
+        # maps (CRNN_OPT_PAD_SKIP) and the round-quantization tile rule (CRNN_OPT_QUANT_TILE): only
+        # exact-zero products and the kernel choice change. Row classes, the skip and the fwd on
+        # either kernel accumulate the same K order (bit-identical); a dgrad moved to the 128x128
+        # kernel sums each 32-deep MFMA step in its permuted k order (gemm.hpp kmap), so it agrees
+        # to fp32 summation order (bf16 outputs within one rounding step)
+        for key in (L.OPT_ROW_CLASS, L.OPT_PAD_SKIP, L.OPT_QUANT_TILE):
             outs = []
             for v in (1, 0):
                 L.call("crnn_set_option", key, v)
@@ -176,7 +177,7 @@ def test_conv_fwd_dgrad_wgrad(cfg, dtype):
                 finally:
                     L.call("crnn_set_option", key, 1)
             assert torch.equal(outs[0][0], outs[1][0])
-            if key == L.OPT_ROW_CLASS:
+            if key != L.OPT_QUANT_TILE:
                 assert torch.equal(outs[0][1], outs[1][1])
             else:
                 a, b = outs[0][1].float(), outs[1][1].float()
