@@ -69,7 +69,9 @@ enum { CRNN_OPT_GEMM_STAGGER = 0,    /* 256-row conv GEMM: waves 4-7 one barrier
                                         < 70 % runs on the 128x128 kernel (default), 0 = off */
        CRNN_OPT_PAD_SKIP = 11,       /* 3x3 conv fwd / dgrad over 4-row maps on the 256-row kernel: 1 = skip the MFMAs
                                         of the fragment rows that read only zero padding (default) */
-       CRNN_OPT_COUNT = 12 };
+       CRNN_OPT_LSTM_BWD_PART = 12,  /* persistent BPTT: 1 = partial-sum form (own dgates x own W_hh rows, partials
+                                        handed off as tagged granules), 0 = dgates + counter hand-off (default) */
+       CRNN_OPT_COUNT = 13 };
 int crnn_set_option(int key, int value);
 
 /* ------------------------------------------------------------------ layout */

@@ -451,6 +451,181 @@ __global__ __launch_bounds__(256) void lstm_seq_bwd_kernel(const bf16* __restric
   }
 }
 
+// ---------------------------------------------------------------- BPTT sweep, partial-sum form
+// (CRNN_OPT_LSTM_BWD_PART = 1; measured against the counter form in one process: cfg2 6.42 vs
+// 5.92 us per step, long config 6.24 vs 6.39 — so the counter form stays the default,
+// profiles/r02l_lstm_bwd_partial_ab.log). Each workgroup multiplies its OWN dgates by its own
+// packed W_hh' rows: partial[b][h] = sum over its 4U gate rows k of dgates_t[b][k] W_hh'[k][h]
+// (wave w: the h quarter [w H/4, (w+1) H/4); W_hh'^T fragments resident in VGPRs), and publishes
+// the partial as data-tagged granules {2 bf16, u32 tag = step + 1} (the forward's handoff-1to1
+// form). The finalising lanes of the next step gather, for their 16 samples x 4 units, the
+// partials of all H/U workgroups of their (d, bs) group and sum them in fp32: per step a
+// workgroup gathers S x U x (H/U) partials (cfg2: 16 KB of bf16 + tags) instead of the S x 4H
+// dgates the counter form needs (64 KB), the MFMA needs no remote data, and nothing drains,
+// barriers or counts on the hand-off. Ring: [2 slots][2 d][B][H/U producers][H] granule
+// positions (4 B per value), zeroed per launch; slot s & 1 is rewritten at step s + 2 only after
+// its consumers' gathers of step s + 1 returned (they precede their step s + 1 publish, which the
+// producer's own step s + 2 gather waited for).
+template <int H, int S, int U>
+__global__ __launch_bounds__(256) void lstm_seq_bwdp_kernel(const bf16* __restrict__ dhseq,
+                                                            const bf16* __restrict__ whh_t,
+                                                            const bf16* __restrict__ gsv,
+                                                            const float* __restrict__ csv, bf16* dgates,
+                                                            unsigned* cnt, unsigned* err, uint2* ring, int B,
+                                                            int Tn, unsigned long long* stamps) {
+  constexpr int GR = 4 * U, KK = GR / 32;   // MFMA k: the workgroup's packed gate rows
+  constexpr int HQ = H / 4, NJ = HQ / 16;   // wave w: h in [w HQ, (w + 1) HQ)
+  constexpr int H4 = 4 * H, MI = S / 16, NU = U / 16, NBLK = MI * NU;
+  constexpr int DP = GR + 8;                // dgates tile pitch (bf16): rows 16 B off-bank
+  static_assert(S % 16 == 0 && U % 16 == 0 && HQ % 16 == 0 && NBLK <= 4 && GR % 32 == 0, "shape");
+  __shared__ __attribute__((aligned(16))) bf16 dgt[2][S][DP];
+
+  const int nsl = H / U, nbs = B / S;
+  int d, bs, ns;
+  seq_coords(nsl, nbs, d, bs, ns);
+  const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int b0 = bs * S, u0 = ns * U;
+  unsigned* mycnt = cnt + d * nbs + bs;
+
+  // W_hh'^T fragments (MFMA A operand): row h = w HQ + 16j + c of whh_t[d] ([H][4H]), k = the
+  // packed gate rows 4 u0 + 32kk + 8g .. +7
+  bf16x8 wf[NJ][KK];
+  {
+    const bf16* wb = whh_t + (size_t)d * H * H4;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk)
+        wf[j][kk] = *reinterpret_cast<const bf16x8*>(wb + (size_t)(w * HQ + 16 * j + c) * H4 + 4 * u0 + 32 * kk + 8 * g);
+  }
+  const __amdgpu_buffer_rsrc_t rr = rsrc_of(ring);
+  // granule position of value (slot, b, producer p, h): 4 bytes per value, two values per granule
+  auto gpos = [&](int slot, int b, int p, int h) -> uint32_t {
+    return (uint32_t)(((((size_t)(slot * 2 + d) * B + b) * nsl + p) * H + h) * 4u);
+  };
+  const bool fin = w < NBLK;
+  const int fi = fin ? w % MI : 0, fj = fin ? w / MI : 0;
+  const int bl = 16 * fi + c, b = b0 + bl;
+  const int u = u0 + 16 * fj + 4 * g;  // this lane's 4 units u..u+3
+  float dcs[4] = {0.f, 0.f, 0.f, 0.f};
+
+  bf16x8 gv0, gv1;
+  f32x4 cv, cpv, dhv;
+  float has_prev_f = 0.f;
+  auto load_in = [&](int t) {
+    const size_t gi = ((size_t)(d * Tn + t) * B + b) * H4 + 4 * u;
+    gv0 = *reinterpret_cast<const bf16x8*>(gsv + gi);
+    gv1 = *reinterpret_cast<const bf16x8*>(gsv + gi + 8);
+    cv = *reinterpret_cast<const f32x4*>(csv + ((size_t)(d * Tn + t) * B + b) * H + u);
+    const int tf = d == 0 ? t - 1 : t + 1;
+    const bool has_prev = d == 0 ? t > 0 : t < Tn - 1;
+    const int tfc = has_prev ? tf : t;
+    cpv = *reinterpret_cast<const f32x4*>(csv + ((size_t)(d * Tn + tfc) * B + b) * H + u);
+    has_prev_f = has_prev ? 1.f : 0.f;
+    dhv = ld4f<bf16>(dhseq + ((size_t)b * Tn + t) * 2 * H + d * H + u);
+  };
+  load_in(d == 0 ? Tn - 1 : 0);
+
+  bool ok = true;
+  for (int s = 0; s < Tn; ++s) {
+    const int t = d == 0 ? Tn - 1 - s : s;
+    const int buf = s & 1;
+    f32x4 dh = dhv;
+    SEQ_STAMP(0);
+    if (fin) {
+      if (s > 0) {
+        // the previous step's partials of this lane's (sample, 4 units) from every producer
+        const uint32_t want = (uint32_t)s;
+        unsigned long long t0 = 0;
+        constexpr int NP = H / U;
+        u32x4 pv[NP];
+        for (;;) {
+#pragma unroll
+          for (int p = 0; p < NP; ++p) pv[p] = __builtin_amdgcn_raw_buffer_load_b128(rr, gpos((s - 1) & 1, b, p, u), 0, 16);
+          bool mine = true;
+#pragma unroll
+          for (int p = 0; p < NP; ++p) mine &= (pv[p][1] == want) & (pv[p][3] == want);
+          if (__all(mine)) break;
+          const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+          if (t0 == 0) t0 = now;
+          if (now - t0 > SEQ_TIMEOUT_TICKS || __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+            __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            ok = false;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+        SEQ_STAMP(1);
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+          const bf16x4 v = __builtin_bit_cast(bf16x4, uint2{pv[p][0], pv[p][2]});
+          dh += f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
+        }
+      }
+      // cell backward of units u..u+3 (lstm.hip cell_bwd)
+      bf16x8 out0, out1;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const bf16x8& gv = r < 2 ? gv0 : gv1;
+        const int o = (r & 1) * 4;
+        const float ig = (float)gv[o], fg = (float)gv[o + 1], gg = (float)gv[o + 2], og = (float)gv[o + 3];
+        const float tc = tanh_fast(cv[r]);
+        const float dcv = dcs[r] + dh[r] * og * (1.f - tc * tc);
+        const float do_ = dh[r] * tc;
+        const float di = dcv * gg, dg = dcv * ig, df = dcv * cpv[r] * has_prev_f;
+        dcs[r] = dcv * fg;
+        float q0 = di * ig * (1.f - ig), q1 = df * fg * (1.f - fg), q2 = dg * (1.f - gg * gg), q3 = do_ * og * (1.f - og);
+        if (!ok) q0 = q1 = q2 = q3 = __builtin_nanf("");
+        bf16x8& ov = r < 2 ? out0 : out1;
+        ov[o] = (bf16)q0;
+        ov[o + 1] = (bf16)q1;
+        ov[o + 2] = (bf16)q2;
+        ov[o + 3] = (bf16)q3;
+      }
+      *reinterpret_cast<bf16x8*>(&dgt[buf][bl][4 * (u - u0)]) = out0;
+      *reinterpret_cast<bf16x8*>(&dgt[buf][bl][4 * (u - u0) + 8]) = out1;
+      // dgates for the weight gradients: plain stores, off the hand-off path
+      bf16* go = dgates + ((size_t)(d * Tn + t) * B + b) * H4 + 4 * u;
+      *reinterpret_cast<bf16x8*>(go) = out0;
+      *reinterpret_cast<bf16x8*>(go + 8) = out1;
+    }
+    SEQ_STAMP(2);
+    __syncthreads();  // the dgates tile of this step (double-buffered: see the ring note above)
+    SEQ_STAMP(3);
+    if (s + 1 < Tn) {
+      bf16x8 af[MI][KK];
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int kk = 0; kk < KK; ++kk) af[i][kk] = *reinterpret_cast<const bf16x8*>(&dgt[buf][16 * i + c][32 * kk + 8 * g]);
+      // one output tile at a time (a dependent MFMA chain costs no more than independent ones,
+      // MI355X_MICROARCH.md), published as soon as it is complete: its stores overlap the next
+      // tile's MFMAs. Lane: h = w HQ + 16j + 4g .. +3 of sample b0 + 16i + c -> two granules
+      const uint32_t tag = (uint32_t)(s + 1);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int kk = 0; kk < KK; ++kk) mma<bf16>(acc, wf[j][kk], af[i][kk]);
+          const bf16x4 hv = {(bf16)acc[0], (bf16)acc[1], (bf16)acc[2], (bf16)acc[3]};
+          const uint2 hp = __builtin_bit_cast(uint2, hv);
+          __builtin_amdgcn_raw_buffer_store_b128(u32x4{hp.x, tag, hp.y, tag}, rr,
+                                                 gpos(buf, b0 + 16 * i + c, ns, w * HQ + 16 * j + 4 * g), 0, 16);
+        }
+      SEQ_STAMP(4);
+    }
+    SEQ_STAMP(5);
+    SEQ_STAMP(6);
+    // unconditional prefetch of the next step's saved-forward inputs (the last step re-reads its own)
+    load_in(s + 1 < Tn ? (d == 0 ? t - 1 : t + 1) : t);
+  }
+  // the counter-form invariant ((H/U) * T per slice at the end)
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(mycnt, (unsigned)Tn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 int g_cus = -1;
 unsigned long long* g_stamps = nullptr;  // crnn_lstm_seq_debug_stamps
 
@@ -514,7 +689,23 @@ int launch_fwd(int S, int U, dim3 grid, hipStream_t st, const bf16* xg, const bf
 
 template <int H>
 int launch_bwd(int S, int U, dim3 grid, hipStream_t st, const bf16* dhseq, const bf16* whh_t, const bf16* gsv,
-               const float* csv, bf16* dg, unsigned* cnt, unsigned* err, int B, int T) {
+               const float* csv, bf16* dg, unsigned* cnt, unsigned* err, uint2* ring, int B, int T) {
+  if (crnn_option(CRNN_OPT_LSTM_BWD_PART)) {
+    if constexpr (H <= 512) {
+      if (S == 16 && U == 64) {
+        hipLaunchKernelGGL((lstm_seq_bwdp_kernel<H, 16, 64>), grid, dim3(256), 0, st, dhseq, whh_t, gsv, csv, dg, cnt,
+                           err, ring, B, T, g_stamps);
+        return (int)hipGetLastError();
+      }
+    }
+    if (S == 16)
+      hipLaunchKernelGGL((lstm_seq_bwdp_kernel<H, 16, 32>), grid, dim3(256), 0, st, dhseq, whh_t, gsv, csv, dg, cnt,
+                         err, ring, B, T, g_stamps);
+    else
+      hipLaunchKernelGGL((lstm_seq_bwdp_kernel<H, 32, 32>), grid, dim3(256), 0, st, dhseq, whh_t, gsv, csv, dg, cnt,
+                         err, ring, B, T, g_stamps);
+    return (int)hipGetLastError();
+  }
   if constexpr (H <= 512) {
     if (S == 16 && U == 64) {
       hipLaunchKernelGGL((lstm_seq_bwd_kernel<H, 16, 64>), grid, dim3(256), 0, st, dhseq, whh_t, gsv, csv, dg, cnt, err, B, T, g_stamps);
@@ -560,11 +751,17 @@ int crnn_lstm_seq_debug_stamps(unsigned long long* buf) {
 }
 
 // counters: one per (direction, batch slice) of the smallest slice (16 samples), then the error word;
-// then (from byte seq_ring_offset) the forward's 2-slot granule ring: 2 x B x H 8-byte granules
-// (sized for H = 768, the largest supported)
+// then (from byte seq_ring_offset) the granule ring shared by the sweeps (one runs at a time on the
+// stream): the forward's 2 x B x H 8-byte granules, or the partial-sum BPTT's
+// 2 slots x 2 d x B x (H/U) x H 4-byte value positions (sized for H = 768 with U = 32, the largest)
 static size_t seq_ring_offset(int B) { return (size_t)((2 * (B / 16 + 1) + 1 + 63) / 64 * 256); }
+static size_t seq_ring_bytes_bwdp(int B, int H, int U) { return (size_t)2 * 2 * B * (H / U) * H * 4; }
+static size_t seq_ring_bytes(int B) {
+  const size_t f = (size_t)2 * B * 768 * 8, p = seq_ring_bytes_bwdp(B, 768, 32);
+  return f > p ? f : p;
+}
 // after the ring: the sticky status word (zeroed once by the caller when it allocates ws)
-size_t crnn_lstm_seq_status_offset(int B) { return seq_ring_offset(B) + (size_t)2 * B * 768 * 8; }
+size_t crnn_lstm_seq_status_offset(int B) { return seq_ring_offset(B) + seq_ring_bytes(B); }
 size_t crnn_lstm_seq_workspace(int B) { return crnn_lstm_seq_status_offset(B) + 256; }
 
 static int seq_accum_status(unsigned* ws, int B, hipStream_t st, int rc) {
@@ -600,16 +797,19 @@ int crnn_lstm_seq_bwd(const void* dhseq, const void* whh_t, const void* gsv, con
   hipStream_t st = (hipStream_t)stream;
   int S, U;
   if (!seq_config(B, H, true, S, U)) return crnn_set_error(hipErrorInvalidValue, "lstm_seq: unsupported shape");
-  hipError_t e = hipMemsetAsync(ws, 0, seq_ring_offset(B), st);  // counters + error word
+  // counters + error word, and the partial ring this (B, H, U) uses (tag 0 = not yet written)
+  const size_t zero = seq_ring_offset(B) + (crnn_option(CRNN_OPT_LSTM_BWD_PART) ? seq_ring_bytes_bwdp(B, H, U) : 0);
+  hipError_t e = hipMemsetAsync(ws, 0, zero, st);
   if (e != hipSuccess) return (int)e;
   unsigned* cnt = ws;
   unsigned* err = ws + 2 * (B / 16 + 1);
+  uint2* ring = (uint2*)((char*)ws + seq_ring_offset(B));
   const dim3 grid(2 * (B / S) * (H / U));
   const bf16 *dh = (const bf16*)dhseq, *wt = (const bf16*)whh_t, *gv = (const bf16*)gsv;
   int rc;
-  if (H == 256) rc = launch_bwd<256>(S, U, grid, st, dh, wt, gv, csv, (bf16*)dgates, cnt, err, B, T);
-  else if (H == 512) rc = launch_bwd<512>(S, U, grid, st, dh, wt, gv, csv, (bf16*)dgates, cnt, err, B, T);
-  else rc = launch_bwd<768>(S, U, grid, st, dh, wt, gv, csv, (bf16*)dgates, cnt, err, B, T);
+  if (H == 256) rc = launch_bwd<256>(S, U, grid, st, dh, wt, gv, csv, (bf16*)dgates, cnt, err, ring, B, T);
+  else if (H == 512) rc = launch_bwd<512>(S, U, grid, st, dh, wt, gv, csv, (bf16*)dgates, cnt, err, ring, B, T);
+  else rc = launch_bwd<768>(S, U, grid, st, dh, wt, gv, csv, (bf16*)dgates, cnt, err, ring, B, T);
   return seq_accum_status(ws, B, st, rc);
 }
 

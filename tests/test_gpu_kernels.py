@@ -1047,3 +1047,47 @@ def test_lstm_seq_fwd_handoff_forms_agree(BTH):
         L.call("crnn_set_option", L.OPT_LSTM_TILE, 0)
         L.call("crnn_set_option", L.OPT_LSTM_HANDOFF, 1)
     assert outs
+
+
+@pytest.mark.parametrize("BTH", [(256, 32, 512), (64, 20, 768), (32, 7, 256), (128, 9, 512), (16, 1, 256),
+                                 (48, 2, 768)])
+def test_lstm_seq_bwd_forms_agree(BTH):
+    """Persistent BPTT: the partial-sum form (CRNN_OPT_LSTM_BWD_PART = 1: each workgroup's
+    own dgates x its W_hh rows, bf16 partials handed off as tagged granules and summed in fp32)
+    against the dgates + counter form (0, default), for every tile the shape supports. The forms round
+    differently (bf16 partials vs bf16 dgates into an fp32 MFMA sum), so dgates agree to bf16
+    rounding accumulated over the steps; both finite, no timed-out wait, counters complete."""
+    L = _L()
+    B, T, H = BTH
+    g = torch.Generator().manual_seed(12)
+    whh = (torch.randn(2, 4 * H, H, generator=g) / H ** 0.5).to(DEV, torch.bfloat16)
+    whh_t = whh.transpose(1, 2).contiguous()
+    gsv = torch.rand(2, T, B, 4 * H, generator=g).to(DEV, torch.bfloat16)   # gate activations in (0, 1)
+    csv = (torch.randn(2, T, B, H, generator=g) * 0.5).to(DEV)
+    dh = (torch.randn(B, T, 2 * H, generator=g) * 0.5).to(DEV, torch.bfloat16)
+    st = L.stream_ptr()
+    n = 0
+    try:
+        for force in (1, 2, 3):
+            L.call("crnn_set_option", L.OPT_LSTM_TILE, force)
+            if not L.lib().crnn_lstm_seq_supported(L.dtype_code(torch.bfloat16), B, H):
+                continue
+            outs = {}
+            for part in (1, 0):
+                L.call("crnn_set_option", L.OPT_LSTM_BWD_PART, part)
+                dg = torch.full((2, T, B, 4 * H), 3.0, dtype=torch.bfloat16, device=DEV)
+                ws = torch.full((L.lib().crnn_lstm_seq_workspace(B) // 4,), 7, dtype=torch.int32, device=DEV)
+                L.call("crnn_lstm_seq_bwd", dh.data_ptr(), whh_t.data_ptr(), gsv.data_ptr(), csv.data_ptr(),
+                       dg.data_ptr(), ws.data_ptr(), B, T, H, st)
+                torch.cuda.synchronize()
+                S, U = seq_tile(B, H, 1)
+                assert int(ws[2 * (B // 16 + 1)].item()) == 0      # error word: no timed-out wait
+                assert int(ws[: 2 * (B // S)].min().item()) == H // U * T
+                assert torch.isfinite(dg.float()).all()
+                outs[part] = dg.float().cpu()
+            assert relerr(outs[1], outs[0]) < 1e-2, (BTH, force, relerr(outs[1], outs[0]))
+            n += 1
+    finally:
+        L.call("crnn_set_option", L.OPT_LSTM_TILE, 0)
+        L.call("crnn_set_option", L.OPT_LSTM_BWD_PART, 0)
+    assert n
