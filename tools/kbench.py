@@ -60,7 +60,8 @@ def main():
         y = torch.empty(a.batch, d.Ho, d.Wo, cs.co, device=dev, dtype=T)
         dy = torch.randn_like(y)
         dx = torch.empty_like(x)
-        rows = L.lib().crnn_conv_stat_rows(L.BF16, d)
+        # BN partial rows: sized for the smallest tile (an --opt variant may change the kernel's tile)
+        rows = max(L.lib().crnn_conv_stat_rows(L.BF16, d), 2 * ((a.batch * d.Ho * d.Wo + 63) // 64))
         ps = torch.empty(rows, cs.co, device=dev)
         pq = torch.empty(rows, cs.co, device=dev)
         need = L.lib().crnn_conv_wgrad_workspace(L.BF16, d)
