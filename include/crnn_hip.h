@@ -71,7 +71,10 @@ enum { CRNN_OPT_GEMM_STAGGER = 0,    /* 256-row conv GEMM: waves 4-7 one barrier
                                         of the fragment rows that read only zero padding (default) */
        CRNN_OPT_LSTM_BWD_PART = 12,  /* persistent BPTT: 1 = partial-sum form (own dgates x own W_hh rows, partials
                                         handed off as tagged granules), 0 = dgates + counter hand-off (default) */
-       CRNN_OPT_COUNT = 13 };
+       CRNN_OPT_LSTM_L2_HANDOFF = 13,  /* persistent BPTT (2: and forward): hand-off payload kept in the XCD's L2 (plain
+                                          stores) for groups verified (HW_REG_XCC_ID) to run on one XCD (1, default);
+                                          0 = always sc1 */
+       CRNN_OPT_COUNT = 14 };
 int crnn_set_option(int key, int value);
 
 /* ------------------------------------------------------------------ layout */

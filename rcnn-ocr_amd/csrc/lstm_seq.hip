@@ -79,6 +79,40 @@ __device__ __forceinline__ void seq_coords(int nsl, int nbs, int& d, int& bs, in
   d = id / (nsl * nbs);
 }
 
+// XCD-local hand-off (CRNN_OPT_LSTM_L2_HANDOFF = 1, default): true when every workgroup of this
+// (d, bs) group runs on this workgroup's XCD. Each workgroup's lane 0 publishes its XCC id
+// (HW_REG_XCC_ID + 1, relaxed agent-scope store) into a per-launch table (zeroed with the counters)
+// and polls its group's entries. HIP promises no placement, so it is checked, never assumed: on one
+// XCD the group's hand-off payload may be written with plain stores that keep the lines in that
+// XCD's L2, where the consumers' sc1 loads (L1-bypassing, L2-served) find them — an sc1 store drops
+// the line from L2 and makes every consumer read at the cross-XCD rate (MI355X_MICROARCH.md,
+// inter-workgroup visibility). Split groups keep the sc1 stores. Bounded wait (error word).
+__device__ __noinline__ bool seq_group_local(unsigned* tab, int gbase, int nsl, int ns, unsigned* err) {
+  __shared__ int flag;
+  if (threadIdx.x == 0) {
+    unsigned x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+    x = (x & 15u) + 1u;
+    __hip_atomic_store(tab + gbase + ns, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    bool same = true;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    for (int p = 0; p < nsl && same; ++p) {
+      unsigned v;
+      while ((v = __hip_atomic_load(tab + gbase + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0u) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > SEQ_TIMEOUT_TICKS) {
+          __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      same = v == x;
+    }
+    flag = same ? 1 : 0;
+  }
+  __syncthreads();
+  return flag != 0;
+}
+
 // ---------------------------------------------------------------- forward sweep
 // Workgroup = (direction, S samples, U units = 4U gate rows); wave w holds the K-quarter
 // [w*H/4, (w+1)*H/4) of the W_hh' slice (NJ = 4U/16 row fragments x KK k-steps) in VGPRs and
@@ -97,7 +131,7 @@ template <int H, int S, int U, bool TAG>
 __global__ __launch_bounds__(256) void lstm_seq_fwd_kernel(const bf16* __restrict__ xg, const bf16* __restrict__ whh,
                                                            bf16* hseq, bf16* __restrict__ gsv, float* __restrict__ csv,
                                                            unsigned* cnt, unsigned* err, uint2* ring, int B, int Tn,
-                                                           unsigned long long* stamps) {
+                                                           unsigned long long* stamps, unsigned* xtab) {
   constexpr int KW = H / 4, KK = KW / 32;
   constexpr int GR = 4 * U, NJ = GR / 16, MI = S / 16;
   constexpr int QB = MI * NJ / 4;   // blocks finalised per wave
@@ -132,6 +166,7 @@ __global__ __launch_bounds__(256) void lstm_seq_fwd_kernel(const bf16* __restric
   }
   const __amdgpu_buffer_rsrc_t rh = rsrc_of(hseq);
   const __amdgpu_buffer_rsrc_t rr = rsrc_of(ring);
+  const bool l2_handoff = TAG && xtab && seq_group_local(xtab, (d * nbs + bs) * nsl, nsl, ns, err);
   float cst[QB];
 #pragma unroll
   for (int q = 0; q < QB; ++q) cst[q] = 0.f;
@@ -273,8 +308,9 @@ __global__ __launch_bounds__(256) void lstm_seq_fwd_kernel(const bf16* __restric
         const u32x4 hv = __builtin_bit_cast(u32x4, *reinterpret_cast<const bf16x8*>(&htile[row][8 * (gp >> 1)]));
         const uint32_t tag = (uint32_t)(s + 1);
         const u32x4 v = (gp & 1) ? u32x4{hv[2], tag, hv[3], tag} : u32x4{hv[0], tag, hv[1], tag};
-        __builtin_amdgcn_raw_buffer_store_b128(
-            v, rr, (uint32_t)((((size_t)(s & 1) * B + b0 + row) * H + (d * H + ns * U + 4 * gp) / 2) * 8u), 0, 16);
+        const uint32_t ro = (uint32_t)((((size_t)(s & 1) * B + b0 + row) * H + (d * H + ns * U + 4 * gp) / 2) * 8u);
+        if (l2_handoff) __builtin_amdgcn_raw_buffer_store_b128(v, rr, ro, 0, 0);   // stays in the XCD's L2
+        else __builtin_amdgcn_raw_buffer_store_b128(v, rr, ro, 0, 16);            // sc1: written through
       }
       SEQ_STAMP(5);
       // h_t for the next layer / BPTT: plain stores, off the critical path
@@ -320,7 +356,7 @@ template <int H, int S, int U>
 __global__ __launch_bounds__(256) void lstm_seq_bwd_kernel(const bf16* __restrict__ dhseq, const bf16* __restrict__ whh_t,
                                                            const bf16* __restrict__ gsv, const float* __restrict__ csv,
                                                            bf16* dgates, unsigned* cnt, unsigned* err, int B, int Tn,
-                                                           unsigned long long* stamps) {
+                                                           unsigned long long* stamps, unsigned* xtab) {
   constexpr int KW = H, KK = KW / 32;
   constexpr int H4 = 4 * H, MI = S / 16, NU = U / 16, NBLK = MI * NU;
   static_assert(H % 32 == 0 && NBLK <= 4 && S % 16 == 0 && U % 16 == 0, "shape");
@@ -348,6 +384,9 @@ __global__ __launch_bounds__(256) void lstm_seq_bwd_kernel(const bf16* __restric
       }
   }
   const __amdgpu_buffer_rsrc_t rg = rsrc_of(dgates);
+  // dgates payload: plain stores + the drained counter when the group is on one XCD (the
+  // consumers' sc1 loads then hit the shared L2), sc1 stores otherwise (seq_group_local)
+  const bool l2_handoff = xtab && seq_group_local(xtab, (d * nbs + bs) * nsl, nsl, ns, err);
   const bool fin = w < NBLK;
   const int fi = fin ? w % MI : 0, fj = fin ? w / MI : 0;
   const int bl = 16 * fi + c, b = b0 + bl;
@@ -440,8 +479,13 @@ __global__ __launch_bounds__(256) void lstm_seq_bwd_kernel(const bf16* __restric
       }
       SEQ_STAMP(4);
       const uint32_t go = (uint32_t)((((size_t)(d * Tn + t) * B + b) * H4 + 4 * u) * sizeof(bf16));
-      st_sc1(rg, go, out0);
-      st_sc1(rg, go + 16, out1);
+      if (l2_handoff) {   // the group is on one XCD: the lines stay in its L2
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, out0), rg, go, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, out1), rg, go + 16, 0, 0);
+      } else {
+        st_sc1(rg, go, out0);
+        st_sc1(rg, go + 16, out1);
+      }
     }
     SEQ_STAMP(5);
     seq_publish(mycnt);
@@ -661,35 +705,35 @@ bool seq_config(int B, int H, bool bwd, int& S, int& U) {
 
 template <int H, int S, int U>
 void launch_fwd_tile(bool tag, dim3 grid, hipStream_t st, const bf16* xg, const bf16* whh, bf16* hseq, bf16* gsv,
-                     float* csv, unsigned* cnt, unsigned* err, uint2* ring, int B, int T) {
+                     float* csv, unsigned* cnt, unsigned* err, uint2* ring, int B, int T, unsigned* xtab) {
   if (tag)
     hipLaunchKernelGGL((lstm_seq_fwd_kernel<H, S, U, true>), grid, dim3(256), 0, st, xg, whh, hseq, gsv, csv, cnt, err,
-                       ring, B, T, g_stamps);
+                       ring, B, T, g_stamps, xtab);
   else
     hipLaunchKernelGGL((lstm_seq_fwd_kernel<H, S, U, false>), grid, dim3(256), 0, st, xg, whh, hseq, gsv, csv, cnt,
-                       err, ring, B, T, g_stamps);
+                       err, ring, B, T, g_stamps, nullptr);
 }
 
 template <int H>
 int launch_fwd(int S, int U, dim3 grid, hipStream_t st, const bf16* xg, const bf16* whh, bf16* hseq, bf16* gsv,
-               float* csv, unsigned* cnt, unsigned* err, uint2* ring, int B, int T) {
+               float* csv, unsigned* cnt, unsigned* err, uint2* ring, int B, int T, unsigned* xtab) {
   const bool tag = crnn_option(CRNN_OPT_LSTM_HANDOFF) != 0;
   if constexpr (H <= 512) {  // 16 x 64 would spill at H = 768 (seq_config never picks it)
     if (S == 16 && U == 64) {
-      launch_fwd_tile<H, 16, 64>(tag, grid, st, xg, whh, hseq, gsv, csv, cnt, err, ring, B, T);
+      launch_fwd_tile<H, 16, 64>(tag, grid, st, xg, whh, hseq, gsv, csv, cnt, err, ring, B, T, xtab);
       return (int)hipGetLastError();
     }
   }
   if (S == 16)
-    launch_fwd_tile<H, 16, 32>(tag, grid, st, xg, whh, hseq, gsv, csv, cnt, err, ring, B, T);
+    launch_fwd_tile<H, 16, 32>(tag, grid, st, xg, whh, hseq, gsv, csv, cnt, err, ring, B, T, xtab);
   else
-    launch_fwd_tile<H, 32, 32>(tag, grid, st, xg, whh, hseq, gsv, csv, cnt, err, ring, B, T);
+    launch_fwd_tile<H, 32, 32>(tag, grid, st, xg, whh, hseq, gsv, csv, cnt, err, ring, B, T, xtab);
   return (int)hipGetLastError();
 }
 
 template <int H>
 int launch_bwd(int S, int U, dim3 grid, hipStream_t st, const bf16* dhseq, const bf16* whh_t, const bf16* gsv,
-               const float* csv, bf16* dg, unsigned* cnt, unsigned* err, uint2* ring, int B, int T) {
+               const float* csv, bf16* dg, unsigned* cnt, unsigned* err, uint2* ring, int B, int T, unsigned* xtab) {
   if (crnn_option(CRNN_OPT_LSTM_BWD_PART)) {
     if constexpr (H <= 512) {
       if (S == 16 && U == 64) {
@@ -708,14 +752,14 @@ int launch_bwd(int S, int U, dim3 grid, hipStream_t st, const bf16* dhseq, const
   }
   if constexpr (H <= 512) {
     if (S == 16 && U == 64) {
-      hipLaunchKernelGGL((lstm_seq_bwd_kernel<H, 16, 64>), grid, dim3(256), 0, st, dhseq, whh_t, gsv, csv, dg, cnt, err, B, T, g_stamps);
+      hipLaunchKernelGGL((lstm_seq_bwd_kernel<H, 16, 64>), grid, dim3(256), 0, st, dhseq, whh_t, gsv, csv, dg, cnt, err, B, T, g_stamps, xtab);
       return (int)hipGetLastError();
     }
   }
   if (S == 16)
-    hipLaunchKernelGGL((lstm_seq_bwd_kernel<H, 16, 32>), grid, dim3(256), 0, st, dhseq, whh_t, gsv, csv, dg, cnt, err, B, T, g_stamps);
+    hipLaunchKernelGGL((lstm_seq_bwd_kernel<H, 16, 32>), grid, dim3(256), 0, st, dhseq, whh_t, gsv, csv, dg, cnt, err, B, T, g_stamps, xtab);
   else
-    hipLaunchKernelGGL((lstm_seq_bwd_kernel<H, 32, 32>), grid, dim3(256), 0, st, dhseq, whh_t, gsv, csv, dg, cnt, err, B, T, g_stamps);
+    hipLaunchKernelGGL((lstm_seq_bwd_kernel<H, 32, 32>), grid, dim3(256), 0, st, dhseq, whh_t, gsv, csv, dg, cnt, err, B, T, g_stamps, xtab);
   return (int)hipGetLastError();
 }
 
@@ -754,7 +798,10 @@ int crnn_lstm_seq_debug_stamps(unsigned long long* buf) {
 // then (from byte seq_ring_offset) the granule ring shared by the sweeps (one runs at a time on the
 // stream): the forward's 2 x B x H 8-byte granules, or the partial-sum BPTT's
 // 2 slots x 2 d x B x (H/U) x H 4-byte value positions (sized for H = 768 with U = 32, the largest)
-static size_t seq_ring_offset(int B) { return (size_t)((2 * (B / 16 + 1) + 1 + 63) / 64 * 256); }
+// then (from byte seq_tab_offset, zeroed with the counters) the XCC table of seq_group_local: one
+// word per workgroup of the grid (<= the CU count; 1024 words)
+static size_t seq_tab_offset(int B) { return (size_t)((2 * (B / 16 + 1) + 1 + 63) / 64 * 256); }
+static size_t seq_ring_offset(int B) { return seq_tab_offset(B) + 4096; }
 static size_t seq_ring_bytes_bwdp(int B, int H, int U) { return (size_t)2 * 2 * B * (H / U) * H * 4; }
 static size_t seq_ring_bytes(int B) {
   const size_t f = (size_t)2 * B * 768 * 8, p = seq_ring_bytes_bwdp(B, 768, 32);
@@ -784,11 +831,15 @@ int crnn_lstm_seq_fwd(const void* xg, const void* whh, void* hseq, void* gsv, fl
   unsigned* err = ws + 2 * (B / 16 + 1);
   uint2* ring = (uint2*)((char*)ws + seq_ring_offset(B));
   const dim3 grid(2 * (B / S) * (H / U));
+  if (grid.x > 1024) return crnn_set_error(hipErrorInvalidValue, "lstm_seq: grid exceeds the XCC table");
+  // the forward's granule hand-off gains ~1 % from the XCD-local form, less than the check costs
+  // (one extra group hand-off per launch): only the BPTT, whose gather is 4x larger, uses it
+  unsigned* xtab = crnn_option(CRNN_OPT_LSTM_L2_HANDOFF) > 1 ? (unsigned*)((char*)ws + seq_tab_offset(B)) : nullptr;
   const bf16 *x = (const bf16*)xg, *w = (const bf16*)whh;
   int rc;
-  if (H == 256) rc = launch_fwd<256>(S, U, grid, st, x, w, (bf16*)hseq, (bf16*)gsv, csv, cnt, err, ring, B, T);
-  else if (H == 512) rc = launch_fwd<512>(S, U, grid, st, x, w, (bf16*)hseq, (bf16*)gsv, csv, cnt, err, ring, B, T);
-  else rc = launch_fwd<768>(S, U, grid, st, x, w, (bf16*)hseq, (bf16*)gsv, csv, cnt, err, ring, B, T);
+  if (H == 256) rc = launch_fwd<256>(S, U, grid, st, x, w, (bf16*)hseq, (bf16*)gsv, csv, cnt, err, ring, B, T, xtab);
+  else if (H == 512) rc = launch_fwd<512>(S, U, grid, st, x, w, (bf16*)hseq, (bf16*)gsv, csv, cnt, err, ring, B, T, xtab);
+  else rc = launch_fwd<768>(S, U, grid, st, x, w, (bf16*)hseq, (bf16*)gsv, csv, cnt, err, ring, B, T, xtab);
   return seq_accum_status(ws, B, st, rc);
 }
 
@@ -805,11 +856,13 @@ int crnn_lstm_seq_bwd(const void* dhseq, const void* whh_t, const void* gsv, con
   unsigned* err = ws + 2 * (B / 16 + 1);
   uint2* ring = (uint2*)((char*)ws + seq_ring_offset(B));
   const dim3 grid(2 * (B / S) * (H / U));
+  if (grid.x > 1024) return crnn_set_error(hipErrorInvalidValue, "lstm_seq: grid exceeds the XCC table");
+  unsigned* xtab = crnn_option(CRNN_OPT_LSTM_L2_HANDOFF) ? (unsigned*)((char*)ws + seq_tab_offset(B)) : nullptr;
   const bf16 *dh = (const bf16*)dhseq, *wt = (const bf16*)whh_t, *gv = (const bf16*)gsv;
   int rc;
-  if (H == 256) rc = launch_bwd<256>(S, U, grid, st, dh, wt, gv, csv, (bf16*)dgates, cnt, err, ring, B, T);
-  else if (H == 512) rc = launch_bwd<512>(S, U, grid, st, dh, wt, gv, csv, (bf16*)dgates, cnt, err, ring, B, T);
-  else rc = launch_bwd<768>(S, U, grid, st, dh, wt, gv, csv, (bf16*)dgates, cnt, err, ring, B, T);
+  if (H == 256) rc = launch_bwd<256>(S, U, grid, st, dh, wt, gv, csv, (bf16*)dgates, cnt, err, ring, B, T, xtab);
+  else if (H == 512) rc = launch_bwd<512>(S, U, grid, st, dh, wt, gv, csv, (bf16*)dgates, cnt, err, ring, B, T, xtab);
+  else rc = launch_bwd<768>(S, U, grid, st, dh, wt, gv, csv, (bf16*)dgates, cnt, err, ring, B, T, xtab);
   return seq_accum_status(ws, B, st, rc);
 }
 

@@ -1091,3 +1091,46 @@ def test_lstm_seq_bwd_forms_agree(BTH):
         L.call("crnn_set_option", L.OPT_LSTM_TILE, 0)
         L.call("crnn_set_option", L.OPT_LSTM_BWD_PART, 0)
     assert n
+
+
+@pytest.mark.parametrize("BTH", [(256, 32, 512), (64, 20, 768), (32, 7, 256), (16, 1, 256), (48, 2, 768)])
+def test_lstm_seq_l2_handoff_identical(BTH):
+    """Persistent BiLSTM sweeps with the XCD-local hand-off (CRNN_OPT_LSTM_L2_HANDOFF = 1, default:
+    plain payload stores for groups verified to share an XCD) and with write-through sc1 stores (0):
+    the same arithmetic, so h, the saved gates, the cell states and the BPTT dgates are bit-identical;
+    no timed-out wait, counters complete."""
+    L = _L()
+    B, T, H = BTH
+    g = torch.Generator().manual_seed(13)
+    xg = (torch.randn(B, T, 2, 4 * H, generator=g) * 0.7).to(DEV, torch.bfloat16)
+    whh = (torch.randn(2, 4 * H, H, generator=g) / H ** 0.5).to(DEV, torch.bfloat16)
+    whh_t = whh.transpose(1, 2).contiguous()
+    dh = (torch.randn(B, T, 2 * H, generator=g) * 0.5).to(DEV, torch.bfloat16)
+    st = L.stream_ptr()
+    outs = {}
+    try:
+        for l2 in (2, 0):   # 2: the forward too (1, the default, uses it in the BPTT only)
+            L.call("crnn_set_option", L.OPT_LSTM_L2_HANDOFF, l2)
+            hseq = torch.full((B, T, 2 * H), 3.0, dtype=torch.bfloat16, device=DEV)
+            gsv = torch.full((2, T, B, 4 * H), 3.0, dtype=torch.bfloat16, device=DEV)
+            csv = torch.full((2, T, B, H), 3.0, device=DEV)
+            dg = torch.full((2, T, B, 4 * H), 3.0, dtype=torch.bfloat16, device=DEV)
+            ws = torch.full((L.lib().crnn_lstm_seq_workspace(B) // 4,), 7, dtype=torch.int32, device=DEV)
+            L.call("crnn_lstm_seq_fwd", xg.data_ptr(), whh.data_ptr(), hseq.data_ptr(), gsv.data_ptr(),
+                   csv.data_ptr(), ws.data_ptr(), B, T, H, st)
+            torch.cuda.synchronize()
+            assert int(ws[2 * (B // 16 + 1)].item()) == 0
+            S, U = seq_tile(B, H)
+            assert int(ws[: 2 * (B // S)].min().item()) == H // U * T
+            L.call("crnn_lstm_seq_bwd", dh.data_ptr(), whh_t.data_ptr(), gsv.data_ptr(), csv.data_ptr(),
+                   dg.data_ptr(), ws.data_ptr(), B, T, H, st)
+            torch.cuda.synchronize()
+            assert int(ws[2 * (B // 16 + 1)].item()) == 0
+            S, U = seq_tile(B, H, 1)
+            assert int(ws[: 2 * (B // S)].min().item()) == H // U * T
+            outs[l2] = (hseq, gsv, csv, dg)
+    finally:
+        L.call("crnn_set_option", L.OPT_LSTM_L2_HANDOFF, 1)
+    for x, y in zip(outs[2], outs[0]):
+        assert torch.isfinite(x.float()).all()
+        assert torch.equal(x, y), BTH
