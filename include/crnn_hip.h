@@ -74,7 +74,9 @@ enum { CRNN_OPT_GEMM_STAGGER = 0,    /* 256-row conv GEMM: waves 4-7 one barrier
        CRNN_OPT_LSTM_L2_HANDOFF = 13,  /* persistent BPTT (2: and forward): hand-off payload kept in the XCD's L2 (plain
                                           stores) for groups verified (HW_REG_XCC_ID) to run on one XCD (1, default);
                                           0 = always sc1 */
-       CRNN_OPT_COUNT = 14 };
+       CRNN_OPT_GEMM4W = 14,         /* 256-row GEMM family: 1 = the 4-wave form (one wave per SIMD, 128 x BN/2
+                                        per wave, fragments double-buffered in registers), 0 = the 8-wave form */
+       CRNN_OPT_COUNT = 15 };
 int crnn_set_option(int key, int value);
 
 /* ------------------------------------------------------------------ layout */

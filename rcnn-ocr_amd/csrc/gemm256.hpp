@@ -27,9 +27,13 @@
 #include "gemm.hpp"
 
 #include <type_traits>
+#include <utility>
 #include "crnn_hip.h"
 int crnn_option(int key);  // capi.cpp (crnn_set_option)
 int crnn_cu_count();       // capi.cpp: compute units of the current device (cached)
+#ifndef GEMM_GROUP_M
+#define GEMM_GROUP_M 8   // grouped tile order (launch kernels below); 0 = plain row-major tile order
+#endif
 
 namespace gemm {
 
@@ -48,6 +52,22 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds_seg, u
 __device__ __forceinline__ void lds_wait_all() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
+}
+
+// lgkmcnt(0) the compiler's waitcnt pass knows about (an inline-asm wait is opaque to it, so it
+// would still count the waited reads as outstanding and add its own, later, waits)
+__device__ __forceinline__ void lds_wait_all_known() {
+  __builtin_amdgcn_s_waitcnt(0xC07F);   // gfx9 encoding: vmcnt 63, expcnt 7, lgkmcnt 0
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// compile-time loop: f(integral_constant<int, i>) for i = 0 .. N-1
+template <class F, int... I>
+__device__ __forceinline__ void sfor_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F> __device__ __forceinline__ void sfor(F&& f) {
+  sfor_impl(f, std::make_integer_sequence<int, N>{});
 }
 
 __device__ __forceinline__ void raw_barrier() {
@@ -100,9 +120,10 @@ __device__ __forceinline__ void wave_col_stats(const f32x4 (&acc)[MI][NI], const
 //    8g+4+q (hi): a lane then holds k = 8g..8g+7 — the same k map as a K-contiguous ds_read_b128,
 //    so mixed operands need no permuted (bank-conflicting) 8-byte reads. fsw keeps the 32 lanes
 //    of each read pass on distinct banks for both R (checked by enumeration).
-template <class L, int R, int Q> struct Op256 {
+template <class L, int R, int Q, int NW = 8> struct Op256 {   // NW: waves of the workgroup
   static constexpr bool RV = L::kRowVec;
-  static constexpr int I = R / 128;        // DMA wave-instructions per wave per half-tile
+  static constexpr int I = R * 8 / (128 * NW);  // DMA wave-instructions per wave per half-tile
+  static constexpr int kR = R, kQ = Q;
   static constexpr int TB = R * 64 * 2;    // tile bytes
   static constexpr int HB = TB / 2;
   typename L::Ctx ctx[2][I];
@@ -368,7 +389,14 @@ __global__ __launch_bounds__(512) void gemm256_kernel(LA la, LB lb, EPI epi, int
   // one work item per block: ((batch * nsplit + split) * tiles_m + m_tile) * tiles_n + n_tile
   const int nwg = tiles_m * tiles_n * nsplit * nbatch;
   const int wg = xcd_remap(blockIdx.x, nwg);
-  const int n_tile = wg % tiles_n, m_tile = (wg / tiles_n) % tiles_m, kz = (wg / (tiles_n * tiles_m)) % nsplit;
+  int n_tile = wg % tiles_n, m_tile = (wg / tiles_n) % tiles_m;
+  const int kz = (wg / (tiles_n * tiles_m)) % nsplit;
+  if constexpr (GEMM_GROUP_M > 0) {   // grouped tile order: GEMM_GROUP_M m-tiles share each n sweep (L2 reuse)
+    const int pid = wg % (tiles_n * tiles_m), per = GEMM_GROUP_M * tiles_n, g0 = (pid / per) * GEMM_GROUP_M;
+    const int gs = min(tiles_m - g0, GEMM_GROUP_M);
+    m_tile = g0 + (pid % per) % gs;
+    n_tile = (pid % per) / gs;
+  }
   if (nbatch > 1) {
     const int bz = wg / (tiles_n * tiles_m * nsplit);
     if constexpr (has_set_batch<LA>::value) la.set_batch(bz);
@@ -610,6 +638,229 @@ __global__ __launch_bounds__(512) void gemm256p_kernel(LA la, LB lb, EPI epi, in
   if (stagger && wr == 0) raw_barrier();
 }
 
+// 4-wave form helper: N fragments of one 32-deep k sub-step KK (see Op256::load), fragments
+// F0 .. F0+N-1 of quadrant half H
+template <class OP, int H, int N, int KK, int F0 = 0>
+__device__ __forceinline__ void load_kk(const OP& op, bf16x8* fr, const char* tile, uint32_t lds, int rb0, int lane) {
+  constexpr int R = OP::kR, Q = OP::kQ, HB = OP::HB;
+  if constexpr (!OP::RV) {
+#pragma unroll
+    for (int f = 0; f < N; ++f)
+      fr[f] = gemm::frag<bf16, R, false, false, 64>(reinterpret_cast<const bf16*>(tile), rb0 + H * Q + (F0 + f) * 16, KK, lane);
+  } else {
+    const uint32_t bl = lds + op.plo, bh = lds + op.phi;
+#pragma unroll
+    for (int f = 0; f < N; ++f) {
+      const uint32_t al = bl ^ (uint32_t)(32 * (F0 + f)), ah = bh ^ (uint32_t)(32 * (F0 + f));
+      fr[f] = OP::cat(OP::template trd<H * HB + KK * 32 * R>(al), OP::template trd<H * HB + KK * 32 * R>(ah));
+    }
+  }
+}
+
+// ---------------------------------------------------------------- 4-wave form (CRNN_OPT_GEMM4W)
+// Same tile, K-tile, LDS image and operand loaders as gemm256_item, with ONE wave per SIMD: 4 waves
+// as 2(M) x 2(N), each owning 128 x BN/2 (MI x NI = 8 x 8 fragments: all 256 AGPRs hold
+// accumulators, so the MFMAs are asm tied to their AGPRs — the builtin's untied form would rotate
+// them through VGPRs). The fragments of the two 32-deep k sub-steps live in two register sets
+// (F0, F1), so every LDS read and LDS-DMA issue runs in the shadow of MFMAs of the other set. Per
+// K-tile t (stage b = t & 1), S = 2 NM MFMA slots, one memory op after the MFMA of its slot:
+//   slots [0, NR)            read F1(t) from b (one fragment per slot)
+//   slot  B1 = NR + 8        lgkmcnt(0), s_barrier: every wave is done with stage b (WAR)
+//   slots [B1, V)            LDS-DMA of tile t+2 -> b, spread evenly
+//   slot  V = S - NR - 8     vmcnt(ND) [tile t+1, issued a K-tile earlier, landed], s_barrier (RAW)
+//   slots [V, V + NR)        read F0(t+1) from b^1
+// (r02j's 4-wave form read F1 and issued all DMA after one mid-tile barrier and waited for tile t+1
+// half a tile after issuing it: the waves waited 21 % of their cycles.) Measured equal to the
+// 8-wave form on this path (profiles/r02r_gemm4w_dma_study.log: the main-loop LDS-DMA issue stalls
+// on the memory side in both), so it stays an option, off by default.
+template <int BM, int BN, int SKIP, class LA, class LB, class EPI>
+__device__ __forceinline__ void gemm4w_item(LA la, LB lb, EPI epi, int M, int K, int klen, int m_tile, int n_tile,
+                                            int kz, int ktk) {
+  static_assert(BM == 256 && (BN == 256 || BN == 128), "tile");
+  constexpr int KS = 64, NW = 4;
+  constexpr int WM = BM / 2, WN = BN / 2;        // per-wave output block (128 x 128 or 128 x 64)
+  constexpr int MI = WM / 16, NI = WN / 16;      // fragments per wave
+  constexpr int MQ = MI / 2, NQ = NI / 2;        // fragments per quadrant (LDS half)
+  constexpr int QM = WM / 2, QN = WN / 2;
+  using OA = Op256<LA, BM, QM, NW>;
+  using OB = Op256<LB, BN, QN, NW>;
+  constexpr int STAGE = OA::TB + OB::TB;
+  constexpr int NM = MI * NI, NR = MI + NI, NDA = 2 * OA::I, ND = NDA + 2 * OB::I;
+  constexpr int S = 2 * NM, B1 = NR + 8, V = S - NR - 8;
+  static_assert(B1 + ND <= V && V + NR <= S, "schedule");
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+
+  const int m0 = m_tile * BM, n0 = n_tile * BN;
+  const int kbeg = kz * klen, kend = min(K, kbeg + klen);
+  const int nk = kend > kbeg ? (kend - kbeg + KS - 1) / KS : 0;
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wid >> 1, wc = wid & 1;
+
+  OA oa;
+  OB ob;
+  oa.init(la, m0, wid, lane, wr);
+  ob.init(lb, n0, wid, lane, wc);
+  const __amdgpu_buffer_rsrc_t ra = la.rsrc(), rb = lb.rsrc();
+
+  f32x4 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // DMA wave-instruction d (< ND) of a tile into the stage at `stg`
+  auto dma = [&](auto dc, char* stg, const typename LA::Prep& pa, const typename LB::Prep& pb) {
+    constexpr int d = decltype(dc)::value;
+    if constexpr (d < NDA) {
+      constexpr int h = d / OA::I, i = d % OA::I;
+      dma16(ra, stg + oa.seg[h][i], la.offs(oa.ctx[h][i], pa, oa.kofs[h][i]));
+    } else {
+      constexpr int h = (d - NDA) / OB::I, i = (d - NDA) % OB::I;
+      dma16(rb, stg + OA::TB + ob.seg[h][i], lb.offs(ob.ctx[h][i], pb, ob.kofs[h][i]));
+    }
+  };
+  auto dma_tile = [&](int t, int buf) {
+    const typename LA::Prep pa = la.prep(kbeg + t * KS);
+    const typename LB::Prep pb = lb.prep(kbeg + t * KS);
+    sfor<ND>([&](auto dc) { dma(dc, smem + buf * STAGE, pa, pb); });
+  };
+  // fragment r (< NR: A rows, then B columns) of k sub-step KK from the stage at As
+  auto read_one = [&](auto rc, auto kkc, const char* As, bf16x8 (&af)[MI], bf16x8 (&bfr)[NI]) {
+    constexpr int r = decltype(rc)::value, KK = decltype(kkc)::value;
+    const char* Bs = As + OA::TB;
+    if constexpr (r < MI) {
+      load_kk<OA, r / MQ, 1, KK, r % MQ>(oa, af + r, As, lds_addr(As), wr * WM, lane);
+    } else {
+      constexpr int rr = r - MI;
+      load_kk<OB, rr / NQ, 1, KK, rr % NQ>(ob, bfr + rr, Bs, lds_addr(Bs), wc * WN, lane);
+    }
+  };
+
+  bf16x8 a0[MI], b0[NI], a1[MI], b1[NI];
+  if (nk > 0) {
+    dma_tile(0, 0);
+    dma_tile(min(1, nk - 1), 1);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(ND) : "memory");   // tile 0 landed
+    raw_barrier();
+    const char* As = smem;
+    sfor<NR>([&](auto rc) { read_one(rc, std::integral_constant<int, 0>{}, As, a0, b0); });
+  }
+  // Past the last K-tile the DMA re-fetches tile nk-1 into the stage nobody reads again and the
+  // reads of F0(nk) fill registers nobody uses: no runtime guard inside the MFMA stream.
+  auto ktile = [&](auto fmc, int t) {
+    constexpr uint32_t FM = decltype(fmc)::value;
+    const int b = t & 1;
+    lds_wait_all_known();                               // F0(t) in registers
+    const int kn = kbeg + min(t + 2, nk - 1) * KS;
+    const typename LA::Prep pa = la.prep(kn);
+    const typename LB::Prep pb = lb.prep(kn);
+    const char* As = smem + b * STAGE;
+    const char* As1 = smem + (b ^ 1) * STAGE;
+    char* st = smem + b * STAGE;
+    __builtin_amdgcn_s_setprio(1);
+    sfor<S>([&](auto mc) {
+      constexpr int m = decltype(mc)::value;
+      constexpr int mm = m < NM ? m : m - NM, i = mm / NI, j = mm % NI;
+      if constexpr ((FM >> i) & 1u) {
+        if constexpr (m < NM)
+          asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(b0[j]), "v"(a0[i]));
+        else
+          asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(b1[j]), "v"(a1[i]));
+      }
+      if constexpr (m < NR) read_one(std::integral_constant<int, m>{}, std::integral_constant<int, 1>{}, As, a1, b1);
+      if constexpr (m == B1) {
+        lds_wait_all_known();                           // F1(t) in registers: done with stage b
+        raw_barrier();
+      }
+      sfor<ND>([&](auto dc) {
+        constexpr int d = decltype(dc)::value;
+        if constexpr (m == B1 + d * (V - B1) / ND) dma(dc, st, pa, pb);
+      });
+      if constexpr (m == V) {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"i"(ND) : "memory");   // tile t+1 landed (this wave)
+        raw_barrier();                                                // ... for every wave
+      }
+      if constexpr (m >= V && m < V + NR)
+        read_one(std::integral_constant<int, m - V>{}, std::integral_constant<int, 0>{}, As1, a0, b0);
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    __builtin_amdgcn_s_setprio(0);
+  };
+  // asm MFMAs are invisible to hipcc's hazard padding: the accumulator zeroing must be 2+ wait
+  // states ahead of the first MFMA reading it
+  asm volatile("s_nop 4" ::);
+  __builtin_amdgcn_sched_barrier(0);
+  if constexpr (SKIP == 0) {
+    for (int t = 0; t < nk; ++t) ktile(std::integral_constant<uint32_t, 0xffu>{}, t);
+  } else {   // gemm256_item: compile-time padding-row segments of 4-row maps
+    constexpr uint32_t M0 = SKIP == 1 ? 0xfcu : 0x3fu, M2 = SKIP == 1 ? 0x3fu : 0xfcu;
+    const int e0 = min(nk, ktk), e1 = min(nk, 2 * ktk);
+    int t = 0;
+    for (; t < e0; ++t) ktile(std::integral_constant<uint32_t, M0>{}, t);
+    for (; t < e1; ++t) ktile(std::integral_constant<uint32_t, 0xffu>{}, t);
+    for (; t < nk; ++t) ktile(std::integral_constant<uint32_t, M2>{}, t);
+  }
+  // ... and the last MFMA's result 11+ wait states (8-pass XDL) ahead of its first VALU / LDS read
+  asm volatile("s_nop 15\n\ts_nop 15" ::);
+  __builtin_amdgcn_sched_barrier(0);
+
+  const int mr = lane & 15, nq = 4 * (lane >> 4);
+  if constexpr (!EPI::kStats && !has_tile_hook<EPI>::value) {
+    // through wave-private LDS (MI/2 fragment rows at a time): a rolled store loop instead of an
+    // unrolled epilogue over 64 register fragments, whose pressure would spill the accumulators
+    constexpr int RH = MI / 2;
+    static_assert(NW * RH * NI * 64 * 16 <= 2 * STAGE, "epilogue LDS");
+    f32x4* ws = reinterpret_cast<f32x4*>(smem) + wid * RH * NI * 64 + lane;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the re-fetch DMA past the last K-tile
+    lds_wait_all_known();
+    raw_barrier();                                      // every wave is done with the operand tiles
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+      for (int i = 0; i < RH; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j) ws[(i * NI + j) * 64] = acc[h * RH + i][j];
+#pragma unroll 1
+      for (int f = 0; f < RH * NI; ++f) {
+        const f32x4 v = ws[f * 64];
+        const int i = h * RH + f / NI, j = f % NI;
+        epi.store(m0 + wr * WM + i * 16 + mr, n0 + wc * WN + j * 16 + nq, v, kz);
+      }
+    }
+    return;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) epi.store(m0 + wr * WM + i * 16 + mr, n0 + wc * WN + j * 16 + nq, acc[i][j], kz);
+  if constexpr (EPI::kStats) wave_col_stats<MI, NI>(acc, epi, M, m0 + wr * WM, m_tile * 2 + wr, n0 + wc * WN, lane);
+  if constexpr (has_tile_hook<EPI>::value) epi.template tile<MI, NI>(acc, M, m0 + wr * WM, m_tile * 2 + wr, n0 + wc * WN, lane);
+}
+
+template <int BM, int BN, int SKIP, class LA, class LB, class EPI>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm4w_kernel(
+    LA la, LB lb, EPI epi, int M, int N, int K, int klen, int tiles_m, int tiles_n, int nsplit, int nbatch, int ktk) {
+  const int nwg = tiles_m * tiles_n * nsplit * nbatch;
+  const int wg = xcd_remap(blockIdx.x, nwg);
+  int n_tile = wg % tiles_n, m_tile = (wg / tiles_n) % tiles_m;
+  const int kz = (wg / (tiles_n * tiles_m)) % nsplit;
+  if constexpr (GEMM_GROUP_M > 0) {   // grouped tile order: GEMM_GROUP_M m-tiles share each n sweep (L2 reuse)
+    const int pid = wg % (tiles_n * tiles_m), per = GEMM_GROUP_M * tiles_n, g0 = (pid / per) * GEMM_GROUP_M;
+    const int gs = min(tiles_m - g0, GEMM_GROUP_M);
+    m_tile = g0 + (pid % per) % gs;
+    n_tile = (pid % per) / gs;
+  }
+  if (nbatch > 1) {
+    const int bz = wg / (tiles_n * tiles_m * nsplit);
+    if constexpr (has_set_batch<LA>::value) la.set_batch(bz);
+    if constexpr (has_set_batch<LB>::value) lb.set_batch(bz);
+    if constexpr (has_set_batch<EPI>::value) epi.set_batch(bz);
+  }
+  gemm4w_item<BM, BN, SKIP>(la, lb, epi, M, K, klen, m_tile, n_tile, kz, ktk);
+}
+
 // nsplit: split-K factor (K ranges of split_len(K, nsplit), multiples of 64)
 // nbatch: independent GEMMs of one shape in one launch (loaders / epilogue with set_batch(int))
 // SKIP (1: conv fwd, 2: stride-1 dgrad, 3x3 over 4-row maps of 128 pixels; nsplit 1): the
@@ -624,6 +875,11 @@ inline int launch256(const LA& la, const LB& lb, const EPI& epi, int M, int N, i
   const int items = tm * tn * nsplit * nbatch;
   const int ncu = crnn_cu_count();
   const int popt = crnn_option(CRNN_OPT_GEMM_PERSISTENT);   // 1: when items > CUs, 2: always
+  if (crnn_option(CRNN_OPT_GEMM4W)) {
+    hipLaunchKernelGGL((gemm4w_kernel<BM, BN, SKIP, LA, LB, EPI>), dim3(items), dim3(256), 0, st, la, lb, epi, M, N, K,
+                       klen, tm, tn, nsplit, nbatch, ktk);
+    return (int)hipGetLastError();
+  }
   if (SKIP == 0 && ((popt == 1 && items > ncu) || popt == 2)) {
     hipLaunchKernelGGL((gemm256p_kernel<BM, BN, LA, LB, EPI>), dim3(items < ncu ? items : ncu), dim3(512), 0, st, la,
                        lb, epi, M, N, K, klen, tm, tn, nsplit, crnn_option(CRNN_OPT_GEMM_STAGGER), nbatch);

@@ -190,6 +190,28 @@ def test_conv_fwd_dgrad_wgrad(cfg, dtype):
                 assert float((a - b).abs().max()) <= 2 ** -7 * float(b.abs().max()) and relerr(a, b) < 2e-3
             # BN partials: the partial grouping may change with the tile (sums agree to fp32 order)
             assert relerr(outs[0][2], outs[1][2]) < 1e-5
+        # the 4-wave form of the 256-row GEMM (CRNN_OPT_GEMM4W): the same fragments, K order, split-K
+        # and per-wave statistic rows as the 8-wave form, so the same bits
+        outs = []
+        for v in (1, 0):
+            L.call("crnn_set_option", L.OPT_GEMM4W, v)
+            try:
+                y2 = torch.empty_like(yd)
+                ps2, pq2 = torch.zeros_like(ps), torch.zeros_like(pq)
+                L.call("crnn_conv_fwd", dt, d, xd.data_ptr(), wd.data_ptr(), y2.data_ptr(), ps2.data_ptr(),
+                       pq2.data_ptr(), st)
+                dx2 = torch.zeros(B, H, W, Cip, dtype=dtype, device=DEV)
+                if Ci % 8 == 0:
+                    L.call("crnn_conv_dgrad", dt, d, dyd.data_ptr(), wd.data_ptr(), dx2.data_ptr(), None, None, 0, st)
+                dw2 = torch.empty_like(dw)
+                L.call("crnn_conv_wgrad", dt, d, dyd.data_ptr(), xd.data_ptr(), dw2.data_ptr(), ws.data_ptr(), need,
+                       0.0, st)
+                torch.cuda.synchronize()
+                outs.append((y2, dx2, dw2, ps2, pq2))
+            finally:
+                L.call("crnn_set_option", L.OPT_GEMM4W, 0)
+        for a, b in zip(*outs):
+            assert torch.equal(a, b), d
 
 
 def test_conv_halo_vs_gemm():
