@@ -161,6 +161,8 @@ class CRNNEngine:
         self._sticky_carry = 0
         self._status_host = None
         self._status_evt = None
+        self._side = None           # side stream of the running backward (wgrad_stream)
+        self._side_stream = None
         self.debug = False      # when set, backward keeps copies of block-boundary gradients
         self._last_partials = None  # (psum, rows, rows_per_partial) of the latest training-mode conv
         self._drop_seed = int(torch.initial_seed()) & 0xFFFFFFFFFFFFFFFF  # enc_dropout mask stream
@@ -317,6 +319,13 @@ class CRNNEngine:
     # persistent whole-sequence BiLSTM kernels (lstm_seq.hip): bf16, supported shapes only;
     # CRNN_LSTM_PER_STEP=1 forces the per-step launches (A/B and fallback coverage)
     use_seq = os.environ.get("CRNN_LSTM_PER_STEP", "0") != "1"
+    # conv weight gradients on a second stream (CRNN_WGRAD_STREAM, default 0): the wgrad GEMMs are
+    # off the dgrad chain's critical path, so they overlap the chain's HBM-bound BN / SE backward
+    # passes and fill its GEMMs' last rounds of tiles. Each wgrad's input gradient then gets a
+    # buffer of its own (no rotation), and the compute stream joins the side stream before
+    # backward() returns. Measured (profiles/r02t_wgrad_side_stream_ab.log): the two streams
+    # time-share the CUs, the wgrad launches take twice as long, and the step gains 0.4 %, so off.
+    wgrad_stream = os.environ.get("CRNN_WGRAD_STREAM", "0") == "1"
 
     def _seq_ok(self, B):
         return self.use_seq and bool(L.lib().crnn_lstm_seq_supported(self.dt, B, self.H))
@@ -646,7 +655,23 @@ class CRNNEngine:
         call("crnn_bn_bwd_apply", self.dt, d, ptr(mg), ptr(mgx), ptr(out), s)
         return out
 
+    def _dz(self, tag, scratch, n):
+        """the BN-backward output that a conv's dgrad AND wgrad read: a view of the rotating scratch
+        buffer, or (wgrads on the side stream) a buffer of its own, so the dgrad chain cannot
+        overwrite it before the side stream has read it"""
+        if self._side is None:
+            return scratch[:n]
+        return self.ws.get("g.dz." + tag, (n,), self.dtype)
+
     def _wgrad(self, cs: ConvSpec, dz, x, b, h, w):
+        if self._side is not None:
+            # ordered after everything the compute stream has enqueued so far (dz's producer)
+            self._side.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(self._side):
+                return self._wgrad_launch(cs, dz, x, b, h, w)
+        return self._wgrad_launch(cs, dz, x, b, h, w)
+
+    def _wgrad_launch(self, cs: ConvSpec, dz, x, b, h, w):
         d = cs.desc(b, h, w)
         need = L.lib().crnn_conv_wgrad_workspace(self.dt, d)
         wsb = self.ws.get("wgrad.ws", (self._wg_cap,), torch.float32)
@@ -689,8 +714,24 @@ class CRNNEngine:
         denc: instead of dlogits, d loss / d encoder output [B,T,hidden] (fp32; the attention
         decoder's backward, crnn_hip/attn.py) — the CTC head is skipped (its grads are zeroed
         unless accumulating)."""
-        done = stage_done if stage_done is not None else (lambda prefixes: None)
         sv = self._saved
+        self._side = None
+        if self.wgrad_stream:
+            if self._side_stream is None:
+                self._side_stream = torch.cuda.Stream(self.device)
+            self._side = self._side_stream
+        if stage_done is None:
+            done = lambda prefixes: None  # noqa: E731
+        elif self._side is None:
+            done = stage_done
+        else:
+            def done(prefixes):
+                # the stage's weight gradients come from the side stream, its BN / SE ones from
+                # the compute stream: issue the hook (an all-reduce orders itself after the
+                # caller's current stream) on the side stream once it has caught up with both
+                self._side.wait_stream(torch.cuda.current_stream(self.device))
+                with torch.cuda.stream(self._side):
+                    stage_done(prefixes)
         if sv is None:
             raise RuntimeError("forward(save_for_backward=True) must precede backward")
         self.g = grads
@@ -714,7 +755,12 @@ class CRNNEngine:
             self._head_backward(dlogits, grads, acc, dx)
         if sv["drop"] is not None:  # enc_dropout backward: the forward's mask, from its seed
             call("crnn_dropout", dt, ptr(dx), ptr(dx), M * Hd, sv["drop"][0], sv["drop"][1], s)
-        self._backward_encoder(dx, grads, acc, done)
+        try:
+            self._backward_encoder(dx, grads, acc, done)
+        finally:
+            if self._side is not None:
+                torch.cuda.current_stream(self.device).wait_stream(self._side)
+                self._side = None
         self.poll_status()
 
     def _head_backward(self, dlogits, grads, acc, dx):
@@ -796,14 +842,14 @@ class CRNNEngine:
         else:
             dyf = bufA[: B * h3 * w3 * 512].view(B, h3, w3, 512)
             call("crnn_hpool_bwd", dt, ptr(dseq), ptr(dyf), B, h3, w3, 512, s)
-        dz = bufB[: B * h3 * w3 * 512]
+        dz = self._dz("co1", bufB, B * h3 * w3 * 512)
         self._bn_bwd(1, dyf, co["z1"], (co["m1"], co["i1"], co["sc1"], co["sh1"]), self.co1.bn, B * h3 * w3, 512,
                      out=dz, accumulate_params=accumulate)
         self._wgrad(self.co1, dz, co["a0"], B, co["h2"], co["w2"])
         da = bufC[: B * co["h2"] * co["w2"] * 512]
         self._conv_call("dgrad", self.conv_flops(self.co1, B, co["h2"], co["w2"]), "crnn_conv_dgrad", dt, self.co1.desc(B, co["h2"], co["w2"]), ptr(dz), ptr(self.packed[self.co1.name]),
              ptr(da), None, None, 0, s)
-        dz0 = bufA[: B * co["h2"] * co["w2"] * 512]
+        dz0 = self._dz("co0", bufA, B * co["h2"] * co["w2"] * 512)
         self._bn_bwd(1, da, co["z0"], (co["m0"], co["i0"], co["sc0"], co["sh0"]), self.co0.bn,
                      B * co["h2"] * co["w2"], 512, out=dz0, accumulate_params=accumulate)
         self._wgrad(self.co0, dz0, co["x"], B, co["h"], co["w"])
@@ -839,7 +885,7 @@ class CRNNEngine:
                  ptr(self.p[blk.prefix + ".se.fc.0.weight"]), ptr(self.p[blk.prefix + ".se.fc.2.weight"]),
                  ptr(dsig), ptr(dhid), ptr(dpool), ptr(self._gview(blk.prefix + ".se.fc.0.weight")),
                  ptr(self._gview(blk.prefix + ".se.fc.2.weight")), B, P, Cr, HW, acc, s)
-            dz2 = bufs[o1][: Mo * P]
+            dz2 = self._dz(f"b{bi}.c2", bufs[o1], Mo * P)
             self._bn_bwd(3, dyb, sb["z2"], (sb["m2"], sb["i2"], sb["sc2"], sb["sh2"]), blk.conv2.bn, Mo, P, HW=HW,
                          y=sb["y"], se=sb["s"], dpool=dpool, out=dz2, accumulate_params=accumulate,
                          se_abc=(abc, B))
@@ -859,7 +905,7 @@ class CRNNEngine:
             else:
                 self._conv_call("dgrad", self.conv_flops(blk.conv2, B, ho, wo), "crnn_conv_dgrad", dt, d2, ptr(dz2),
                                 ptr(self.packed[blk.conv2.name]), ptr(da1), None, None, 0, s)
-            dz1 = bufs[o1][: Mo * P]
+            dz1 = self._dz(f"b{bi}.c1", bufs[o1], Mo * P)
             self._bn_bwd(1, da1, sb["z1"], (sb["m1"], sb["i1"], sb["sc1"], sb["sh1"]), blk.conv1.bn, Mo, P,
                          out=dz1, accumulate_params=accumulate, sums=sums)
             self._wgrad(blk.conv1, dz1, sb["x"], B, h, w)
@@ -873,7 +919,7 @@ class CRNNEngine:
                 self._conv_call("dgrad", self.conv_flops(blk.conv1, B, h, w), "crnn_conv_dgrad", dt, blk.conv1.desc(B, h, w), ptr(dz1), ptr(self.packed[blk.conv1.name]),
                      ptr(dxb), None, None, 0, s)
                 dsv = sb["ds"]
-                dzd = bufs[o1][: Mo * P]
+                dzd = self._dz(f"b{bi}.ds", bufs[o1], Mo * P)
                 self._bn_bwd(2, dyb, dsv["zd"], (dsv["m"], dsv["i"], dsv["sc"], dsv["sh"]), blk.ds.bn, Mo, P,
                              y=sb["y"], out=dzd, accumulate_params=accumulate)
                 self._wgrad(blk.ds, dzd, sb["x"], B, h, w)
@@ -889,14 +935,14 @@ class CRNNEngine:
         h1, w1 = st["h1"], st["w1"]
         # BN -> ReLU -> MaxPool backward in one pass pair (CRNN_BNG_POOL: the pooled gradient is
         # routed to each window's first maximum inside the BN-backward reduce / apply kernels)
-        dz1 = bufs[o2][: B * h1 * w1 * 128]
+        dz1 = self._dz("s1", bufs[o2], B * h1 * w1 * 128)
         self._bn_bwd(4, dp, st["z1"], (st["m1"], st["i1"], st["sc1"], st["sh1"]), self.stem1.bn, B * h1 * w1, 128,
                      HW=w1, out=dz1, accumulate_params=accumulate)
         self._wgrad(self.stem1, dz1, st["a0"], B, h1, w1)
         da0 = bufs[o1][: B * h1 * w1 * 64]
         self._conv_call("dgrad", self.conv_flops(self.stem1, B, h1, w1), "crnn_conv_dgrad", dt, self.stem1.desc(B, h1, w1), ptr(dz1), ptr(self.packed[self.stem1.name]),
              ptr(da0), None, None, 0, s)
-        dz0 = bufs[cur][: B * h1 * w1 * 64]
+        dz0 = self._dz("s0", bufs[cur], B * h1 * w1 * 64)
         self._bn_bwd(1, da0, st["z0"], (st["m0"], st["i0"], st["sc0"], st["sh0"]), self.stem0.bn, B * h1 * w1, 64,
                      out=dz0, accumulate_params=accumulate)
         self._wgrad(self.stem0, dz0, st["x0"], B, st["H"], st["W"])

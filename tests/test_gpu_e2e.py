@@ -291,6 +291,36 @@ def test_train_step_bf16_runs_and_descends():
     assert losses[-1] < losses[0]
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_wgrad_side_stream_bit_identical(dtype):
+    """conv weight gradients on the side stream (CRNNEngine.wgrad_stream) give exactly the
+    gradients of the one-stream backward, over two steps (the second overwrites the first's
+    buffers while the side stream may still lag behind the compute stream)."""
+    from crnn_hip.ctc import ctc_loss
+    from crnn_hip.recipe import recipe_state_dict, synthetic_batch
+    sd = recipe_state_dict(O.param_shapes(256, 194), 7)
+    model = build_model(sd, 256, dtype).train()
+    x, _, tg, tl = synthetic_batch(32, 32, 256, 32, 194, seed=21)
+    x = x.to(DEV)
+    out = []
+    for side in (False, True, False, True):
+        model(x)                       # build the engine
+        model._engine.wgrad_stream = side
+        model.zero_grad(set_to_none=True)
+        for _ in range(2):
+            model.zero_grad(set_to_none=True)
+            ctc_loss(model(x), tg, tl).backward()
+        out.append({k: p.grad.detach().clone() for k, p in model.named_parameters()})
+    for k in out[0]:
+        for o in out[1:]:
+            if k.startswith("cnn."):
+                assert torch.equal(out[0][k], o[k]), k
+            else:
+                # head / BiLSTM gradients (same stream either way); some sum with fp32 atomics
+                # (crnn_colsum, the fp32 BiLSTM weight gradients), so only to fp32 order
+                assert torch.allclose(out[0][k], o[k], rtol=1e-5, atol=1e-7), k
+
+
 def test_enc_dropout_train():
     """enc_dropout (model/model.py:201,220) in training: the head sees the encoder output with a
     Bernoulli(1 - p) mask scaled by 1/(1-p) (keep share within 4 sigma), the logits are the head
