@@ -63,6 +63,8 @@ _SIGS = {
     "crnn_pack_conv_weight": ([i32, vp, vp, i32, i32, i32, i32, i32, vp], i32),
     "crnn_pack_rows": ([i32, vp, vp, vp, i32, i32, i32, vp], i32),
     "crnn_conv_fwd": ([i32, C.POINTER(ConvDesc), vp, vp, vp, vp, vp, vp], i32),
+    "crnn_conv_fwd_bnrelu_supported": ([i32, C.POINTER(ConvDesc)], i32),
+    "crnn_conv_fwd_bnrelu": ([i32, C.POINTER(ConvDesc), vp, vp, vp, vp, vp, vp], i32),
     "crnn_conv_stat_rows": ([i32, C.POINTER(ConvDesc)], i32),
     "crnn_conv_stat_rows_per_partial": ([i32, C.POINTER(ConvDesc)], i32),
     "crnn_conv_dgrad": ([i32, C.POINTER(ConvDesc), vp, vp, vp, vp, vp, i32, vp], i32),

@@ -326,6 +326,9 @@ class CRNNEngine:
     # backward() returns. Measured (profiles/r02t_wgrad_side_stream_ab.log): the two streams
     # time-share the CUs, the wgrad launches take twice as long, and the step gains 0.4 %, so off.
     wgrad_stream = os.environ.get("CRNN_WGRAD_STREAM", "0") == "1"
+    # eval forward without saved activations: conv -> BN -> ReLU pairs as one conv launch with the
+    # running-stat affine + ReLU in the epilogue (CRNN_EVAL_FUSE, default 1)
+    eval_fuse = os.environ.get("CRNN_EVAL_FUSE", "1") == "1"
 
     def _seq_ok(self, B):
         return self.use_seq and bool(L.lib().crnn_lstm_seq_supported(self.dt, B, self.H))
@@ -425,6 +428,19 @@ class CRNNEngine:
             stats = self._bn_finalize(cs.bn, None, None, 0, b * ho * wo, False, tag)
         return (z,) + stats + (ho, wo)
 
+    def _conv_bn_relu_eval(self, cs: ConvSpec, x, b, h, w, tag, out_name):
+        """eval-mode conv -> BN (running statistics) -> ReLU as ONE conv launch when the geometry is
+        on the implicit-GEMM path (crnn_conv_fwd_bnrelu: the affine + ReLU on the fp32 accumulators,
+        no z tensor, no bn_act pass); None otherwise (the caller runs conv, finalize, bn_act)."""
+        d = cs.desc(b, h, w)
+        if not self.eval_fuse or not L.lib().crnn_conv_fwd_bnrelu_supported(self.dt, d):
+            return None
+        _, _, sc, sh = self._bn_finalize(cs.bn, None, None, 0, b * d.Ho * d.Wo, False, tag)
+        a = self.ws.get(out_name, (b, d.Ho, d.Wo, cs.co), self.dtype)
+        self._conv_call("fwd", self.conv_flops(cs, b, h, w), "crnn_conv_fwd_bnrelu", self.dt, d, ptr(x),
+                        ptr(self.packed[cs.name]), ptr(a), ptr(sc), ptr(sh), L.stream_ptr())
+        return a, d.Ho, d.Wo
+
     def _stat_capacity(self, B, H, W):
         cap = 0
         lib = L.lib()
@@ -492,12 +508,18 @@ class CRNNEngine:
         x, h, w = xp, h // 2, w // 2
         # residual stages
         blk_saved = []
+        fuse = not train and not save_for_backward   # eval inference: conv1 -> bn1 -> relu in one launch
         for bi, blk in enumerate(self.blocks):
             tag = f"b{bi}"
             P = blk.planes
-            z1b, bm1, bi1, bs1, bh1, ho, wo = self._conv_bn(blk.conv1, x, B, h, w, train, tag + ".c1")
-            a1 = ws.get(tag + ".a1", (B, ho, wo, P), T)
-            call("crnn_bn_act", dt, ptr(z1b), ptr(bs1), ptr(bh1), ptr(a1), B * ho * wo, P, 1, s)
+            fused = self._conv_bn_relu_eval(blk.conv1, x, B, h, w, tag + ".c1", tag + ".a1") if fuse else None
+            if fused is not None:
+                a1, ho, wo = fused
+                z1b = bm1 = bi1 = bs1 = bh1 = None
+            else:
+                z1b, bm1, bi1, bs1, bh1, ho, wo = self._conv_bn(blk.conv1, x, B, h, w, train, tag + ".c1")
+                a1 = ws.get(tag + ".a1", (B, ho, wo, P), T)
+                call("crnn_bn_act", dt, ptr(z1b), ptr(bs1), ptr(bh1), ptr(a1), B * ho * wo, P, 1, s)
             z2, bm2, bi2, bs2, bh2, _, _ = self._conv_bn(blk.conv2, a1, B, ho, wo, train, tag + ".c2")
             HW = ho * wo
             Cr = P // 16
@@ -528,9 +550,14 @@ class CRNNEngine:
             x, h, w = y, ho, wo
         sv["blocks"] = blk_saved
         # conv_out (model/seresnet31.py:129-136) + height collapse (model/model.py:191,216-218)
-        zc0, cm0, ci0, cs0, ch0, h2, w2 = self._conv_bn(self.co0, x, B, h, w, train, "co0")
-        ac0 = ws.get("co0.a", (B, h2, w2, 512), T)
-        call("crnn_bn_act", dt, ptr(zc0), ptr(cs0), ptr(ch0), ptr(ac0), B * h2 * w2, 512, 1, s)
+        fused = self._conv_bn_relu_eval(self.co0, x, B, h, w, "co0", "co0.a") if fuse else None
+        if fused is not None:
+            ac0, h2, w2 = fused
+            zc0 = cm0 = ci0 = cs0 = ch0 = None
+        else:
+            zc0, cm0, ci0, cs0, ch0, h2, w2 = self._conv_bn(self.co0, x, B, h, w, train, "co0")
+            ac0 = ws.get("co0.a", (B, h2, w2, 512), T)
+            call("crnn_bn_act", dt, ptr(zc0), ptr(cs0), ptr(ch0), ptr(ac0), B * h2 * w2, 512, 1, s)
         zc1, cm1, ci1, cs1, ch1, h3, w3 = self._conv_bn(self.co1, ac0, B, h2, w2, train, "co1")
         Tn = w3
         seq = ws.get("seq", (B, Tn, 512), T)

@@ -439,14 +439,23 @@ inline int wgrad_fast_kind(const Geo& g) {
 }
 
 // ---- epilogues
+// y = acc, or (eval-mode BN, esc != nullptr) y = ReLU(acc * esc[n] + esh[n]): the running-stat
+// affine and the ReLU applied to the fp32 accumulators, so no z tensor and no bn_act pass
 template <typename T> struct FwdEpi {
   static constexpr bool kStats = true;
   T* y;
   float* psum;
   float* psq;
   int M, N;
+  const float* esc = nullptr;
+  const float* esh = nullptr;
   __device__ __forceinline__ void store(int m, int n, f32x4 v, int) const {
-    if (m < M && n < N) st4<T>(y + (size_t)m * N + n, v);
+    if (m >= M || n >= N) return;
+    if (esc) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = fmaxf(fmaf(v[r], esc[n + r], esh[n + r]), 0.f);
+    }
+    st4<T>(y + (size_t)m * N + n, v);
   }
   __device__ __forceinline__ void stats(int row, int n, f32x4 s, f32x4 q) const {
     if (psum == nullptr || n >= N) return;
@@ -632,11 +641,11 @@ inline bool pad_skip_ok(const Geo& g, int rows, int cols) {
 
 template <typename T, bool UT>
 int conv_fwd_tt(const Geo& g, const crnn_conv_desc* d, const void* x, const void* w, void* y, float* psum,
-                float* psq, hipStream_t st) {
+                float* psq, const float* esc, const float* esh, hipStream_t st) {
   int M = g.B * g.Ho * g.Wo, N = g.Co, K = g.KH * g.KW * g.Ci;
   FwdA<T, UT> la{(const T*)x, g, M, K, nbytes((long)g.B * g.Hi * g.Wi * g.Ci, sizeof(T))};
   RowMajorK<T> lb{(const T*)w, K, N, K};
-  FwdEpi<T> ep{(T*)y, psum, psq, M, N};
+  FwdEpi<T> ep{(T*)y, psum, psq, M, N, esc, esh};
   int bm, bn;
   crnn_conv_fwd_tile(sizeof(T) == 2 ? CRNN_BF16 : CRNN_F32, d, &bm, &bn);
   if constexpr (sizeof(T) == 2 && UT) {
@@ -654,10 +663,11 @@ int conv_fwd_tt(const Geo& g, const crnn_conv_desc* d, const void* x, const void
 }
 
 template <typename T> int conv_fwd_t(const crnn_conv_desc* d, const void* x, const void* w, void* y,
-                                     float* psum, float* psq, hipStream_t st) {
+                                     float* psum, float* psq, hipStream_t st, const float* esc = nullptr,
+                                     const float* esh = nullptr) {
   Geo g = geo(d);
-  if (g.Ci % kstage<T>() == 0) return conv_fwd_tt<T, true>(g, d, x, w, y, psum, psq, st);
-  return conv_fwd_tt<T, false>(g, d, x, w, y, psum, psq, st);
+  if (g.Ci % kstage<T>() == 0) return conv_fwd_tt<T, true>(g, d, x, w, y, psum, psq, esc, esh, st);
+  return conv_fwd_tt<T, false>(g, d, x, w, y, psum, psq, esc, esh, st);
 }
 
 inline int ilog2s(int s) { return s == 1 ? 0 : (s == 2 ? 1 : -1); }
@@ -927,6 +937,20 @@ int crnn_conv_fwd(int dtype, const crnn_conv_desc* d, const void* x, const void*
   if (use_halo(dtype, d, false)) return conv_halo_fwd(d, x, w, y, psum, psq, st);
   return dtype == CRNN_BF16 ? conv_fwd_t<bf16>(d, x, w, y, psum, psq, st)
                             : conv_fwd_t<float>(d, x, w, y, psum, psq, st);
+}
+
+int crnn_conv_fwd_bnrelu_supported(int dtype, const crnn_conv_desc* d) {
+  return d->Ci % 8 == 0 && d->Co % 8 == 0 && !use_halo(dtype, d, false) ? 1 : 0;
+}
+
+int crnn_conv_fwd_bnrelu(int dtype, const crnn_conv_desc* d, const void* x, const void* w, void* y,
+                         const float* scale, const float* shift, void* stream) {
+  if (!crnn_conv_fwd_bnrelu_supported(dtype, d))
+    return crnn_set_error(hipErrorInvalidValue, "conv_fwd_bnrelu: geometry not on the implicit-GEMM path");
+  if (scale == nullptr || shift == nullptr) return crnn_set_error(hipErrorInvalidValue, "conv_fwd_bnrelu: null affine");
+  hipStream_t st = (hipStream_t)stream;
+  return dtype == CRNN_BF16 ? conv_fwd_t<bf16>(d, x, w, y, nullptr, nullptr, st, scale, shift)
+                            : conv_fwd_t<float>(d, x, w, y, nullptr, nullptr, st, scale, shift);
 }
 
 int crnn_conv_dgrad(int dtype, const crnn_conv_desc* d, const void* dy, const void* w, void* dx,

@@ -321,6 +321,35 @@ def test_wgrad_side_stream_bit_identical(dtype):
                 assert torch.allclose(out[0][k], o[k], rtol=1e-5, atol=1e-7), k
 
 
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 2e-2)])
+def test_eval_fused_conv_bn_relu_matches_unfused(dtype, tol):
+    """eval inference runs conv1 -> bn1 -> relu (and conv_out's first pair) as one conv launch with
+    the running-stat affine + ReLU in the epilogue (crnn_conv_fwd_bnrelu): logits equal the
+    unfused conv / finalize / bn_act path (fp32: to rounding; bf16: the fused path skips one bf16
+    rounding of z), with running statistics that are not the identity."""
+    from crnn_hip.recipe import recipe_state_dict, synthetic_batch
+    sd = recipe_state_dict(O.param_shapes(256, 194), 3)
+    g = torch.Generator().manual_seed(5)
+    for k in list(sd):
+        if k.endswith("running_mean"):
+            sd[k] = torch.randn(sd[k].shape, generator=g) * 0.1
+        elif k.endswith("running_var"):
+            sd[k] = torch.rand(sd[k].shape, generator=g) + 0.5
+    model = build_model(sd, 256, dtype).eval()
+    x, _, _, _ = synthetic_batch(8, 32, 256, 32, 194, seed=4)
+    x = x.to(DEV)
+    out = []
+    for fuse in (True, False):
+        with torch.no_grad():
+            model(x)
+            model._engine.eval_fuse = fuse
+            out.append(model(x).float().cpu())
+    err = float((out[0] - out[1]).norm() / out[1].norm())
+    assert err < tol, err
+    if dtype == torch.float32:
+        assert torch.equal(out[0].argmax(-1), out[1].argmax(-1))
+
+
 def test_enc_dropout_train():
     """enc_dropout (model/model.py:201,220) in training: the head sees the encoder output with a
     Bernoulli(1 - p) mask scaled by 1/(1-p) (keep share within 4 sigma), the logits are the head
