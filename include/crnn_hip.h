@@ -329,6 +329,7 @@ int crnn_lstm_seq_config(int B, int H, int bwd, int* S, int* U);
  * device buffer of (grid * T * 8) u64 (NULL: off) */
 int crnn_lstm_seq_debug_stamps(unsigned long long* buf);
 size_t crnn_lstm_seq_workspace(int B);
+/* gsv / csv: the gates and cell states BPTT reads, or both NULL (inference: not stored) */
 int crnn_lstm_seq_fwd(const void* xg, const void* whh, void* hseq, void* gsv, float* csv, unsigned* ws, int B, int T,
                       int H, void* stream);
 /* BPTT: dhseq [B][T][2H] upstream grad, whh_t [2][H][4H] -> dgates [2][T][B][4H] */

@@ -326,8 +326,9 @@ class CRNNEngine:
     # backward() returns. Measured (profiles/r02t_wgrad_side_stream_ab.log): the two streams
     # time-share the CUs, the wgrad launches take twice as long, and the step gains 0.4 %, so off.
     wgrad_stream = os.environ.get("CRNN_WGRAD_STREAM", "0") == "1"
-    # eval forward without saved activations: conv -> BN -> ReLU pairs as one conv launch with the
-    # running-stat affine + ReLU in the epilogue (CRNN_EVAL_FUSE, default 1)
+    # forward without saved activations: eval conv -> BN -> ReLU pairs as one conv launch with the
+    # running-stat affine + ReLU in the epilogue, and the BiLSTM sweeps store no gates / cell
+    # states (CRNN_EVAL_FUSE, default 1)
     eval_fuse = os.environ.get("CRNN_EVAL_FUSE", "1") == "1"
 
     def _seq_ok(self, B):
@@ -582,8 +583,10 @@ class CRNNEngine:
             whh = self.packed[pre + ".whh"]
             t0 = self._mark()
             if self._seq_ok(B):
-                call("crnn_lstm_seq_fwd", ptr(xg), ptr(whh), ptr(hseq), ptr(gsv), ptr(csv), ptr(self._seq_ws(B)), B,
-                     Tn, Hd, s)
+                # without saved activations the sweep stores no gates / cell states (inference)
+                keep = save_for_backward or not self.eval_fuse
+                call("crnn_lstm_seq_fwd", ptr(xg), ptr(whh), ptr(hseq), ptr(gsv) if keep else None,
+                     ptr(csv) if keep else None, ptr(self._seq_ws(B)), B, Tn, Hd, s)
             else:
                 for st in range(Tn):
                     call("crnn_lstm_step_fwd", dt, ptr(xg), ptr(whh), ptr(hseq), ptr(gsv), ptr(csv), B, Tn, Hd, st, s)

@@ -332,14 +332,17 @@ __global__ __launch_bounds__(256) void lstm_seq_fwd_kernel(const bf16* __restric
       SEQ_STAMP(6);
     }
     // saved-forward stores for BPTT, off the hand-off's critical path (issued after the signal;
-    // the next step's vmcnt(0) drains them long after they completed)
+    // the next step's vmcnt(0) drains them long after they completed). gsv == nullptr: inference,
+    // nothing saved (a uniform branch on a kernel argument)
+    if (gsv != nullptr) {
 #pragma unroll
-    for (int q = 0; q < QB; ++q) {
-      const int bi = w * QB + q, i = bi / NJ, j = bi % NJ;
-      const int b = b0 + 16 * i + c;
-      const int n = n0 + 16 * j + 4 * g, u = n >> 2;
-      csv[((size_t)(d * Tn + t) * B + b) * H + u] = cst[q];
-      st4<bf16>(gsv + ((size_t)(d * Tn + t) * B + b) * H4 + n, gq[q]);
+      for (int q = 0; q < QB; ++q) {
+        const int bi = w * QB + q, i = bi / NJ, j = bi % NJ;
+        const int b = b0 + 16 * i + c;
+        const int n = n0 + 16 * j + 4 * g, u = n >> 2;
+        csv[((size_t)(d * Tn + t) * B + b) * H + u] = cst[q];
+        st4<bf16>(gsv + ((size_t)(d * Tn + t) * B + b) * H4 + n, gq[q]);
+      }
     }
     if constexpr (!TAG) load_xg(tn);
   }
@@ -823,6 +826,8 @@ int crnn_lstm_seq_fwd(const void* xg, const void* whh, void* hseq, void* gsv, fl
   hipStream_t st = (hipStream_t)stream;
   int S, U;
   if (!seq_config(B, H, false, S, U)) return crnn_set_error(hipErrorInvalidValue, "lstm_seq: unsupported shape");
+  if ((gsv == nullptr) != (csv == nullptr))
+    return crnn_set_error(hipErrorInvalidValue, "lstm_seq_fwd: gates and cell are saved together or not at all");
   // counters + error word, and the ring slots this (B, H) uses (tag 0 = not yet written)
   const size_t zero = seq_ring_offset(B) + (crnn_option(CRNN_OPT_LSTM_HANDOFF) ? (size_t)2 * B * H * 8 : 0);
   hipError_t e = hipMemsetAsync(ws, 0, zero, st);
