@@ -161,6 +161,8 @@ class CRNNEngine:
         self._sticky_carry = 0
         self._status_host = None
         self._status_evt = None
+        self._cur_ver = None
+        self._eval_affine: Dict[str, tuple] = {}   # BN tag -> version key of its cached eval affine
         self._side = None           # side stream of the running backward (wgrad_stream)
         self._side_stream = None
         self.debug = False      # when set, backward keeps copies of block-boundary gradients
@@ -188,6 +190,7 @@ class CRNNEngine:
         """fp32 reference-layout parameters -> compute-dtype kernel layouts: every weight in one
         crnn_pack_batch launch (job table built once; all pointers are persistent views)."""
         ver = (self.version, self.version_source() if self.version_source is not None else 0)
+        self._cur_ver = ver
         if self.packed_version == ver:
             return
         if self._pack_jobs is None:
@@ -391,6 +394,16 @@ class CRNNEngine:
         sh = ws.get(tag + ".shift", (C,), torch.float32)
         rm = self.buf[prefix + ".running_mean"]
         rv = self.buf[prefix + ".running_var"]
+        if not train:
+            # eval affine from the running statistics: recomputed only when the parameters or the
+            # running statistics have changed since (train forwards clear the cache: their kernels
+            # update the statistics and these buffers without bumping a torch version counter)
+            key = (self._cur_ver, rm._version, rv._version)   # _cur_ver: this forward's pack() key
+            if self._eval_affine.get(tag) == key:
+                return mean, inv, sc, sh
+            self._eval_affine[tag] = key
+        else:
+            self._eval_affine.clear()
         call("crnn_bn_finalize", ptr(psum) if train else None, ptr(psq) if train else None, rows, rpp, C, count,
              ptr(self.p[prefix + ".weight"]), ptr(self.p[prefix + ".bias"]),
              ptr(rm), ptr(rv), BN_MOMENTUM if self.update_running else 0.0, BN_EPS, 1 if train else 0,

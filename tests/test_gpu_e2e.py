@@ -348,6 +348,24 @@ def test_eval_fused_conv_bn_relu_matches_unfused(dtype, tol):
     assert err < tol, err
     if dtype == torch.float32:
         assert torch.equal(out[0].argmax(-1), out[1].argmax(-1))
+    # the eval affine is cached between forwards: an in-place edit of a running statistic, a
+    # training forward and an optimizer-style parameter edit must each be seen by the next eval
+    model._engine.eval_fuse = True
+    bufs = dict(model.named_buffers())
+    prm = dict(model.named_parameters())
+    with torch.no_grad():
+        bufs["cnn.layer3.0.bn1.running_mean"].add_(0.3)
+        prm["cnn.layer2.0.bn1.weight"].mul_(1.5)
+        got = model(x).float().cpu()
+        model.train()
+        model(x)                        # updates running stats on the device
+        model.eval()
+        got2 = model(x).float().cpu()
+    ref = build_model({k: v.detach().cpu() for k, v in model.state_dict().items()}, 256, dtype).eval()
+    with torch.no_grad():
+        want2 = ref(x).float().cpu()
+    assert float((got2 - want2).norm() / want2.norm()) < 1e-6
+    assert float((got - out[0]).norm() / out[0].norm()) > 1e-4   # the edits changed the output
 
 
 def test_enc_dropout_train():
