@@ -48,6 +48,9 @@ def parse():
                          "teacher-forced attention decoder, 26 steps, cross-entropy, backward, AdamW); preprocess: "
                          "the input pipeline (ResizeAndPadA + Normalize of ragged uint8 crops into the encoder "
                          "layout, SURVEY 8f next-2)")
+    ap.add_argument("--kernel-timing", default="all", choices=["all", "last", "off"],
+                    help="HIP events around every conv / BiLSTM launch (the roofline's per-launch durations) in "
+                         "all timed steps, only the last timed step, or none (A/B of the events' own cost)")
     ap.add_argument("--config", default=None, choices=["long"],
                     help="long: BASELINE configs[4] shapes (32x1024 crops, 4x768 BiLSTM, batch 64/GPU)")
     a = ap.parse_args()
@@ -135,7 +138,7 @@ def pmc_traffic():
         return json.load(f), os.path.relpath(fs[-1], REPO)
 
 
-def lstm_roofline(lstm, args, eng):
+def lstm_roofline(lstm, args, eng, tsteps):
     """HBM roofline of the BiLSTM recurrence (north star: >= 40% on the step at B=256): algorithmic
     bytes per step (CRNNEngine.lstm_step_bytes) x steps / measured sweep time."""
     out = {}
@@ -143,7 +146,7 @@ def lstm_roofline(lstm, args, eng):
         gbs = byt / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
         out[k] = {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                   "frac": round(gbs / PEAK_HBM_GBS, 4), "traffic": None,
-                  "sweeps_per_step": n // args.steps, "us_per_sweep": round(ms / n * 1e3, 2),
+                  "sweeps_per_step": n // tsteps, "us_per_sweep": round(ms / n * 1e3, 2),
                   "us_per_timestep": round(ms / n / (args.width // 8) * 1e3, 3),
                   "algorithmic_bytes_per_timestep": byt / n / (args.width // 8)}
     seq = eng._seq_ok(args.batch)
@@ -331,9 +334,11 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    eng.enable_timing(True)
+    eng.enable_timing(args.kernel_timing == "all")
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
+        if args.kernel_timing == "last" and i == args.steps - 1:
+            eng.enable_timing(True)
         loss = step()
     torch.cuda.synchronize()
     if world > 1:
@@ -341,6 +346,7 @@ def main():
         torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     timing = eng.conv_timing()
+    tsteps = {"all": args.steps, "last": 1, "off": 1}[args.kernel_timing]   # steps the events covered
     eng.enable_timing(False)
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
@@ -371,7 +377,7 @@ def main():
             conv_mfma_busy = pmc["conv"].get("mfma_busy_frac")
             conv_traffic_note = (f"measured HBM bytes per conv launch (mean over fwd/dgrad/wgrad launches, "
                                  f"2*FETCH_SIZE + WRITE_SIZE), {src}; algorithmic per-launch FLOPs above")
-        per_kind = {k: {"launches_per_step": v[0] // args.steps, "ms_per_step": round(v[1] / args.steps, 3),
+        per_kind = {k: {"launches_per_step": v[0] // tsteps, "ms_per_step": round(v[1] / tsteps, 3),
                         "tflops": round(v[2] / (v[1] * 1e-3) / 1e12, 1) if v[1] > 0 else None}
                     for k, v in timing.items()}
         out = {
@@ -416,12 +422,14 @@ def main():
                          "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": conv_traffic,
                          "traffic_note": conv_traffic_note, "mfma_busy_frac_pmc": conv_mfma_busy,
-                         "algorithmic_flop_per_step": conv_flop / args.steps,
-                         "launches_per_step": conv_launches // args.steps,
-                         "kernel_ms_per_step": round(conv_ms / args.steps, 3),
-                         "timing": "HIP events around every conv launch on the launch stream, timed region"},
+                         "algorithmic_flop_per_step": conv_flop / tsteps,
+                         "launches_per_step": conv_launches // tsteps,
+                         "kernel_ms_per_step": round(conv_ms / tsteps, 3),
+                         "timing": ("HIP events around every conv launch on the launch stream, "
+                                    + {"all": "every timed step", "last": "the last timed step",
+                                       "off": "off (no figures)"}[args.kernel_timing])},
             "kernels": per_kind,
-            "roofline_lstm": lstm_roofline(lstm, args, eng),
+            "roofline_lstm": lstm_roofline(lstm, args, eng, tsteps),
             "final_loss": round(final_loss, 4),
             **({"options": opts} if opts else {}),
             "dp": ({"allreduce": "RCCL sum of the flat fp32 gradient, bucketed and overlapped with the backward",
