@@ -421,7 +421,7 @@ class CRNNEngine:
             t = self.ws.bufs["bn.fin_ws"] = torch.zeros(n, dtype=torch.float32, device=self.device)
         return t
 
-    def _conv_bn(self, cs: ConvSpec, x, b, h, w, train, tag):
+    def _conv_bn(self, cs: ConvSpec, x, b, h, w, train, tag, partials=False):
         """z = conv(x); BN statistics (train) or running stats (eval) -> (z, mean, inv, scale, shift, ho, wo)."""
         d = cs.desc(b, h, w)
         ho, wo = d.Ho, d.Wo
@@ -436,6 +436,16 @@ class CRNNEngine:
             rpp = L.lib().crnn_conv_stat_rows_per_partial(self.dt, d)
             stats = self._bn_finalize(cs.bn, psum, psq, rows, b * ho * wo, True, tag, rpp)
             self._last_partials = (psum, rows, rpp)
+        elif partials:
+            # eval, but the conv's per-tile sums are wanted (the SE squeeze reads them instead of
+            # making a pass over z: mean over HW of the running-stat affine is affine in mean(z))
+            rows = L.lib().crnn_conv_stat_rows(self.dt, d)
+            psum = self.ws.get("stat.sum", (self._stat_cap,), torch.float32)[: rows * cs.co].view(rows, cs.co)
+            psq = self.ws.get("stat.sq", (self._stat_cap,), torch.float32)[: rows * cs.co].view(rows, cs.co)
+            self._conv_call("fwd", self.conv_flops(cs, b, h, w), "crnn_conv_fwd", self.dt, d, ptr(x),
+                            ptr(self.packed[cs.name]), ptr(z), ptr(psum), ptr(psq), s)
+            stats = self._bn_finalize(cs.bn, None, None, 0, b * ho * wo, False, tag)
+            self._last_partials = (psum, rows, L.lib().crnn_conv_stat_rows_per_partial(self.dt, d))
         else:
             self._conv_call("fwd", self.conv_flops(cs, b, h, w), "crnn_conv_fwd", self.dt, d, ptr(x),
                             ptr(self.packed[cs.name]), ptr(z), None, None, s)
@@ -499,7 +509,8 @@ class CRNNEngine:
             if Cin != 3:
                 raise ValueError("expected 3-channel crops")
         s = L.stream_ptr()
-        self._stat_cap = self._stat_capacity(B, H, W) if train else 0
+        fuse = not train and not save_for_backward and self.eval_fuse   # eval inference fusions
+        self._stat_cap = self._stat_capacity(B, H, W) if train or fuse else 0
         self._nbt = []
         sv = {}
 
@@ -522,7 +533,6 @@ class CRNNEngine:
         x, h, w = xp, h // 2, w // 2
         # residual stages
         blk_saved = []
-        fuse = not train and not save_for_backward   # eval inference: conv1 -> bn1 -> relu in one launch
         for bi, blk in enumerate(self.blocks):
             tag = f"b{bi}"
             P = blk.planes
@@ -534,13 +544,14 @@ class CRNNEngine:
                 z1b, bm1, bi1, bs1, bh1, ho, wo = self._conv_bn(blk.conv1, x, B, h, w, train, tag + ".c1")
                 a1 = ws.get(tag + ".a1", (B, ho, wo, P), T)
                 call("crnn_bn_act", dt, ptr(z1b), ptr(bs1), ptr(bh1), ptr(a1), B * ho * wo, P, 1, s)
-            z2, bm2, bi2, bs2, bh2, _, _ = self._conv_bn(blk.conv2, a1, B, ho, wo, train, tag + ".c2")
+            self._last_partials = None
+            z2, bm2, bi2, bs2, bh2, _, _ = self._conv_bn(blk.conv2, a1, B, ho, wo, train, tag + ".c2", partials=fuse)
             HW = ho * wo
             Cr = P // 16
             pooled = ws.get(tag + ".pooled", (B, P), torch.float32)
             hid = ws.get(tag + ".hid", (B, Cr), torch.float32)
             se = ws.get(tag + ".s", (B, P), torch.float32)
-            lp = self._last_partials if train else None
+            lp = self._last_partials if train or fuse else None
             if lp is not None and HW % lp[2] == 0 and lp[1] * lp[2] == B * HW:
                 # squeeze from conv2's BN partial sums (no pass over z2)
                 call("crnn_se_pool_partials", ptr(lp[0]), lp[1], lp[2], ptr(bs2), ptr(bh2), ptr(pooled), B, HW, P, s)
