@@ -48,9 +48,11 @@ def parse():
                          "teacher-forced attention decoder, 26 steps, cross-entropy, backward, AdamW); preprocess: "
                          "the input pipeline (ResizeAndPadA + Normalize of ragged uint8 crops into the encoder "
                          "layout, SURVEY 8f next-2)")
-    ap.add_argument("--kernel-timing", default="all", choices=["all", "last", "off"],
+    ap.add_argument("--kernel-timing", default="last", choices=["all", "last", "off"],
                     help="HIP events around every conv / BiLSTM launch (the roofline's per-launch durations) in "
-                         "all timed steps, only the last timed step, or none (A/B of the events' own cost)")
+                         "all timed steps, only the last timed step (default: the ~170 event records of an "
+                         "instrumented step cost 0.5 ms of GPU time, profiles/r02s_infer_fuse_and_timing_ab.log), "
+                         "or none")
     ap.add_argument("--config", default=None, choices=["long"],
                     help="long: BASELINE configs[4] shapes (32x1024 crops, 4x768 BiLSTM, batch 64/GPU)")
     a = ap.parse_args()
