@@ -146,6 +146,13 @@ int crnn_conv_fwd_bnrelu_supported(int dtype, const crnn_conv_desc* d);
 int crnn_conv_fwd_bnrelu(int dtype, const crnn_conv_desc* d, const void* x, const void* w, void* y, const float* scale, const float* shift, void* stream);
 /* dx[B][Hi][Wi][Ci] = dgrad(dy) (+= dx if accumulate) (+ dres*(yres>0) if dres != NULL). */
 int crnn_conv_dgrad(int dtype, const crnn_conv_desc* d, const void* dy, const void* w, void* dx, const void* dres, const void* yres, int accumulate, void* stream);
+/* dgrad of a residual block's strided pair in one pass (model/seresnet31.py:56 conv1 3x3 stride 2
+ * and :64-67 downsample 1x1 stride 2, both reading the block input x): dx = dgrad_conv1(dy) +
+ * dgrad_downsample(dy_ds), the downsample being one more tap of conv1's parity class (0, 0).
+ * Layout contract: dy_ds follows dy in memory (dy + B*Ho*Wo*Co elements) and the downsample's
+ * packed [Co][1][1][Ci] weights follow w (w + Co*9*Ci elements). d: conv1, dds: the downsample. */
+int crnn_conv_dgrad_ds_supported(int dtype, const crnn_conv_desc* d, const crnn_conv_desc* dds);
+int crnn_conv_dgrad_ds(int dtype, const crnn_conv_desc* d, const crnn_conv_desc* dds, const void* dy, const void* w, void* dx, void* stream);
 /* dgrad fused with the BatchNorm backward sums of the layer before (conv input = ReLU(BN(z))):
  * dx as crnn_conv_dgrad (no accumulate / residual), plus per partial row r (128 rows of dx)
  * pg[r][c] = sum g, pgx[r][c] = sum g (z - mean) invstd with g = dx (z scale + shift > 0) — the

@@ -68,6 +68,8 @@ _SIGS = {
     "crnn_conv_stat_rows": ([i32, C.POINTER(ConvDesc)], i32),
     "crnn_conv_stat_rows_per_partial": ([i32, C.POINTER(ConvDesc)], i32),
     "crnn_conv_dgrad": ([i32, C.POINTER(ConvDesc), vp, vp, vp, vp, vp, i32, vp], i32),
+    "crnn_conv_dgrad_ds_supported": ([i32, C.POINTER(ConvDesc), C.POINTER(ConvDesc)], i32),
+    "crnn_conv_dgrad_ds": ([i32, C.POINTER(ConvDesc), C.POINTER(ConvDesc), vp, vp, vp, vp], i32),
     "crnn_conv_dgrad_bnrelu_rows": ([i32, C.POINTER(ConvDesc)], i32),
     "crnn_conv_dgrad_bnrelu": ([i32, C.POINTER(ConvDesc), vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp], i32),
     "crnn_conv_wgrad": ([i32, C.POINTER(ConvDesc), vp, vp, vp, vp, sz, f32, vp], i32),

@@ -210,6 +210,15 @@ class CRNNEngine:
             return dst.numel()
 
         sizes = []
+        # a strided block's conv1 and downsample weights back to back (crnn_conv_dgrad_ds reads the
+        # downsample's [Co][Ci] rows right after conv1's)
+        for blk in self.blocks:
+            if blk.ds is not None and blk.conv1.name not in self.packed:
+                c1, ds = blk.conv1, blk.ds
+                n1 = c1.co * c1.kh * c1.kw * c1.ci
+                cat = torch.empty(n1 + ds.co * ds.kh * ds.kw * ds.ci, dtype=T, device=self.device)
+                self.packed[c1.name] = cat[:n1].view(c1.co, c1.kh, c1.kw, c1.ci)
+                self.packed[ds.name] = cat[n1:].view(ds.co, ds.kh, ds.kw, ds.ci)
         # conv weights: their own launch, one block per output channel (crnn_pack_conv_batch)
         rows, slab = 0, 0
         for cs in self.convs():
@@ -333,6 +342,8 @@ class CRNNEngine:
     # running-stat affine + ReLU in the epilogue, and the BiLSTM sweeps store no gates / cell
     # states (CRNN_EVAL_FUSE, default 1)
     eval_fuse = os.environ.get("CRNN_EVAL_FUSE", "1") == "1"
+    # strided blocks: conv1's and the downsample's dgrads as one launch (CRNN_DS_FUSE, default 1)
+    ds_fuse = os.environ.get("CRNN_DS_FUSE", "1") == "1"
 
     def _seq_ok(self, B):
         return self.use_seq and bool(L.lib().crnn_lstm_seq_supported(self.dt, B, self.H))
@@ -959,7 +970,17 @@ class CRNNEngine:
             else:
                 self._conv_call("dgrad", self.conv_flops(blk.conv2, B, ho, wo), "crnn_conv_dgrad", dt, d2, ptr(dz2),
                                 ptr(self.packed[blk.conv2.name]), ptr(da1), None, None, 0, s)
-            dz1 = self._dz(f"b{bi}.c1", bufs[o1], Mo * P)
+            d1 = blk.conv1.desc(B, h, w)
+            dds = blk.ds.desc(B, h, w) if blk.ds is not None else None
+            # the downsample's dgrad as one more tap of conv1's parity class (0, 0): its input gradient
+            # dzd follows dz1 in one buffer (crnn_conv_dgrad_ds's layout contract)
+            fuse_ds = (dds is not None and self.ds_fuse and 2 * Mo * P <= bufs[o1].numel()
+                       and L.lib().crnn_conv_dgrad_ds_supported(dt, d1, dds))
+            if fuse_ds:
+                dzcat = self._dz(f"b{bi}.c1ds", bufs[o1], 2 * Mo * P)
+                dz1 = dzcat[: Mo * P]
+            else:
+                dz1 = self._dz(f"b{bi}.c1", bufs[o1], Mo * P)
             self._bn_bwd(1, da1, sb["z1"], (sb["m1"], sb["i1"], sb["sc1"], sb["sh1"]), blk.conv1.bn, Mo, P,
                          out=dz1, accumulate_params=accumulate, sums=sums)
             self._wgrad(blk.conv1, dz1, sb["x"], B, h, w)
@@ -968,6 +989,16 @@ class CRNNEngine:
             if blk.ds is None:
                 self._conv_call("dgrad", self.conv_flops(blk.conv1, B, h, w), "crnn_conv_dgrad", dt, blk.conv1.desc(B, h, w), ptr(dz1), ptr(self.packed[blk.conv1.name]),
                      ptr(dxb), ptr(dyb), ptr(sb["y"]), 0, s)
+                cur = o2
+            elif fuse_ds:
+                dsv = sb["ds"]
+                dzd = dzcat[Mo * P:]
+                self._bn_bwd(2, dyb, dsv["zd"], (dsv["m"], dsv["i"], dsv["sc"], dsv["sh"]), blk.ds.bn, Mo, P,
+                             y=sb["y"], out=dzd, accumulate_params=accumulate)
+                self._wgrad(blk.ds, dzd, sb["x"], B, h, w)
+                self._conv_call("dgrad", self.conv_flops(blk.conv1, B, h, w) + self.conv_flops(blk.ds, B, h, w),
+                                "crnn_conv_dgrad_ds", dt, d1, dds, ptr(dzcat), ptr(self.packed[blk.conv1.name]),
+                                ptr(dxb), s)
                 cur = o2
             else:
                 self._conv_call("dgrad", self.conv_flops(blk.conv1, B, h, w), "crnn_conv_dgrad", dt, blk.conv1.desc(B, h, w), ptr(dz1), ptr(self.packed[blk.conv1.name]),

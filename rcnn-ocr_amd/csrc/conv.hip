@@ -203,6 +203,11 @@ template <typename T> struct DgradB {
 struct TapTable {
   int n;
   int dh[4], dw[4], id[4];  // per class tap: ho offset, wo offset, kh*KW + kw
+  // fused 1x1 stride-2 downsample (crnn_conv_dgrad_ds): tap xtap reads the downsample's gradient,
+  // stored right after dy (A: dw = B*Ho*Wo rows further, always in range), and its [Co][Ci]
+  // weights, stored right after w (B: rows of Ci from element xb); -1 when absent
+  int xtap = -1;
+  int xb = 0;
 };
 
 
@@ -225,7 +230,8 @@ template <typename T> struct DgradClsA {
     c.mask = 0;
     if (m < M)
       for (int t = 0; t < tt.n; ++t)
-        if ((unsigned)((int)i + tt.dh[t]) < (unsigned)g.Ho && (unsigned)((int)j + tt.dw[t]) < (unsigned)g.Wo)
+        if (t == tt.xtap ||
+            ((unsigned)((int)i + tt.dh[t]) < (unsigned)g.Ho && (unsigned)((int)j + tt.dw[t]) < (unsigned)g.Wo))
           c.mask |= 1u << t;
     return c;
   }
@@ -265,12 +271,14 @@ template <typename T> struct DgradClsB {
     p.tap = (int)g.dCo.divmod((uint32_t)k0, co);
     p.c0 = (int)co;
     p.kh = tt.id[p.tap < tt.n ? p.tap : 0];
+    p.kw = p.tap == tt.xtap;  // the downsample's weights: rows of Ci after w
     return p;
   }
   __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc() const { return mk_rsrc(w, bytes); }
   __device__ __forceinline__ uint32_t offs(const Ctx& c, const Prep& p, int kofs) const {
     const bool ok = c.ok && p.tap < tt.n;
-    return boff<T>((uint32_t)(((p.c0 + kofs) * g.KH * g.KW + p.kh) * g.Ci + c.ci), ok);
+    const int e = p.kw ? tt.xb + (p.c0 + kofs) * g.Ci + c.ci : ((p.c0 + kofs) * g.KH * g.KW + p.kh) * g.Ci + c.ci;
+    return boff<T>((uint32_t)e, ok);
   }
   __device__ __forceinline__ typename VT<T>::v8 load(const Ctx& c, const Prep& p, int kofs) const {
     return bld8<T>(rsrc(), offs(c, p, kofs));
@@ -696,11 +704,15 @@ inline double quant_eff(int bn) { return bn == 256 ? 0.4 : 0.6; }
 // rows: row classes (each input row its own class, Hc = 1) instead of parity classes in height —
 // for maps of 1-2 output rows (conv_out[1]: Ho = 1), where half of a generic dgrad's taps read
 // nothing but padding rows; the stride may then be 1
+// ds: the 1x1 stride-2 downsample of the same block is fused in (crnn_conv_dgrad_ds): its gradient
+// (B*Ho*Wo*Co, right after dy) and weights ([Co][Ci], right after w) are one more tap of the class
+// (0, 0), whose pixels (2i, 2j) it reaches from output (i, j)
 template <typename T>
 int conv_dgrad_strided(const Geo& g, const void* dy, const void* w, void* dx, const void* dres, const void* yres,
-                       int accumulate, hipStream_t st, bool rows = false) {
-  const uint32_t dyb = nbytes((long)g.B * g.Ho * g.Wo * g.Co, sizeof(T));
-  const uint32_t wb = nbytes((long)g.Co * g.KH * g.KW * g.Ci, sizeof(T));
+                       int accumulate, hipStream_t st, bool rows = false, bool ds = false) {
+  const long dyn = (long)g.B * g.Ho * g.Wo * g.Co, wn = (long)g.Co * g.KH * g.KW * g.Ci;
+  const uint32_t dyb = nbytes(ds ? 2 * dyn : dyn, sizeof(T));
+  const uint32_t wb = nbytes(ds ? wn + (long)g.Co * g.Ci : wn, sizeof(T));
   for (int pch = 0; pch < (rows ? g.Hi : g.sh); ++pch)
     for (int pcw = 0; pcw < g.sw; ++pcw) {
       TapTable tt{};
@@ -715,6 +727,15 @@ int conv_dgrad_strided(const Geo& g, const void* dy, const void* w, void* dx, co
           tt.id[tt.n] = kh * g.KW + kw;
           ++tt.n;
         }
+      }
+      if (ds && pch == 0 && pcw == 0) {
+        if (tt.n >= 4) return crnn_set_error(hipErrorInvalidValue, "conv_dgrad_ds: class (0, 0) is full");
+        tt.xtap = tt.n;
+        tt.xb = (int)wn;
+        tt.dh[tt.n] = 0;
+        tt.dw[tt.n] = g.B * g.Ho * g.Wo;  // A rows: the downsample's gradient follows dy
+        tt.id[tt.n] = 0;
+        ++tt.n;
       }
       const int Hc = rows ? 1 : (g.Hi - pch + g.sh - 1) / g.sh, Wc = (g.Wi - pcw + g.sw - 1) / g.sw;
       if (Hc <= 0 || Wc <= 0) continue;
@@ -960,6 +981,27 @@ int crnn_conv_dgrad(int dtype, const crnn_conv_desc* d, const void* dy, const vo
   if (dres == nullptr && !accumulate && use_halo(dtype, d, true)) return conv_halo_dgrad(d, dy, w, dx, st);
   return dtype == CRNN_BF16 ? conv_dgrad_t<bf16>(d, dy, w, dx, dres, yres, accumulate, st)
                             : conv_dgrad_t<float>(d, dy, w, dx, dres, yres, accumulate, st);
+}
+
+int crnn_conv_dgrad_ds_supported(int dtype, const crnn_conv_desc* d, const crnn_conv_desc* dds) {
+  const int ks = dtype == CRNN_BF16 ? kstage<bf16>() : kstage<float>();
+  return d->KH == 3 && d->KW == 3 && d->sh == 2 && d->sw == 2 && d->ph == 1 && d->pw == 1 && dds->KH == 1 &&
+                 dds->KW == 1 && dds->sh == 2 && dds->sw == 2 && dds->ph == 0 && dds->pw == 0 && d->B == dds->B &&
+                 d->Hi == dds->Hi && d->Wi == dds->Wi && d->Ci == dds->Ci && d->Ho == dds->Ho && d->Wo == dds->Wo &&
+                 d->Co == dds->Co && d->Ci % 8 == 0 && d->Co % ks == 0 && d->Hi == 2 * d->Ho && d->Wi == 2 * d->Wo &&
+                 (long)d->B * d->Ho * d->Wo * d->Co * 2 < (1L << 31)
+             ? 1
+             : 0;
+}
+
+int crnn_conv_dgrad_ds(int dtype, const crnn_conv_desc* d, const crnn_conv_desc* dds, const void* dy, const void* w,
+                       void* dx, void* stream) {
+  if (!crnn_conv_dgrad_ds_supported(dtype, d, dds))
+    return crnn_set_error(hipErrorInvalidValue, "conv_dgrad_ds: not a 3x3/2 conv + 1x1/2 downsample pair");
+  Geo g = geo(d);
+  hipStream_t st = (hipStream_t)stream;
+  return dtype == CRNN_BF16 ? conv_dgrad_strided<bf16>(g, dy, w, dx, nullptr, nullptr, 0, st, false, true)
+                            : conv_dgrad_strided<float>(g, dy, w, dx, nullptr, nullptr, 0, st, false, true);
 }
 
 int crnn_conv_dgrad_bnrelu_rows(int dtype, const crnn_conv_desc* d) {

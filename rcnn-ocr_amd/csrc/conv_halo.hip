@@ -391,13 +391,13 @@ bool conv_halo_fits(const crnn_conv_desc* d, bool dgrad) {
 
 // rows per band: the memory-bound input conv (few FLOPs per row, several workgroups per CU) takes
 // short bands so more of them are in flight; the MFMA-bound ones walk the whole height
-// (tuning: CRNN_OPT_HALO_CONV = n >= 2 sets n rows for the others, when it divides H)
+// (tuning: CRNN_OPT_HALO_CONV = n >= 2 sets n rows for every halo forward, when it divides H)
 static int band_rows(int H, int ci) {
+  const int opt = crnn_option(CRNN_OPT_HALO_CONV);
+  if (opt >= 2 && H % opt == 0) return opt;
   if (ci == 8)
     for (int rb : {8, 4, 2})
       if (H % rb == 0 && H > rb) return rb;
-  const int opt = crnn_option(CRNN_OPT_HALO_CONV);
-  if (opt >= 2 && H % opt == 0) return opt;
   if (ci == 64 && H % 16 == 0 && H > 16) return 16;  // 4 bands per CU: measured 7 % faster than H
   return H;
 }

@@ -70,6 +70,51 @@ CONVS_DEEP = [
 ]
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("geo", [(4, 128, 16, 32, 256), (3, 256, 8, 64, 512), (256, 128, 16, 128, 256)])
+def test_conv_dgrad_ds_fused(geo, dtype):
+    """crnn_conv_dgrad_ds: a strided block's conv1 (3x3/2) and downsample (1x1/2) input gradients
+    in one pass (the downsample as one more tap of class (0, 0)) == the sum of both dgrads (torch fp32);
+    the operands in the contract's layout (dy_ds after dy, the downsample's weights after conv1's).
+    The last geometry is layer1.0's at B=256."""
+    L = _L()
+    B, Ci, H, W, Co = geo
+    g = torch.Generator().manual_seed(3)
+    w1 = torch.randn(Co, Ci, 3, 3, generator=g) / math.sqrt(9 * Ci)
+    wd = torch.randn(Co, Ci, 1, 1, generator=g) / math.sqrt(Ci)
+    Ho, Wo = H // 2, W // 2
+    dy1 = torch.randn(B, Co, Ho, Wo, generator=g)
+    dyd = torch.randn(B, Co, Ho, Wo, generator=g)
+    if dtype == torch.bfloat16:
+        w1, wd, dy1, dyd = (t.bfloat16().float() for t in (w1, wd, dy1, dyd))
+    x = torch.zeros(B, Ci, H, W, requires_grad=True)
+    y1 = F.conv2d(x, w1, stride=2, padding=1)
+    yd = F.conv2d(x, wd, stride=2)
+    (y1 * dy1).sum().backward(retain_graph=True)
+    (yd * dyd).sum().backward()
+    ref = x.grad
+    dt = L.dtype_code(dtype)
+    d1 = L.ConvDesc(B, H, W, Ci, Ho, Wo, Co, 3, 3, 2, 2, 1, 1, Ci)
+    dd = L.ConvDesc(B, H, W, Ci, Ho, Wo, Co, 1, 1, 2, 2, 0, 0, Ci)
+    assert L.lib().crnn_conv_dgrad_ds_supported(dt, d1, dd) == 1
+    n1 = Co * 9 * Ci
+    wcat = torch.empty(n1 + Co * Ci, dtype=dtype, device=DEV)
+    st = L.stream_ptr()
+    L.call("crnn_pack_conv_weight", dt, w1.to(DEV).data_ptr(), wcat.data_ptr(), Co, Ci, 3, 3, Ci, st)
+    L.call("crnn_pack_conv_weight", dt, wd.to(DEV).data_ptr(), wcat[n1:].data_ptr(), Co, Ci, 1, 1, Ci, st)
+    m = B * Ho * Wo * Co
+    dycat = torch.empty(2 * m, dtype=dtype, device=DEV)
+    dycat[:m].copy_(to_nhwc(dy1, None, dtype).reshape(-1))
+    dycat[m:].copy_(to_nhwc(dyd, None, dtype).reshape(-1))
+    dx = torch.full((B, H, W, Ci), float("nan"), dtype=dtype, device=DEV)
+    L.call("crnn_conv_dgrad_ds", dt, d1, dd, dycat.data_ptr(), wcat.data_ptr(), dx.data_ptr(), st)
+    got = dx.float().permute(0, 3, 1, 2).cpu()
+    assert relerr(got, ref) < (1e-5 if dtype == torch.float32 else 1e-2)
+    # a mismatched pair is refused
+    bad = L.ConvDesc(B, H, W, Ci, Ho, Wo, Co, 3, 3, 1, 1, 1, 1, Ci)
+    assert L.lib().crnn_conv_dgrad_ds_supported(dt, bad, dd) == 0
+
+
 @pytest.mark.parametrize("dtype,cfg", [(dt, c) for c in CONVS for dt in (torch.float32, torch.bfloat16)]
                          + [(torch.bfloat16, c) for c in CONVS_DEEP])
 def test_conv_fwd_dgrad_wgrad(cfg, dtype):
