@@ -140,8 +140,8 @@ int crnn_conv_stat_rows_per_partial(int dtype, const crnn_conv_desc* d);
 /* eval-mode conv -> BatchNorm (running statistics) -> ReLU in one launch
  * (model/seresnet31.py:56-57, conv1 -> bn1 -> relu of BasicBlock; :129-131 conv_out):
  * y = max(conv(x, w) * scale[c] + shift[c], 0) from the fp32 accumulators (scale / shift:
- * crnn_bn_finalize with train = 0). Supported on the implicit-GEMM path only
- * (crnn_conv_fwd_bnrelu_supported: 1 / 0; the full-resolution halo convs are not). */
+ * crnn_bn_finalize with train = 0), on the implicit-GEMM and the halo (stem) kernels alike
+ * (crnn_conv_fwd_bnrelu_supported: 1 / 0). */
 int crnn_conv_fwd_bnrelu_supported(int dtype, const crnn_conv_desc* d);
 int crnn_conv_fwd_bnrelu(int dtype, const crnn_conv_desc* d, const void* x, const void* w, void* y, const float* scale, const float* shift, void* stream);
 /* dx[B][Hi][Wi][Ci] = dgrad(dy) (+= dx if accumulate) (+ dres*(yres>0) if dres != NULL). */

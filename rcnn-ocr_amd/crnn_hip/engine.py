@@ -464,9 +464,9 @@ class CRNNEngine:
         return (z,) + stats + (ho, wo)
 
     def _conv_bn_relu_eval(self, cs: ConvSpec, x, b, h, w, tag, out_name):
-        """eval-mode conv -> BN (running statistics) -> ReLU as ONE conv launch when the geometry is
-        on the implicit-GEMM path (crnn_conv_fwd_bnrelu: the affine + ReLU on the fp32 accumulators,
-        no z tensor, no bn_act pass); None otherwise (the caller runs conv, finalize, bn_act)."""
+        """eval-mode conv -> BN (running statistics) -> ReLU as ONE conv launch (crnn_conv_fwd_bnrelu:
+        the affine + ReLU on the fp32 accumulators of the implicit-GEMM or halo kernel, no z tensor,
+        no bn_act pass); None when unsupported (the caller runs conv, finalize, bn_act)."""
         d = cs.desc(b, h, w)
         if not self.eval_fuse or not L.lib().crnn_conv_fwd_bnrelu_supported(self.dt, d):
             return None
@@ -531,9 +531,14 @@ class CRNNEngine:
             x0 = ws.get("in", (B, H, W, 8), T)
             call("crnn_nchw_to_nhwc", dt, ptr(images), ptr(x0), B, 3, H, W, 8, s)
         # stem (model/seresnet31.py:81-89)
-        z0, m0, i0, sc0, sh0, h, w = self._conv_bn(self.stem0, x0, B, H, W, train, "s0")
-        a0 = ws.get("s0.a", (B, h, w, 64), T)
-        call("crnn_bn_act", dt, ptr(z0), ptr(sc0), ptr(sh0), ptr(a0), B * h * w, 64, 1, s)
+        fused = self._conv_bn_relu_eval(self.stem0, x0, B, H, W, "s0", "s0.a") if fuse else None
+        if fused is not None:
+            a0, h, w = fused
+            z0 = m0 = i0 = sc0 = sh0 = None
+        else:
+            z0, m0, i0, sc0, sh0, h, w = self._conv_bn(self.stem0, x0, B, H, W, train, "s0")
+            a0 = ws.get("s0.a", (B, h, w, 64), T)
+            call("crnn_bn_act", dt, ptr(z0), ptr(sc0), ptr(sh0), ptr(a0), B * h * w, 64, 1, s)
         z1, m1, i1, sc1, sh1, h, w = self._conv_bn(self.stem1, a0, B, h, w, train, "s1")
         if h % 2 or w % 2:
             raise ValueError("stem maxpool expects even H and W")

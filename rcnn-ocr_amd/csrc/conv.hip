@@ -19,7 +19,7 @@ using namespace gemm;
 // conv_halo.hip: direct 3x3 / stride-1 kernel for the full-resolution stem conv
 bool conv_halo_fits(const crnn_conv_desc* d, bool dgrad);
 int conv_halo_fwd(const crnn_conv_desc* d, const void* x, const void* w, void* y, float* psum, float* psq,
-                  hipStream_t st);
+                  hipStream_t st, const float* esc = nullptr, const float* esh = nullptr);
 int conv_halo_dgrad(const crnn_conv_desc* d, const void* dy, const void* w, void* dx, hipStream_t st);
 int conv_halo_wgrad_slabs(const crnn_conv_desc* d);
 int conv_halo_wgrad(const crnn_conv_desc* d, const void* dy, const void* x, float* ws, hipStream_t st);
@@ -961,15 +961,16 @@ int crnn_conv_fwd(int dtype, const crnn_conv_desc* d, const void* x, const void*
 }
 
 int crnn_conv_fwd_bnrelu_supported(int dtype, const crnn_conv_desc* d) {
-  return d->Ci % 8 == 0 && d->Co % 8 == 0 && !use_halo(dtype, d, false) ? 1 : 0;
+  return d->Ci % 8 == 0 && d->Co % 8 == 0 ? 1 : 0;
 }
 
 int crnn_conv_fwd_bnrelu(int dtype, const crnn_conv_desc* d, const void* x, const void* w, void* y,
                          const float* scale, const float* shift, void* stream) {
   if (!crnn_conv_fwd_bnrelu_supported(dtype, d))
-    return crnn_set_error(hipErrorInvalidValue, "conv_fwd_bnrelu: geometry not on the implicit-GEMM path");
+    return crnn_set_error(hipErrorInvalidValue, "conv_fwd_bnrelu: channels must be multiples of 8");
   if (scale == nullptr || shift == nullptr) return crnn_set_error(hipErrorInvalidValue, "conv_fwd_bnrelu: null affine");
   hipStream_t st = (hipStream_t)stream;
+  if (use_halo(dtype, d, false)) return conv_halo_fwd(d, x, w, y, nullptr, nullptr, st, scale, shift);
   return dtype == CRNN_BF16 ? conv_fwd_t<bf16>(d, x, w, y, nullptr, nullptr, st, scale, shift)
                             : conv_fwd_t<float>(d, x, w, y, nullptr, nullptr, st, scale, shift);
 }

@@ -44,7 +44,9 @@ template <int CI> struct Ring {
 template <int CI, int CO, bool FLIP>
 __global__ __launch_bounds__(512) void halo3x3_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wp,
                                                       bf16* __restrict__ y, float* __restrict__ psum,
-                                                      float* __restrict__ psq, int H, int W, int RB, uint32_t xbytes) {
+                                                      float* __restrict__ psq, int H, int W, int RB, uint32_t xbytes,
+                                                      const float* __restrict__ esc = nullptr,
+                                                      const float* __restrict__ esh = nullptr) {
   using R = Ring<CI>;
   // CI = 8 (TAPK): a 32-deep k-step holds 4 taps x 8 channels, lane group g takes tap 4ks + g
   // (taps 9..11 of the last step: zero weights, any finite data)
@@ -182,6 +184,18 @@ __global__ __launch_bounds__(512) void halo3x3_kernel(const bf16* __restrict__ x
 
     // outputs: lane (c, g) of fragment (i, j) = pixel pw*64 + 16i + c, channels co .. co+3
     const size_t m0 = ((size_t)b * H + yy) * W + x0;
+    if (esc != nullptr) {  // eval-mode BN (running statistics) + ReLU on the accumulators
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int co = cw * CW + 16 * j + 4 * g;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float a = esc[co + r], h = esh[co + r];
+#pragma unroll
+          for (int i = 0; i < MI; ++i) acc[i][j][r] = fmaxf(fmaf(acc[i][j][r], a, h), 0.f);
+        }
+      }
+    }
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -403,16 +417,16 @@ static int band_rows(int H, int ci) {
 }
 
 int conv_halo_fwd(const crnn_conv_desc* d, const void* x, const void* w, void* y, float* psum, float* psq,
-                  hipStream_t st) {
+                  hipStream_t st, const float* esc, const float* esh) {
   const int rb = band_rows(d->Hi, d->Ci);
   const dim3 grid(d->B * (d->Wi / TW) * (d->Hi / rb));
   const uint32_t xbytes = (uint32_t)((size_t)d->B * d->Hi * d->Wi * d->Ci * 2);
   if (d->Ci == 8)
     hipLaunchKernelGGL((halo3x3_kernel<8, 64, false>), grid, dim3(512), 0, st, (const bf16*)x, (const bf16*)w,
-                       (bf16*)y, psum, psq, d->Hi, d->Wi, rb, xbytes);
+                       (bf16*)y, psum, psq, d->Hi, d->Wi, rb, xbytes, esc, esh);
   else
     hipLaunchKernelGGL((halo3x3_kernel<64, 128, false>), grid, dim3(512), 0, st, (const bf16*)x, (const bf16*)w,
-                       (bf16*)y, psum, psq, d->Hi, d->Wi, rb, xbytes);
+                       (bf16*)y, psum, psq, d->Hi, d->Wi, rb, xbytes, esc, esh);
   return (int)hipGetLastError();
 }
 
