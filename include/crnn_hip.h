@@ -143,6 +143,10 @@ int crnn_conv_stat_rows_per_partial(int dtype, const crnn_conv_desc* d);
  * crnn_bn_finalize with train = 0), on the implicit-GEMM and the halo (stem) kernels alike
  * (crnn_conv_fwd_bnrelu_supported: 1 / 0). */
 int crnn_conv_fwd_bnrelu_supported(int dtype, const crnn_conv_desc* d);
+/* the same with the stem's 2x2 / stride-2 max-pool after the ReLU (model/seresnet31.py:81-89,
+ * conv0.3 -> conv0.4 -> relu -> maxpool): y[B][Ho/2][Wo/2][Co]; bf16, the halo stem geometry only */
+int crnn_conv_fwd_bnrelu_pool_supported(int dtype, const crnn_conv_desc* d);
+int crnn_conv_fwd_bnrelu_pool(int dtype, const crnn_conv_desc* d, const void* x, const void* w, void* y, const float* scale, const float* shift, void* stream);
 int crnn_conv_fwd_bnrelu(int dtype, const crnn_conv_desc* d, const void* x, const void* w, void* y, const float* scale, const float* shift, void* stream);
 /* dx[B][Hi][Wi][Ci] = dgrad(dy) (+= dx if accumulate) (+ dres*(yres>0) if dres != NULL). */
 int crnn_conv_dgrad(int dtype, const crnn_conv_desc* d, const void* dy, const void* w, void* dx, const void* dres, const void* yres, int accumulate, void* stream);

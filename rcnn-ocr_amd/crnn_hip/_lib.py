@@ -65,6 +65,8 @@ _SIGS = {
     "crnn_conv_fwd": ([i32, C.POINTER(ConvDesc), vp, vp, vp, vp, vp, vp], i32),
     "crnn_conv_fwd_bnrelu_supported": ([i32, C.POINTER(ConvDesc)], i32),
     "crnn_conv_fwd_bnrelu": ([i32, C.POINTER(ConvDesc), vp, vp, vp, vp, vp, vp], i32),
+    "crnn_conv_fwd_bnrelu_pool_supported": ([i32, C.POINTER(ConvDesc)], i32),
+    "crnn_conv_fwd_bnrelu_pool": ([i32, C.POINTER(ConvDesc), vp, vp, vp, vp, vp, vp], i32),
     "crnn_conv_stat_rows": ([i32, C.POINTER(ConvDesc)], i32),
     "crnn_conv_stat_rows_per_partial": ([i32, C.POINTER(ConvDesc)], i32),
     "crnn_conv_dgrad": ([i32, C.POINTER(ConvDesc), vp, vp, vp, vp, vp, i32, vp], i32),

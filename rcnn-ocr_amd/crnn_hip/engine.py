@@ -539,11 +539,21 @@ class CRNNEngine:
             z0, m0, i0, sc0, sh0, h, w = self._conv_bn(self.stem0, x0, B, H, W, train, "s0")
             a0 = ws.get("s0.a", (B, h, w, 64), T)
             call("crnn_bn_act", dt, ptr(z0), ptr(sc0), ptr(sh0), ptr(a0), B * h * w, 64, 1, s)
-        z1, m1, i1, sc1, sh1, h, w = self._conv_bn(self.stem1, a0, B, h, w, train, "s1")
-        if h % 2 or w % 2:
+        d1 = self.stem1.desc(B, h, w)
+        if d1.Ho % 2 or d1.Wo % 2:
             raise ValueError("stem maxpool expects even H and W")
-        xp = ws.get("s1.pool", (B, h // 2, w // 2, 128), T)
-        call("crnn_bn_relu_maxpool", dt, ptr(z1), ptr(sc1), ptr(sh1), ptr(xp), B, h, w, 128, s)
+        if fuse and L.lib().crnn_conv_fwd_bnrelu_pool_supported(dt, d1):
+            # eval inference: conv -> BN -> ReLU -> max-pool in the halo kernel's epilogue
+            _, _, sc1, sh1 = self._bn_finalize(self.stem1.bn, None, None, 0, B * d1.Ho * d1.Wo, False, "s1")
+            xp = ws.get("s1.pool", (B, d1.Ho // 2, d1.Wo // 2, 128), T)
+            self._conv_call("fwd", self.conv_flops(self.stem1, B, h, w), "crnn_conv_fwd_bnrelu_pool", dt, d1,
+                            ptr(a0), ptr(self.packed[self.stem1.name]), ptr(xp), ptr(sc1), ptr(sh1), s)
+            h, w = d1.Ho, d1.Wo
+            z1 = m1 = i1 = None
+        else:
+            z1, m1, i1, sc1, sh1, h, w = self._conv_bn(self.stem1, a0, B, h, w, train, "s1")
+            xp = ws.get("s1.pool", (B, h // 2, w // 2, 128), T)
+            call("crnn_bn_relu_maxpool", dt, ptr(z1), ptr(sc1), ptr(sh1), ptr(xp), B, h, w, 128, s)
         sv["stem"] = dict(x0=x0, z0=z0, m0=m0, i0=i0, sc0=sc0, sh0=sh0, a0=a0, z1=z1, m1=m1, i1=i1, sc1=sc1,
                           sh1=sh1, H=H, W=W, h1=h, w1=w)
         x, h, w = xp, h // 2, w // 2

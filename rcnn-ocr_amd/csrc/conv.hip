@@ -21,6 +21,9 @@ bool conv_halo_fits(const crnn_conv_desc* d, bool dgrad);
 int conv_halo_fwd(const crnn_conv_desc* d, const void* x, const void* w, void* y, float* psum, float* psq,
                   hipStream_t st, const float* esc = nullptr, const float* esh = nullptr);
 int conv_halo_dgrad(const crnn_conv_desc* d, const void* dy, const void* w, void* dx, hipStream_t st);
+bool conv_halo_pool_fits(const crnn_conv_desc* d);
+int conv_halo_fwd_pool(const crnn_conv_desc* d, const void* x, const void* w, void* y, const float* esc,
+                       const float* esh, hipStream_t st);
 int conv_halo_wgrad_slabs(const crnn_conv_desc* d);
 int conv_halo_wgrad(const crnn_conv_desc* d, const void* dy, const void* x, float* ws, hipStream_t st);
 static bool use_halo(int dtype, const crnn_conv_desc* d, bool dgrad) {
@@ -982,6 +985,18 @@ int crnn_conv_dgrad(int dtype, const crnn_conv_desc* d, const void* dy, const vo
   if (dres == nullptr && !accumulate && use_halo(dtype, d, true)) return conv_halo_dgrad(d, dy, w, dx, st);
   return dtype == CRNN_BF16 ? conv_dgrad_t<bf16>(d, dy, w, dx, dres, yres, accumulate, st)
                             : conv_dgrad_t<float>(d, dy, w, dx, dres, yres, accumulate, st);
+}
+
+int crnn_conv_fwd_bnrelu_pool_supported(int dtype, const crnn_conv_desc* d) {
+  return dtype == CRNN_BF16 && use_halo(dtype, d, false) && conv_halo_pool_fits(d) ? 1 : 0;
+}
+
+int crnn_conv_fwd_bnrelu_pool(int dtype, const crnn_conv_desc* d, const void* x, const void* w, void* y,
+                              const float* scale, const float* shift, void* stream) {
+  if (!crnn_conv_fwd_bnrelu_pool_supported(dtype, d))
+    return crnn_set_error(hipErrorInvalidValue, "conv_fwd_bnrelu_pool: not the halo stem geometry");
+  if (scale == nullptr || shift == nullptr) return crnn_set_error(hipErrorInvalidValue, "conv_fwd_bnrelu_pool: null affine");
+  return conv_halo_fwd_pool(d, x, w, y, scale, shift, (hipStream_t)stream);
 }
 
 int crnn_conv_dgrad_ds_supported(int dtype, const crnn_conv_desc* d, const crnn_conv_desc* dds) {

@@ -41,7 +41,7 @@ template <int CI> struct Ring {
 // FLIP = false: y = conv(x, W), W packed [CO][3][3][CI] (conv.hip's OHWI pack).
 // FLIP = true : dx = conv(dy, W'), W'[o][t][c] = W[c][8 - t][o], read from the forward pack
 //               [CI][3][3][CO] (CI = forward Co, CO = forward Ci).
-template <int CI, int CO, bool FLIP>
+template <int CI, int CO, bool FLIP, bool POOL = false>
 __global__ __launch_bounds__(512) void halo3x3_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wp,
                                                       bf16* __restrict__ y, float* __restrict__ psum,
                                                       float* __restrict__ psq, int H, int W, int RB, uint32_t xbytes,
@@ -141,6 +141,9 @@ __global__ __launch_bounds__(512) void halo3x3_kernel(const bf16* __restrict__ x
   __syncthreads();
 
   const uint32_t abase = (uint32_t)((pw * 64 + c) * R::PITCH + (TAPK ? 0 : 16 * g));
+  // POOL: the even row's activations (bf16: rounding is monotonic, so max and rounding commute) in
+  // this lane's slice of LDS, max-combined with the odd row's (same lane: no barrier)
+  __shared__ __attribute__((aligned(16))) bf16 keep[POOL ? 512 * MI * NJ * 4 : 4];
   for (int yy = r0; yy < r0 + RB; ++yy) {
     load_row(yy + 2);  // lands while this row computes; stored to the free slot below
     f32x4 acc[MI][NJ];
@@ -196,11 +199,39 @@ __global__ __launch_bounds__(512) void halo3x3_kernel(const bf16* __restrict__ x
         }
       }
     }
+    if constexpr (POOL) {
+      // eval inference (stem, model/seresnet31.py:81-89): BN -> ReLU -> 2x2 max-pool in the epilogue;
+      // rows yy, yy+1 of a window are consecutive rows of this band (r0, RB even), pixels 2p, 2p+1
+      // are lanes c, c^1 of one fragment row: y is the pooled [B][H/2][W/2][CO] map
+      bf16* kp = keep + (size_t)threadIdx.x * (MI * NJ * 4);
+      if ((yy & 1) == 0) {
 #pragma unroll
-    for (int i = 0; i < MI; ++i)
+        for (int i = 0; i < MI; ++i)
 #pragma unroll
-      for (int j = 0; j < NJ; ++j)
-        st4<bf16>(y + (m0 + pw * 64 + 16 * i + c) * CO + cw * CW + 16 * j + 4 * g, acc[i][j]);
+          for (int j = 0; j < NJ; ++j) st4<bf16>(kp + (i * NJ + j) * 4, acc[i][j]);
+      } else {
+        const size_t p0 = ((size_t)b * (H / 2) + (yy >> 1)) * (W / 2) + (x0 >> 1);
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) {
+            f32x4 v;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float a = fmaxf(acc[i][j][r], (float)kp[(i * NJ + j) * 4 + r]);
+              v[r] = fmaxf(a, __shfl_xor(a, 1));
+            }
+            if ((c & 1) == 0)
+              st4<bf16>(y + (p0 + ((pw * 64 + 16 * i + c) >> 1)) * CO + cw * CW + 16 * j + 4 * g, v);
+          }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+          st4<bf16>(y + (m0 + pw * 64 + 16 * i + c) * CO + cw * CW + 16 * j + 4 * g, acc[i][j]);
+    }
 
     if (psum != nullptr) {
       // BN partial statistics: (sum, M2 about the partial mean) of this wave's 64 pixels, one
@@ -427,6 +458,22 @@ int conv_halo_fwd(const crnn_conv_desc* d, const void* x, const void* w, void* y
   else
     hipLaunchKernelGGL((halo3x3_kernel<64, 128, false>), grid, dim3(512), 0, st, (const bf16*)x, (const bf16*)w,
                        (bf16*)y, psum, psq, d->Hi, d->Wi, rb, xbytes, esc, esh);
+  return (int)hipGetLastError();
+}
+
+bool conv_halo_pool_fits(const crnn_conv_desc* d) {
+  return d->Ci == 64 && d->Co == 128 && d->Hi % 2 == 0 && d->Wi % 2 == 0 && band_rows(d->Hi, d->Ci) % 2 == 0;
+}
+
+// eval stem: conv -> BN (running statistics) -> ReLU -> 2x2 max-pool in one launch, y = the pooled map
+int conv_halo_fwd_pool(const crnn_conv_desc* d, const void* x, const void* w, void* y, const float* esc,
+                       const float* esh, hipStream_t st) {
+  const int rb = band_rows(d->Hi, d->Ci);
+  if (d->Ci != 64 || d->Hi % 2 || d->Wi % 2 || rb % 2) return crnn_set_error(hipErrorInvalidValue, "halo pool: shape");
+  const dim3 grid(d->B * (d->Wi / TW) * (d->Hi / rb));
+  const uint32_t xbytes = (uint32_t)((size_t)d->B * d->Hi * d->Wi * d->Ci * 2);
+  hipLaunchKernelGGL((halo3x3_kernel<64, 128, false, true>), grid, dim3(512), 0, st, (const bf16*)x,
+                     (const bf16*)w, (bf16*)y, (float*)nullptr, (float*)nullptr, d->Hi, d->Wi, rb, xbytes, esc, esh);
   return (int)hipGetLastError();
 }
 
