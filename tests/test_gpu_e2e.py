@@ -356,7 +356,9 @@ def test_eval_fused_conv_bn_relu_matches_unfused(dtype, tol):
             ref = m32(x).float().cpu()
         e_f = float((out[0] - ref).norm() / ref.norm())
         e_u = float((out[1] - ref).norm() / ref.norm())
-        assert e_f < tol and e_f <= 1.1 * e_u + 1e-3, (e_f, e_u, err)
+        # (which path lands closer after 28 bf16 layers is noise; per-kernel rounding is pinned
+        # exactly in test_gpu_kernels.py::test_halo_eval_bnrelu_epilogue)
+        assert e_f < tol and e_f <= 1.5 * e_u, (e_f, e_u, err)
     # the eval affine is cached between forwards: an in-place edit of a running statistic, a
     # training forward and an optimizer-style parameter edit must each be seen by the next eval
     model._engine.eval_fuse = True

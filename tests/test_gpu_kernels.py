@@ -70,6 +70,50 @@ CONVS_DEEP = [
 ]
 
 
+@pytest.mark.parametrize("pool", [False, True])
+def test_halo_eval_bnrelu_epilogue(pool):
+    """the stem conv (halo kernel) with the eval BN affine + ReLU (+ 2x2 max-pool) in its epilogue
+    (crnn_conv_fwd_bnrelu / crnn_conv_fwd_bnrelu_pool) vs torch fp32: within bf16 rounding per
+    element (one rounding, of the final value), and no further from fp32 than the unfused
+    conv -> bn_relu_maxpool path (which also rounds z)."""
+    L = _L()
+    B, Ci, H, W, Co = 3, 64, 8, 256, 128
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(B, Ci, H, W, generator=g).bfloat16().float()
+    w = (torch.randn(Co, Ci, 3, 3, generator=g) / 24).bfloat16().float()
+    sc = torch.rand(Co, generator=g) + 0.5
+    sh = torch.randn(Co, generator=g) * 0.3
+    ref = torch.relu(F.conv2d(x, w, padding=1) * sc[None, :, None, None] + sh[None, :, None, None])
+    if pool:
+        ref = F.max_pool2d(ref, 2)
+    ref = ref.permute(0, 2, 3, 1).contiguous()
+    dt = L.BF16
+    d = L.ConvDesc(B, H, W, Ci, H, W, Co, 3, 3, 1, 1, 1, 1, Ci)
+    st = L.stream_ptr()
+    xd = to_nhwc(x, None, torch.bfloat16)
+    wd = torch.empty(Co, 3, 3, Ci, dtype=torch.bfloat16, device=DEV)
+    L.call("crnn_pack_conv_weight", dt, w.to(DEV).data_ptr(), wd.data_ptr(), Co, Ci, 3, 3, Ci, st)
+    scd, shd = sc.to(DEV), sh.to(DEV)
+    out = torch.empty(ref.shape, dtype=torch.bfloat16, device=DEV)
+    if pool:
+        assert L.lib().crnn_conv_fwd_bnrelu_pool_supported(dt, d) == 1
+        L.call("crnn_conv_fwd_bnrelu_pool", dt, d, xd.data_ptr(), wd.data_ptr(), out.data_ptr(), scd.data_ptr(),
+               shd.data_ptr(), st)
+    else:
+        L.call("crnn_conv_fwd_bnrelu", dt, d, xd.data_ptr(), wd.data_ptr(), out.data_ptr(), scd.data_ptr(),
+               shd.data_ptr(), st)
+    z = torch.empty(B, H, W, Co, dtype=torch.bfloat16, device=DEV)
+    L.call("crnn_conv_fwd", dt, d, xd.data_ptr(), wd.data_ptr(), z.data_ptr(), None, None, st)
+    unf = torch.empty(ref.shape, dtype=torch.bfloat16, device=DEV)
+    if pool:
+        L.call("crnn_bn_relu_maxpool", dt, z.data_ptr(), scd.data_ptr(), shd.data_ptr(), unf.data_ptr(), B, H, W, Co, st)
+    else:
+        L.call("crnn_bn_act", dt, z.data_ptr(), scd.data_ptr(), shd.data_ptr(), unf.data_ptr(), B * H * W, Co, 1, st)
+    got, unf = out.float().cpu(), unf.float().cpu()
+    assert float(((got - ref).abs() - (ref.abs() * 2 ** -8 + 1e-3)).max()) <= 0, "fused epilogue off by more than bf16 rounding"
+    assert relerr(got, ref) <= relerr(unf, ref) * 1.05 + 1e-6
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("geo", [(4, 128, 16, 32, 256), (3, 256, 8, 64, 512), (256, 128, 16, 128, 256)])
 def test_conv_dgrad_ds_fused(geo, dtype):
