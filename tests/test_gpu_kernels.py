@@ -773,6 +773,37 @@ def test_greedy_decode_golden(itos):
     assert texts == ref["texts"]
 
 
+@pytest.mark.parametrize("shape", [(256, 32, 194), (3, 130, 37), (5, 1, 300), (7, 64, 194), (1, 200, 5)])
+def test_greedy_kernel_vs_oracle(shape):
+    """crnn_ctc_greedy (workgroup per sample, frames in parallel, ballot collapse) against the
+    oracle's argmax + collapse (training/utils.py:122-150): ids, lens and the zero padding past
+    each length. Coarse logits give exact ties (first index wins) and long runs of repeats and
+    blanks; T = 130 / 200 cross the 64-frame collapse chunks; a padded row stride (ldc > C)."""
+    L = _L()
+    import crnn_oracle as O
+    B, T, C = shape
+    g = torch.Generator().manual_seed(B * 1000 + T)
+    lg = torch.randint(0, 4, (B, T, C), generator=g).float()
+    lg[:, :, 0] += torch.randint(0, 3, (B, T), generator=g).float()           # frequent blanks
+    rep = torch.rand(B, T, generator=g) < 0.4                                  # repeated frames
+    for t in range(1, T):
+        lg[:, t][rep[:, t]] = lg[:, t - 1][rep[:, t]]
+    ldc = C + 3
+    pad = torch.full((B, T, ldc), 1e30)
+    pad[:, :, :C] = lg
+    dev = pad.to(DEV)
+    ids = torch.full((B, T), -7, dtype=torch.int32, device=DEV)
+    lens = torch.full((B,), -7, dtype=torch.int32, device=DEV)
+    L.call("crnn_ctc_greedy", dev.data_ptr(), ldc, B, T, C, ids.data_ptr(), lens.data_ptr(), L.stream_ptr())
+    torch.cuda.synchronize()
+    want = O.greedy_decode(lg.numpy())
+    ids_h, lens_h = ids.cpu(), lens.cpu().tolist()
+    assert lens_h == [len(w) for w in want]
+    for b in range(B):
+        assert ids_h[b, : lens_h[b]].tolist() == want[b]
+        assert bool((ids_h[b, lens_h[b]:] == 0).all())
+
+
 @pytest.mark.parametrize("offset", [0, 1])
 def test_adamw_vs_oracle(offset):
     """offset 0: 16-B aligned buffers (vector kernel + n % 4 tail); 1: misaligned (scalar kernel)"""
