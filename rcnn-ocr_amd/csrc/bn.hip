@@ -883,6 +883,13 @@ __global__ void nchw_to_nhwc_kernel(const float* __restrict__ x, T* __restrict__
   const long n = (long)B * H * W;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     long b = i / ((long)H * W), hw = i - b * H * W;
+    if (Cp == 8 && C <= 8) {   // the encoder input: one 16-B (bf16) / 32-B (fp32) vector store per pixel
+      float v[8];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) v[c] = c < C ? x[(b * C + c) * H * W + hw] : 0.f;
+      st8<T>(y + i * 8, pack8<T>(v));
+      continue;
+    }
     for (int c = 0; c < Cp; ++c) {
       float v = c < C ? x[(b * C + c) * H * W + hw] : 0.f;
       y[i * Cp + c] = fromf<T>(v);

@@ -773,6 +773,24 @@ def test_greedy_decode_golden(itos):
     assert texts == ref["texts"]
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("C,Cp", [(3, 8), (1, 8), (3, 16)])
+def test_nchw_to_nhwc_pad(dtype, C, Cp):
+    """crnn_nchw_to_nhwc (the encoder's input layout, engine.py): NCHW fp32 -> [B][H][W][Cp] in the
+    compute dtype, channels >= C zero; the Cp = 8 vector-store path and the generic loop."""
+    L = _L()
+    g = torch.Generator().manual_seed(C * 100 + Cp)
+    B, H, W = 3, 5, 37
+    x = torch.randn(B, C, H, W, generator=g)
+    want = torch.zeros(B, H, W, Cp)
+    want[..., :C] = x.permute(0, 2, 3, 1)
+    y = torch.full((B, H, W, Cp), 7.0, dtype=dtype, device=DEV)
+    xd = x.to(DEV)
+    L.call("crnn_nchw_to_nhwc", L.dtype_code(dtype), xd.data_ptr(), y.data_ptr(), B, C, H, W, Cp, L.stream_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(y.cpu(), want.to(dtype))
+
+
 @pytest.mark.parametrize("shape", [(256, 32, 194), (3, 130, 37), (5, 1, 300), (7, 64, 194), (1, 200, 5)])
 def test_greedy_kernel_vs_oracle(shape):
     """crnn_ctc_greedy (workgroup per sample, frames in parallel, ballot collapse) against the
