@@ -433,7 +433,8 @@ int crnn_ctc_loss(const float* logits, int ldc, int B, int T, int C, const int* 
 /* mean_b(loss_b / max(len_b,1)) -> out[0] */
 int crnn_ctc_reduce_mean(const float* loss, const int* lengths, int B, float* out, void* stream);
 /* greedy decode (training/utils.py:122-150 semantics, explicit [B][T] layout):
- * ids [B][T] collapsed labels (blank & repeats removed), lens [B] */
+ * ids [B][T] collapsed labels (blank & repeats removed, zero past lens[b]), lens [B];
+ * logits rows have stride ldc >= C; T <= 16384 (the per-sample argmax row lives in LDS) */
 int crnn_ctc_greedy(const float* logits, int ldc, int B, int T, int C, int* ids, int* lens, void* stream);
 
 /* ------------------------------------------------------------------ optimiser */
