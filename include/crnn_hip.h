@@ -239,6 +239,12 @@ int crnn_se_pool_partials(const float* psum, int rows, long rows_per_partial, co
                           const float* shift, float* pooled, int B, int HW, int C, void* stream);
 /* hid = relu(pooled W1^T) [B][Cr]; s = sigmoid(hid W2^T) [B][C] (fp32; W1 [Cr][C], W2 [C][Cr]) */
 int crnn_se_mlp_fwd(const float* pooled, const float* w1, const float* w2, float* hid, float* s, int B, int C, int Cr, void* stream);
+/* crnn_se_pool_partials + crnn_se_mlp_fwd in ONE launch (the squeeze computed in the excitation
+ * kernel's load stage, same arithmetic: pooled / hid / s bit-identical to the pair); pooled is
+ * still written (the backward reads it). model/seresnet31.py:22-40 */
+int crnn_se_pool_mlp_fwd(const float* psum, int rows, long rows_per_partial, const float* scale, const float* shift,
+                         float* pooled, const float* w1, const float* w2, float* hid, float* s, int B, int HW, int C,
+                         int Cr, void* stream);
 /* y = relu((z2*scale+shift)*s[b][c] + idn'), idn' = idn*iscale+ishift if iscale else idn */
 int crnn_se_residual_fwd(int dtype, const void* z2, const float* scale, const float* shift, const float* s,
                          const void* idn, const float* iscale, const float* ishift, void* y, int B, int HW, int C, void* stream);

@@ -91,6 +91,7 @@ _SIGS = {
     "crnn_se_bn_bwd_reduce": ([i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, vp], i32),
     "crnn_se_bn_partials": ([vp, vp, vp, vp, vp, i32, i32, i32, vp], i32),
     "crnn_se_mlp_fwd": ([vp, vp, vp, vp, vp, i32, i32, i32, vp], i32),
+    "crnn_se_pool_mlp_fwd": ([vp, i32, i64, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, vp], i32),
     "crnn_se_residual_fwd": ([i32, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, vp], i32),
     "crnn_se_bwd_reduce": ([i32, vp, vp, vp, vp, vp, vp, i32, i32, i32, vp], i32),
     "crnn_se_mlp_bwd": ([vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, vp], i32),

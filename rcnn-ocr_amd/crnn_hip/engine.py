@@ -578,13 +578,14 @@ class CRNNEngine:
             hid = ws.get(tag + ".hid", (B, Cr), torch.float32)
             se = ws.get(tag + ".s", (B, P), torch.float32)
             lp = self._last_partials if train or fuse else None
+            w1, w2 = self.p[blk.prefix + ".se.fc.0.weight"], self.p[blk.prefix + ".se.fc.2.weight"]
             if lp is not None and HW % lp[2] == 0 and lp[1] * lp[2] == B * HW:
-                # squeeze from conv2's BN partial sums (no pass over z2)
-                call("crnn_se_pool_partials", ptr(lp[0]), lp[1], lp[2], ptr(bs2), ptr(bh2), ptr(pooled), B, HW, P, s)
+                # squeeze from conv2's BN partial sums (no pass over z2), fused into the excitation launch
+                call("crnn_se_pool_mlp_fwd", ptr(lp[0]), lp[1], lp[2], ptr(bs2), ptr(bh2), ptr(pooled), ptr(w1),
+                     ptr(w2), ptr(hid), ptr(se), B, HW, P, Cr, s)
             else:
                 call("crnn_se_pool", dt, ptr(z2), ptr(bs2), ptr(bh2), ptr(pooled), B, HW, P, s)
-            call("crnn_se_mlp_fwd", ptr(pooled), ptr(self.p[blk.prefix + ".se.fc.0.weight"]),
-                 ptr(self.p[blk.prefix + ".se.fc.2.weight"]), ptr(hid), ptr(se), B, P, Cr, s)
+                call("crnn_se_mlp_fwd", ptr(pooled), ptr(w1), ptr(w2), ptr(hid), ptr(se), B, P, Cr, s)
             dsv = None
             if blk.ds is not None:
                 zd, dm, di, dsc, dsh, _, _ = self._conv_bn(blk.ds, x, B, h, w, train, tag + ".ds")

@@ -608,10 +608,21 @@ __device__ __forceinline__ void reduce_scatter32(float (&v)[32], int lane) {
 
 __device__ __forceinline__ float dot4(f32x4 a, f32x4 b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2] + a[3] * b[3]; }
 
-template <int C>
+// the squeeze from conv2's BN partial sums (crnn_se_pool_partials' arithmetic, same order), computed
+// in the excitation kernel's load stage when FP: psum [B * per_b][C] rows, pooled written out for
+// the backward
+struct SePoolSrc {
+  const float* psum;
+  const float* scale;
+  const float* shift;
+  float* pooled;
+  int per_b, HW;
+};
+
+template <int C, bool FP = false>
 __global__ __launch_bounds__(256) void se_mlp_fwd_kernel(const float* __restrict__ pooled, const float* __restrict__ w1,
                                                          const float* __restrict__ w2, float* __restrict__ hid,
-                                                         float* __restrict__ s, int B) {
+                                                         float* __restrict__ s, int B, SePoolSrc src = {}) {
   constexpr int Cr = C / 16, KC = C / 256;   // KC: 16-B column pieces per lane per w1 row
   __shared__ __attribute__((aligned(16))) float p[SE_SB][C];
   __shared__ __attribute__((aligned(16))) float h[SE_SB][Cr];
@@ -620,7 +631,17 @@ __global__ __launch_bounds__(256) void se_mlp_fwd_kernel(const float* __restrict
 #pragma unroll
   for (int q = 0; q < SE_SB * C / 1024; ++q) {
     const int i = 4 * tid + 1024 * q, sb = i / C;
-    const f32x4 v = *reinterpret_cast<const f32x4*>(pooled + (size_t)(b0 + min(sb, nb - 1)) * C + i % C);
+    const int bb = b0 + min(sb, nb - 1), c = i % C;
+    f32x4 v;
+    if constexpr (FP) {
+      f32x4 a = {0.f, 0.f, 0.f, 0.f};
+      for (int k = 0; k < src.per_b; ++k) a += *reinterpret_cast<const f32x4*>(src.psum + ((size_t)bb * src.per_b + k) * C + c);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = src.scale[c + r] * (a[r] / (float)src.HW) + src.shift[c + r];
+      if (sb < nb) *reinterpret_cast<f32x4*>(src.pooled + (size_t)bb * C + c) = v;
+    } else {
+      v = *reinterpret_cast<const f32x4*>(pooled + (size_t)bb * C + c);
+    }
     *reinterpret_cast<f32x4*>(&p[0][0] + i) = sb < nb ? v : f32x4{0.f, 0.f, 0.f, 0.f};
   }
   __syncthreads();
@@ -1597,6 +1618,23 @@ int crnn_se_pool_partials(const float* psum, int rows, long rows_per_partial, co
     return crnn_set_error(hipErrorInvalidValue, "se_pool_partials: partial rows must tile every sample");
   hipLaunchKernelGGL(se_pool_partials_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, psum,
                      (int)(HW / rows_per_partial), scale, shift, pooled, HW, C);
+  return (int)hipGetLastError();
+}
+
+int crnn_se_pool_mlp_fwd(const float* psum, int rows, long rows_per_partial, const float* scale, const float* shift,
+                         float* pooled, const float* w1, const float* w2, float* hid, float* s, int B, int HW, int C,
+                         int Cr, void* stream) {
+  if (rows_per_partial <= 0 || HW % rows_per_partial || (long)rows * rows_per_partial != (long)B * HW)
+    return crnn_set_error(hipErrorInvalidValue, "se_pool_mlp_fwd: partial rows must tile every sample");
+  if (Cr * 16 != C || (C != 256 && C != 512)) return crnn_set_error(hipErrorInvalidValue, "se_pool_mlp_fwd: C in {256, 512}, Cr = C/16");
+  const SePoolSrc src{psum, scale, shift, pooled, (int)(HW / rows_per_partial), HW};
+  const dim3 grid((B + SE_SB - 1) / SE_SB);
+  if (C == 256)
+    hipLaunchKernelGGL((se_mlp_fwd_kernel<256, true>), grid, dim3(256), 0, (hipStream_t)stream, nullptr, w1, w2, hid, s,
+                       B, src);
+  else
+    hipLaunchKernelGGL((se_mlp_fwd_kernel<512, true>), grid, dim3(256), 0, (hipStream_t)stream, nullptr, w1, w2, hid, s,
+                       B, src);
   return (int)hipGetLastError();
 }
 

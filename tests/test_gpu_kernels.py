@@ -773,6 +773,45 @@ def test_greedy_decode_golden(itos):
     assert texts == ref["texts"]
 
 
+@pytest.mark.parametrize("C,B,HW,rpp", [(256, 5, 64, 16), (512, 256, 32, 8), (512, 7, 128, 128), (256, 4, 96, 32)])
+def test_se_pool_mlp_fwd_fused_bit_identical(C, B, HW, rpp):
+    """crnn_se_pool_mlp_fwd (squeeze from conv2's BN partial sums inside the excitation launch)
+    against the crnn_se_pool_partials + crnn_se_mlp_fwd pair: pooled, hid and s bit-identical,
+    ragged B (not a multiple of the 4 samples per block) included; and against torch fp32 of
+    SELayer (model/seresnet31.py:5-20) on the pooled values."""
+    L = _L()
+    g = torch.Generator().manual_seed(C + B + HW)
+    Cr = C // 16
+    rows = B * HW // rpp
+    psum = torch.randn(rows, C, generator=g).to(DEV) * rpp
+    sc, sh = (torch.rand(C, generator=g) + 0.5).to(DEV), (torch.randn(C, generator=g) * 0.2).to(DEV)
+    w1 = (torch.randn(Cr, C, generator=g) * C ** -0.5).to(DEV)
+    w2 = (torch.randn(C, Cr, generator=g) * Cr ** -0.5).to(DEV)
+    st = L.stream_ptr()
+    out = []
+    for fused in (False, True):
+        pooled = torch.full((B, C), float("nan"), device=DEV)
+        hid = torch.full((B, Cr), float("nan"), device=DEV)
+        s = torch.full((B, C), float("nan"), device=DEV)
+        if fused:
+            L.call("crnn_se_pool_mlp_fwd", psum.data_ptr(), rows, rpp, sc.data_ptr(), sh.data_ptr(), pooled.data_ptr(),
+                   w1.data_ptr(), w2.data_ptr(), hid.data_ptr(), s.data_ptr(), B, HW, C, Cr, st)
+        else:
+            L.call("crnn_se_pool_partials", psum.data_ptr(), rows, rpp, sc.data_ptr(), sh.data_ptr(), pooled.data_ptr(),
+                   B, HW, C, st)
+            L.call("crnn_se_mlp_fwd", pooled.data_ptr(), w1.data_ptr(), w2.data_ptr(), hid.data_ptr(), s.data_ptr(),
+                   B, C, Cr, st)
+        torch.cuda.synchronize()
+        out.append((pooled.cpu(), hid.cpu(), s.cpu()))
+    for a, b in zip(*out):
+        assert torch.equal(a, b)
+    pooled = out[1][0]
+    want_pool = sc.cpu() * (psum.cpu().view(B, HW // rpp, C).sum(1) / HW) + sh.cpu()
+    assert relerr(pooled, want_pool) < 1e-5
+    want_s = torch.sigmoid(torch.relu(pooled @ w1.cpu().t()) @ w2.cpu().t())
+    assert relerr(out[1][2], want_s) < 1e-5
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("C,Cp", [(3, 8), (1, 8), (3, 16)])
 def test_nchw_to_nhwc_pad(dtype, C, Cp):
