@@ -39,8 +39,13 @@ def parse():
     ap.add_argument("--layers", type=int, default=2)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample", type=int, default=32, help="batch of the CPU baseline sample")
-    ap.add_argument("--cpu-steps", type=int, default=6)
+    ap.add_argument("--cpu-sample", type=int, default=None,
+                    help="batch of the CPU baseline sample (default: the bench batch, B=256, as BASELINE.md)")
+    ap.add_argument("--cpu-steps", type=int, default=1, help="timed CPU steps (after one warm-up at B=32)")
+    ap.add_argument("--path", default="api", choices=["api", "engine"],
+                    help="train mode: api = the reference user's path (RCNN forward -> crnn_hip.ctc_loss -> "
+                         "loss.backward() -> optimizer.step(), model/model.py:223-227, training/train.py:493-518); "
+                         "engine = CRNNEngine forward / ctc / backward called directly (A/B of the API overhead)")
     ap.add_argument("--mode", default="train", choices=["train", "infer", "attn", "attn_train", "preprocess"],
                     help="train: BASELINE configs[2]/[3] (the headline); infer: configs[1] (eval forward + greedy "
                          "CTC decode on device); attn: eval encode + the reference's attention head, 26-step greedy "
@@ -61,14 +66,43 @@ def parse():
     return a
 
 
-def cpu_baseline(args, threads, attn_params=None):
-    """oracle (CPU fp32 restatement, 'port') train step / inference on a bounded sample."""
+def usable_cpus():
+    """host cores this process may use: the affinity mask, capped by a cgroup CPU quota (on the GPU
+    box os.cpu_count() reports the whole machine, while the job gets a share of it)"""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline(args, threads, shapes, attn_params=None):
+    """oracle (CPU fp32 restatement, 'port') train step / inference on a bounded sample: the bench's
+    own batch (B=256 by default) after one B=32 warm-up step; the CTC loss is torch's
+    F.ctc_loss (CPU) as the reference path would call it."""
     import crnn_oracle as O
     from crnn_hip.recipe import recipe_state_dict, synthetic_batch
     torch.set_num_threads(threads)
     C = 194
     T = args.width // 8
-    sd = recipe_state_dict(O.param_shapes(args.hidden, C, args.layers), 0)
+    B = args.cpu_sample or args.batch
+    sd = recipe_state_dict(shapes, 0)
     p = {k: (v.clone().requires_grad_(True) if v.is_floating_point() and "running" not in k else v)
          for k, v in sd.items()}
     ap = None
@@ -77,10 +111,13 @@ def cpu_baseline(args, threads, attn_params=None):
     params = [v for v in p.values() if getattr(v, "requires_grad", False)]
     params += [v for v in (ap or {}).values() if v.requires_grad]
     opt = torch.optim.AdamW(params, lr=1e-4)
-    x, _, tg, tl = synthetic_batch(args.cpu_sample, args.height, args.width, T, C, seed=99)
-    text, ty = attn_text(tg, tl, args.cpu_sample)
 
-    def step():
+    def ctc(logits, tg, tl):
+        lp = torch.nn.functional.log_softmax(logits, -1).permute(1, 0, 2)
+        il = torch.full((logits.shape[0],), logits.shape[1], dtype=torch.long)
+        return torch.nn.functional.ctc_loss(lp, tg, il, tl, blank=0, reduction="mean", zero_infinity=True)
+
+    def step(x, tg, tl, text, ty):
         if args.mode == "attn":
             with torch.no_grad():
                 O.attn_greedy(attn_params, O.encode(x, p, O.Ctx(train=False), args.layers), 26, 1, 3, C)
@@ -97,19 +134,29 @@ def cpu_baseline(args, threads, attn_params=None):
             return
         opt.zero_grad(set_to_none=True)
         logits = O.head(O.encode(x, p, O.Ctx(train=True), args.layers), p)
-        O.ctc_loss(logits, tg, tl).backward()
+        ctc(logits, tg, tl).backward()
         opt.step()
 
-    step()  # warm-up
+    def batch(n, seed):
+        x, _, tg, tl = synthetic_batch(n, args.height, args.width, T, C, seed=seed)
+        return (x, tg, tl) + attn_text(tg, tl, n)
+
+    step(*batch(min(32, B), 98))  # warm-up
+    data = batch(B, 99)
     t0 = time.perf_counter()
     for _ in range(args.cpu_steps):
-        step()
+        step(*data)
     dt = time.perf_counter() - t0
-    return {"value": round(args.cpu_sample * args.cpu_steps / dt, 3), "unit": "text-lines/s",
-            "cores": threads, "kind": "port",
-            "sample": f"oracle/crnn_oracle.py fp32 torch-CPU {'train step (fwd + teacher-forced attention decode + CE + bwd + AdamW)' if args.mode == 'attn_train' else 'eval encode + 26-step greedy attention decode' if args.mode == 'attn' else 'eval forward + argmax' if args.mode == 'infer' else 'train step (fwd + numpy CTC + bwd + AdamW)'}, "
-                      f"B={args.cpu_sample} x {args.cpu_steps} steps (+1 warm-up) at {args.height}x{args.width}, "
-                      f"hidden {args.hidden}; {dt:.1f} s"}
+    what = ("train step (fwd + teacher-forced attention decode + CE + bwd + AdamW)" if args.mode == "attn_train"
+            else "eval encode + 26-step greedy attention decode" if args.mode == "attn"
+            else "eval forward + argmax" if args.mode == "infer"
+            else "train step (fwd + F.ctc_loss + bwd + AdamW)")
+    return {"value": round(B * args.cpu_steps / dt, 3), "unit": "text-lines/s", "cores": threads,
+            "cpu_model": cpu_model(), "kind": "port",
+            "sample": f"oracle/crnn_oracle.py fp32 torch-CPU {what}, B={B} x {args.cpu_steps} timed step(s) "
+                      f"(+1 warm-up step at B={min(32, B)}) at {args.height}x{args.width}, hidden {args.hidden}, "
+                      f"{args.layers} BiLSTM layers; {dt:.1f} s; torch.set_num_threads({threads}) = the cores "
+                      f"this process may use (os.cpu_count() = {os.cpu_count()} on this host)"}
 
 
 def attn_text(tg, tl, B, steps=26, sos=1, eos=2):
@@ -130,14 +177,20 @@ def attn_text(tg, tl, B, steps=26, sos=1, eos=2):
 
 
 def pmc_traffic():
-    """latest committed PMC summary (tools/gpu_pmc.sh + tools/pmc_traffic.py -> profiles/*_pmc_traffic.json):
-    measured HBM bytes per launch of the hot kernels; None when absent."""
+    """the committed PMC summary (tools/gpu_pmc.sh + tools/pmc_traffic.py -> profiles/*_pmc_traffic.json)
+    taken on THIS source tree: measured HBM bytes per launch of the hot kernels. A summary whose
+    source_hash differs from the running tree's (crnn_hip._lib.source_hash) is stale and not used:
+    -> (None, reason)."""
     import glob
+    from crnn_hip._lib import source_hash
+    want = source_hash()
     fs = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_traffic.json")))
-    if not fs:
-        return None, None
-    with open(fs[-1]) as f:
-        return json.load(f), os.path.relpath(fs[-1], REPO)
+    for f in reversed(fs):
+        with open(f) as fh:
+            d = json.load(fh)
+        if d.get("source_hash") == want:
+            return d, os.path.relpath(f, REPO)
+    return None, f"no profiles/*_pmc_traffic.json taken on this tree (source_hash {want})"
 
 
 def lstm_roofline(lstm, args, eng, tsteps):
@@ -231,7 +284,7 @@ def bench_preprocess(args, world, rank, dev):
         }
         if world == 1 and not args.no_cpu_baseline:
             import preprocess_oracle as P
-            sample = crops[: max(1, args.cpu_sample // 4)]
+            sample = crops[: max(1, (args.cpu_sample or 32) // 4)]
             t1 = time.perf_counter()
             for im in sample:
                 P.preprocess(im, H, W)
@@ -253,7 +306,7 @@ def main():
     if args.mode == "preprocess":
         return bench_preprocess(args, world, rank, dev)
 
-    import crnn_oracle as O
+    from crnn_hip.ctc import ctc_loss
     from crnn_hip.optim import FusedAdamW
     from crnn_hip.recipe import recipe_state_dict, synthetic_batch
     from model.model import RCNN
@@ -264,7 +317,8 @@ def main():
     attn = args.mode in ("attn", "attn_train")
     model = RCNN(num_classes=C, hidden_size=args.hidden, blank_id=3 if attn else None, num_rnn_layers=args.layers,
                  compute_dtype=dtype, decoder="attn" if attn else "ctc")
-    model.load_state_dict(recipe_state_dict(O.param_shapes(args.hidden, C, args.layers), 0), strict=False)
+    shapes = [(k, tuple(v.shape)) for k, v in model.state_dict().items()]   # the model's own parameter table
+    model.load_state_dict(recipe_state_dict(shapes, 0), strict=False)
     model = model.to(dev).train(args.mode in ("train", "attn_train"))
     x, _, tg, tl = synthetic_batch(args.batch, args.height, args.width, T, C, seed=1234 + rank)
     x = x.to(dev)
@@ -281,6 +335,7 @@ def main():
     # DP: bucketed RCCL all-reduce of the flat gradient, issued stage by stage during the backward
     # (head / BiLSTM first, stem last) so it overlaps the remaining backward kernels
     reducer = D.OverlappedAllReduce(model._flat_grad, model.flat_offsets()) if world > 1 else None
+    model.stage_done = reducer.ready if reducer is not None else None   # the API path's backward hook
 
     ids = torch.empty(args.batch, T, dtype=torch.int32, device=dev)
     lens = torch.empty(args.batch, dtype=torch.int32, device=dev)
@@ -322,6 +377,14 @@ def main():
             return attn_train_step()
         if args.mode == "infer":
             return infer_step()
+        if args.path == "api":   # the reference user's step (training/train.py:493-518) on the drop-in API
+            opt.zero_grad(set_to_none=True)
+            loss = ctc_loss(model(x), tg, tl)
+            loss.backward()
+            if reducer is not None:
+                reducer.finish()
+            opt.step(grad_scale=inv_world)
+            return loss
         eng.forward(x, train=True, save_for_backward=True, dropout_p=model.enc_dropout.p)
         loss, dl = eng.ctc(eng.logits_padded(), tg, tl)
         eng.backward(dl, grads, accumulate=False, stage_done=reducer.ready if reducer else None)
@@ -372,7 +435,8 @@ def main():
         conv_flop = sum(v[2] for v in timing.values())
         achieved = conv_flop / (conv_ms * 1e-3) / 1e12 if conv_ms > 0 else 0.0
         pmc, src = pmc_traffic()
-        conv_traffic = conv_traffic_note = conv_mfma_busy = None
+        conv_traffic = conv_mfma_busy = None
+        conv_traffic_note = None if pmc else src
         if pmc and "conv" in pmc and args.mode == "train" and args.batch == 256 and args.width == 256 \
                 and dtype == torch.bfloat16:
             conv_traffic = pmc["conv"]["hbm_bytes_per_launch"]
@@ -419,6 +483,10 @@ def main():
                        "global_batch": args.batch * world, "per_gpu_batch": args.batch,
                        "crop": f"{args.height}x{args.width}", "seq_len": T, "hidden": args.hidden,
                        "rnn_layers": args.layers, "num_classes": C,
+                       **({"path": ("RCNN API: model(x) -> crnn_hip.ctc_loss -> loss.backward() -> "
+                                    "FusedAdamW.step()" if args.path == "api" else
+                                    "CRNNEngine forward / ctc / backward called directly")}
+                          if args.mode == "train" else {}),
                        "parallelism": f"dp{world}" if world > 1 else "single"},
             "roofline": {"bound": "mfma", "kernel": "implicit-GEMM conv (fwd+dgrad+wgrad, all 28 convs)",
                          "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
@@ -439,10 +507,10 @@ def main():
         }
         if world == 1 and not args.no_cpu_baseline:
             try:
-                threads = min(16, os.cpu_count() or 1)
+                threads = usable_cpus()
                 ap_cpu = ({k[5:]: v.detach().float().cpu() for k, v in model.state_dict().items()
                            if k.startswith("attn.")} if attn else None)
-                out["cpu_baseline"] = cpu_baseline(args, threads, ap_cpu)
+                out["cpu_baseline"] = cpu_baseline(args, threads, shapes, ap_cpu)
             except Exception as e:  # report, never fake
                 out["cpu_baseline"] = {"value": None, "error": repr(e)}
         print(json.dumps(out), flush=True)

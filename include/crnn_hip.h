@@ -17,7 +17,9 @@
  *   crnn_lstm_*            nn.LSTM(bidirectional, batch_first)               model/model.py:152-163
  *   crnn_gemm_*            nn.Linear (BiLSTM output, CTC head)                model/model.py:157,162
  *   crnn_ctc_*             F.ctc_loss(blank=0) / ctc_greedy_decoder            training/utils.py:122-162
+ *   crnn_adam_step         torch.optim.Adam (L2) / AdamW step                 training/train.py:292-295
  *   crnn_adamw             torch.optim.AdamW step                             training/train.py:294-295
+ *   crnn_sgd_step          torch.optim.SGD(momentum) step                     training/train.py:296-299
  *
  * Conventions
  *   - dtype: CRNN_F32 (parity mode, exact-f32 MFMA) or CRNN_BF16 (perf mode,
@@ -444,7 +446,23 @@ int crnn_ctc_reduce_mean(const float* loss, const int* lengths, int B, float* ou
 int crnn_ctc_greedy(const float* logits, int ldc, int B, int T, int C, int* ids, int* lens, void* stream);
 
 /* ------------------------------------------------------------------ optimiser */
-/* fused AdamW over a flat fp32 buffer; g is multiplied by grad_scale first (DP averaging). */
+/* fused Adam / AdamW over a flat fp32 buffer (one launch; replaces torch.optim.Adam / AdamW,
+ * training/train.py:292-295): g is multiplied by grad_scale first (DP averaging); coupled = 1 is
+ * torch.optim.Adam's L2 decay (g += weight_decay * p before the moments, the reference's default
+ * optimizer "Adam"), coupled = 0 AdamW's decoupled decay (p *= 1 - lr * weight_decay).
+ * skip: null, or a device int32 status word (the persistent BiLSTM's sticky error word,
+ * crnn_lstm_seq_status_offset): when it is non-zero the kernel leaves p, m and v untouched.
+ * step counts from 1 (bias corrections 1 - beta^step). */
+int crnn_adam_step(float* p, const float* g, float* m, float* v, long n, float lr, float beta1, float beta2,
+                   float eps, float weight_decay, int step, float grad_scale, int coupled, const int* skip,
+                   void* stream);
+/* fused SGD (torch.optim.SGD with momentum, dampening 0, no Nesterov; training/train.py:296-299):
+ * d = grad_scale*g + weight_decay*p; momentum_buf = d on the first step (first_step = 1), else
+ * momentum*momentum_buf + d; p -= lr*momentum_buf (momentum = 0: p -= lr*d, buffer unused).
+ * skip as crnn_adam_step. */
+int crnn_sgd_step(float* p, const float* g, float* momentum_buf, long n, float lr, float momentum,
+                  float weight_decay, float grad_scale, int first_step, const int* skip, void* stream);
+/* AdamW without a status guard: crnn_adam_step(..., coupled = 0, skip = null) */
 int crnn_adamw(float* p, const float* g, float* m, float* v, long n, float lr, float beta1, float beta2, float eps,
                float weight_decay, int step, float grad_scale, void* stream);
 

@@ -40,14 +40,24 @@ class Ctx:
     `force` (test use): ReLU masks / 2x2 max-pool window indices, by decision-site name, that
     replace the oracle's own decisions. An fp64 evaluation that takes an fp32 path's decisions
     is that path's exact reference: fp32 ties (|pre-activation| within rounding of 0) no longer
-    decide which side of a ReLU kink the two evaluations land on."""
+    decide which side of a ReLU kink the two evaluations land on.
 
-    def __init__(self, train: bool, record: bool = False, force: Optional[Dict[str, torch.Tensor]] = None):
+    `store` (test use): applied to every tensor the HIP path keeps in its compute dtype between
+    kernels (conv outputs before BN, BN-ReLU outputs, pooled / block outputs, the sequence, the
+    LSTM input projections and hidden states, the BiLSTM outputs); e.g. bf16 round-to-nearest
+    makes this the bf16-storage model of the computation, the error bar of a bf16 HIP run.
+    BN statistics are taken before `store`, as the HIP conv epilogue sums its fp32 accumulators.
+    `momentum`: BN running-statistics momentum (1.0: running stats := this batch's)."""
+
+    def __init__(self, train: bool, record: bool = False, force: Optional[Dict[str, torch.Tensor]] = None,
+                 store=None, momentum: float = BN_MOMENTUM):
         self.train = train
         self.record = record
         self.acts: Dict[str, torch.Tensor] = {}
         self.running: Dict[str, torch.Tensor] = {}
         self.force = force or {}
+        self.store = store if store is not None else (lambda t: t)
+        self.momentum = momentum
 
     def rec(self, name, t):
         if self.record:
@@ -75,6 +85,7 @@ def batchnorm(x, p, prefix, ctx: Ctx):
     """nn.BatchNorm2d (torch defaults eps=1e-5, momentum=0.1): train mode normalises
     with the biased batch variance and folds the unbiased one into running_var."""
     w, b = p[prefix + ".weight"], p[prefix + ".bias"]
+    xs = ctx.store(x)
     if ctx.train:
         n = x.numel() // x.shape[1]
         mean = x.mean(dim=(0, 2, 3))
@@ -82,12 +93,13 @@ def batchnorm(x, p, prefix, ctx: Ctx):
         with torch.no_grad():
             rm = p[prefix + ".running_mean"]
             rv = p[prefix + ".running_var"]
-            ctx.running[prefix + ".running_mean"] = (1 - BN_MOMENTUM) * rm + BN_MOMENTUM * mean.detach()
-            ctx.running[prefix + ".running_var"] = (1 - BN_MOMENTUM) * rv + BN_MOMENTUM * var.detach() * n / max(1, n - 1)
+            m = ctx.momentum
+            ctx.running[prefix + ".running_mean"] = (1 - m) * rm + m * mean.detach()
+            ctx.running[prefix + ".running_var"] = (1 - m) * rv + m * var.detach() * n / max(1, n - 1)
     else:
         mean, var = p[prefix + ".running_mean"], p[prefix + ".running_var"]
     inv = torch.rsqrt(var + BN_EPS)
-    return (x - mean.view(1, -1, 1, 1)) * (inv * w).view(1, -1, 1, 1) + b.view(1, -1, 1, 1)
+    return (xs - mean.view(1, -1, 1, 1)) * (inv * w).view(1, -1, 1, 1) + b.view(1, -1, 1, 1)
 
 
 def se_layer(x, p, prefix, ctx: Optional[Ctx] = None):
@@ -102,7 +114,7 @@ def se_layer(x, p, prefix, ctx: Optional[Ctx] = None):
 def se_block(x, p, prefix, stride, has_ds, ctx):
     """SEBasicBlock.forward, model/seresnet31.py:55-67 (dropblock = Identity at p=0)."""
     out = F.conv2d(x, p[prefix + ".conv1.weight"], stride=stride, padding=1)
-    out = relu(ctx, prefix + ".bn1", batchnorm(out, p, prefix + ".bn1", ctx))
+    out = ctx.store(relu(ctx, prefix + ".bn1", batchnorm(out, p, prefix + ".bn1", ctx)))
     out = F.conv2d(out, p[prefix + ".conv2.weight"], stride=1, padding=1)
     out = batchnorm(out, p, prefix + ".bn2", ctx)
     out = se_layer(out, p, prefix + ".se", ctx)
@@ -111,16 +123,16 @@ def se_block(x, p, prefix, stride, has_ds, ctx):
         idn = batchnorm(idn, p, prefix + ".downsample.1", ctx)
     else:
         idn = x
-    return relu(ctx, prefix + ".out", out + idn)
+    return ctx.store(relu(ctx, prefix + ".out", out + idn))
 
 
 def backbone(x, p, ctx):
     """SEResNet31.forward, model/seresnet31.py:180-187."""
-    x = F.conv2d(x, p["cnn.conv0.0.weight"], padding=1)
-    x = relu(ctx, "cnn.conv0.1", batchnorm(x, p, "cnn.conv0.1", ctx))
+    x = F.conv2d(ctx.store(x), p["cnn.conv0.0.weight"], padding=1)
+    x = ctx.store(relu(ctx, "cnn.conv0.1", batchnorm(x, p, "cnn.conv0.1", ctx)))
     x = F.conv2d(x, p["cnn.conv0.3.weight"], padding=1)
     x = relu(ctx, "cnn.conv0.4", batchnorm(x, p, "cnn.conv0.4", ctx))
-    x = maxpool2(ctx, "stem.pool", x)
+    x = ctx.store(maxpool2(ctx, "stem.pool", x))
     ctx.rec("stem", x)
     for name, blocks, stride, inp, planes in STAGES:
         for i in range(blocks):
@@ -131,19 +143,21 @@ def backbone(x, p, ctx):
         ctx.rec(name, x)
     # conv_out, model/seresnet31.py:129-136
     x = F.conv2d(x, p["cnn.conv_out.0.weight"], stride=(2, 1), padding=(0, 1))
-    x = relu(ctx, "cnn.conv_out.1", batchnorm(x, p, "cnn.conv_out.1", ctx))
+    x = ctx.store(relu(ctx, "cnn.conv_out.1", batchnorm(x, p, "cnn.conv_out.1", ctx)))
     x = F.conv2d(x, p["cnn.conv_out.3.weight"], stride=1, padding=0)
     x = relu(ctx, "cnn.conv_out.4", batchnorm(x, p, "cnn.conv_out.4", ctx))
     ctx.rec("cnn_out", x)
     return x
 
 
-def lstm_direction(x, w_ih, w_hh, b_ih, b_hh, reverse):
+def lstm_direction(x, w_ih, w_hh, b_ih, b_hh, reverse, store=None):
     """nn.LSTM single direction, gate order i,f,g,o; h0 = c0 = 0.
-    Reverse direction runs over the flipped sequence (model/model.py:152-163)."""
+    Reverse direction runs over the flipped sequence (model/model.py:152-163).
+    store: applied to the input projections and to each h_t (Ctx.store)."""
     B, T, _ = x.shape
     H = w_hh.shape[1]
-    xg = x @ w_ih.t() + b_ih + b_hh
+    st = store if store is not None else (lambda t: t)
+    xg = st(x @ w_ih.t() + b_ih + b_hh)
     h = x.new_zeros(B, H)
     c = x.new_zeros(B, H)
     outs = [None] * T
@@ -152,29 +166,30 @@ def lstm_direction(x, w_ih, w_hh, b_ih, b_hh, reverse):
         g = xg[:, t] + h @ w_hh.t()
         i, f, gg, o = g.split(H, dim=1)
         c = torch.sigmoid(f) * c + torch.sigmoid(i) * torch.tanh(gg)
-        h = torch.sigmoid(o) * torch.tanh(c)
+        h = st(torch.sigmoid(o) * torch.tanh(c))
         outs[t] = h
     return torch.stack(outs, dim=1)
 
 
-def bilstm(x, p, prefix):
+def bilstm(x, p, prefix, store=None):
     """BidirectionalLSTM.forward, model/model.py:159-163."""
     r = prefix + ".rnn."
     hf = lstm_direction(x, p[r + "weight_ih_l0"], p[r + "weight_hh_l0"], p[r + "bias_ih_l0"],
-                        p[r + "bias_hh_l0"], False)
+                        p[r + "bias_hh_l0"], False, store)
     hb = lstm_direction(x, p[r + "weight_ih_l0_reverse"], p[r + "weight_hh_l0_reverse"],
-                        p[r + "bias_ih_l0_reverse"], p[r + "bias_hh_l0_reverse"], True)
+                        p[r + "bias_ih_l0_reverse"], p[r + "bias_hh_l0_reverse"], True, store)
     h = torch.cat([hf, hb], dim=2)
-    return h @ p[prefix + ".linear.weight"].t() + p[prefix + ".linear.bias"]
+    out = h @ p[prefix + ".linear.weight"].t() + p[prefix + ".linear.bias"]
+    return store(out) if store is not None else out
 
 
 def encode(x, p, ctx, num_rnn_layers=2):
     """RCNN.encode, model/model.py:215-221 (enc_dropout identity: eval or p=0)."""
     f = backbone(x, p, ctx)
-    seq = f.mean(dim=2).permute(0, 2, 1)       # AdaptiveAvgPool2d((1,None)) + squeeze + permute
+    seq = ctx.store(f.mean(dim=2).permute(0, 2, 1))   # AdaptiveAvgPool2d((1,None)) + squeeze + permute
     ctx.rec("seq", seq)
     for i in range(num_rnn_layers):
-        seq = bilstm(seq, p, f"enc_rnn.{i}")
+        seq = bilstm(seq, p, f"enc_rnn.{i}", ctx.store)
         ctx.rec(f"rnn{i}", seq)
     return seq
 

@@ -67,6 +67,9 @@ _SIGS = {
     "crnn_conv_fwd_bnrelu": ([i32, C.POINTER(ConvDesc), vp, vp, vp, vp, vp, vp], i32),
     "crnn_conv_fwd_bnrelu_pool_supported": ([i32, C.POINTER(ConvDesc)], i32),
     "crnn_conv_fwd_bnrelu_pool": ([i32, C.POINTER(ConvDesc), vp, vp, vp, vp, vp, vp], i32),
+    "crnn_conv_fwd_tile": ([i32, C.POINTER(ConvDesc), C.POINTER(C.c_int), C.POINTER(C.c_int)], None),
+    "crnn_conv_wgrad_plan": ([i32, C.POINTER(ConvDesc), C.POINTER(C.c_int), C.POINTER(C.c_int),
+                              C.POINTER(C.c_int)], None),
     "crnn_conv_stat_rows": ([i32, C.POINTER(ConvDesc)], i32),
     "crnn_conv_stat_rows_per_partial": ([i32, C.POINTER(ConvDesc)], i32),
     "crnn_conv_dgrad": ([i32, C.POINTER(ConvDesc), vp, vp, vp, vp, vp, i32, vp], i32),
@@ -135,6 +138,8 @@ _SIGS = {
     "crnn_ctc_reduce_mean": ([vp, vp, i32, vp, vp], i32),
     "crnn_ctc_greedy": ([vp, i32, i32, i32, i32, vp, vp, vp], i32),
     "crnn_adamw": ([vp, vp, vp, vp, i64, f32, f32, f32, f32, f32, i32, f32, vp], i32),
+    "crnn_adam_step": ([vp, vp, vp, vp, i64, f32, f32, f32, f32, f32, i32, f32, i32, vp, vp], i32),
+    "crnn_sgd_step": ([vp, vp, vp, i64, f32, f32, f32, f32, i32, vp, vp], i32),
 }
 
 _lib = None
@@ -166,6 +171,29 @@ def lib():
             fn.restype = res
         _lib = h
     return _lib
+
+
+def source_hash() -> str:
+    """sha256 (16 hex digits) over the sources that decide what the bench's kernels do: the HIP
+    sources, the C header, the host package (rcnn-ocr_amd/**/*.py) and bench.py. Measured-counter
+    files (profiles/*_pmc_traffic.json) carry the hash of the tree they were taken on; bench.py
+    attaches them only when it equals the running tree's (no git on the GPU box)."""
+    import hashlib
+    repo = os.path.dirname(PKG)
+    files = []
+    for root, dirs, names in os.walk(PKG):
+        dirs[:] = sorted(d for d in dirs if d != "__pycache__")
+        for n in sorted(names):
+            if n.endswith((".hip", ".hpp", ".cpp", ".h", ".py")) or n == "Makefile":
+                files.append(os.path.join(root, n))
+    files += [os.path.join(repo, "include", "crnn_hip.h"), os.path.join(repo, "bench.py")]
+    h = hashlib.sha256()
+    for f in files:
+        if os.path.exists(f):
+            h.update(os.path.relpath(f, repo).encode())
+            with open(f, "rb") as fh:
+                h.update(fh.read())
+    return h.hexdigest()[:16]
 
 
 def exported_symbols():

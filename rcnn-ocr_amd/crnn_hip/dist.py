@@ -70,37 +70,66 @@ def allreduce_grads(flat_grad: torch.Tensor, bucket_bytes: int = BUCKET_BYTES):
 
 class OverlappedAllReduce:
     """bucketed sum all-reduce of a flat gradient buffer, overlapped with the backward: call
-    ready(prefixes) from CRNNEngine.backward's stage_done hook, then finish()."""
+    ready(prefixes) from CRNNEngine.backward's stage_done hook, then finish().
+
+    Readiness is tracked per parameter: the issuable region is the longest SUFFIX of the buffer
+    whose parameters have all been reported final, whatever order the stages report in (a stage
+    that finishes out of layout order just waits until everything after it is final). Each issued
+    bucket is recorded in `issued` as (lo, hi) for tests."""
 
     def __init__(self, flat_grad: torch.Tensor, offsets, min_bucket_bytes: int = 8 << 20):
         """offsets: {param name: (start, numel)} into flat_grad (the model's flat layout)."""
         self.flat = flat_grad
         self.offsets = offsets
+        spans = sorted((s, s + n, k) for k, (s, n) in offsets.items())
+        pos = 0
+        for s, e, k in spans:
+            if s != pos:
+                raise ValueError(f"offsets must tile the flat buffer contiguously (gap / overlap at {k})")
+            pos = e
+        if pos != flat_grad.numel():
+            raise ValueError("offsets do not cover the flat buffer")
+        self.spans = spans
         self.min_elems = max(1, min_bucket_bytes // flat_grad.element_size())
         self.active = dist.is_initialized() and dist.get_world_size() > 1
+        self.issued = []
+        self.last_issued = []
         self.reset()
 
     def reset(self):
+        self.last_issued, self.issued = self.issued, []
+        self.done = set()                # parameter names reported final
+        self.cursor = len(self.spans)    # spans[cursor:] are final (a suffix)
         self.hi = self.flat.numel()      # [hi, end) already issued
-        self.lo = self.hi                # [lo, end) final
         self.works = []
 
+    @property
+    def lo(self) -> int:
+        """start of the final suffix"""
+        return self.spans[self.cursor][0] if self.cursor < len(self.spans) else self.flat.numel()
+
     def ready(self, prefixes):
-        starts = [s for k, (s, n) in self.offsets.items() if any(k.startswith(p) for p in prefixes)]
-        if starts:
-            self.lo = min(self.lo, min(starts))
+        for k in self.offsets:
+            if any(k.startswith(p) for p in prefixes):
+                self.done.add(k)
+        while self.cursor > 0 and self.spans[self.cursor - 1][2] in self.done:
+            self.cursor -= 1
         if self.active and self.hi - self.lo >= self.min_elems:
             self._issue(self.lo, self.hi)
 
     def _issue(self, lo, hi):
+        self.issued.append((lo, hi))
         self.works.append(dist.all_reduce(self.flat[lo:hi], async_op=True))
         self.hi = lo
 
     def finish(self):
+        """issue what is left (everything must be final by now) and make the caller's stream wait"""
         if self.active:
             if self.hi > 0:
+                missing = [k for _, _, k in self.spans[:self.cursor] if k not in self.done]
+                if missing:
+                    raise RuntimeError(f"finish(): gradients never reported final: {missing[:4]}")
                 self._issue(0, self.hi)
             for w in self.works:
                 w.wait()
         self.reset()
-

@@ -159,6 +159,7 @@ class CRNNEngine:
         # persistent BiLSTM status (see poll_status)
         self._seq_used = False
         self._sticky_carry = 0
+        self._sticky_index = 0      # int32 index of the status word in rnn.seq_ws (set with the buffer)
         self._status_host = None
         self._status_evt = None
         self._cur_ver = None
@@ -173,7 +174,11 @@ class CRNNEngine:
 
     # ------------------------------------------------------------------ weights
     def mark_params_changed(self):
+        """call after editing parameters or BN buffers in a way torch's version counters do not see
+        (kernel-side updates, writes through `.data`): the packed weights and the cached eval
+        affines are rebuilt at the next forward."""
         self.version += 1
+        self._eval_affine.clear()
 
     def convs(self):
         yield self.stem0
@@ -350,27 +355,32 @@ class CRNNEngine:
 
     def _seq_ws(self, B):
         n = (L.lib().crnn_lstm_seq_workspace(B) + 3) // 4
-        self._seq_err_index = 2 * (B // 16 + 1)   # include/crnn_hip.h: counters, then the error word
         t = self.ws.bufs.get("rnn.seq_ws")
         if t is None or t.numel() != n:
             if t is not None:
                 self._fold_sticky(t)
             # zeroed at allocation: the sticky status word (after the ring) is never zeroed again
             t = self.ws.bufs["rnn.seq_ws"] = torch.zeros(n, dtype=torch.int32, device=self.device)
+            # the library's own layout (include/crnn_hip.h crnn_lstm_seq_status_offset), kept with the buffer
+            self._sticky_index = int(L.lib().crnn_lstm_seq_status_offset(B)) // 4
         self._seq_used = True
         return t
 
     def _fold_sticky(self, old):
-        self._sticky_carry |= int(old[self._sticky_idx_of(old)].item())
+        self._sticky_carry |= int(old[self._sticky_index].item())
 
-    def _sticky_idx_of(self, t):
-        return t.numel() - 64   # crnn_lstm_seq_workspace = status offset + 256 bytes
+    def status_word(self) -> Optional[torch.Tensor]:
+        """the persistent BiLSTM's sticky status word (int32 device view, 0 = ok), or None when no
+        persistent sweep has run: FusedAdamW passes it to its kernel, which skips the update when it
+        is set (a timed-out sweep leaves NaN gradients that must not reach the weights)."""
+        t = self.ws.bufs.get("rnn.seq_ws") if self._seq_used else None
+        return None if t is None else t[self._sticky_index:self._sticky_index + 1]
 
     def seq_status(self) -> int:
         """OR of the error words of every persistent BiLSTM launch so far (0 = ok; non-zero: a
         bounded wait timed out and that sweep's outputs are NaN). Synchronises."""
         t = self.ws.bufs.get("rnn.seq_ws")
-        return self._sticky_carry | (0 if t is None else int(t[self._sticky_idx_of(t)].item()))
+        return self._sticky_carry | (0 if t is None else int(t[self._sticky_index].item()))
 
     def check_status(self):
         """raise if any persistent BiLSTM sweep has timed out (synchronises)"""
@@ -391,7 +401,7 @@ class CRNNEngine:
             t = self.ws.bufs["rnn.seq_ws"]
             if self._status_host is None:
                 self._status_host = torch.zeros(1, dtype=torch.int32).pin_memory()
-            i = self._sticky_idx_of(t)
+            i = self._sticky_index
             self._status_host.copy_(t[i:i + 1], non_blocking=True)
             self._status_evt = torch.cuda.Event()
             self._status_evt.record()
@@ -408,8 +418,10 @@ class CRNNEngine:
         if not train:
             # eval affine from the running statistics: recomputed only when the parameters or the
             # running statistics have changed since (train forwards clear the cache: their kernels
-            # update the statistics and these buffers without bumping a torch version counter)
-            key = (self._cur_ver, rm._version, rv._version)   # _cur_ver: this forward's pack() key
+            # update the statistics and these buffers without bumping a torch version counter).
+            # Writes through `.data` bump no version counter: mark_params_changed() clears the cache
+            # (a replaced `.data` tensor is caught by its storage pointer)
+            key = (self._cur_ver, rm._version, rv._version, rm.data_ptr(), rv.data_ptr())
             if self._eval_affine.get(tag) == key:
                 return mean, inv, sc, sh
             self._eval_affine[tag] = key
@@ -619,6 +631,37 @@ class CRNNEngine:
         if self._nbt:
             torch._foreach_add_(self._nbt, 1)   # BN num_batches_tracked, one launch
         # BiLSTM stack (model/model.py:195-198)
+        xin, rnn_saved = self._rnn_forward(seq, B, Tn, save_for_backward)
+        sv["rnn"] = rnn_saved
+        Hd = self.H
+        # enc_dropout (model/model.py:201,220): identity in eval; in training a counter-based mask
+        # (crnn_dropout) whose seed is saved so the backward regenerates it
+        sv["drop"] = None
+        if train and dropout_p > 0.0:
+            self._drop_calls += 1
+            seed = (self._drop_seed + 0x9E3779B97F4A7C15 * self._drop_calls) & 0xFFFFFFFFFFFFFFFF
+            xdr = ws.get("enc.drop", (B, Tn, Hd), T)
+            call("crnn_dropout", dt, ptr(xin), ptr(xdr), B * Tn * Hd, float(dropout_p), seed, s)
+            sv["drop"] = (float(dropout_p), seed)
+            xin = xdr
+        sv["enc"] = xin
+        sv["B"], sv["T"] = B, Tn
+        logits = None
+        if self.has_head:   # CTC head
+            logits = ws.get("logits", (B, Tn, self.Cpad), torch.float32)
+            call("crnn_gemm_nt", dt, ptr(xin), Hd, ptr(self.packed["head.w"]), Hd, ptr(logits), self.Cpad,
+                 ptr(self.packed["head.b"]), B * Tn, self.Cpad, Hd, 1, 0, s)
+        self.poll_status()
+        if save_for_backward:
+            self.fwd_gen += 1
+            sv["gen"] = self.fwd_gen
+        self._saved = sv if save_for_backward else None
+        return logits[:, :, : self.C] if logits is not None else None
+
+    def _rnn_forward(self, seq, B, Tn, save_for_backward):
+        """the BiLSTM stack (model/model.py:151-163, 195-198) over seq [B, T, enc_dim] (compute dtype)
+        -> (output [B, T, hidden], per-layer saved tensors)"""
+        ws, dt, T, s = self.ws, self.dt, self.dtype, L.stream_ptr()
         Hd = self.H
         xin = seq
         rnn_saved = []
@@ -647,30 +690,31 @@ class CRNNEngine:
                  ptr(self.p[pre + ".linear.bias"]), B * Tn, Hd, 2 * Hd, 0, 0, s)
             rnn_saved.append(dict(x=xin, hseq=hseq, gates=gsv, c=csv, out=out))
             xin = out
-        sv["rnn"] = rnn_saved
-        # enc_dropout (model/model.py:201,220): identity in eval; in training a counter-based mask
-        # (crnn_dropout) whose seed is saved so the backward regenerates it
-        sv["drop"] = None
-        if train and dropout_p > 0.0:
-            self._drop_calls += 1
-            seed = (self._drop_seed + 0x9E3779B97F4A7C15 * self._drop_calls) & 0xFFFFFFFFFFFFFFFF
-            xdr = ws.get("enc.drop", (B, Tn, Hd), T)
-            call("crnn_dropout", dt, ptr(xin), ptr(xdr), B * Tn * Hd, float(dropout_p), seed, s)
-            sv["drop"] = (float(dropout_p), seed)
-            xin = xdr
-        sv["enc"] = xin
-        sv["B"], sv["T"] = B, Tn
-        logits = None
-        if self.has_head:   # CTC head
-            logits = ws.get("logits", (B, Tn, self.Cpad), torch.float32)
-            call("crnn_gemm_nt", dt, ptr(xin), Hd, ptr(self.packed["head.w"]), Hd, ptr(logits), self.Cpad,
-                 ptr(self.packed["head.b"]), B * Tn, self.Cpad, Hd, 1, 0, s)
+        return xin, rnn_saved
+
+    def bilstm_stack(self, seq: torch.Tensor, dout: Optional[torch.Tensor] = None, grads=None):
+        """The BiLSTM stack alone (model/model.py:195-198) on seq [B, T, enc_dim] fp32: -> output
+        [B, T, hidden] fp32; with dout (d loss / d output, fp32) also the BiLSTM parameter gradients
+        into `grads` (overwritten) and -> (output, d seq fp32). The same kernels and workspace as the
+        full forward / backward (tests: the 4 x 768 stack golden, tests/golden/bilstm_stack.npz)."""
+        L.require_device(seq)
+        self.pack()
+        B, Tn, _ = seq.shape
+        s = L.stream_ptr()
+        xs = self.ws.get("stack.in", tuple(seq.shape), self.dtype)
+        xs.copy_(seq)
+        out, saved = self._rnn_forward(xs, B, Tn, dout is not None)
         self.poll_status()
-        if save_for_backward:
-            self.fwd_gen += 1
-            sv["gen"] = self.fwd_gen
-        self._saved = sv if save_for_backward else None
-        return logits[:, :, : self.C] if logits is not None else None
+        y = out.float().clone()
+        if dout is None:
+            return y
+        self.g = grads
+        self.accumulate = False
+        dx = self.ws.get("stack.dout", (B, Tn, self.H), self.dtype)
+        dx.copy_(dout)
+        dseq = self._rnn_backward(dx, saved, B, Tn, 0)
+        self.poll_status()
+        return y, dseq.float().clone()
 
     def check_generation(self, gen: int):
         """raise unless the saved activations are those of forward generation `gen`: a second
@@ -785,6 +829,13 @@ class CRNNEngine:
         upd(self.co1, h, w)
         return cap
 
+    @staticmethod
+    def backward_stages() -> List[List[str]]:
+        """the parameter-name prefixes backward() reports final through stage_done, in its order"""
+        blocks = backbone_specs()[2]
+        return ([["ctc_head.", "enc_rnn."], ["cnn.conv_out."]] + [[b.prefix + "."] for b in reversed(blocks)]
+                + [["cnn.conv0."]])
+
     def backward(self, dlogits: Optional[torch.Tensor], grads: Dict[str, torch.Tensor], accumulate: bool = False,
                  stage_done=None, denc: Optional[torch.Tensor] = None):
         """Full backward from d loss / d logits [B,T,Cpad] fp32 into `grads` (fp32, reference layouts).
@@ -858,16 +909,16 @@ class CRNNEngine:
         call("crnn_gemm_nn", dt, ptr(dlT), self.Cpad, ptr(self.packed["head.w"]), Hd, ptr(dx), Hd, M, Hd,
              self.Cpad, 0, 0, s)
 
-    def _backward_encoder(self, dx, grads, acc, done):
-        sv, ws, dt, T, s = self._saved, self.ws, self.dt, self.dtype, L.stream_ptr()
-        B, Tn, Hd = sv["B"], sv["T"], self.H
+    def _rnn_backward(self, dx, rnn_saved, B, Tn, acc):
+        """BPTT through the BiLSTM stack: d output [B, T, hidden] -> d input [B, T, enc_dim]; the
+        parameter gradients straight into self.g (reference layouts)"""
+        ws, dt, T, s = self.ws, self.dt, self.dtype, L.stream_ptr()
+        Hd = self.H
         M = B * Tn
-        accumulate = self.accumulate
-        st = sv["stem"]
-        # ---- BiLSTM stack, reverse
+        grads = self.g
         for l in reversed(range(self.nl)):
             pre = f"enc_rnn.{l}"
-            r = sv["rnn"][l]
+            r = rnn_saved[l]
             ind = r["x"].shape[-1]
             dh = ws.get("rnn.dhseq", (B, Tn, 2 * Hd), T)
             call("crnn_gemm_nn", dt, ptr(dx), Hd, ptr(self.packed[pre + ".lin"]), 2 * Hd, ptr(dh), 2 * Hd, M,
@@ -888,7 +939,7 @@ class CRNNEngine:
                          ptr(dg), ptr(dc), ptr(bws), B, Tn, Hd, stp, s)
             self._record("lstm_bwd", Tn * self.lstm_bptt_step_bytes(B, Hd, T), t0)
             rr = pre + ".rnn."
-            gq = lambda n: ptr(self._gview(rr + n))
+            gq = lambda n: ptr(self._gview(rr + n))  # noqa: E731
             # gradients straight into the parameters' .grad views (reference row order)
             if T == torch.bfloat16:   # all four in one batched split-K launch + slab reduce
                 need = L.lib().crnn_lstm_wgrad_workspace(B, Tn, Hd, ind)
@@ -907,6 +958,16 @@ class CRNNEngine:
             nxt = ws.get(f"rnn.dx_l{l}", (B, Tn, ind), T)
             call("crnn_lstm_dx", dt, ptr(dg), ptr(self.packed[pre + ".wih"]), ptr(nxt), B, Tn, Hd, ind, s)
             dx = nxt
+        return dx
+
+    def _backward_encoder(self, dx, grads, acc, done):
+        sv, ws, dt, T, s = self._saved, self.ws, self.dt, self.dtype, L.stream_ptr()
+        B, Tn, Hd = sv["B"], sv["T"], self.H
+        M = B * Tn
+        accumulate = self.accumulate
+        st = sv["stem"]
+        # ---- BiLSTM stack, reverse
+        dx = self._rnn_backward(dx, sv["rnn"], B, Tn, acc)
         dseq = dx  # [B, T, 512]
         if self.debug:
             self.dbg["dseq"] = dseq.clone()

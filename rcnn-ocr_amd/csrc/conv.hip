@@ -1001,11 +1001,15 @@ int crnn_conv_fwd_bnrelu_pool(int dtype, const crnn_conv_desc* d, const void* x,
 
 int crnn_conv_dgrad_ds_supported(int dtype, const crnn_conv_desc* d, const crnn_conv_desc* dds) {
   const int ks = dtype == CRNN_BF16 ? kstage<bf16>() : kstage<float>();
+  // the concatenated gradient (dz1 | dzd) and weights (conv1 | downsample) are each addressed by one
+  // 32-bit buffer-resource range (nbytes): guard on their BYTE sizes in this dtype
+  const long es = dtype == CRNN_BF16 ? 2 : 4;
+  const long dyn = (long)d->B * d->Ho * d->Wo * d->Co, wn = (long)d->Co * d->KH * d->KW * d->Ci + (long)d->Co * d->Ci;
   return d->KH == 3 && d->KW == 3 && d->sh == 2 && d->sw == 2 && d->ph == 1 && d->pw == 1 && dds->KH == 1 &&
                  dds->KW == 1 && dds->sh == 2 && dds->sw == 2 && dds->ph == 0 && dds->pw == 0 && d->B == dds->B &&
                  d->Hi == dds->Hi && d->Wi == dds->Wi && d->Ci == dds->Ci && d->Ho == dds->Ho && d->Wo == dds->Wo &&
                  d->Co == dds->Co && d->Ci % 8 == 0 && d->Co % ks == 0 && d->Hi == 2 * d->Ho && d->Wi == 2 * d->Wo &&
-                 (long)d->B * d->Ho * d->Wo * d->Co * 2 < (1L << 31)
+                 2 * dyn * es < (1L << 32) && wn * es < (1L << 32)
              ? 1
              : 0;
 }

@@ -168,9 +168,14 @@ __global__ __launch_bounds__(GREEDY_NT) void greedy_kernel(const float* __restri
   if (lane == 0) lens[b] = n;
 }
 
-__device__ __forceinline__ void adamw_elem(float& pv, float gr, float& mv, float& vv, float lr, float b1, float b2,
-                                           float eps, float wd, float step_size, float inv_sqrt_bc2) {
-  pv *= 1.f - lr * wd;
+// one element of torch.optim.AdamW (COUPLED = false: p *= 1 - lr*wd, decoupled decay) or
+// torch.optim.Adam (COUPLED = true: L2 decay folded into the gradient, g += wd*p, before the moments;
+// training/train.py:292-295). The moment and bias-correction arithmetic is the same.
+template <bool COUPLED>
+__device__ __forceinline__ void adam_elem(float& pv, float gr, float& mv, float& vv, float b1, float b2, float eps,
+                                          float decay, float step_size, float inv_sqrt_bc2) {
+  if constexpr (COUPLED) gr += decay * pv;   // decay = wd
+  else pv *= decay;                          // decay = 1 - lr*wd
   mv = mv + (1.f - b1) * (gr - mv);
   vv = vv * b2 + (1.f - b2) * gr * gr;
   const float denom = sqrtf(vv) * inv_sqrt_bc2 + eps;
@@ -179,17 +184,21 @@ __device__ __forceinline__ void adamw_elem(float& pv, float gr, float& mv, float
 
 // VEC: one 16-B vector of p, g, m, v per thread and iteration (HBM-bound: 28 B per parameter),
 // the n % 4 tail elements by the first threads one at a time; !VEC (pointers not 16-B aligned):
-// one element per thread and iteration
-template <bool VEC>
-__global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
-                                                    float* __restrict__ m, float* __restrict__ v, long n, float lr,
-                                                    float b1, float b2, float eps, float wd, float step_size,
-                                                    float inv_sqrt_bc2, float gs) {
+// one element per thread and iteration.
+// skip: a device status word (the persistent BiLSTM's sticky error word) or null; when it is set
+// the update is skipped entirely, so a timed-out sweep's NaN gradients never reach the weights or
+// the moments (the host raises at its next status poll)
+template <bool VEC, bool COUPLED>
+__global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                   float* __restrict__ m, float* __restrict__ v, long n, float b1,
+                                                   float b2, float eps, float decay, float step_size,
+                                                   float inv_sqrt_bc2, float gs, const int* __restrict__ skip) {
+  if (skip != nullptr && *skip != 0) return;
   const long tid = blockIdx.x * (long)blockDim.x + threadIdx.x, nth = (long)gridDim.x * blockDim.x;
   if constexpr (!VEC) {
     for (long i = tid; i < n; i += nth) {
       float pv = p[i], mv = m[i], vv = v[i];
-      adamw_elem(pv, g[i] * gs, mv, vv, lr, b1, b2, eps, wd, step_size, inv_sqrt_bc2);
+      adam_elem<COUPLED>(pv, g[i] * gs, mv, vv, b1, b2, eps, decay, step_size, inv_sqrt_bc2);
       p[i] = pv;
       m[i] = mv;
       v[i] = vv;
@@ -205,7 +214,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       float pe = pv[r], me = mv[r], ve = vv[r];
-      adamw_elem(pe, gv[r] * gs, me, ve, lr, b1, b2, eps, wd, step_size, inv_sqrt_bc2);
+      adam_elem<COUPLED>(pe, gv[r] * gs, me, ve, b1, b2, eps, decay, step_size, inv_sqrt_bc2);
       pv[r] = pe;
       mv[r] = me;
       vv[r] = ve;
@@ -217,10 +226,39 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const
   const long i = 4 * n4 + tid;
   if (i < n) {
     float pv = p[i], mv = m[i], vv = v[i];
-    adamw_elem(pv, g[i] * gs, mv, vv, lr, b1, b2, eps, wd, step_size, inv_sqrt_bc2);
+    adam_elem<COUPLED>(pv, g[i] * gs, mv, vv, b1, b2, eps, decay, step_size, inv_sqrt_bc2);
     p[i] = pv;
     m[i] = mv;
     v[i] = vv;
+  }
+}
+
+template <bool COUPLED>
+void launch_adam(bool vec, float* p, const float* g, float* m, float* v, long n, float b1, float b2, float eps,
+                 float decay, float step_size, float inv_sqrt_bc2, float gs, const int* skip, hipStream_t st) {
+  if (vec)
+    hipLaunchKernelGGL((adam_kernel<true, COUPLED>), dim3(grid_for((n + 3) / 4, 256, 8192)), dim3(256), 0, st, p, g,
+                       m, v, n, b1, b2, eps, decay, step_size, inv_sqrt_bc2, gs, skip);
+  else
+    hipLaunchKernelGGL((adam_kernel<false, COUPLED>), dim3(grid_for(n, 256, 16384)), dim3(256), 0, st, p, g, m, v,
+                       n, b1, b2, eps, decay, step_size, inv_sqrt_bc2, gs, skip);
+}
+
+// torch.optim.SGD (dampening 0, no Nesterov; training/train.py:296-299): d = g*gs + wd*p;
+// buf = d on the first step, else momentum*buf + d; p -= lr*buf (momentum 0: p -= lr*d, buf unused)
+__global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                  float* __restrict__ buf, long n, float lr, float mom, float wd,
+                                                  float gs, int first, const int* __restrict__ skip) {
+  if (skip != nullptr && *skip != 0) return;
+  const long nth = (long)gridDim.x * blockDim.x;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += nth) {
+    float pv = p[i];
+    float d = g[i] * gs + wd * pv;
+    if (mom != 0.f) {
+      d = first ? d : mom * buf[i] + d;
+      buf[i] = d;
+    }
+    p[i] = pv - lr * d;
   }
 }
 
@@ -256,20 +294,38 @@ int crnn_ctc_greedy(const float* logits, int ldc, int B, int T, int C, int* ids,
   return (int)hipGetLastError();
 }
 
-int crnn_adamw(float* p, const float* g, float* m, float* v, long n, float lr, float beta1, float beta2, float eps,
-               float weight_decay, int step, float grad_scale, void* stream) {
+int crnn_adam_step(float* p, const float* g, float* m, float* v, long n, float lr, float beta1, float beta2,
+                   float eps, float weight_decay, int step, float grad_scale, int coupled, const int* skip,
+                   void* stream) {
+  if (n <= 0) return 0;
+  if (step < 1) return crnn_set_error(hipErrorInvalidValue, "adam_step: step counts from 1");
   double bc1 = 1.0 - pow((double)beta1, (double)step);
   double bc2 = 1.0 - pow((double)beta2, (double)step);
   float step_size = (float)((double)lr / bc1);
   float inv_sqrt_bc2 = (float)(1.0 / sqrt(bc2));
   const bool vec = ((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) % 16 == 0;
-  if (vec)
-    hipLaunchKernelGGL(adamw_kernel<true>, dim3(grid_for((n + 3) / 4, 256, 8192)), dim3(256), 0, (hipStream_t)stream,
-                       p, g, m, v, n, lr, beta1, beta2, eps, weight_decay, step_size, inv_sqrt_bc2, grad_scale);
+  hipStream_t st = (hipStream_t)stream;
+  if (coupled)
+    launch_adam<true>(vec, p, g, m, v, n, beta1, beta2, eps, weight_decay, step_size, inv_sqrt_bc2, grad_scale, skip,
+                      st);
   else
-    hipLaunchKernelGGL(adamw_kernel<false>, dim3(grid_for(n, 256, 16384)), dim3(256), 0, (hipStream_t)stream, p, g,
-                       m, v, n, lr, beta1, beta2, eps, weight_decay, step_size, inv_sqrt_bc2, grad_scale);
+    launch_adam<false>(vec, p, g, m, v, n, beta1, beta2, eps, 1.f - lr * weight_decay, step_size, inv_sqrt_bc2,
+                       grad_scale, skip, st);
   return (int)hipGetLastError();
+}
+
+int crnn_sgd_step(float* p, const float* g, float* momentum_buf, long n, float lr, float momentum,
+                  float weight_decay, float grad_scale, int first_step, const int* skip, void* stream) {
+  if (n <= 0) return 0;
+  if (momentum != 0.f && momentum_buf == nullptr) return crnn_set_error(hipErrorInvalidValue, "sgd_step: no momentum buffer");
+  hipLaunchKernelGGL(sgd_kernel, dim3(grid_for(n, 256, 16384)), dim3(256), 0, (hipStream_t)stream, p, g, momentum_buf,
+                     n, lr, momentum, weight_decay, grad_scale, first_step, skip);
+  return (int)hipGetLastError();
+}
+
+int crnn_adamw(float* p, const float* g, float* m, float* v, long n, float lr, float beta1, float beta2, float eps,
+               float weight_decay, int step, float grad_scale, void* stream) {
+  return crnn_adam_step(p, g, m, v, n, lr, beta1, beta2, eps, weight_decay, step, grad_scale, 0, nullptr, stream);
 }
 
 }  // extern "C"

@@ -64,7 +64,7 @@ class _EncodeFn(torch.autograd.Function):
         dl[:, :, C:].zero_()
         dl[:, :, :C].copy_(grad_logits)
         grads, accumulate = model._grad_views()
-        eng.backward(dl, grads, accumulate=accumulate)
+        eng.backward(dl, grads, accumulate=accumulate, stage_done=model.stage_done)
         return None, None, None, None
 
 
@@ -94,7 +94,7 @@ class _AttnTrainFn(torch.autograd.Function):
         grads, accumulate = model._grad_views()
         attn_grads = {k[len("attn."):]: v for k, v in grads.items() if k.startswith("attn.")}
         denc = model._attn_dec.backward(grad_logits.contiguous(), attn_grads, accumulate)
-        model._engine.backward(None, grads, accumulate=accumulate, denc=denc)
+        model._engine.backward(None, grads, accumulate=accumulate, denc=denc, stage_done=model.stage_done)
         return None, None, None, None, None
 
 
@@ -151,6 +151,10 @@ class RCNN(nn.Module):
         self._engine: Optional[CRNNEngine] = None
         self._flat_param: Optional[torch.Tensor] = None
         self._flat_grad: Optional[torch.Tensor] = None
+        # data parallel: called by every backward with the parameter-name prefixes whose gradients
+        # have become final (crnn_hip.dist.OverlappedAllReduce.ready), so the gradient all-reduce
+        # overlaps the rest of the backward; None = single process
+        self.stage_done = None
 
     # ------------------------------------------------------------------ engine plumbing
     def _param_dict(self) -> Dict[str, torch.Tensor]:

@@ -14,11 +14,15 @@ Fixtures:
   train_<case>.npz       train-mode fwd (BN batch stats, dropout 0) + F.ctc_loss + backward
   ctc_cases.npz          F.ctc_loss(blank=0, mean, zero_infinity) values + grads, incl. infeasible labels
   decode.npz/.json       training/utils.py:122-150 ctc_greedy_decoder strings at T < B
+  decode_b8_t16.npz/.json  BASELINE configs[0]'s decode shape, B=8 / T=16 (T > B: the reference's
+                         layout heuristic would swap the axes there): the reference's
+                         decoder run on the 8 samples padded with 17 extra rows to B=25 > T, so its
+                         heuristic reads the intended (B, T, C) layout; only the 8 real rows are kept
   bilstm_stack.npz       4 x BidirectionalLSTM(768) stack (model/model.py:151-163)
   attn_decoder.npz       the attention decoder (model/model.py:23-148) on a
                          fixed encoder output: eval greedy decode (incl. blank masking) and
                          teacher-forced logits, with its (seeded, generator-scaled) weights
-Only some:  python tests/golden/make_goldens.py attn
+Only some:  python tests/golden/make_goldens.py attn | decode_b8
 """
 from __future__ import annotations
 
@@ -267,6 +271,28 @@ def gen_decode(itos):
     print("wrote decode", texts[:3])
 
 
+def gen_decode_b8(itos):
+    """B=8, T=16 (configs[0]): explicit (B, T, C) strings from the reference's decoder itself."""
+    alpha_list = itos[1:]
+    g = torch.Generator().manual_seed(92)
+    B, T, C, PAD_B = 8, 16, len(itos), 25
+    logits = torch.randn(B, T, C, generator=g)
+    boost = torch.randint(0, 3, (B, T), generator=g)
+    logits[..., 0] += (boost == 0).float() * 4.0
+    rep = torch.randint(0, 2, (B, T), generator=g).bool()       # frequent repeats of the previous argmax
+    for t in range(1, T):
+        logits[:, t][rep[:, t]] = logits[:, t - 1][rep[:, t]]
+    padded = torch.cat([logits, torch.zeros(PAD_B - B, T, C)], 0)   # B=25 > T=16: no axis swap
+    texts, seqs = ctc_greedy_decoder(padded, alpha_list, blank=0)
+    # what the heuristic does with the bare B=8 batch (for the record: it decodes the wrong axis)
+    texts_bare, _ = ctc_greedy_decoder(logits, alpha_list, blank=0)
+    np.savez_compressed(os.path.join(HERE, "decode_b8_t16.npz"), logits=logits.numpy())
+    with open(os.path.join(HERE, "decode_b8_t16.json"), "w", encoding="utf-8") as f:
+        json.dump({"texts": texts[:B], "seqs": seqs[:B], "layout": "BTC", "B": B, "T": T,
+                   "padded_to": PAD_B, "heuristic_on_bare_batch_rows": len(texts_bare)}, f, ensure_ascii=False)
+    print("wrote decode_b8_t16", texts[:2], "bare heuristic rows:", len(texts_bare))
+
+
 def gen_bilstm_stack():
     torch.manual_seed(0)
     layers = [BidirectionalLSTM(512, 768, 768)] + [BidirectionalLSTM(768, 768, 768) for _ in range(3)]
@@ -318,12 +344,16 @@ def main():
         gen_attn()
         return
     itos = load_charset(os.path.join(REF, "configs", "charset.txt"))
+    if sys.argv[1:] == ["decode_b8"]:
+        gen_decode_b8(itos)
+        return
     with open(os.path.join(HERE, "charset.txt"), "w", encoding="utf-8") as f:
         for t in itos:
             f.write(t + "\n")
     torch.set_num_threads(8)
     gen_ctc()
     gen_decode(itos)
+    gen_decode_b8(itos)
     gen_bilstm_stack()
     gen_eval(itos)
     gen_train(itos)

@@ -32,9 +32,7 @@ def test_ctypes_table_covers_header():
     from crnn_hip import _lib as L
     decl = set(header_symbols())
     bound = set(L.exported_symbols())
-    helpers = {"crnn_conv_fwd_tile", "crnn_conv_wgrad_plan"}
-    assert decl - bound <= helpers, decl - bound - helpers
-    assert bound <= decl
+    assert decl == bound, (decl - bound, bound - decl)
 
 
 def test_library_loads_without_gpu():

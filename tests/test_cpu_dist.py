@@ -73,7 +73,35 @@ def _worker(rank, world, port, q):
                 red.ready(pre)
             red.finish()
             ok_ov = ok_ov and torch.allclose(g2, torch.arange(1000, dtype=torch.float32) * 3)
-        q.put((rank, ok_sum, ok_bc, ok_dp and ok_ov))
+        # the REAL layout and stage order: RCNN.flat_offsets() and CRNNEngine.backward_stages() (the
+        # sequence backward() reports), in order and shuffled; buckets must tile the buffer exactly
+        # once, each issued only once all of its parameters were reported final
+        from crnn_hip.engine import CRNNEngine
+        from model.model import RCNN
+        offs = RCNN(num_classes=10, hidden_size=16).flat_offsets()
+        n = sum(k for _, k in offs.values())
+        stages = CRNNEngine.backward_stages()
+        covered = set()
+        for st in stages:
+            covered |= {k for k in offs if any(k.startswith(p) for p in st)}
+        ok_real = covered == set(offs)
+        orders = [stages, list(reversed(stages)), stages[:3] + stages[5:] + stages[3:5]]
+        for order in orders:
+            for mb in (4, 4 << 20, 1 << 40):
+                g3 = torch.ones(n) * (rank + 1)
+                red = D.OverlappedAllReduce(g3, offs, min_bucket_bytes=mb)
+                seen = []
+                for st in order:
+                    red.ready(st)
+                    seen += [k for k in offs if any(k.startswith(p) for p in st)]
+                    for lo, hi in red.issued:   # every bucket so far holds only reported parameters
+                        ok_real = ok_real and all(k in seen for k, (s0, c) in offs.items() if s0 < hi and s0 + c > lo)
+                red.finish()
+                spans = sorted(red.last_issued)
+                ok_real = ok_real and spans[0][0] == 0 and spans[-1][1] == n and all(
+                    a[1] == b[0] for a, b in zip(spans, spans[1:]))
+                ok_real = ok_real and bool((g3 == 3).all())
+        q.put((rank, ok_sum, ok_bc, ok_dp and ok_ov and ok_real))
     finally:
         dist.destroy_process_group()
 

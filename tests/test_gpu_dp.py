@@ -1,0 +1,118 @@
+"""Data-parallel step on the HIP path at world size 2: two
+processes share the one GPU of the box (gloo over device tensors, the per-step BiLSTM kernels: the
+persistent sweeps need the whole chip and must not run from two processes at once). Each rank runs
+the RCNN API's train step on its own shard with the model's REAL flat layout and the engine's REAL
+stage_done sequence driving crnn_hip.dist.OverlappedAllReduce (RCNN.stage_done), then FusedAdamW.
+
+Checked: the stage sequence equals CRNNEngine.backward_stages(); the issued buckets tile the flat
+buffer exactly once; the reduced gradient equals the sum of the per-rank gradients of the same
+step (each rank's own backward, summed separately); and after the optimizer step both replicas hold
+bit-identical weights. RCCL itself runs only on the driver's 8-GPU node."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), CRNN_SHARE_DEVICE="1", CRNN_LSTM_PER_STEP="1",
+                      HSA_ENABLE_IPC_MODE_LEGACY="0")
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    for sub in ("../rcnn-ocr_amd", "../oracle"):
+        sys.path.insert(0, os.path.join(here, sub))
+    import torch.distributed as dist
+    try:
+        import crnn_oracle as O
+        from crnn_hip import dist as D
+        from crnn_hip.ctc import ctc_loss
+        from crnn_hip.engine import CRNNEngine
+        from crnn_hip.optim import FusedAdamW
+        from crnn_hip.recipe import recipe_state_dict, synthetic_batch
+        from model.model import RCNN
+        world_, rank_, local = D.init_from_env("gloo")
+        dev = torch.device("cuda", local)
+        torch.cuda.set_device(dev)
+        m = RCNN(num_classes=194, hidden_size=64, blank_id=None, compute_dtype=torch.bfloat16, enc_dropout_p=0.0)
+        # rank 1 starts from different weights: the broadcast must replace them
+        m.load_state_dict(recipe_state_dict(O.param_shapes(64, 194), 5 + rank), strict=False)
+        m = m.to(dev).train()
+        x, _, tg, tl = synthetic_batch(16, 32, 128, 16, 194, seed=100 + rank)
+        x = x.to(dev)
+        m(x)                                   # builds the engine and the flat buffers
+        D.broadcast_params(m._flat_param)
+        m.mark_params_changed()
+        opt = FusedAdamW(m, lr=1e-3)
+        # per-rank gradient of this step, summed over ranks on the host: the expected reduction
+        opt.zero_grad()
+        ctc_loss(m(x), tg, tl).backward()
+        torch.cuda.synchronize()
+        want = m._flat_grad.detach().cpu().clone()
+        dist.all_reduce(want)
+        # the DP step: stage hooks drive the overlapped bucketed all-reduce during the backward
+        red = D.OverlappedAllReduce(m._flat_grad, m.flat_offsets(), min_bucket_bytes=1 << 20)
+        seq = []
+
+        def hook(prefixes):
+            seq.append(list(prefixes))
+            red.ready(prefixes)
+        m.stage_done = hook
+        opt.zero_grad()
+        ctc_loss(m(x), tg, tl).backward()
+        red.finish()
+        torch.cuda.synchronize()
+        got = m._flat_grad.detach().cpu()
+        ok_seq = seq == CRNNEngine.backward_stages()
+        spans = sorted(red.last_issued)
+        n = m._flat_grad.numel()
+        ok_tile = (len(spans) > 1 and spans[0][0] == 0 and spans[-1][1] == n
+                   and all(a[1] == b[0] for a, b in zip(spans, spans[1:])))
+        err = float((got - want).abs().max() / (want.abs().max() + 1e-30))
+        opt.step(grad_scale=1.0 / world)
+        torch.cuda.synchronize()
+        c = m._flat_param.detach().double().sum().reshape(1).cpu()
+        cmax, cmin = c.clone(), c.clone()
+        dist.all_reduce(cmax, op=dist.ReduceOp.MAX)
+        dist.all_reduce(cmin, op=dist.ReduceOp.MIN)
+        q.put((rank, ok_seq, ok_tile, len(spans), err, float(cmax - cmin), None))
+    except Exception as e:   # report to the parent instead of hanging it
+        import traceback
+        q.put((rank, False, False, 0, float("inf"), float("inf"), traceback.format_exc()))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_dp_world2_on_one_device_overlapped_allreduce():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=100) for _ in ps)
+    for p in ps:
+        p.join(timeout=30)
+    print("dp world 2:", [r[:6] for r in res])
+    for r in res:
+        assert r[6] is None, r[6]
+        rank, ok_seq, ok_tile, nb, err, spread, _ = r
+        assert ok_seq, "stage_done sequence differs from CRNNEngine.backward_stages()"
+        assert ok_tile, "issued buckets do not tile the flat buffer"
+        assert err < 1e-5, err
+        assert spread == 0.0, spread

@@ -569,7 +569,10 @@ def _pack_lstm(w_ih, w_hh, b_ih, b_hh, H, dtype, L):
     (torch.bfloat16, (64, 5, 768, 512), "seq"), (torch.bfloat16, (256, 4, 512, 512), "seq"),
     (torch.bfloat16, (64, 6, 512, 512), "seq1"), (torch.bfloat16, (64, 6, 512, 512), "seq2"),
     (torch.bfloat16, (32, 5, 256, 128), "seq1"), (torch.bfloat16, (32, 5, 768, 128), "seq2"),
-    (torch.bfloat16, (64, 5, 768, 512), "seq1"), (torch.bfloat16, (64, 5, 512, 256), "seq3")])
+    (torch.bfloat16, (64, 5, 768, 512), "seq1"), (torch.bfloat16, (64, 5, 512, 256), "seq3"),
+    # the bench's own lengths: configs[2] (T = 32, B = 256, H = 512) and configs[4] (T = 128, B = 64,
+    # H = 768, input 768 = a stacked layer), against the oracle with the bf16-storage bar
+    (torch.bfloat16, (256, 32, 512, 512), "seq"), (torch.bfloat16, (64, 128, 768, 768), "seq")])
 def test_bilstm_fwd_bwd(BTHI, dtype, oneshot):
     """bf16 steps run the one-shot LDS-DMA GEMM (forward: fused cell; backward with whh_t: split-K
     partials + sum/cell pass; H = 512 -> 4 splits); oneshot=False passes no whh_t (staged kernel);
@@ -640,7 +643,18 @@ def _bilstm_case(L, BTHI, dtype, oneshot):
             L.call("crnn_lstm_step_fwd", dt, xg.data_ptr(), whh.data_ptr(), hseq.data_ptr(), gsv.data_ptr(),
                    csv.data_ptr(), B, T, H, s, st)
     tol = 2e-5 if dtype == torch.float32 else 3e-2
-    assert relerr(hseq.float().cpu(), href.detach()) < tol
+    err = relerr(hseq.float().cpu(), href.detach())
+    assert err < tol
+    if dtype == torch.bfloat16:
+        # principled bar: the oracle with the kernels' bf16 storage (input projections and each h_t
+        # rounded, crnn_oracle.lstm_direction store=); the HIP sweep may be no further from fp32
+        rb = lambda t: t.bfloat16().float()  # noqa: E731
+        with torch.no_grad():
+            he = torch.cat([O.lstm_direction(x, w_ih[0], w_hh[0], b_ih[0], b_hh[0], False, rb),
+                            O.lstm_direction(x, w_ih[1], w_hh[1], b_ih[1], b_hh[1], True, rb)], 2)
+        err_model = relerr(he, href.detach())
+        print(f"BiLSTM B={B} T={T} H={H}: hseq rel err {err:.3e}, bf16-storage model {err_model:.3e}")
+        assert err <= 1.5 * err_model + 1e-4, (err, err_model)
     dh = dh_out.to(DEV, dtype).contiguous()
     dg = torch.empty(2, T, B, 4 * H, dtype=dtype, device=DEV)
     dc = torch.empty(2, B, H, device=DEV)
@@ -771,6 +785,17 @@ def test_greedy_decode_golden(itos):
     texts, seqs = ctc_greedy_decoder(torch.from_numpy(z["logits"]).to(DEV), itos[1:])
     assert seqs == ref["seqs"]
     assert texts == ref["texts"]
+    # configs[0]'s B=8 / T=16 (T > B: the reference's layout heuristic cannot decode it directly;
+    # its strings come from its decoder on a batch padded past T, decode_b8_t16.json):
+    # the explicit layout decodes it, and the TBC view of the same logits gives the same strings
+    z = load("decode_b8_t16.npz")
+    with open(os.path.join(GOLDEN, "decode_b8_t16.json"), encoding="utf-8") as f:
+        ref = json.load(f)
+    lg = torch.from_numpy(z["logits"]).to(DEV)
+    texts, seqs = ctc_greedy_decoder(lg, itos[1:], layout="BTC")
+    assert seqs == ref["seqs"] and texts == ref["texts"]
+    texts, seqs = ctc_greedy_decoder(lg.permute(1, 0, 2).contiguous(), itos[1:], layout="TBC")
+    assert seqs == ref["seqs"] and texts == ref["texts"]
 
 
 @pytest.mark.parametrize("C,B,HW,rpp", [(256, 5, 64, 16), (512, 256, 32, 8), (512, 7, 128, 128), (256, 4, 96, 32)])

@@ -79,6 +79,14 @@ def test_oracle_decode(itos):
     seqs = O.greedy_decode(z["logits"])
     assert seqs == ref["seqs"]
     assert O.ids_to_text(seqs, itos) == ref["texts"]
+    # B=8 / T=16 (configs[0]; T > B): the reference's strings from a batch padded past T
+    z = load("decode_b8_t16.npz")
+    with open(os.path.join(GOLDEN, "decode_b8_t16.json"), encoding="utf-8") as f:
+        ref = json.load(f)
+    assert ref["B"] == 8 and ref["T"] == 16 and z["logits"].shape == (8, 16, 194)
+    seqs = O.greedy_decode(z["logits"])
+    assert seqs == ref["seqs"]
+    assert O.ids_to_text(seqs, itos) == ref["texts"]
 
 
 def test_oracle_bilstm_stack():

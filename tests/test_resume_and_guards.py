@@ -68,8 +68,7 @@ def test_fused_adamw_load_before_flat_buffers_defers():
     src = _FlatModel(shapes)
     o = FusedAdamW(src)
     o.step_count = 5
-    o._m = torch.arange(10.0)
-    o._v = torch.arange(10.0) * 2
+    o._bufs = [torch.arange(10.0), torch.arange(10.0) * 2]
     sd = o.state_dict()
     m = _FlatModel(shapes)
     flat = m._flat_param
@@ -77,7 +76,7 @@ def test_fused_adamw_load_before_flat_buffers_defers():
     o2 = FusedAdamW(m)
     o2.load_state_dict(sd)
     assert o2._m is None and o2.step_count == 5
-    o2._alloc_moments(flat)
+    o2._alloc_state(flat)
     assert torch.equal(o2._m, torch.arange(10.0)) and torch.equal(o2._v, torch.arange(10.0) * 2)
 
 
@@ -192,7 +191,9 @@ def test_seq_status_word_is_sticky_and_polled():
     """the persistent BiLSTM's error words are ORed into a sticky word; check_status() raises on
     it and the per-call non-blocking poll raises once its copy has landed."""
     _gpu()
+    from crnn_hip import _lib as L
     from crnn_hip.ctc import ctc_loss
+    from crnn_hip.optim import FusedAdam, FusedAdamW, FusedSGD
     from crnn_hip.recipe import recipe_state_dict, synthetic_batch
     from model.model import RCNN
     m = RCNN(num_classes=194, hidden_size=256, blank_id=None, compute_dtype=torch.bfloat16, enc_dropout_p=0.0)
@@ -205,9 +206,22 @@ def test_seq_status_word_is_sticky_and_polled():
     assert eng._seq_used, "B=16, H=256 bf16 should run the persistent BiLSTM kernels"
     eng.check_status()                     # clean
     ws = eng.ws.bufs["rnn.seq_ws"]
-    ws[eng._sticky_idx_of(ws)] = 1        # as if a sweep had timed out
+    # the library's layout, not a hard-coded one
+    assert eng._sticky_index == L.lib().crnn_lstm_seq_status_offset(16) // 4
+    ws[eng._sticky_index] = 1             # as if a sweep had timed out
     with pytest.raises(RuntimeError, match="timed out"):
         eng.check_status()
+    # the optimizer kernels read the sticky word and leave weights and moments untouched (ADVICE r02:
+    # a timed-out sweep's NaN gradients must not reach a checkpoint)
+    for make in (lambda: FusedAdam(m, lr=1e-2, weight_decay=1e-2), lambda: FusedAdamW(m, lr=1e-2),
+                 lambda: FusedSGD(m, lr=1e-2, momentum=0.9)):
+        opt = make()
+        before = m._flat_param.clone()
+        m._flat_grad.fill_(float("nan"))
+        opt.step()
+        torch.cuda.synchronize()
+        assert torch.equal(m._flat_param, before)
+        assert all(torch.count_nonzero(b) == 0 for b in opt._bufs)
     with pytest.raises(RuntimeError, match="timed out"):
         for _ in range(4):
             ctc_loss(m(x), tg, tl).backward()

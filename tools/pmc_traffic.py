@@ -34,7 +34,10 @@ def read(d):
 
 
 def main(p_fetch, p_write, p_mfma):
+    sys.path.insert(0, __import__("os").path.join(__import__("os").path.dirname(__file__), "..", "rcnn-ocr_amd"))
+    from crnn_hip._lib import source_hash
     out = {"source": "rocprofv3 --pmc passes over `bench.py --steps 3 --warmup 1` (tools/gpu_pmc.sh)",
+           "source_hash": source_hash(),
            "correction": "hbm = 2 x FETCH_SIZE (gfx950 half-count of 16-B/lane streaming reads) + WRITE_SIZE"}
     acc = defaultdict(lambda: defaultdict(float))
     for path, ctr in ((p_fetch, "FETCH_SIZE"), (p_write, "WRITE_SIZE")):
