@@ -78,7 +78,9 @@ enum { CRNN_OPT_GEMM_STAGGER = 0,    /* 256-row conv GEMM: waves 4-7 one barrier
                                           0 = always sc1 */
        CRNN_OPT_GEMM4W = 14,         /* 256-row GEMM family: 1 = the 4-wave form (one wave per SIMD, 128 x BN/2
                                         per wave, fragments double-buffered in registers), 0 = the 8-wave form */
-       CRNN_OPT_COUNT = 15 };
+       CRNN_OPT_DIAG = 15,           /* diagnostics only (default 0): bit 0 = conv fwd / plain dgrad / wgrad GEMMs
+                                        skip their epilogue stores (the measured epilogue cost; results invalid) */
+       CRNN_OPT_COUNT = 16 };
 int crnn_set_option(int key, int value);
 
 /* ------------------------------------------------------------------ layout */

@@ -657,6 +657,7 @@ int conv_fwd_tt(const Geo& g, const crnn_conv_desc* d, const void* x, const void
   FwdA<T, UT> la{(const T*)x, g, M, K, nbytes((long)g.B * g.Hi * g.Wi * g.Ci, sizeof(T))};
   RowMajorK<T> lb{(const T*)w, K, N, K};
   FwdEpi<T> ep{(T*)y, psum, psq, M, N, esc, esh};
+  if (crnn_option(CRNN_OPT_DIAG) & 1) ep.M = 0;   // diagnostic: no output stores
   int bm, bn;
   crnn_conv_fwd_tile(sizeof(T) == 2 ? CRNN_BF16 : CRNN_F32, d, &bm, &bn);
   if constexpr (sizeof(T) == 2 && UT) {
@@ -779,6 +780,7 @@ template <typename T> int conv_dgrad_t(const crnn_conv_desc* d, const void* dy, 
   DgradA<T> la{(const T*)dy, g, M, K, lsh, lsw, nbytes((long)g.B * g.Ho * g.Wo * g.Co, sizeof(T))};
   DgradB<T> lb{(const T*)w, g, K, nbytes((long)g.Co * g.KH * g.KW * g.Ci, sizeof(T))};
   DgradEpi<T> ep{(T*)dx, (const T*)dres, (const T*)yres, M, N, accumulate};
+  if (crnn_option(CRNN_OPT_DIAG) & 1) ep.M = 0;   // diagnostic: no output stores
   if constexpr (sizeof(T) == 2) {
     int deep = deep_dgrad_bn<T>(M, N, g.Co, 128);
     if (deep && crnn_option(CRNN_OPT_QUANT_TILE) && round_eff(((long)M + 255) / 256 * (N / deep)) < quant_eff(deep)) deep = 0;
@@ -842,6 +844,7 @@ template <typename T> int conv_wgrad_t(const crnn_conv_desc* d, const void* dy, 
   WgradA<T> la{(const T*)dy, g.Co, Mp, nbytes((long)Mp * g.Co, sizeof(T))};
   WgradB<T> lb{(const T*)x, g, Kp, Mp, nbytes((long)g.B * g.Hi * g.Wi * g.Ci, sizeof(T))};
   SlabEpi ep{ws, g.Co, Kp};
+  if (crnn_option(CRNN_OPT_DIAG) & 1) ep.M = 0;   // diagnostic: no slab stores
   if constexpr (sizeof(T) == 2) {
     const int fk = bm == 256 ? wgrad_fast_kind(g) : 0;
     if (fk) {
