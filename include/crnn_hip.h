@@ -124,6 +124,12 @@ int crnn_pack_batch(int dtype, const crnn_pack_job* jobs, int njobs, long total,
  * max_slab = the largest Ci*KH*KW (<= 16384). Same output as crnn_pack_batch for these jobs. */
 int crnn_pack_conv_batch(int dtype, const crnn_pack_job* jobs, int njobs, long total_rows, int max_slab,
                          void* stream);
+/* transposed, flipped conv kernels for crnn_conv_dgrad_tw (kind CRNN_PACK_CONV_T, a..d = Co, Ci, KH, KW;
+ * Ci % 8 == 0, KH*KW <= 9): dst[ci][kh][kw][co] = src_OIHW[co][ci][KH-1-kh][KW-1-kw] in dtype. One workgroup per
+ * 32 x 32 (co, ci) tile, coalesced both ways through LDS; job.start = the job's first tile in the
+ * concatenation (a job has ceil(Co/32) * ceil(Ci/32) tiles, co-tile major); total_tiles = all. */
+#define CRNN_PACK_CONV_T 4
+int crnn_pack_conv_t_batch(int dtype, const crnn_pack_job* jobs, int njobs, long total_tiles, void* stream);
 
 /* ------------------------------------------------------------------ conv */
 typedef struct {
@@ -171,6 +177,19 @@ int crnn_conv_dgrad_bnrelu_rows(int dtype, const crnn_conv_desc* d);
 int crnn_conv_dgrad_bnrelu(int dtype, const crnn_conv_desc* d, const void* dy, const void* w, void* dx, const void* z,
                            const float* mean, const float* invstd, const float* scale, const float* shift, float* pg,
                            float* pgx, void* stream);
+/* stride-1 dgrad on the forward conv path: wt = the transposed, flipped kernel
+ * wt[Ci][KH][KW][Co] = w[Co][KH-1-kh][KW-1-kw][Ci] (crnn_pack_conv_batch kind CRNN_PACK_CONV_T),
+ * K-contiguous like a forward weight, so dgrad(dy) is the forward conv of dy with pad K-1-pad and
+ * runs the forward's loaders, tiles and padding-row skip. Same outputs and epilogues as
+ * crnn_conv_dgrad / crnn_conv_dgrad_bnrelu. bf16, stride 1, Co % 64 == 0, geometries on the 256-row
+ * kernel: crnn_conv_dgrad_tw_rows = the pg / pgx partial rows of the bnrelu form (2 per 256 dx rows),
+ * 0 when the geometry is not supported. */
+int crnn_conv_dgrad_tw_rows(int dtype, const crnn_conv_desc* d);
+int crnn_conv_dgrad_tw(int dtype, const crnn_conv_desc* d, const void* dy, const void* wt, void* dx, const void* dres,
+                       const void* yres, int accumulate, void* stream);
+int crnn_conv_dgrad_bnrelu_tw(int dtype, const crnn_conv_desc* d, const void* dy, const void* wt, void* dx,
+                              const void* z, const float* mean, const float* invstd, const float* scale,
+                              const float* shift, float* pg, float* pgx, void* stream);
 /* dw_oihw (fp32, reference layout) = beta*dw + wgrad(dy, x); ws = split-K slabs. */
 int crnn_conv_wgrad(int dtype, const crnn_conv_desc* d, const void* dy, const void* x, float* dw_oihw, float* ws, size_t ws_bytes, float beta, void* stream);
 size_t crnn_conv_wgrad_workspace(int dtype, const crnn_conv_desc* d);

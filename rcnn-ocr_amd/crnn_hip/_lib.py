@@ -49,11 +49,12 @@ class PackJob(C.Structure):  # crnn_pack_job
  OPT_WGRAD_REDUCE, OPT_WGRAD_FAST, OPT_ROW_CLASS, OPT_QUANT_TILE, OPT_PAD_SKIP, OPT_LSTM_BWD_PART,
  OPT_LSTM_L2_HANDOFF, OPT_GEMM4W, OPT_DIAG) = range(16)
 
-PACK_CONV, PACK_ROWS, PACK_ROWS_SUM, PACK_TRANSPOSE = 0, 1, 2, 3
+PACK_CONV, PACK_ROWS, PACK_ROWS_SUM, PACK_TRANSPOSE, PACK_CONV_T = 0, 1, 2, 3, 4
 
 _SIGS = {
     "crnn_pack_batch": ([i32, vp, i32, i64, vp], i32),
     "crnn_pack_conv_batch": ([i32, vp, i32, i64, i32, vp], i32),
+    "crnn_pack_conv_t_batch": ([i32, vp, i32, i64, vp], i32),
     "crnn_version": ([], i32),
     "crnn_set_option": ([i32, i32], i32),
     "crnn_last_error_string": ([], C.c_char_p),
@@ -76,6 +77,9 @@ _SIGS = {
     "crnn_conv_dgrad_ds_supported": ([i32, C.POINTER(ConvDesc), C.POINTER(ConvDesc)], i32),
     "crnn_conv_dgrad_ds": ([i32, C.POINTER(ConvDesc), C.POINTER(ConvDesc), vp, vp, vp, vp], i32),
     "crnn_conv_dgrad_bnrelu_rows": ([i32, C.POINTER(ConvDesc)], i32),
+    "crnn_conv_dgrad_tw_rows": ([i32, C.POINTER(ConvDesc)], i32),
+    "crnn_conv_dgrad_tw": ([i32, C.POINTER(ConvDesc), vp, vp, vp, vp, vp, i32, vp], i32),
+    "crnn_conv_dgrad_bnrelu_tw": ([i32, C.POINTER(ConvDesc), vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp], i32),
     "crnn_conv_dgrad_bnrelu": ([i32, C.POINTER(ConvDesc), vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp], i32),
     "crnn_conv_wgrad": ([i32, C.POINTER(ConvDesc), vp, vp, vp, vp, sz, f32, vp], i32),
     "crnn_conv_wgrad_workspace": ([i32, C.POINTER(ConvDesc)], sz),

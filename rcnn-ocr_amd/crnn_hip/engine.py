@@ -191,6 +191,27 @@ class CRNNEngine:
         yield self.co0
         yield self.co1
 
+    def tw_convs(self):
+        """the convs whose input gradient can run on the forward path (crnn_conv_dgrad_tw): bf16,
+        stride 1, KH*KW <= 9, Co % 64 == 0, unpadded Ci % 8 == 0; not the stem (halo kernels)"""
+        if not self.dgrad_tw or self.dtype != torch.bfloat16:
+            return []
+        return [cs for cs in self.convs() if cs not in (self.stem0, self.stem1) and cs.sh == 1 and cs.sw == 1
+                and cs.kh * cs.kw <= 9 and cs.co % 64 == 0 and cs.ci % 8 == 0 and cs.ci == cs.ci_real]
+
+    def _dgrad(self, cs: "ConvSpec", b, h, w, dy, dx, dres=None, yres=None, accumulate=0):
+        """input gradient of conv `cs` (input map h x w): the forward-path form where packed and
+        supported, else the native dgrad kernels"""
+        d = cs.desc(b, h, w)
+        wt = self.packed.get(cs.name + ".t")
+        fl = self.conv_flops(cs, b, h, w)
+        if wt is not None and L.lib().crnn_conv_dgrad_tw_rows(self.dt, d) > 0:
+            self._conv_call("dgrad", fl, "crnn_conv_dgrad_tw", self.dt, d, ptr(dy), ptr(wt), ptr(dx), ptr(dres),
+                            ptr(yres), accumulate, L.stream_ptr())
+        else:
+            self._conv_call("dgrad", fl, "crnn_conv_dgrad", self.dt, d, ptr(dy), ptr(self.packed[cs.name]), ptr(dx),
+                            ptr(dres), ptr(yres), accumulate, L.stream_ptr())
+
     def pack(self):
         """fp32 reference-layout parameters -> compute-dtype kernel layouts: every weight in one
         crnn_pack_batch launch (job table built once; all pointers are persistent views)."""
@@ -200,9 +221,11 @@ class CRNNEngine:
             return
         if self._pack_jobs is None:
             self._build_pack_jobs()
-        (cjobs, cn, crows, cslab), (jobs, n, total) = self._pack_jobs
+        (cjobs, cn, crows, cslab), (jobs, n, total), (tjobs, tn, ttiles) = self._pack_jobs
         call("crnn_pack_conv_batch", self.dt, ptr(cjobs), cn, crows, cslab, L.stream_ptr())
         call("crnn_pack_batch", self.dt, ptr(jobs), n, total, L.stream_ptr())
+        if tn:
+            call("crnn_pack_conv_t_batch", self.dt, ptr(tjobs), tn, ttiles, L.stream_ptr())
         self.packed_version = ver
 
     def _build_pack_jobs(self):
@@ -236,6 +259,20 @@ class CRNNEngine:
         craw = torch.frombuffer(bytearray(bytes(carr)), dtype=torch.uint8).to(self.device)
         conv_tab = (craw, len(jobs), rows, slab)
         jobs.clear()
+        # transposed, flipped kernels [Ci][KH][KW][Co] of the stride-1 convs (crnn_conv_dgrad_tw)
+        tiles = 0
+        for cs in self.tw_convs():
+            out = self._pbuf(cs.name + ".t", (cs.ci, cs.kh, cs.kw, cs.co), T)
+            job(L.PACK_CONV_T, self.p[cs.name], out, cs.co, cs.ci, cs.kh, cs.kw)
+            jobs[-1].start = tiles
+            tiles += ((cs.co + 31) // 32) * ((cs.ci + 31) // 32)
+        if jobs:
+            tarr = (L.PackJob * len(jobs))(*jobs)
+            traw = torch.frombuffer(bytearray(bytes(tarr)), dtype=torch.uint8).to(self.device)
+        else:
+            traw = None
+        tw_tab = (traw, len(jobs), tiles)
+        jobs.clear()
         for l in range(self.nl):
             pre = f"enc_rnn.{l}"
             ind = self.enc_dim if l == 0 else H
@@ -266,7 +303,7 @@ class CRNNEngine:
             start += n
         arr = (L.PackJob * len(jobs))(*jobs)
         raw = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(self.device)
-        self._pack_jobs = (conv_tab, (raw, len(jobs), start))
+        self._pack_jobs = (conv_tab, (raw, len(jobs), start), tw_tab)
 
     # ------------------------------------------------------------------ instrumentation
     def enable_timing(self, on: bool = True):
@@ -349,6 +386,10 @@ class CRNNEngine:
     eval_fuse = os.environ.get("CRNN_EVAL_FUSE", "1") == "1"
     # strided blocks: conv1's and the downsample's dgrads as one launch (CRNN_DS_FUSE, default 1)
     ds_fuse = os.environ.get("CRNN_DS_FUSE", "1") == "1"
+    # stride-1 conv dgrads on the FORWARD conv path with a transposed, flipped weight pack
+    # (crnn_conv_dgrad_tw; CRNN_DGRAD_TW, default 1): the forward's K-contiguous B operand, tiles and
+    # padding-row skip instead of the dgrad loader's transposed LDS reads
+    dgrad_tw = os.environ.get("CRNN_DGRAD_TW", "1") == "1"
 
     def _seq_ok(self, B):
         return self.use_seq and bool(L.lib().crnn_lstm_seq_supported(self.dt, B, self.H))
@@ -989,15 +1030,13 @@ class CRNNEngine:
                      out=dz, accumulate_params=accumulate)
         self._wgrad(self.co1, dz, co["a0"], B, co["h2"], co["w2"])
         da = bufC[: B * co["h2"] * co["w2"] * 512]
-        self._conv_call("dgrad", self.conv_flops(self.co1, B, co["h2"], co["w2"]), "crnn_conv_dgrad", dt, self.co1.desc(B, co["h2"], co["w2"]), ptr(dz), ptr(self.packed[self.co1.name]),
-             ptr(da), None, None, 0, s)
+        self._dgrad(self.co1, B, co["h2"], co["w2"], dz, da)
         dz0 = self._dz("co0", bufA, B * co["h2"] * co["w2"] * 512)
         self._bn_bwd(1, da, co["z0"], (co["m0"], co["i0"], co["sc0"], co["sh0"]), self.co0.bn,
                      B * co["h2"] * co["w2"], 512, out=dz0, accumulate_params=accumulate)
         self._wgrad(self.co0, dz0, co["x"], B, co["h"], co["w"])
         dy = bufB[: B * co["h"] * co["w"] * 512]
-        self._conv_call("dgrad", self.conv_flops(self.co0, B, co["h"], co["w"]), "crnn_conv_dgrad", dt, self.co0.desc(B, co["h"], co["w"]), ptr(dz0), ptr(self.packed[self.co0.name]),
-             ptr(dy), None, None, 0, s)
+        self._dgrad(self.co0, B, co["h"], co["w"], dz0, dy)
         done(["cnn.conv_out."])
         # ---- residual blocks, reverse
         bufs = [bufA, bufB, bufC]
@@ -1034,19 +1073,23 @@ class CRNNEngine:
             self._wgrad(blk.conv2, dz2, sb["a1"], B, ho, wo)
             da1 = bufs[o2][: Mo * P]
             d2 = blk.conv2.desc(B, ho, wo)
-            frows = L.lib().crnn_conv_dgrad_bnrelu_rows(dt, d2)
+            wt2 = self.packed.get(blk.conv2.name + ".t")
+            frows = L.lib().crnn_conv_dgrad_tw_rows(dt, d2) if wt2 is not None else 0
+            fname, fw = ("crnn_conv_dgrad_bnrelu_tw", wt2) if frows > 0 else \
+                ("crnn_conv_dgrad_bnrelu", self.packed[blk.conv2.name])
+            if frows == 0:
+                frows = L.lib().crnn_conv_dgrad_bnrelu_rows(dt, d2)
             sums = None
             if frows > 0 and frows * P <= 1024 * 512:
                 # dgrad + BN1's backward sums in the epilogue (no reduce pass over da1, z1)
                 pg = ws.get("bnb.pg", (1024 * 512,), torch.float32)[: frows * P]
                 pgx = ws.get("bnb.pgx", (1024 * 512,), torch.float32)[: frows * P]
-                self._conv_call("dgrad", self.conv_flops(blk.conv2, B, ho, wo), "crnn_conv_dgrad_bnrelu", dt, d2,
-                                ptr(dz2), ptr(self.packed[blk.conv2.name]), ptr(da1), ptr(sb["z1"]), ptr(sb["m1"]),
+                self._conv_call("dgrad", self.conv_flops(blk.conv2, B, ho, wo), fname, dt, d2,
+                                ptr(dz2), ptr(fw), ptr(da1), ptr(sb["z1"]), ptr(sb["m1"]),
                                 ptr(sb["i1"]), ptr(sb["sc1"]), ptr(sb["sh1"]), ptr(pg), ptr(pgx), s)
                 sums = (pg, pgx, frows)
             else:
-                self._conv_call("dgrad", self.conv_flops(blk.conv2, B, ho, wo), "crnn_conv_dgrad", dt, d2, ptr(dz2),
-                                ptr(self.packed[blk.conv2.name]), ptr(da1), None, None, 0, s)
+                self._dgrad(blk.conv2, B, ho, wo, dz2, da1)
             d1 = blk.conv1.desc(B, h, w)
             dds = blk.ds.desc(B, h, w) if blk.ds is not None else None
             # the downsample's dgrad as one more tap of conv1's parity class (0, 0): its input gradient
@@ -1064,8 +1107,7 @@ class CRNNEngine:
             Ci = blk.conv1.ci
             dxb = bufs[o2][: B * h * w * Ci]
             if blk.ds is None:
-                self._conv_call("dgrad", self.conv_flops(blk.conv1, B, h, w), "crnn_conv_dgrad", dt, blk.conv1.desc(B, h, w), ptr(dz1), ptr(self.packed[blk.conv1.name]),
-                     ptr(dxb), ptr(dyb), ptr(sb["y"]), 0, s)
+                self._dgrad(blk.conv1, B, h, w, dz1, dxb, dres=dyb, yres=sb["y"])
                 cur = o2
             elif fuse_ds:
                 dsv = sb["ds"]

@@ -1030,6 +1030,39 @@ __global__ __launch_bounds__(256) void pack_conv_kernel(const crnn_pack_job* __r
   }
 }
 
+// transposed, flipped conv kernel (crnn_conv_dgrad_tw's B operand): one workgroup per (32 co x 32 ci)
+// tile of a job. The source rows [co][ci0 .. ci0+31][KH*KW] are contiguous runs (coalesced reads into
+// LDS, row pitch 32*KHW + 1 words); the destination rows [ci][tap'][co0 .. co0+31] are written as
+// 64-B runs of consecutive co.
+template <typename T>
+__global__ __launch_bounds__(256) void pack_conv_t_kernel(const crnn_pack_job* __restrict__ jobs, int njobs) {
+  __shared__ float tile[32 * (32 * 9 + 1)];    // KH*KW <= 9 (the header's contract)
+  const long bid = blockIdx.x;
+  int lo = 0, hi = njobs - 1;
+  while (lo < hi) {  // last job with start (first tile) <= bid
+    const int mid = (lo + hi + 1) >> 1;
+    if (jobs[mid].start <= bid) lo = mid;
+    else hi = mid - 1;
+  }
+  const crnn_pack_job jb = jobs[lo];
+  const int Co = jb.a, Ci = jb.b, KHW = jb.c * jb.d;
+  if (KHW > 9) return;
+  const int tci = (Ci + 31) / 32;
+  const int tl = (int)(bid - jb.start), co0 = (tl / tci) * 32, ci0 = (tl % tci) * 32;
+  const int nco = min(32, Co - co0), nci = min(32, Ci - ci0), run = nci * KHW, P = 32 * KHW + 1;
+  for (int i = threadIdx.x; i < 32 * run; i += blockDim.x) {
+    const int r = i / run, e = i - r * run;
+    tile[r * P + e] = r < nco ? jb.src[((size_t)(co0 + r) * Ci + ci0) * KHW + e] : 0.f;
+  }
+  __syncthreads();
+  T* dst = (T*)jb.dst;
+  for (int i = threadIdx.x; i < 32 * run; i += blockDim.x) {
+    const int co = i & 31, rest = i >> 5;
+    const int tp = rest % KHW, ci = rest / KHW;   // destination tap (flipped source tap KHW-1-tp)
+    if (co < nco) dst[((size_t)(ci0 + ci) * KHW + tp) * Co + co0 + co] = fromf<T>(tile[co * P + ci * KHW + (KHW - 1 - tp)]);
+  }
+}
+
 // ------------------------------------------------------------ dropout (enc_dropout, model/model.py:201,220)
 // Counter-based: element i of a call with seed s is kept iff hash(s, i) >= p * 2^32, so the
 // backward regenerates the forward's mask from (seed, index) and nothing is stored. The hash is
@@ -1758,6 +1791,13 @@ int crnn_pack_batch(int dtype, const crnn_pack_job* jobs, int njobs, long total,
   const long chunk = (total + blocks - 1) / blocks;
   DISPATCH(dtype, hipLaunchKernelGGL(pack_batch_kernel<T>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
                                      jobs, njobs, total, chunk));
+  return (int)hipGetLastError();
+}
+
+int crnn_pack_conv_t_batch(int dtype, const crnn_pack_job* jobs, int njobs, long total_tiles, void* stream) {
+  if (njobs <= 0 || total_tiles <= 0) return 0;
+  DISPATCH(dtype, hipLaunchKernelGGL(pack_conv_t_kernel<T>, dim3((unsigned)total_tiles), dim3(256), 0,
+                                     (hipStream_t)stream, jobs, njobs));
   return (int)hipGetLastError();
 }
 

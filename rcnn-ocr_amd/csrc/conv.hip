@@ -829,6 +829,51 @@ int conv_dgrad_bnrelu(const crnn_conv_desc* d, const void* dy, const void* w, vo
   return launch256<256, 128>(la, lb, ep, M, N, K, st);
 }
 
+// ---- stride-1 dgrad on the FORWARD conv path ("tw": transposed weights)
+// dgrad(dy)[b,hi,wi,ci] = sum_{kh',kw',co} dy[b, hi - (KH-1-ph) + kh', wi - (KW-1-pw) + kw', co] * wt[ci][kh'][kw'][co]
+// with wt[ci][kh'][kw'][co] = w[co][KH-1-kh'][KW-1-kw'][ci]: a forward conv of dy (Ci' = Co, Co' = Ci,
+// pad' = K-1-pad) with the flipped, transposed kernel, packed K-contiguous like a forward weight. So
+// the dgrad runs the forward's A loader, its K-contiguous B fragments (ds_read_b128, not the
+// row-contiguous transposed reads of DgradB), its tile rules and its padding-row skip, with the
+// dgrad epilogues (DgradEpi / DgradBnEpi store by (input pixel, ci) exactly like the native path).
+inline crnn_conv_desc dgrad_fwd_desc(const crnn_conv_desc* d) {
+  crnn_conv_desc t{d->B, d->Ho, d->Wo, d->Co, d->Hi, d->Wi, d->Ci, d->KH, d->KW, 1, 1,
+                   d->KH - 1 - d->ph, d->KW - 1 - d->pw, d->Co};
+  return t;
+}
+
+// the tw path takes this geometry: bf16, stride 1, whole 64-channel K stages, the 256-row tile
+inline bool dgrad_tw_ok(const crnn_conv_desc* d) {
+  if (d->sh != 1 || d->sw != 1 || d->Co % 64 || d->Ci % 8) return false;
+  if (d->ph > d->KH - 1 || d->pw > d->KW - 1) return false;
+  if (use_halo(CRNN_BF16, d, true)) return false;
+  const crnn_conv_desc t = dgrad_fwd_desc(d);
+  if (t.Ho != d->Hi || t.Wo != d->Wi) return false;
+  int bm, bn;
+  crnn_conv_fwd_tile(CRNN_BF16, &t, &bm, &bn);
+  return bm == 256;
+}
+
+template <class EPI>
+int conv_dgrad_tw_launch(const crnn_conv_desc* d, const void* dy, const void* wt, const EPI& ep, hipStream_t st) {
+  using T = bf16;
+  const crnn_conv_desc t = dgrad_fwd_desc(d);
+  const Geo g = geo(&t);
+  const int M = g.B * g.Ho * g.Wo, N = g.Co, K = g.KH * g.KW * g.Ci;
+  FwdA<T, true> la{(const T*)dy, g, M, K, nbytes((long)g.B * g.Hi * g.Wi * g.Ci, sizeof(T))};
+  RowMajorK<T> lb{(const T*)wt, K, N, K};
+  int bm, bn;
+  crnn_conv_fwd_tile(CRNN_BF16, &t, &bm, &bn);
+  if (bm != 256) return crnn_set_error(hipErrorInvalidValue, "conv_dgrad_tw: geometry not on the 256-row path");
+  if (pad_skip_ok(g, g.Ho, g.Wo)) {
+    const int ktk = g.KW * g.Ci / 64;
+    if (bn == 256) return launch256<256, 256, 1>(la, lb, ep, M, N, K, st, 1, 1, ktk);
+    return launch256<256, 128, 1>(la, lb, ep, M, N, K, st, 1, 1, ktk);
+  }
+  if (bn == 256) return launch256<256, 256>(la, lb, ep, M, N, K, st);
+  return launch256<256, 128>(la, lb, ep, M, N, K, st);
+}
+
 template <typename T> int conv_wgrad_t(const crnn_conv_desc* d, const void* dy, const void* x, float* dw,
                                        float* ws, size_t ws_bytes, float beta, hipStream_t st) {
   Geo g = geo(d);
@@ -1037,6 +1082,30 @@ int crnn_conv_dgrad_bnrelu(int dtype, const crnn_conv_desc* d, const void* dy, c
   if (dtype != CRNN_BF16 || dgrad_bnrelu_rows(d) == 0)
     return crnn_set_error(hipErrorInvalidValue, "conv_dgrad_bnrelu: geometry not on the 256-row path");
   return conv_dgrad_bnrelu(d, dy, w, dx, z, mean, invstd, scale, shift, pg, pgx, (hipStream_t)stream);
+}
+
+int crnn_conv_dgrad_tw_rows(int dtype, const crnn_conv_desc* d) {
+  return dtype == CRNN_BF16 && dgrad_tw_ok(d) ? (int)(((long)d->B * d->Hi * d->Wi + 255) / 256 * 2) : 0;
+}
+
+int crnn_conv_dgrad_tw(int dtype, const crnn_conv_desc* d, const void* dy, const void* wt, void* dx, const void* dres,
+                       const void* yres, int accumulate, void* stream) {
+  if (!crnn_conv_dgrad_tw_rows(dtype, d))
+    return crnn_set_error(hipErrorInvalidValue, "conv_dgrad_tw: not a bf16 stride-1 geometry on the 256-row path");
+  const int M = d->B * d->Hi * d->Wi, N = d->Ci;
+  DgradEpi<bf16> ep{(bf16*)dx, (const bf16*)dres, (const bf16*)yres, M, N, accumulate};
+  if (crnn_option(CRNN_OPT_DIAG) & 1) ep.M = 0;   // diagnostic: no output stores
+  return conv_dgrad_tw_launch(d, dy, wt, ep, (hipStream_t)stream);
+}
+
+int crnn_conv_dgrad_bnrelu_tw(int dtype, const crnn_conv_desc* d, const void* dy, const void* wt, void* dx,
+                              const void* z, const float* mean, const float* invstd, const float* scale,
+                              const float* shift, float* pg, float* pgx, void* stream) {
+  if (!crnn_conv_dgrad_tw_rows(dtype, d))
+    return crnn_set_error(hipErrorInvalidValue, "conv_dgrad_bnrelu_tw: not a bf16 stride-1 geometry on the 256-row path");
+  const int M = d->B * d->Hi * d->Wi, N = d->Ci;
+  DgradBnEpi<bf16> ep{(bf16*)dx, M, N, (const bf16*)z, mean, invstd, scale, shift, pg, pgx};
+  return conv_dgrad_tw_launch(d, dy, wt, ep, (hipStream_t)stream);
 }
 
 int crnn_conv_wgrad(int dtype, const crnn_conv_desc* d, const void* dy, const void* x, float* dw_oihw,

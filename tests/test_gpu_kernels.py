@@ -402,6 +402,84 @@ def test_dgrad_bnrelu_fused(geo):
         assert relerr(b, a) < 5e-3   # fp32 accumulators vs the bf16-rounded dx of the unfused pass
 
 
+TW_CONVS = [
+    # B, Ci, H, W, Co, k, pad: layer1/2 (8 x 64, 256 ch), layer3/4 (4 x 32, 512 ch: the padding-row
+    # skip), conv_out[1] (2x2, pad 0 -> dgrad pad 1), a ragged last tile; batches large enough for the
+    # 256-row kernel (the tile rules of crnn_conv_fwd_tile on the transposed geometry)
+    (64, 256, 8, 64, 256, (3, 3), (1, 1)),
+    (128, 512, 4, 32, 512, (3, 3), (1, 1)),
+    (256, 512, 2, 33, 512, (2, 2), (0, 0)),
+    (52, 256, 16, 63, 256, (3, 3), (1, 1)),
+]
+
+
+@pytest.mark.parametrize("geo", TW_CONVS)
+def test_conv_dgrad_tw_forward_path(geo):
+    """stride-1 dgrad on the forward conv path (crnn_conv_dgrad_tw / _bnrelu_tw) with the transposed,
+    flipped kernel from crnn_pack_conv_t_batch: the pack equals w.flip(kh, kw).permute(ci, kh, kw, co)
+    exactly; dx vs torch fp32 (autograd) within bf16 rounding and vs the native dgrad kernel; the
+    residual epilogue (dres * (y > 0)) and accumulate; the BN-ReLU backward sums of the bnrelu form
+    against the native form's (fp32 accumulators, different summation order)."""
+    L = _L()
+    import ctypes
+    B, Ci, H, W, Co, k, pad = geo
+    g = torch.Generator().manual_seed(B + Ci + H)
+    w = torch.randn(Co, Ci, *k, generator=g) / math.sqrt(Ci * k[0] * k[1])
+    x = torch.zeros(B, Ci, H, W, requires_grad=True)
+    y = F.conv2d(x, w.bfloat16().float(), padding=pad)
+    dy = torch.randn(y.shape, generator=g).bfloat16().float()
+    (y * dy).sum().backward()
+    ref = x.grad.permute(0, 2, 3, 1).contiguous()
+    dt, st = L.BF16, L.stream_ptr()
+    Ho, Wo = y.shape[2], y.shape[3]
+    d = L.ConvDesc(B, H, W, Ci, Ho, Wo, Co, k[0], k[1], 1, 1, pad[0], pad[1], Ci)
+    rows = L.lib().crnn_conv_dgrad_tw_rows(dt, d)
+    assert rows == (B * H * W + 255) // 256 * 2
+    wdev = w.to(DEV).contiguous()
+    job = L.PackJob(L.PACK_CONV_T, 0, Co, Ci, k[0], k[1], 0, 0, 0, wdev.data_ptr(), None, None, 0)
+    wt = torch.empty(Ci, k[0], k[1], Co, dtype=torch.bfloat16, device=DEV)
+    job.dst = wt.data_ptr()
+    tab = torch.frombuffer(bytearray(bytes(job)), dtype=torch.uint8).to(DEV)
+    ntiles = ((Co + 31) // 32) * ((Ci + 31) // 32)
+    L.call("crnn_pack_conv_t_batch", dt, tab.data_ptr(), 1, ntiles, st)
+    want_wt = w.flip(2, 3).permute(1, 2, 3, 0).contiguous().bfloat16()
+    assert torch.equal(wt.cpu(), want_wt)
+    wn = torch.empty(Co, k[0], k[1], Ci, dtype=torch.bfloat16, device=DEV)
+    L.call("crnn_pack_conv_weight", dt, wdev.data_ptr(), wn.data_ptr(), Co, Ci, k[0], k[1], Ci, st)
+    dyd = dy.permute(0, 2, 3, 1).contiguous().to(DEV, torch.bfloat16)
+    dx_tw = torch.empty(B, H, W, Ci, dtype=torch.bfloat16, device=DEV)
+    dx_nt = torch.empty_like(dx_tw)
+    L.call("crnn_conv_dgrad_tw", dt, d, dyd.data_ptr(), wt.data_ptr(), dx_tw.data_ptr(), None, None, 0, st)
+    L.call("crnn_conv_dgrad", dt, d, dyd.data_ptr(), wn.data_ptr(), dx_nt.data_ptr(), None, None, 0, st)
+    torch.cuda.synchronize()
+    e_tw, e_nt = relerr(dx_tw.float(), ref), relerr(dx_nt.float(), ref)
+    print(f"dgrad {geo}: tw {e_tw:.2e} native {e_nt:.2e}")
+    assert e_tw < 6e-3 and e_tw <= 1.2 * e_nt + 1e-4
+    # residual epilogue + accumulate
+    dres = torch.randn(B, H, W, Ci, generator=g).to(DEV, torch.bfloat16)
+    yres = torch.randn(B, H, W, Ci, generator=g).to(DEV, torch.bfloat16)
+    base = torch.randn(B, H, W, Ci, generator=g).to(DEV, torch.bfloat16)
+    acc = base.clone()
+    L.call("crnn_conv_dgrad_tw", dt, d, dyd.data_ptr(), wt.data_ptr(), acc.data_ptr(), dres.data_ptr(),
+           yres.data_ptr(), 1, st)
+    want = base.float().cpu() + ref + torch.where(yres.float() > 0, dres.float(), 0.0).cpu()
+    assert relerr(acc.float(), want) < 6e-3
+    # the bnrelu form: dx identical to the plain tw form, sums close to the native bnrelu form's
+    z = torch.randn(B, H, W, Ci, generator=g).to(DEV, torch.bfloat16)
+    mean, inv = torch.randn(Ci, generator=g).to(DEV) * 0.1, (torch.rand(Ci, generator=g) + 0.5).to(DEV)
+    sc, sh = (torch.rand(Ci, generator=g) + 0.5).to(DEV), (torch.randn(Ci, generator=g) * 0.2).to(DEV)
+    pg, pgx = torch.empty(rows, Ci, device=DEV), torch.empty(rows, Ci, device=DEV)
+    dx_b = torch.empty_like(dx_tw)
+    L.call("crnn_conv_dgrad_bnrelu_tw", dt, d, dyd.data_ptr(), wt.data_ptr(), dx_b.data_ptr(), z.data_ptr(),
+           mean.data_ptr(), inv.data_ptr(), sc.data_ptr(), sh.data_ptr(), pg.data_ptr(), pgx.data_ptr(), st)
+    torch.cuda.synchronize()
+    assert torch.equal(dx_b, dx_tw)
+    gm = torch.where(z.float() * sc + sh > 0, dx_b.float(), 0.0)
+    xh = (z.float() - mean) * inv
+    s_ref, q_ref = gm.reshape(-1, Ci).sum(0), (gm * xh).reshape(-1, Ci).sum(0)
+    assert relerr(pg.sum(0), s_ref) < 1e-2 and relerr(pgx.sum(0), q_ref) < 1e-2
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_dropout_mask(dtype):
     """crnn_dropout: keep share ~ 1-p, kept values x/(1-p), the mask is a function of (seed, index)

@@ -68,18 +68,23 @@ def main():
         ws = torch.empty(need // 4 + 1, device=dev)
         dw = torch.empty(cs.co, cs.ci_real, cs.kh, cs.kw, device=dev)
         flop = 2.0 * a.batch * d.Ho * d.Wo * cs.co * cs.ci_real * cs.kh * cs.kw
+        twt = None
+        if L.lib().crnn_conv_dgrad_tw_rows(L.BF16, d) > 0:   # the forward-path dgrad's transposed kernel
+            twt = wt.flip(1, 2).permute(3, 1, 2, 0).contiguous()
         ops = {
             "fwd": lambda: L.call("crnn_conv_fwd", L.BF16, d, x.data_ptr(), wt.data_ptr(), y.data_ptr(),
                                   ps.data_ptr(), pq.data_ptr(), s),
             "dgrad": lambda: L.call("crnn_conv_dgrad", L.BF16, d, dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), None,
                                     None, 0, s),
+            "dgradtw": (lambda: L.call("crnn_conv_dgrad_tw", L.BF16, d, dy.data_ptr(), twt.data_ptr(), dx.data_ptr(),
+                                       None, None, 0, s)) if twt is not None else None,
             "wgrad": lambda: L.call("crnn_conv_wgrad", L.BF16, d, dy.data_ptr(), x.data_ptr(), dw.data_ptr(),
                                     ws.data_ptr(), need, 0.0, s),
         }
         line = f"{li:2d} {name:8s} Ci={cs.ci:3d} Co={cs.co:3d} k={cs.kh}x{cs.kw} s={cs.sh},{cs.sw} in={h}x{w} " \
                f"GF={flop / 1e9:7.1f} |"
         for k, fn in ops.items():
-            if a.only and k != a.only:
+            if fn is None or (a.only and k not in a.only.split(",")):
                 continue
             if k == "dgrad" and name == "stem0":
                 continue
