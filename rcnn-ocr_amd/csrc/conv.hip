@@ -452,8 +452,28 @@ inline int wgrad_fast_kind(const Geo& g) {
 // ---- epilogues
 // y = acc, or (eval-mode BN, esc != nullptr) y = ReLU(acc * esc[n] + esh[n]): the running-stat
 // affine and the ReLU applied to the fp32 accumulators, so no z tensor and no bn_act pass
+// 8 consecutive columns (two f32x4) as one row vector of T
+template <typename T> __device__ __forceinline__ void st8f(T* p, f32x4 lo, f32x4 hi) {
+  typename VT<T>::v8 v;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    v[r] = fromf<T>(lo[r]);
+    v[4 + r] = fromf<T>(hi[r]);
+  }
+  st8<T>(p, v);
+}
+template <typename T> __device__ __forceinline__ void ld8f(const T* p, f32x4& lo, f32x4& hi) {
+  const typename VT<T>::v8 v = ld8<T>(p);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    lo[r] = tof(v[r]);
+    hi[r] = tof(v[4 + r]);
+  }
+}
+
 template <typename T> struct FwdEpi {
   static constexpr bool kStats = true;
+  static constexpr bool kRow8 = true;
   T* y;
   float* psum;
   float* psq;
@@ -468,6 +488,17 @@ template <typename T> struct FwdEpi {
     }
     st4<T>(y + (size_t)m * N + n, v);
   }
+  __device__ __forceinline__ void store8(int m, int n, f32x4 lo, f32x4 hi, int) const {
+    if (m >= M || n >= N) return;
+    if (esc) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        lo[r] = fmaxf(fmaf(lo[r], esc[n + r], esh[n + r]), 0.f);
+        hi[r] = fmaxf(fmaf(hi[r], esc[n + 4 + r], esh[n + 4 + r]), 0.f);
+      }
+    }
+    st8f<T>(y + (size_t)m * N + n, lo, hi);
+  }
   __device__ __forceinline__ void stats(int row, int n, f32x4 s, f32x4 q) const {
     if (psum == nullptr || n >= N) return;
     *reinterpret_cast<f32x4*>(psum + (size_t)row * N + n) = s;
@@ -479,6 +510,7 @@ template <typename T> struct FwdEpi {
 // residual block whose output went through ReLU, model/seresnet31.py:66)
 template <typename T> struct DgradEpi {
   static constexpr bool kStats = false;
+  static constexpr bool kRow8 = true;
   T* dx;
   const T* dres;
   const T* yres;
@@ -493,6 +525,27 @@ template <typename T> struct DgradEpi {
       for (int r = 0; r < 4; ++r) v[r] += yy[r] > 0.f ? d[r] : 0.f;
     }
     st4<T>(dx + o, v);
+  }
+  __device__ __forceinline__ void store8(int m, int n, f32x4 lo, f32x4 hi, int) const {
+    if (m >= M || n >= N) return;
+    const size_t o = (size_t)m * N + n;
+    if (accumulate) {
+      f32x4 a, b;
+      ld8f<T>(dx + o, a, b);
+      lo += a;
+      hi += b;
+    }
+    if (dres) {
+      f32x4 d0, d1, y0, y1;
+      ld8f<T>(dres + o, d0, d1);
+      ld8f<T>(yres + o, y0, y1);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        lo[r] += y0[r] > 0.f ? d0[r] : 0.f;
+        hi[r] += y1[r] > 0.f ? d1[r] : 0.f;
+      }
+    }
+    st8f<T>(dx + o, lo, hi);
   }
   __device__ __forceinline__ void stats(int, int, f32x4, f32x4) const {}
 };
@@ -513,8 +566,12 @@ template <typename T> struct DgradBnEpi {
   const float* shift;
   float* pg;
   float* pgx;
+  static constexpr bool kRow8 = true;
   __device__ __forceinline__ void store(int m, int n, f32x4 v, int) const {
     if (m < M && n < N) st4<T>(dx + (size_t)m * N + n, v);
+  }
+  __device__ __forceinline__ void store8(int m, int n, f32x4 lo, f32x4 hi, int) const {
+    if (m < M && n < N) st8f<T>(dx + (size_t)m * N + n, lo, hi);
   }
   __device__ __forceinline__ void stats(int, int, f32x4, f32x4) const {}
   template <int MI, int NI>
@@ -1107,6 +1164,15 @@ int crnn_conv_dgrad_bnrelu_tw(int dtype, const crnn_conv_desc* d, const void* dy
   DgradBnEpi<bf16> ep{(bf16*)dx, M, N, (const bf16*)z, mean, invstd, scale, shift, pg, pgx};
   return conv_dgrad_tw_launch(d, dy, wt, ep, (hipStream_t)stream);
 }
+
+#if CRNN_GEMM_STAMPS
+// diagnostic build only (not in crnn_hip.h): the 256-row GEMM stamps of this TU's kernels
+int crnn_diag_gemm_stamps(unsigned long long* host, int nblocks) {
+  const size_t n = (size_t)(nblocks < GEMM_STAMP_BLOCKS ? nblocks : GEMM_STAMP_BLOCKS) * GEMM_STAMP_SLOTS;
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_gemm_stamps), n * sizeof(unsigned long long), 0,
+                                  hipMemcpyDeviceToHost);
+}
+#endif
 
 int crnn_conv_wgrad(int dtype, const crnn_conv_desc* d, const void* dy, const void* x, float* dw_oihw,
                     float* ws, size_t ws_bytes, float beta, void* stream) {

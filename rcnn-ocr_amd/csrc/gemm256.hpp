@@ -81,6 +81,15 @@ __device__ __forceinline__ void raw_barrier() {
 template <class E, class = void> struct has_tile_hook : std::false_type {};
 template <class E> struct has_tile_hook<E, std::void_t<decltype(E::kTileHook)>> : std::bool_constant<E::kTileHook> {};
 
+// optional row-vector stores: an EPI with `static constexpr bool kRow8 = true` gets
+// epi.store8(m, n, f32x4 lo, f32x4 hi, kz) for 8 consecutive columns n..n+7 of row m (one 16-B bf16
+// store) instead of store() per 4 columns. The accumulators are transposed through LDS first (the
+// MFMA layout gives a lane 4 columns of a row): a wave-instruction then stores whole 128-B row
+// pieces with half the store instructions — the epilogue's store tail is issue-bound
+// (MI355X_MICROARCH.md, epilogue store tail).
+template <class E, class = void> struct has_row8 : std::false_type {};
+template <class E> struct has_row8<E, std::void_t<decltype(E::kRow8)>> : std::bool_constant<E::kRow8> {};
+
 // per-wave, per-column partial statistics (sum, sum of squared deviations from the partial
 // mean) over this wave's WM accumulator rows — the BN two-pass-in-registers epilogue
 template <int MI, int NI, class EPI>
@@ -211,6 +220,72 @@ __device__ __forceinline__ uint32_t lds_addr(const char* p) {
   return (uint32_t)(size_t)((const __attribute__((address_space(3))) char*)p);
 }
 
+#ifndef CRNN_ROW8_EPILOGUE
+#define CRNN_ROW8_EPILOGUE 1
+#endif
+constexpr bool crnn_row8_on = CRNN_ROW8_EPILOGUE != 0;
+
+// The wave's WM x WN accumulator block through its own LDS region (the pipeline's stage buffers are
+// free once the K loop is done): two halves of 64 rows, fp32 row-major with the 16-B chunk index
+// XOR-swizzled by the row (the 16 lanes of a write pass put one row each into distinct banks),
+// then each lane reads 8 consecutive columns of a row and the epilogue stores them as one vector.
+template <int MI, int NI, int WM, int WN, class EPI>
+__device__ __forceinline__ void row8_epilogue(const f32x4 (&acc)[MI][NI], const EPI& epi, char* smem, int wid,
+                                              int lane, int rbase, int cbase, int kz) {
+  static_assert(WM == 128 && (WN == 64 || WN == 32), "row8 epilogue: 256-row tiles");
+  constexpr int CH = WN / 4;            // 16-B chunks per row
+  constexpr int LPR = WN / 8;           // lanes per row in the read-back
+  constexpr int RPI = 64 / LPR;         // rows per read-back instruction
+  float* stg = reinterpret_cast<float*>(smem) + wid * (64 * WN);
+  const int mr = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+#pragma unroll
+    for (int ii = 0; ii < MI / 2; ++ii)
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const int r = ii * 16 + mr, q = (4 * j + g) ^ (r & (CH - 1));
+        *reinterpret_cast<f32x4*>(stg + r * WN + 4 * q) = acc[h * (MI / 2) + ii][j];
+      }
+#pragma unroll
+    for (int it = 0; it < 64 / RPI; ++it) {
+      const int r = it * RPI + lane / LPR, c = (lane % LPR) * 8;
+      const int q0 = (c / 4) ^ (r & (CH - 1)), q1 = (c / 4 + 1) ^ (r & (CH - 1));
+      const f32x4 lo = *reinterpret_cast<const f32x4*>(stg + r * WN + 4 * q0);
+      const f32x4 hi = *reinterpret_cast<const f32x4*>(stg + r * WN + 4 * q1);
+      epi.store8(rbase + h * 64 + r, cbase + c, lo, hi, kz);
+    }
+  }
+}
+
+// Diagnostic build only (-DCRNN_GEMM_STAMPS=1, tools/gemm_stamps.py): per workgroup s_memrealtime
+// stamps (10 ns) at entry, after the prologue, after the K loop, after the epilogue's stores are
+// issued and after they completed, plus the XCC / hardware ids, into a per-TU device array read
+// back by crnn_diag_gemm_stamps (defined in conv.hip). The stamps go to that array only.
+#ifndef CRNN_GEMM_STAMPS
+#define CRNN_GEMM_STAMPS 0
+#endif
+#if CRNN_GEMM_STAMPS
+constexpr int GEMM_STAMP_SLOTS = 6;
+constexpr int GEMM_STAMP_BLOCKS = 8192;
+static __device__ unsigned long long g_gemm_stamps[GEMM_STAMP_BLOCKS * GEMM_STAMP_SLOTS];
+__device__ __forceinline__ void gemm_stamp(int p) {
+  if (threadIdx.x == 0 && blockIdx.x < GEMM_STAMP_BLOCKS)
+    g_gemm_stamps[blockIdx.x * GEMM_STAMP_SLOTS + p] = __builtin_amdgcn_s_memrealtime();
+}
+__device__ __forceinline__ void gemm_stamp_ids() {
+  if (threadIdx.x == 0 && blockIdx.x < GEMM_STAMP_BLOCKS) {
+    unsigned x, h;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(h));
+    g_gemm_stamps[blockIdx.x * GEMM_STAMP_SLOTS + 5] = ((unsigned long long)x << 32) | h;
+  }
+}
+#define GEMM_STAMP(p) gemm_stamp(p)
+#else
+#define GEMM_STAMP(p)
+#endif
+
 // One work item of the grid kernel: tile (m_tile, n_tile), K range [kz*klen, min(K, (kz+1)*klen)).
 template <int BM, int BN, int SKIP, class LA, class LB, class EPI>
 __device__ __forceinline__ void gemm256_item(LA la, LB lb, EPI epi, int M, int K, int klen, int m_tile, int n_tile,
@@ -231,6 +306,10 @@ __device__ __forceinline__ void gemm256_item(LA la, LB lb, EPI epi, int M, int K
   const int m0 = m_tile * BM, n0 = n_tile * BN;
   const int kbeg = kz * klen, kend = min(K, kbeg + klen);
   const int nk = kend > kbeg ? (kend - kbeg + KS - 1) / KS : 0;
+  GEMM_STAMP(0);
+#if CRNN_GEMM_STAMPS
+  gemm_stamp_ids();
+#endif
 
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -271,6 +350,7 @@ __device__ __forceinline__ void gemm256_item(LA la, LB lb, EPI epi, int M, int K
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   raw_barrier();
+  GEMM_STAMP(1);
   // ping-pong: waves 4-7 (wr == 1, one per SIMD) run one barrier behind waves 0-3, so each SIMD
   // alternates one wave's MFMA cluster with its partner's ds_read / LDS-DMA issue segment
   if (stagger && wr == 1) raw_barrier();
@@ -371,14 +451,25 @@ __device__ __forceinline__ void gemm256_item(LA la, LB lb, EPI epi, int M, int K
     for (; t < nk; ++t) ktile(std::integral_constant<uint32_t, M2>{}, t);
   }
   if (stagger && wr == 0) raw_barrier();
+  GEMM_STAMP(2);
 
   const int mr = lane & 15, nq = 4 * (lane >> 4);
+  if constexpr (has_row8<EPI>::value && crnn_row8_on) {
+    row8_epilogue<MI, NI, WM, WN>(acc, epi, smem, wid, lane, m0 + wr * WM, n0 + wc * WN, kz);
+  } else {
 #pragma unroll
-  for (int i = 0; i < MI; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
-    for (int j = 0; j < NI; ++j) epi.store(m0 + wr * WM + i * 16 + mr, n0 + wc * WN + j * 16 + nq, acc[i][j], kz);
+      for (int j = 0; j < NI; ++j) epi.store(m0 + wr * WM + i * 16 + mr, n0 + wc * WN + j * 16 + nq, acc[i][j], kz);
+  }
   if constexpr (EPI::kStats) wave_col_stats<MI, NI>(acc, epi, M, m0 + wr * WM, m_tile * 2 + wr, n0 + wc * WN, lane);
   if constexpr (has_tile_hook<EPI>::value) epi.template tile<MI, NI>(acc, M, m0 + wr * WM, m_tile * 2 + wr, n0 + wc * WN, lane);
+#if CRNN_GEMM_STAMPS
+  GEMM_STAMP(3);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  GEMM_STAMP(4);
+#endif
 }
 
 // One block per work item (the default): the K-loop above, block-level.
