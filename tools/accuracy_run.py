@@ -22,11 +22,13 @@ FONTS = ["/usr/share/fonts/truetype/dejavu/DejaVuSans.ttf", "/usr/share/fonts/tr
          "/usr/share/fonts/truetype/dejavu/DejaVuSerif.ttf", "/usr/share/fonts/truetype/dejavu/DejaVuSans-Bold.ttf"]
 
 
-def alphabet(charset):
+def alphabet(charset, which):
     from data.transforms import load_charset
     itos, _ = load_charset(charset)
-    # single characters of the reference charset (Latin, Cyrillic, digits, punctuation), no space
-    return [t for t in itos[3:] if len(t) == 1 and t != " "]
+    chars = [t for t in itos[3:] if len(t) == 1 and t != " "]
+    if which == "full":   # every single character of the reference charset (Latin, Cyrillic, digits,
+        return chars      # punctuation): Latin / Cyrillic look-alikes make it ambiguous to read
+    return [c for c in chars if c in "abcdefghijklmnopqrstuvwxyz0123456789"]
 
 
 def render_set(root, n, rng, chars, max_chars):
@@ -56,15 +58,17 @@ def render_set(root, n, rng, chars, max_chars):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default="gpurun_out/acc")
-    ap.add_argument("--train", type=int, default=12000)
+    ap.add_argument("--train", type=int, default=60000)
     ap.add_argument("--test", type=int, default=2000)
-    ap.add_argument("--epochs", type=int, default=15)
+    ap.add_argument("--epochs", type=int, default=10)
     ap.add_argument("--hidden", type=int, default=256)
     ap.add_argument("--batch", type=int, default=128)
-    ap.add_argument("--lr", type=float, default=5.1e-4)
+    ap.add_argument("--lr", type=float, default=1e-3)
+    ap.add_argument("--alphabet", default="latin", choices=["latin", "full"],
+                    help="latin: lowercase Latin + digits (unambiguous glyphs); full: the whole reference charset")
     a = ap.parse_args()
     charset = os.path.join(REPO, "tests", "golden", "charset.txt")
-    chars = alphabet(charset)
+    chars = alphabet(charset, a.alphabet)
     rng = random.Random(20261017)
     t0 = time.time()
     for name, n in (("train", a.train), ("val", 1000), ("test", a.test)):
@@ -92,7 +96,7 @@ def main():
            "train_samples": a.train, "test_samples": ev["samples"], "epochs": a.epochs, "hidden": a.hidden,
            "batch": a.batch, "val_acc_best": res["val_acc"], "test_accuracy": ev["accuracy"], "test_cer": ev["cer"],
            "test_wer": ev["wer"], "render_s": round(t_render, 1), "train_s": round(t_train, 1),
-           "alphabet_size": len(chars)}
+           "alphabet": a.alphabet, "alphabet_size": len(chars), "lr": a.lr}
     print(json.dumps(out), flush=True)
 
 
