@@ -125,11 +125,13 @@ int crnn_pack_batch(int dtype, const crnn_pack_job* jobs, int njobs, long total,
 int crnn_pack_conv_batch(int dtype, const crnn_pack_job* jobs, int njobs, long total_rows, int max_slab,
                          void* stream);
 /* transposed, flipped conv kernels for crnn_conv_dgrad_tw (kind CRNN_PACK_CONV_T, a..d = Co, Ci, KH, KW;
- * Ci % 8 == 0, KH*KW <= 9): dst[ci][kh][kw][co] = src_OIHW[co][ci][KH-1-kh][KW-1-kw] in dtype. One workgroup per
- * 32 x 32 (co, ci) tile, coalesced both ways through LDS; job.start = the job's first tile in the
- * concatenation (a job has ceil(Co/32) * ceil(Ci/32) tiles, co-tile major); total_tiles = all. */
+ * Ci % 16 == 0, KH*KW in {1, 4, 9}): dst[ci][kh][kw][co] = src_OIHW[co][ci][KH-1-kh][KW-1-kw] in dtype. One workgroup per
+ * 64 x 16 (co, ci) tile, coalesced both ways through LDS; job.start = the job's first tile in the
+ * concatenation (a job has ceil(Co/64) * ceil(Ci/16) tiles, co-tile major); total_tiles = all. */
 #define CRNN_PACK_CONV_T 4
 int crnn_pack_conv_t_batch(int dtype, const crnn_pack_job* jobs, int njobs, long total_tiles, void* stream);
+/* workgroup tiles of one CRNN_PACK_CONV_T job (the job.start increment) */
+int crnn_pack_conv_t_tiles(int Co, int Ci);
 
 /* ------------------------------------------------------------------ conv */
 typedef struct {
@@ -228,6 +230,12 @@ int crnn_maxpool_bwd(int dtype, const void* z, const float* scale, const float* 
 #define CRNN_BNG_POOL 4  /* BN -> ReLU -> MaxPool2d(2,2): dy = POOLED grad [B][H/2][W/2][C],   \
                             HW = full-res W (even H, W); g = dy at the window's first max of \
                             relu(z*scale+shift) when > 0, else 0 (crnn_maxpool_bwd fused)  */
+#define CRNN_BNG_POOL_OUT 5 /* crnn_bn_bwd_reduce only: the CRNN_BNG_POOL sums from the POOLED output \
+                            y [B][H/2][W/2][C] = maxpool(relu(z*scale+shift)) instead of z: a window \
+                            contributes g = dy where y > 0, at xhat = ((y - shift)/scale - mean)*invstd \
+                            (the max is one value of the window, so its z follows from y); z is read  \
+                            only for channels with scale == 0 (all four tie: the first element). Reads \
+                            the pooled tensors only: a quarter of the full-resolution z              */
 typedef struct {
   const void* dy;
   const void* z;

@@ -55,6 +55,7 @@ _SIGS = {
     "crnn_pack_batch": ([i32, vp, i32, i64, vp], i32),
     "crnn_pack_conv_batch": ([i32, vp, i32, i64, i32, vp], i32),
     "crnn_pack_conv_t_batch": ([i32, vp, i32, i64, vp], i32),
+    "crnn_pack_conv_t_tiles": ([i32, i32], i32),
     "crnn_version": ([], i32),
     "crnn_set_option": ([i32, i32], i32),
     "crnn_last_error_string": ([], C.c_char_p),

@@ -193,11 +193,11 @@ class CRNNEngine:
 
     def tw_convs(self):
         """the convs whose input gradient can run on the forward path (crnn_conv_dgrad_tw): bf16,
-        stride 1, KH*KW <= 9, Co % 64 == 0, unpadded Ci % 8 == 0; not the stem (halo kernels)"""
+        stride 1, KH*KW in (1, 4, 9), Co % 64 == 0, unpadded Ci % 16 == 0; not the stem (halo kernels)"""
         if not self.dgrad_tw or self.dtype != torch.bfloat16:
             return []
         return [cs for cs in self.convs() if cs not in (self.stem0, self.stem1) and cs.sh == 1 and cs.sw == 1
-                and cs.kh * cs.kw <= 9 and cs.co % 64 == 0 and cs.ci % 8 == 0 and cs.ci == cs.ci_real]
+                and cs.kh * cs.kw in (1, 4, 9) and cs.co % 64 == 0 and cs.ci % 16 == 0 and cs.ci == cs.ci_real]
 
     def _dgrad(self, cs: "ConvSpec", b, h, w, dy, dx, dres=None, yres=None, accumulate=0):
         """input gradient of conv `cs` (input map h x w): the forward-path form where packed and
@@ -265,7 +265,7 @@ class CRNNEngine:
             out = self._pbuf(cs.name + ".t", (cs.ci, cs.kh, cs.kw, cs.co), T)
             job(L.PACK_CONV_T, self.p[cs.name], out, cs.co, cs.ci, cs.kh, cs.kw)
             jobs[-1].start = tiles
-            tiles += ((cs.co + 31) // 32) * ((cs.ci + 31) // 32)
+            tiles += L.lib().crnn_pack_conv_t_tiles(cs.co, cs.ci)
         if jobs:
             tarr = (L.PackJob * len(jobs))(*jobs)
             traw = torch.frombuffer(bytearray(bytes(tarr)), dtype=torch.uint8).to(self.device)
@@ -390,6 +390,9 @@ class CRNNEngine:
     # (crnn_conv_dgrad_tw; CRNN_DGRAD_TW, default 1): the forward's K-contiguous B operand, tiles and
     # padding-row skip instead of the dgrad loader's transposed LDS reads
     dgrad_tw = os.environ.get("CRNN_DGRAD_TW", "1") == "1"
+    # the stem's BN-backward sums from the pooled forward output and gradient (CRNN_BNG_POOL_OUT:
+    # a quarter of the bytes of the full-resolution z; CRNN_POOL_OUT_REDUCE, default 1)
+    pool_out_reduce = os.environ.get("CRNN_POOL_OUT_REDUCE", "1") == "1"
 
     def _seq_ok(self, B):
         return self.use_seq and bool(L.lib().crnn_lstm_seq_supported(self.dt, B, self.H))
@@ -792,10 +795,12 @@ class CRNNEngine:
 
     # ------------------------------------------------------------------ backward
     def _bn_bwd(self, mode, dy, z, stats, prefix, M, C, HW=1, y=None, se=None, dpool=None, out=None,
-                accumulate_params=False, se_abc=None, sums=None):
+                accumulate_params=False, se_abc=None, sums=None, reduce_y=None):
         """BN backward: per-channel sums of g (mode, crnn_hip.h CRNN_BNG_*) -> finalize -> apply.
         se_abc = (abc, B): the SE mode's sums come from crnn_se_bn_bwd_reduce's per-sample terms
-        (no second pass over the tensor); sums = (pg, pgx, rows): given by the producing dgrad."""
+        (no second pass over the tensor); sums = (pg, pgx, rows): given by the producing dgrad;
+        reduce_y (pool mode): the pooled forward output, whose sums (CRNN_BNG_POOL_OUT) read the
+        pooled tensors instead of the full-resolution z."""
         mean, inv, sc, sh = stats
         ws = self.ws
         s = L.stream_ptr()
@@ -813,7 +818,11 @@ class CRNNEngine:
             rows = L.lib().crnn_bn_rows(M)
             pg = ws.get("bnb.pg", (1024 * 512,), torch.float32)[: rows * C]
             pgx = ws.get("bnb.pgx", (1024 * 512,), torch.float32)[: rows * C]
-            call("crnn_bn_bwd_reduce", self.dt, d, ptr(pg), ptr(pgx), rows, s)
+            rd = d
+            if reduce_y is not None:
+                rd = BnBwdDesc(ptr(dy), ptr(z), ptr(mean), ptr(inv), ptr(sc), ptr(sh), ptr(reduce_y), None, None,
+                               5, M, C, HW)   # CRNN_BNG_POOL_OUT
+            call("crnn_bn_bwd_reduce", self.dt, rd, ptr(pg), ptr(pgx), rows, s)
         mg = ws.get("bnb.mg", (512,), torch.float32)
         mgx = ws.get("bnb.mgx", (512,), torch.float32)
         call("crnn_bn_bwd_finalize", ptr(pg), ptr(pgx), rows, C, M, ptr(self.g[prefix + ".weight"]),
@@ -1141,7 +1150,8 @@ class CRNNEngine:
         # routed to each window's first maximum inside the BN-backward reduce / apply kernels)
         dz1 = self._dz("s1", bufs[o2], B * h1 * w1 * 128)
         self._bn_bwd(4, dp, st["z1"], (st["m1"], st["i1"], st["sc1"], st["sh1"]), self.stem1.bn, B * h1 * w1, 128,
-                     HW=w1, out=dz1, accumulate_params=accumulate)
+                     HW=w1, out=dz1, accumulate_params=accumulate,
+                     reduce_y=sv["blocks"][0]["x"] if self.pool_out_reduce else None)
         self._wgrad(self.stem1, dz1, st["a0"], B, h1, w1)
         da0 = bufs[o1][: B * h1 * w1 * 64]
         self._conv_call("dgrad", self.conv_flops(self.stem1, B, h1, w1), "crnn_conv_dgrad", dt, self.stem1.desc(B, h1, w1), ptr(dz1), ptr(self.packed[self.stem1.name]),

@@ -1030,13 +1030,50 @@ __global__ __launch_bounds__(256) void pack_conv_kernel(const crnn_pack_job* __r
   }
 }
 
-// transposed, flipped conv kernel (crnn_conv_dgrad_tw's B operand): one workgroup per (32 co x 32 ci)
-// tile of a job. The source rows [co][ci0 .. ci0+31][KH*KW] are contiguous runs (coalesced reads into
-// LDS, row pitch 32*KHW + 1 words); the destination rows [ci][tap'][co0 .. co0+31] are written as
-// 64-B runs of consecutive co.
+// transposed, flipped conv kernel (crnn_conv_dgrad_tw's B operand): one workgroup per (64 co x 16 ci)
+// tile of a job. The source rows [co][ci0 .. ci0+15][KH*KW] are contiguous runs, read as 16-B vectors,
+// all of a thread's loads in flight before its LDS stores (a load-store-load loop runs at the
+// memory latency); LDS row pitch 16*KHW + 1 words (the read-back's 64 consecutive co on distinct
+// banks); the destination rows [ci][tap'][co0 .. co0+63] are written as whole 128-B lines of
+// consecutive co. KHW is a template parameter (3x3 and 2x2 kernels): no runtime divisions.
+constexpr int PT_CO = 64, PT_CI = 16;
+template <typename T, int KHW>
+__device__ __forceinline__ void pack_conv_t_tile(const crnn_pack_job& jb, int tl, float* tile) {
+  const int Co = jb.a, Ci = jb.b;
+  const int tci = (Ci + PT_CI - 1) / PT_CI;
+  const int co0 = (tl / tci) * PT_CO, ci0 = (tl % tci) * PT_CI;
+  const int nco = min(PT_CO, Co - co0);
+  constexpr int RUN = PT_CI * KHW, V4 = RUN / 4, P = RUN + 1, NV = PT_CO * V4;
+  constexpr int PER = (NV + 255) / 256;
+  f32x4 v[PER];
+#pragma unroll
+  for (int u = 0; u < PER; ++u) {
+    const int k = threadIdx.x + 256 * u, r = k / V4, e = k - r * V4;
+    const int rr = (k < NV && r < nco) ? r : 0;   // clamped: every load unconditional
+    v[u] = *reinterpret_cast<const f32x4*>(jb.src + ((size_t)(co0 + rr) * Ci + ci0) * KHW + 4 * e);
+  }
+#pragma unroll
+  for (int u = 0; u < PER; ++u) {
+    const int k = threadIdx.x + 256 * u, r = k / V4, e = k - r * V4;
+    if (k < NV)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) tile[r * P + 4 * e + q] = r < nco ? v[u][q] : 0.f;
+  }
+  __syncthreads();
+  T* dst = (T*)jb.dst;
+#pragma unroll
+  for (int u = 0; u < (PT_CO * RUN + 255) / 256; ++u) {
+    const int i = threadIdx.x + 256 * u;
+    const int co = i % PT_CO, rest = i / PT_CO;
+    const int tp = rest % KHW, ci = rest / KHW;   // destination tap (flipped source tap KHW-1-tp)
+    if (i < PT_CO * RUN && co < nco)
+      dst[((size_t)(ci0 + ci) * KHW + tp) * Co + co0 + co] = fromf<T>(tile[co * P + ci * KHW + (KHW - 1 - tp)]);
+  }
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void pack_conv_t_kernel(const crnn_pack_job* __restrict__ jobs, int njobs) {
-  __shared__ float tile[32 * (32 * 9 + 1)];    // KH*KW <= 9 (the header's contract)
+  __shared__ float tile[PT_CO * (PT_CI * 9 + 1)];   // KH*KW <= 9 (the header's contract)
   const long bid = blockIdx.x;
   int lo = 0, hi = njobs - 1;
   while (lo < hi) {  // last job with start (first tile) <= bid
@@ -1045,22 +1082,11 @@ __global__ __launch_bounds__(256) void pack_conv_t_kernel(const crnn_pack_job* _
     else hi = mid - 1;
   }
   const crnn_pack_job jb = jobs[lo];
-  const int Co = jb.a, Ci = jb.b, KHW = jb.c * jb.d;
-  if (KHW > 9) return;
-  const int tci = (Ci + 31) / 32;
-  const int tl = (int)(bid - jb.start), co0 = (tl / tci) * 32, ci0 = (tl % tci) * 32;
-  const int nco = min(32, Co - co0), nci = min(32, Ci - ci0), run = nci * KHW, P = 32 * KHW + 1;
-  for (int i = threadIdx.x; i < 32 * run; i += blockDim.x) {
-    const int r = i / run, e = i - r * run;
-    tile[r * P + e] = r < nco ? jb.src[((size_t)(co0 + r) * Ci + ci0) * KHW + e] : 0.f;
-  }
-  __syncthreads();
-  T* dst = (T*)jb.dst;
-  for (int i = threadIdx.x; i < 32 * run; i += blockDim.x) {
-    const int co = i & 31, rest = i >> 5;
-    const int tp = rest % KHW, ci = rest / KHW;   // destination tap (flipped source tap KHW-1-tp)
-    if (co < nco) dst[((size_t)(ci0 + ci) * KHW + tp) * Co + co0 + co] = fromf<T>(tile[co * P + ci * KHW + (KHW - 1 - tp)]);
-  }
+  const int KHW = jb.c * jb.d, tl = (int)(bid - jb.start);
+  if (jb.b % PT_CI) return;   // the header's contract: Ci % 16 == 0 (16-B source rows)
+  if (KHW == 9) pack_conv_t_tile<T, 9>(jb, tl, tile);
+  else if (KHW == 4) pack_conv_t_tile<T, 4>(jb, tl, tile);
+  else if (KHW == 1) pack_conv_t_tile<T, 1>(jb, tl, tile);
 }
 
 // ------------------------------------------------------------ dropout (enc_dropout, model/model.py:201,220)
@@ -1163,6 +1189,66 @@ __device__ __forceinline__ void pool_window(const crnn_bn_bwd_desc& d, const Fas
   for (int t = 0; t < 4; ++t)
 #pragma unroll
     for (int k = 0; k < 8; ++k) g[t][k] = (arg[k] == t && z[t][k] * sc[k] + sh[k] > 0.f) ? dp[k] : 0.f;
+}
+
+// CRNN_BNG_POOL_OUT: the pool-mode sums from the pooled output y and the pooled gradient dy (one row
+// per window): y > 0 means the window's first maximum got dy, and that maximum's z is (y - shift) /
+// scale. A channel with scale == 0 (all four values tie at relu(shift)) takes the first element's z
+// (the rare path reads it; the common path never touches the full-resolution tensor).
+template <typename T>
+__global__ __launch_bounds__(NT) void bnb_reduce_pool_out_kernel(crnn_bn_bwd_desc d, FastDiv dWo, long rpb,
+                                                                 float* __restrict__ p0, float* __restrict__ p1) {
+  extern __shared__ float red[];  // [2][rl][C]
+  const int C = d.C;
+  const RowMap q = rowmap(C);
+  float mean[8], inv[8], sc[8], sh[8], rsc[8], a0[8], a1[8];
+  ld8f(d.mean + q.c8, mean);
+  ld8f(d.invstd + q.c8, inv);
+  ld8f(d.scale + q.c8, sc);
+  ld8f(d.shift + q.c8, sh);
+  bool zero_sc = false;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    a0[i] = a1[i] = 0.f;
+    zero_sc |= sc[i] == 0.f;
+    rsc[i] = sc[i] != 0.f ? 1.f / sc[i] : 0.f;
+  }
+  const long mend = d.M / 4;
+  const long m0 = blockIdx.x * rpb, m1 = min(mend, m0 + rpb);
+  for (long m = m0 + q.r; m < m1; m += q.rl) {
+    const size_t o = (size_t)m * C + q.c8;
+    float y[8], dp[8];
+    unpack8<T>(ld8<T>((const T*)d.y + o), y);
+    unpack8<T>(ld8<T>((const T*)d.dy + o), dp);
+    float zf[8];
+    if (__builtin_expect(zero_sc, 0)) {   // first window element's z (full-res row 2*(m / Wo), col 2*(m % Wo))
+      uint32_t wo;
+      const uint32_t bho = dWo.divmod((uint32_t)m, wo);
+      unpack8<T>(ld8<T>((const T*)d.z + ((size_t)(2 * bho) * d.HW + 2 * wo) * C + q.c8), zf);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float g = y[i] > 0.f ? dp[i] : 0.f;
+      const float z = sc[i] != 0.f ? (y[i] - sh[i]) * rsc[i] : zf[i];
+      a0[i] += g;
+      a1[i] += g * ((z - mean[i]) * inv[i]);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    red[q.r * C + q.c8 + i] = a0[i];
+    red[(q.rl + q.r) * C + q.c8 + i] = a1[i];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += NT) {
+    float s0 = 0.f, s1 = 0.f;
+    for (int k = 0; k < q.rl; ++k) {
+      s0 += red[k * C + c];
+      s1 += red[(q.rl + k) * C + c];
+    }
+    p0[(size_t)blockIdx.x * C + c] = s0;
+    p1[(size_t)blockIdx.x * C + c] = s1;
+  }
 }
 
 template <typename T, int MODE>
@@ -1504,7 +1590,7 @@ inline void stream_grid(long M, int C, int* blocks, long* rpb) {
 namespace {
 template <typename T>
 int bnb_reduce_launch(const crnn_bn_bwd_desc* d, float* pg, float* pgx, int rows, hipStream_t st) {
-  const bool pool = d->mode == CRNN_BNG_POOL;
+  const bool pool = d->mode == CRNN_BNG_POOL || d->mode == CRNN_BNG_POOL_OUT;
   const long rpb = ((pool ? d->M / 4 : d->M) + rows - 1) / rows;
   const int rl = NT / (d->C / 8);
   const size_t sm = (size_t)2 * rl * d->C * sizeof(float);
@@ -1512,6 +1598,9 @@ int bnb_reduce_launch(const crnn_bn_bwd_desc* d, float* pg, float* pgx, int rows
   switch (d->mode) {
     case CRNN_BNG_POOL:
       hipLaunchKernelGGL((bnb_reduce_kernel<T, CRNN_BNG_POOL>), dim3(rows), dim3(NT), sm, st, *d, dHW, rpb, pg, pgx);
+      break;
+    case CRNN_BNG_POOL_OUT:
+      hipLaunchKernelGGL((bnb_reduce_pool_out_kernel<T>), dim3(rows), dim3(NT), sm, st, *d, dHW, rpb, pg, pgx);
       break;
     case CRNN_BNG_PLAIN:
       hipLaunchKernelGGL((bnb_reduce_kernel<T, CRNN_BNG_PLAIN>), dim3(rows), dim3(NT), sm, st, *d, dHW, rpb, pg, pgx);
@@ -1630,6 +1719,7 @@ int crnn_bn_bwd_finalize(const float* pg, const float* pgx, int rows, int C, lon
 int crnn_bn_bwd_apply(int dtype, const crnn_bn_bwd_desc* d, const float* mean_g, const float* mean_gx, void* dz,
                       void* stream) {
   if (!rowmap_ok(d->C)) return crnn_set_error(hipErrorInvalidValue, "bn_bwd_apply: C/8 must divide 256");
+  if (d->mode == CRNN_BNG_POOL_OUT) return crnn_set_error(hipErrorInvalidValue, "bn_bwd_apply: POOL_OUT is a reduce-only mode");
   hipStream_t st = (hipStream_t)stream;
   return dtype == CRNN_BF16 ? bnb_apply_launch<bf16>(d, mean_g, mean_gx, dz, st)
                             : bnb_apply_launch<float>(d, mean_g, mean_gx, dz, st);
@@ -1793,6 +1883,8 @@ int crnn_pack_batch(int dtype, const crnn_pack_job* jobs, int njobs, long total,
                                      jobs, njobs, total, chunk));
   return (int)hipGetLastError();
 }
+
+int crnn_pack_conv_t_tiles(int Co, int Ci) { return ((Co + PT_CO - 1) / PT_CO) * ((Ci + PT_CI - 1) / PT_CI); }
 
 int crnn_pack_conv_t_batch(int dtype, const crnn_pack_job* jobs, int njobs, long total_tiles, void* stream) {
   if (njobs <= 0 || total_tiles <= 0) return 0;

@@ -440,7 +440,7 @@ def test_conv_dgrad_tw_forward_path(geo):
     wt = torch.empty(Ci, k[0], k[1], Co, dtype=torch.bfloat16, device=DEV)
     job.dst = wt.data_ptr()
     tab = torch.frombuffer(bytearray(bytes(job)), dtype=torch.uint8).to(DEV)
-    ntiles = ((Co + 31) // 32) * ((Ci + 31) // 32)
+    ntiles = L.lib().crnn_pack_conv_t_tiles(Co, Ci)
     L.call("crnn_pack_conv_t_batch", dt, tab.data_ptr(), 1, ntiles, st)
     want_wt = w.flip(2, 3).permute(1, 2, 3, 0).contiguous().bfloat16()
     assert torch.equal(wt.cpu(), want_wt)
@@ -1277,7 +1277,31 @@ def test_bn_bwd_pool_mode_matches_maxpool_then_relu_mode(dtype, shape):
            B, H, W, C, st)
     dz_u, dgam_u, dbet_u = bwd(1, dfull, H * W)
     dz_p, dgam_p, dbet_p = bwd(4, dpd, W)
+    # CRNN_BNG_POOL_OUT: the same sums from the pooled forward output (crnn_bn_relu_maxpool of z)
+    # instead of the full-resolution z; channel 3 with scale 0 (all four values tie) reads z's first
+    # window element
+    yp = torch.empty(B, H // 2, W // 2, C, dtype=dtype, device=DEV)
+    L.call("crnn_bn_relu_maxpool", dt, zd.data_ptr(), scd.data_ptr(), shd.data_ptr(), yp.data_ptr(), B, H, W, C, st)
+    out = []
+    for zero in (False, True):
+        scz, shz = scd.clone(), shd.clone()
+        if zero:
+            scz[3], shz[3] = 0.0, 0.7
+        ypz = torch.empty_like(yp)
+        L.call("crnn_bn_relu_maxpool", dt, zd.data_ptr(), scz.data_ptr(), shz.data_ptr(), ypz.data_ptr(), B, H, W, C,
+               st)
+        sums = []
+        for mode, yy in ((4, None), (5, ypz)):
+            desc = BnBwdDesc(dpd.data_ptr(), zd.data_ptr(), meand.data_ptr(), invd.data_ptr(), scz.data_ptr(),
+                             shz.data_ptr(), 0 if yy is None else yy.data_ptr(), 0, 0, mode, M, C, W)
+            pg, pgx = torch.empty(rows, C, device=DEV), torch.empty(rows, C, device=DEV)
+            L.call("crnn_bn_bwd_reduce", dt, desc, pg.data_ptr(), pgx.data_ptr(), rows, st)
+            sums.append((pg.sum(0).cpu(), pgx.sum(0).cpu()))
+        out.append(sums)
     torch.cuda.synchronize()
+    for (s4, x4), (s5, x5) in out:
+        assert relerr(s5, s4) < 1e-6          # the same g: exactly the pooled gradients where y > 0
+        assert relerr(x5, x4) < (1e-5 if dtype == torch.float32 else 2e-2)   # xhat from y vs from z
     # fused == unfused up to the order of the fp32 partial sums
     assert relerr(dbet_p, dbet_u) < 1e-5 and relerr(dgam_p, dgam_u) < 1e-5
     assert relerr(dz_p, dz_u) < (1e-5 if dtype == torch.float32 else 1e-2)
