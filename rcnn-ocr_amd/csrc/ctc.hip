@@ -34,7 +34,9 @@ __global__ __launch_bounds__(256) void ctc_kernel(const float* __restrict__ logi
   float* bcur = alpha + (size_t)T * S;  // [S]
   float* bnxt = bcur + S;             // [S]
   float* grow = bnxt + S;             // [C]
-  int* ext = (int*)(grow + C);        // [S]
+  float* evs = grow + C;              // [S] alpha*beta/p terms of the current frame
+  int* ext = (int*)(evs + S);         // [S]
+  int* lnk = ext + S;                 // [S] next odd position with the same label | head flag
   const float* lg = logits + (size_t)b * T * ldc;
 
   for (int t = wid; t < T; t += nw) {
@@ -48,6 +50,22 @@ __global__ __launch_bounds__(256) void ctc_kernel(const float* __restrict__ logi
   }
   for (int s = tid; s < S; s += blockDim.x) ext[s] = (s & 1) ? targets[(size_t)b * Lmax + (s >> 1)] : 0;
   __syncthreads();
+  // the gradient sums each class's terms in a FIXED order (blank: wave 0, lane-strided + butterfly;
+  // a label: its first odd position walks the chain of its later occurrences). LDS float atomics
+  // summed them in wave-arrival order, which varies with load on the device: the bf16 casts
+  // downstream turned that last-bit noise into run-to-run gradient differences (DP replicas).
+  constexpr int HEAD = 1 << 30;
+  for (int s = tid; s < S; s += blockDim.x) {
+    int v = 0;
+    if ((s & 1) && ext[s] != 0) {
+      bool head = true;
+      for (int p = 1; p < s; p += 2) head = head && ext[p] != ext[s];
+      int nx = 0;
+      for (int p = S - 2; p > s; p -= 2) nx = ext[p] == ext[s] ? p : nx;
+      v = nx | (head ? HEAD : 0);
+    }
+    lnk[s] = v;
+  }
 #define LP(t, c) (lg[(size_t)(t) * ldc + (c)] - lse[(t)])
   for (int s = tid; s < S; s += blockDim.x) alpha[s] = s < 2 ? LP(0, ext[s]) : -INFINITY;
   for (int t = 1; t < T; ++t) {
@@ -92,12 +110,24 @@ __global__ __launch_bounds__(256) void ctc_kernel(const float* __restrict__ logi
         v += LP(t, ext[s]);
       }
       bcur[s] = v;
+      const float e = alpha[(size_t)t * S + s] + v - LP(t, ext[s]) - ll;
+      evs[s] = e > -INFINITY ? __expf(e) : 0.f;
     }
     for (int c = tid; c < C; c += blockDim.x) grow[c] = __expf(LP(t, c));
     __syncthreads();
+    if (wid == 0) {   // class 0: every position whose symbol is the blank
+      float a = 0.f;
+      for (int s = lane; s < S; s += 64) a += ext[s] == 0 ? evs[s] : 0.f;
+      a = wave_sum(a);
+      if (lane == 0) grow[0] -= a;
+    }
     for (int s = tid; s < S; s += blockDim.x) {
-      float e = alpha[(size_t)t * S + s] + bcur[s] - LP(t, ext[s]) - ll;
-      if (e > -INFINITY) atomicAdd(&grow[ext[s]], -__expf(e));
+      const int l = lnk[s];
+      if (l & HEAD) {
+        float a = evs[s];
+        for (int n = l & (HEAD - 1); n != 0; n = lnk[n] & (HEAD - 1)) a += evs[n];
+        grow[ext[s]] -= a;
+      }
     }
     __syncthreads();
     for (int c = tid; c < ldc; c += blockDim.x) dl[(size_t)t * ldc + c] = c < C ? grow[c] * scale : 0.f;
@@ -269,7 +299,7 @@ extern "C" {
 int crnn_ctc_loss(const float* logits, int ldc, int B, int T, int C, const int* targets, int Lmax, const int* lengths,
                   float* loss, float* dlogits, int zero_inf, void* stream) {
   const int S = 2 * Lmax + 1;
-  size_t sm = ((size_t)T + (size_t)T * S + 2 * S + C) * sizeof(float) + S * sizeof(int);
+  size_t sm = ((size_t)T + (size_t)T * S + 3 * S + C) * sizeof(float) + 2 * S * sizeof(int);
   if (sm > 160 * 1024) return crnn_set_error(hipErrorInvalidValue, "ctc_loss: T x (2*Lmax+1) too large for LDS");
   static bool attr_set = false;
   if (!attr_set) {

@@ -823,6 +823,36 @@ def test_ctc_long_sequence_vs_oracle():
     np.testing.assert_allclose(xd.grad.cpu().numpy(), ref_grad, rtol=2e-3, atol=1e-6)
 
 
+def test_ctc_grad_bit_identical_under_load():
+    """the CTC gradient sums each class's alignment terms in a fixed order: repeated launches give
+    bit-identical gradients while other work loads the device (a side stream of large copies), with
+    labels drawn from 4 classes so that most classes occur many times per sample. (With LDS float
+    atomics the sum order followed wave arrival, and the bf16 casts after the head turned that into
+    run-to-run gradient differences between data-parallel replicas.)"""
+    _L()
+    from crnn_hip.ctc import ctc_loss
+    g = torch.Generator().manual_seed(21)
+    B, T, C = 64, 64, 194
+    x = (torch.randn(B, T, C, generator=g) * 2).to(DEV)
+    tg = torch.randint(3, 7, (B, 30), generator=g)
+    tl = torch.randint(1, 31, (B,), generator=g)
+    side = torch.cuda.Stream()
+    a = torch.empty(64 << 20, device=DEV)
+    bbuf = torch.empty_like(a)
+    ref = None
+    for i in range(12):
+        with torch.cuda.stream(side):
+            for _ in range(4):
+                bbuf.copy_(a)
+        xd = x.clone().requires_grad_(True)
+        ctc_loss(xd, tg, tl).backward()
+        torch.cuda.synchronize()
+        if ref is None:
+            ref = xd.grad.clone()
+        else:
+            assert torch.equal(xd.grad, ref), f"launch {i}: CTC gradient differs from the first launch"
+
+
 def test_ctc_zero_infinity_keeps_nan():
     """zero_infinity zeroes an infeasible (+inf) sample only; a NaN logit gives a NaN loss and
     NaN gradients for its sample, as torch.nn.functional.ctc_loss does."""
