@@ -80,7 +80,9 @@ enum { CRNN_OPT_GEMM_STAGGER = 0,    /* 256-row conv GEMM: waves 4-7 one barrier
                                         per wave, fragments double-buffered in registers), 0 = the 8-wave form */
        CRNN_OPT_DIAG = 15,           /* diagnostics only (default 0): bit 0 = conv fwd / plain dgrad / wgrad GEMMs
                                         skip their epilogue stores (the measured epilogue cost; results invalid) */
-       CRNN_OPT_COUNT = 16 };
+       CRNN_OPT_DGRAD_GROUP = 16,    /* strided conv dgrad on the 256-row kernel: 1 = all parity classes in ONE launch
+                                        (grouped tile table, longest-K class first; default), 0 = a launch per class */
+       CRNN_OPT_COUNT = 17 };
 int crnn_set_option(int key, int value);
 
 /* ------------------------------------------------------------------ layout */

@@ -199,10 +199,35 @@ template <typename T> struct DgradB {
   }
 };
 
+// 8 consecutive columns (two f32x4) as one row vector of T
+template <typename T> __device__ __forceinline__ void st8f(T* p, f32x4 lo, f32x4 hi) {
+  typename VT<T>::v8 v;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    v[r] = fromf<T>(lo[r]);
+    v[4 + r] = fromf<T>(hi[r]);
+  }
+  st8<T>(p, v);
+}
+template <typename T> __device__ __forceinline__ void ld8f(const T* p, f32x4& lo, f32x4& hi) {
+  const typename VT<T>::v8 v = ld8<T>(p);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    lo[r] = tof(v[r]);
+    hi[r] = tof(v[4 + r]);
+  }
+}
+
 // ---- strided dgrad by parity class (sub-pixel decomposition)
 // Input pixels with (hi % sh, wi % sw) == (pc_h, pc_w) only receive gradient from taps with
 // kh = (pc_h + ph) mod sh (same for w); for those taps ho = i + dh, wo = j + dw, linear in the
 // class coordinates (hi = sh*i + pc_h). Each class is a dense GEMM over its own taps only.
+// a TapTable entry by selects (static indices only: the grouped class kernel keeps its loaders in
+// registers, where a dynamic array index would spill the table to scratch)
+__device__ __forceinline__ int sel4(const int (&a)[4], int i) {
+  return i == 0 ? a[0] : (i == 1 ? a[1] : (i == 2 ? a[2] : a[3]));
+}
+
 struct TapTable {
   int n;
   int dh[4], dw[4], id[4];  // per class tap: ho offset, wo offset, kh*KW + kw
@@ -232,9 +257,10 @@ template <typename T> struct DgradClsA {
     c.off = (((int)b * g.Ho + (int)i) * g.Wo + (int)j) * g.Co;
     c.mask = 0;
     if (m < M)
-      for (int t = 0; t < tt.n; ++t)
-        if (t == tt.xtap ||
-            ((unsigned)((int)i + tt.dh[t]) < (unsigned)g.Ho && (unsigned)((int)j + tt.dw[t]) < (unsigned)g.Wo))
+#pragma unroll
+      for (int t = 0; t < 4; ++t)   // static bound: the table stays in registers (sel4)
+        if (t < tt.n && (t == tt.xtap || ((unsigned)((int)i + tt.dh[t]) < (unsigned)g.Ho &&
+                                          (unsigned)((int)j + tt.dw[t]) < (unsigned)g.Wo)))
           c.mask |= 1u << t;
     return c;
   }
@@ -244,8 +270,8 @@ template <typename T> struct DgradClsA {
     p.tap = (int)g.dCo.divmod((uint32_t)k0, co);
     p.c0 = (int)co;
     const int t = p.tap < tt.n ? p.tap : 0;
-    p.kh = tt.dh[t];
-    p.kw = tt.dw[t];
+    p.kh = sel4(tt.dh, t);
+    p.kw = sel4(tt.dw, t);
     return p;
   }
   __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc() const { return mk_rsrc(dy, bytes); }
@@ -273,7 +299,7 @@ template <typename T> struct DgradClsB {
     uint32_t co;
     p.tap = (int)g.dCo.divmod((uint32_t)k0, co);
     p.c0 = (int)co;
-    p.kh = tt.id[p.tap < tt.n ? p.tap : 0];
+    p.kh = sel4(tt.id, p.tap < tt.n ? p.tap : 0);
     p.kw = p.tap == tt.xtap;  // the downsample's weights: rows of Ci after w
     return p;
   }
@@ -291,6 +317,7 @@ template <typename T> struct DgradClsB {
 // dx at class pixel (b, sh*i + pc_h, sw*j + pc_w) (+= if accumulate) (+ residual)
 template <typename T> struct DgradClsEpi {
   static constexpr bool kStats = false;
+  static constexpr bool kRow8 = true;
   T* dx;
   const T* dres;
   const T* yres;
@@ -311,6 +338,32 @@ template <typename T> struct DgradClsEpi {
       for (int q = 0; q < 4; ++q) v[q] += yy[q] > 0.f ? d[q] : 0.f;
     }
     st4<T>(dx + o, v);
+  }
+  // 8 consecutive channels of one class pixel: one 16-B store (gemm256 row8 epilogue)
+  __device__ __forceinline__ void store8(int m, int n, f32x4 lo, f32x4 hi, int) const {
+    if (m >= M || n >= N) return;
+    uint32_t r, j;
+    const uint32_t b = dHcWc.divmod(m, r);
+    const uint32_t i = dWc.divmod(r, j);
+    const int hi_ = (int)i * g.sh + pch, wi = (int)j * g.sw + pcw;
+    const size_t o = ((size_t)((int)b * g.Hi + hi_) * g.Wi + wi) * N + n;
+    if (accumulate) {
+      f32x4 a, c;
+      ld8f<T>(dx + o, a, c);
+      lo += a;
+      hi += c;
+    }
+    if (dres) {
+      f32x4 d0, d1, y0, y1;
+      ld8f<T>(dres + o, d0, d1);
+      ld8f<T>(yres + o, y0, y1);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        lo[q] += y0[q] > 0.f ? d0[q] : 0.f;
+        hi[q] += y1[q] > 0.f ? d1[q] : 0.f;
+      }
+    }
+    st8f<T>(dx + o, lo, hi);
   }
   __device__ __forceinline__ void stats(int, int, f32x4, f32x4) const {}
 };
@@ -452,24 +505,6 @@ inline int wgrad_fast_kind(const Geo& g) {
 // ---- epilogues
 // y = acc, or (eval-mode BN, esc != nullptr) y = ReLU(acc * esc[n] + esh[n]): the running-stat
 // affine and the ReLU applied to the fp32 accumulators, so no z tensor and no bn_act pass
-// 8 consecutive columns (two f32x4) as one row vector of T
-template <typename T> __device__ __forceinline__ void st8f(T* p, f32x4 lo, f32x4 hi) {
-  typename VT<T>::v8 v;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    v[r] = fromf<T>(lo[r]);
-    v[4 + r] = fromf<T>(hi[r]);
-  }
-  st8<T>(p, v);
-}
-template <typename T> __device__ __forceinline__ void ld8f(const T* p, f32x4& lo, f32x4& hi) {
-  const typename VT<T>::v8 v = ld8<T>(p);
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    lo[r] = tof(v[r]);
-    hi[r] = tof(v[4 + r]);
-  }
-}
 
 template <typename T> struct FwdEpi {
   static constexpr bool kStats = true;
@@ -762,6 +797,62 @@ inline double round_eff(long tiles) {
 // tile) is the break-even share of the CUs: below it the smaller tiles finish first
 inline double quant_eff(int bn) { return bn == 256 ? 0.4 : 0.6; }
 
+// ---- all parity classes of a strided dgrad in ONE launch (CRNN_OPT_DGRAD_GROUP): a grouped tile
+// table over the classes' GEMMs (same N = Ci and tile shape, own M, K and taps), longest K first so
+// the long tiles start in the first round. Per launch this removes the class launches' partial last
+// rounds and their launch gaps (a class GEMM is short-K: 1-4 taps x Co). Each block picks its class
+// from the table (wave-uniform), rebuilds the class's loaders from the shared base and runs the
+// ordinary 256-row work item.
+struct ClsRec {
+  TapTable tt;
+  int Hc, Wc, M, K, pch, pcw, start, tiles;
+  FastDiv dWc, dHcWc;
+};
+constexpr int MAX_CLS = 4;
+template <typename T> struct ClsGroup {
+  DgradClsA<T> la;
+  DgradClsB<T> lb;
+  DgradClsEpi<T> ep;
+  ClsRec c[MAX_CLS];
+  int ng, tn, total;
+};
+
+template <typename T, int BN>
+__global__ __launch_bounds__(512) void dgrad_cls_group_kernel(const ClsGroup<T> G, int stagger) {
+  // blocks in table order (dispatch is round-robin over the XCDs, so every class spreads evenly over
+  // them); the XCD-contiguous remap only WITHIN a class (over the whole table it gave the first XCDs
+  // all of the longest class: 1.4x slower)
+  const int wb = blockIdx.x;
+  int g = 0;
+#pragma unroll
+  for (int i = 1; i < MAX_CLS; ++i) g += (i < G.ng && wb >= G.c[i].start) ? 1 : 0;
+  // the class record by wave-uniform selects (a dynamic index into the kernel-argument array would
+  // copy it to scratch)
+  ClsRec r = G.c[0];
+#pragma unroll
+  for (int i = 1; i < MAX_CLS; ++i)
+    if (g == i) r = G.c[i];
+  DgradClsA<T> la = G.la;
+  la.tt = r.tt;
+  la.Hc = r.Hc;
+  la.Wc = r.Wc;
+  la.M = r.M;
+  la.K = r.K;
+  la.dWc = r.dWc;
+  la.dHcWc = r.dHcWc;
+  DgradClsB<T> lb = G.lb;
+  lb.tt = r.tt;
+  lb.K = r.K;
+  DgradClsEpi<T> ep = G.ep;
+  ep.M = r.M;
+  ep.pch = r.pch;
+  ep.pcw = r.pcw;
+  ep.dWc = r.dWc;
+  ep.dHcWc = r.dHcWc;
+  const int local = xcd_remap(wb - r.start, r.tiles);
+  gemm256_item<256, BN, 0>(la, lb, ep, r.M, r.K, r.K, local / G.tn, local % G.tn, 0, stagger, 0);
+}
+
 // rows: row classes (each input row its own class, Hc = 1) instead of parity classes in height —
 // for maps of 1-2 output rows (conv_out[1]: Ho = 1), where half of a generic dgrad's taps read
 // nothing but padding rows; the stride may then be 1
@@ -774,6 +865,12 @@ int conv_dgrad_strided(const Geo& g, const void* dy, const void* w, void* dx, co
   const long dyn = (long)g.B * g.Ho * g.Wo * g.Co, wn = (long)g.Co * g.KH * g.KW * g.Ci;
   const uint32_t dyb = nbytes(ds ? 2 * dyn : dyn, sizeof(T));
   const uint32_t wb = nbytes(ds ? wn + (long)g.Co * g.Ci : wn, sizeof(T));
+  // grouped form: every class on the 256 x 128 tile of the 256-row kernel (bf16, Ci % 128 == 0)
+  ClsRec recs[MAX_CLS];
+  int nrec = 0;
+  bool group = sizeof(T) == 2 && crnn_option(CRNN_OPT_DGRAD_GROUP) != 0 && !rows && g.Ci % 128 == 0 &&
+               g.Co % 64 == 0 && g.sh * g.sw <= MAX_CLS;
+  for (int pass = group ? 0 : 1; pass < 2; ++pass) {
   for (int pch = 0; pch < (rows ? g.Hi : g.sh); ++pch)
     for (int pcw = 0; pcw < g.sw; ++pcw) {
       TapTable tt{};
@@ -805,6 +902,14 @@ int conv_dgrad_strided(const Geo& g, const void* dy, const void* w, void* dx, co
       if (tt.n == 0 && accumulate && dres == nullptr) continue;
       const int M = g.B * Hc * Wc, N = g.Ci, K = tt.n * g.Co;
       FastDiv dWc(Wc), dHcWc(Hc * Wc);
+      if (pass == 0) {   // grouped form: collect the class; a class off the 256 x 128 tile ends the group
+        if (tt.n == 0 || deep_dgrad_bn<T>(M, N, g.Co, 64) == 0) {
+          group = false;
+          break;
+        }
+        recs[nrec++] = ClsRec{tt, Hc, Wc, M, K, pch, pcw, 0, 0, dWc, dHcWc};
+        continue;
+      }
       DgradClsA<T> la{(const T*)dy, g, tt, Hc, Wc, M, K, dWc, dHcWc, dyb};
       DgradClsB<T> lb{(const T*)w, g, tt, K, wb};
       DgradClsEpi<T> ep{(T*)dx, (const T*)dres, (const T*)yres, g, M, N, accumulate, pch, pcw, dWc, dHcWc};
@@ -820,6 +925,35 @@ int conv_dgrad_strided(const Geo& g, const void* dy, const void* w, void* dx, co
       else rc = launch<T, 64, 64>(la, lb, ep, M, N, K, 1, st);
       if (rc) return rc;
     }
+    if (pass == 0) {
+      if (!group || nrec == 0) continue;    // fall back: a launch per class
+      // longest K first (insertion sort, <= 4 records), then the tile table
+      for (int i = 1; i < nrec; ++i)
+        for (int j = i; j > 0 && recs[j].K > recs[j - 1].K; --j) std::swap(recs[j], recs[j - 1]);
+      ClsGroup<T> G{};
+      const int tn = g.Ci / 128;
+      int total = 0;
+      for (int i = 0; i < nrec; ++i) {
+        recs[i].start = total;
+        recs[i].tiles = (recs[i].M + 255) / 256 * tn;
+        total += recs[i].tiles;
+        G.c[i] = recs[i];
+      }
+      const ClsRec& r0 = recs[0];
+      G.la = DgradClsA<T>{(const T*)dy, g, r0.tt, r0.Hc, r0.Wc, r0.M, r0.K, r0.dWc, r0.dHcWc, dyb};
+      G.lb = DgradClsB<T>{(const T*)w, g, r0.tt, r0.K, wb};
+      G.ep = DgradClsEpi<T>{(T*)dx, (const T*)dres, (const T*)yres, g, r0.M, g.Ci, accumulate, r0.pch, r0.pcw,
+                            r0.dWc, r0.dHcWc};
+      G.ng = nrec;
+      G.tn = tn;
+      G.total = total;
+      if constexpr (sizeof(T) == 2) {
+        hipLaunchKernelGGL((dgrad_cls_group_kernel<T, 128>), dim3(total), dim3(512), 0, st, G,
+                           crnn_option(CRNN_OPT_GEMM_STAGGER));
+        return (int)hipGetLastError();
+      }
+    }
+  }
   return 0;
 }
 

@@ -159,6 +159,63 @@ def test_conv_dgrad_ds_fused(geo, dtype):
     assert L.lib().crnn_conv_dgrad_ds_supported(dt, bad, dd) == 0
 
 
+@pytest.mark.parametrize("geo", [
+    (256, 128, 16, 128, 256, (3, 3), (2, 2), (1, 1), True),    # layer1.0 conv1 + downsample (bench)
+    (64, 256, 8, 64, 512, (3, 3), (2, 2), (1, 1), True),       # layer3.0 conv1 + downsample
+    (64, 256, 8, 64, 512, (3, 3), (2, 2), (1, 1), False),      # layer3.0 conv1 alone
+    (64, 512, 4, 32, 512, (2, 2), (2, 1), (0, 1), False),      # conv_out.0 (two height classes)
+])
+def test_dgrad_class_group(geo):
+    """CRNN_OPT_DGRAD_GROUP: every parity class of a strided bf16 dgrad in ONE grouped launch ==
+    the torch fp32 input gradient within bf16 accuracy, no further from it than a launch per class;
+    bit-identical to the per-class launches where those run on the same 256 x 128 tile (the bench
+    geometry), since each output element sums the same K-tiles in the same order."""
+    L = _L()
+    B, Ci, H, W, Co, k, s, p, with_ds = geo
+    g = torch.Generator().manual_seed(17)
+    w1 = (torch.randn(Co, Ci, *k, generator=g) / math.sqrt(k[0] * k[1] * Ci)).bfloat16().float()
+    wd = (torch.randn(Co, Ci, 1, 1, generator=g) / math.sqrt(Ci)).bfloat16().float()
+    Ho, Wo = (H + 2 * p[0] - k[0]) // s[0] + 1, (W + 2 * p[1] - k[1]) // s[1] + 1
+    dy1 = torch.randn(B, Co, Ho, Wo, generator=g).bfloat16().float()
+    dyd = torch.randn(B, Co, Ho, Wo, generator=g).bfloat16().float()
+    x = torch.zeros(B, Ci, H, W, requires_grad=True)
+    (F.conv2d(x, w1, stride=s, padding=p) * dy1).sum().backward(retain_graph=True)
+    if with_ds:
+        (F.conv2d(x, wd, stride=s) * dyd).sum().backward()
+    ref = x.grad
+    dt = L.BF16
+    d1 = L.ConvDesc(B, H, W, Ci, Ho, Wo, Co, k[0], k[1], s[0], s[1], p[0], p[1], Ci)
+    dd = L.ConvDesc(B, H, W, Ci, Ho, Wo, Co, 1, 1, s[0], s[1], 0, 0, Ci)
+    n1 = Co * k[0] * k[1] * Ci
+    st = L.stream_ptr()
+    wcat = torch.empty(n1 + Co * Ci, dtype=torch.bfloat16, device=DEV)
+    L.call("crnn_pack_conv_weight", dt, w1.to(DEV).data_ptr(), wcat.data_ptr(), Co, Ci, k[0], k[1], Ci, st)
+    L.call("crnn_pack_conv_weight", dt, wd.to(DEV).data_ptr(), wcat[n1:].data_ptr(), Co, Ci, 1, 1, Ci, st)
+    m = B * Ho * Wo * Co
+    dycat = torch.empty(2 * m, dtype=torch.bfloat16, device=DEV)
+    dycat[:m].copy_(to_nhwc(dy1, None, torch.bfloat16).reshape(-1))
+    dycat[m:].copy_(to_nhwc(dyd, None, torch.bfloat16).reshape(-1))
+    outs = {}
+    try:
+        for grouped in (1, 0):
+            L.lib().crnn_set_option(L.OPT_DGRAD_GROUP, grouped)
+            dx = torch.full((B, H, W, Ci), float("nan"), dtype=torch.bfloat16, device=DEV)
+            if with_ds:
+                L.call("crnn_conv_dgrad_ds", dt, d1, dd, dycat.data_ptr(), wcat.data_ptr(), dx.data_ptr(), st)
+            else:
+                L.call("crnn_conv_dgrad", dt, d1, dycat.data_ptr(), wcat.data_ptr(), dx.data_ptr(), None, None, 0, st)
+            torch.cuda.synchronize()
+            outs[grouped] = dx.float().permute(0, 3, 1, 2).cpu()
+    finally:
+        L.lib().crnn_set_option(L.OPT_DGRAD_GROUP, 1)
+    e1, e0 = relerr(outs[1], ref), relerr(outs[0], ref)
+    print(f"dgrad class group {geo}: grouped rel err {e1:.3e}, per class {e0:.3e}")
+    assert torch.isfinite(outs[1]).all()
+    assert e1 < 1e-2 and e1 <= e0 * 1.05 + 1e-6
+    if B == 256:
+        assert torch.equal(outs[1], outs[0]), "grouped launch differs from the per-class launches"
+
+
 @pytest.mark.parametrize("dtype,cfg", [(dt, c) for c in CONVS for dt in (torch.float32, torch.bfloat16)]
                          + [(torch.bfloat16, c) for c in CONVS_DEEP])
 def test_conv_fwd_dgrad_wgrad(cfg, dtype):
