@@ -329,7 +329,7 @@ def main():
     if world > 1:
         D.broadcast_params(model._flat_param)
         model.mark_params_changed()
-    grads, _ = model._grad_views()
+    grads, _, _ = model._grad_views()
     opt = FusedAdamW(model, lr=1e-4, weight_decay=1e-2)
     inv_world = 1.0 / world
     # DP: bucketed RCCL all-reduce of the flat gradient, issued stage by stage during the backward

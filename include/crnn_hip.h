@@ -84,6 +84,8 @@ enum { CRNN_OPT_GEMM_STAGGER = 0,    /* 256-row conv GEMM: waves 4-7 one barrier
                                         (grouped tile table, longest-K class first; default), 0 = a launch per class */
        CRNN_OPT_COUNT = 17 };
 int crnn_set_option(int key, int value);
+/* current value of a tuning switch (0 for an unknown key) */
+int crnn_get_option(int key);
 
 /* ------------------------------------------------------------------ layout */
 /* fp32 NCHW image batch -> dtype NHWC with channels zero-padded to Cp. */

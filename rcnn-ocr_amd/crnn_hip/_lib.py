@@ -58,6 +58,7 @@ _SIGS = {
     "crnn_pack_conv_t_tiles": ([i32, i32], i32),
     "crnn_version": ([], i32),
     "crnn_set_option": ([i32, i32], i32),
+    "crnn_get_option": ([i32], i32),
     "crnn_last_error_string": ([], C.c_char_p),
     "crnn_nchw_to_nhwc": ([i32, vp, vp, i32, i32, i32, i32, i32, vp], i32),
     "crnn_cast_f32": ([i32, vp, vp, i64, vp], i32),

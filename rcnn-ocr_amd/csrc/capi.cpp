@@ -29,6 +29,8 @@ int crnn_cu_count() {
 
 int crnn_option(int key) { return (key >= 0 && key < CRNN_OPT_COUNT) ? g_opts[key] : 0; }
 
+extern "C" int crnn_get_option(int key) { return crnn_option(key); }
+
 extern "C" int crnn_set_option(int key, int value) {
   if (key < 0 || key >= CRNN_OPT_COUNT) return crnn_set_error((int)hipErrorInvalidValue, "crnn_set_option: bad key");
   g_opts[key] = value;

@@ -40,6 +40,10 @@ class BidirectionalLSTM(nn.Module):
         raise NotImplementedError("BiLSTM layers run inside the HIP engine; call RCNN.encode/forward")
 
 
+def _noop():
+    return None
+
+
 class _EncodeFn(torch.autograd.Function):
     """images -> logits via the engine; backward writes parameter gradients
     straight into the flat grad buffer (the params' .grad views)."""
@@ -63,8 +67,9 @@ class _EncodeFn(torch.autograd.Function):
         dl = eng.ws.get("autograd.dlogits", (B, T, eng.Cpad), torch.float32)
         dl[:, :, C:].zero_()
         dl[:, :, :C].copy_(grad_logits)
-        grads, accumulate = model._grad_views()
+        grads, accumulate, attach = model._grad_views()
         eng.backward(dl, grads, accumulate=accumulate, stage_done=model.stage_done)
+        attach()
         return None, None, None, None
 
 
@@ -91,10 +96,11 @@ class _AttnTrainFn(torch.autograd.Function):
     def backward(ctx, grad_logits):
         model = ctx.model
         model._engine.check_generation(ctx.gen)
-        grads, accumulate = model._grad_views()
+        grads, accumulate, attach = model._grad_views()
         attn_grads = {k[len("attn."):]: v for k, v in grads.items() if k.startswith("attn.")}
         denc = model._attn_dec.backward(grad_logits.contiguous(), attn_grads, accumulate)
         model._engine.backward(None, grads, accumulate=accumulate, denc=denc, stage_done=model.stage_done)
+        attach()
         return None, None, None, None, None
 
 
@@ -151,6 +157,7 @@ class RCNN(nn.Module):
         self._engine: Optional[CRNNEngine] = None
         self._flat_param: Optional[torch.Tensor] = None
         self._flat_grad: Optional[torch.Tensor] = None
+        self._gv_cache = None   # (flat grad buffer, [(name, param, grad view)], {name: view})
         # data parallel: called by every backward with the parameter-name prefixes whose gradients
         # have become final (crnn_hip.dist.OverlappedAllReduce.ready), so the gradient all-reduce
         # overlaps the rest of the backward; None = single process
@@ -182,6 +189,7 @@ class RCNN(nn.Module):
             off += k
         self._flat_param, self._flat_grad = flat, gflat
         self._grad_offsets = None
+        self._gv_cache = None
 
     def flat_offsets(self):
         """{parameter name: (start, numel)} in the flat buffer (parameter order: stem first, head last)."""
@@ -192,21 +200,34 @@ class RCNN(nn.Module):
         return out
 
     def _grad_views(self):
-        """(name -> grad tensor, accumulate?) ; re-attaches flat views after zero_grad(set_to_none=True)."""
-        params = list(self.named_parameters())
-        any_none = any(p.grad is None for _, p in params)
-        all_none = all(p.grad is None for _, p in params)
-        if any_none:
-            off = 0
-            for _, p in params:
+        """-> (name -> grad tensor, accumulate?, attach). The flat buffer's gradient views are built
+        once per buffer. After zero_grad(set_to_none=True) the backward OVERWRITES them (accumulate
+        False) and attach() makes them the parameters' .grad again: the caller calls it after it has
+        enqueued the backward kernels, so the host-side .grad assignments (one per parameter) run
+        while the GPU works instead of delaying the first backward launch (profiles/r03x_*: a 0.2 ms
+        GPU bubble per step). Some grads None, some not: the None ones are zeroed and attached first
+        and the backward accumulates."""
+        c = self._gv_cache
+        if c is None or c[0] is not self._flat_grad:
+            items, off = [], 0
+            for n, p in self.named_parameters():
                 k = p.numel()
-                if p.grad is None:
-                    g = self._flat_grad[off:off + k].view_as(p)
-                    if not all_none:
-                        g.zero_()
-                    p.grad = g
+                items.append((n, p, self._flat_grad[off:off + k].view_as(p)))
                 off += k
-        return {n: p.grad for n, p in params}, not all_none
+            c = self._gv_cache = (self._flat_grad, items, {n: v for n, _, v in items})
+        _, items, views = c
+        missing = [(p, v) for _, p, v in items if p.grad is None]
+        if not missing:
+            return {n: p.grad for n, p, _ in items}, True, _noop
+        if len(missing) == len(items):
+            def attach():
+                for p, v in missing:
+                    p.grad = v
+            return views, False, attach
+        for p, v in missing:
+            v.zero_()
+            p.grad = v
+        return {n: p.grad for n, p, _ in items}, True, _noop
 
     def _engine_for(self, images: torch.Tensor) -> CRNNEngine:
         L.require_device(images)

@@ -248,7 +248,7 @@ def test_engine_bilstm_stack_matches_reference_golden(dtype):
     m.flatten_parameters_()
     dummy = torch.zeros(1, 3, 32, 8, device=DEV)
     eng = m._engine_for(dummy)
-    grads, _ = m._grad_views()
+    grads, _, _ = m._grad_views()
     x = torch.from_numpy(z["x"])
     proj = torch.from_numpy(z["proj"])
     y, dx = eng.bilstm_stack(x.to(DEV), proj.to(DEV), grads)
