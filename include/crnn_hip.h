@@ -121,6 +121,8 @@ typedef struct {
   const float* src2;
   const int* perm;
   void* dst;
+  void* dst2;  /* CRNN_PACK_CONV_T only (NULL: none): also the plain OHWI pack dst2[co][kh][kw][ci] of the same
+                  weights from the same staged tile (Cip = Ci), so the source is read once */
 } crnn_pack_job;
 int crnn_pack_batch(int dtype, const crnn_pack_job* jobs, int njobs, long total, void* stream);
 /* conv weights only (kind CRNN_PACK_CONV, a..e = Co, Ci, KH, KW, Cip), one block per output channel:
@@ -129,7 +131,8 @@ int crnn_pack_batch(int dtype, const crnn_pack_job* jobs, int njobs, long total,
 int crnn_pack_conv_batch(int dtype, const crnn_pack_job* jobs, int njobs, long total_rows, int max_slab,
                          void* stream);
 /* transposed, flipped conv kernels for crnn_conv_dgrad_tw (kind CRNN_PACK_CONV_T, a..d = Co, Ci, KH, KW;
- * Ci % 16 == 0, KH*KW in {1, 4, 9}): dst[ci][kh][kw][co] = src_OIHW[co][ci][KH-1-kh][KW-1-kw] in dtype. One workgroup per
+ * Ci % 16 == 0, KH*KW in {1, 4, 9}): dst[ci][kh][kw][co] = src_OIHW[perm ? perm[co] : co][ci][KH-1-kh][KW-1-kw]
+ * in dtype (KH = KW = 1 with perm: a gathered transpose, the BiLSTM's W_hh'^T). One workgroup per
  * 64 x 16 (co, ci) tile, coalesced both ways through LDS; job.start = the job's first tile in the
  * concatenation (a job has ceil(Co/64) * ceil(Ci/16) tiles, co-tile major); total_tiles = all. */
 #define CRNN_PACK_CONV_T 4
@@ -302,6 +305,12 @@ int crnn_se_bn_partials(const float* abc, const float* s, const float* dpool, fl
 int crnn_se_mlp_bwd(const float* ds, const float* pooled, const float* hid, const float* s, const float* w1, const float* w2,
                     float* dsig, float* dhid, float* dpool, float* dw1, float* dw2, int B, int C, int Cr, int HW, int accumulate,
                     void* stream);
+/* the same, plus crnn_se_bn_partials' rows pg / pgx [B][C] from abc (crnn_se_bn_bwd_reduce) in the kernel that
+ * produces dpool: one launch fewer per SE block (abc == NULL: no partials, = crnn_se_mlp_bwd) */
+int crnn_se_mlp_bwd_partials(const float* ds, const float* pooled, const float* hid, const float* s, const float* w1,
+                             const float* w2, float* dsig, float* dhid, float* dpool, float* dw1, float* dw2,
+                             const float* abc, float* pg, float* pgx, int B, int C, int Cr, int HW, int accumulate,
+                             void* stream);
 
 /* ------------------------------------------------------------------ height collapse */
 /* seq[b][w][c] = mean_h relu(z*scale+shift), z [B][Hh][W][C] */

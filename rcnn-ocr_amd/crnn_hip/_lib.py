@@ -41,7 +41,7 @@ class BnBwdDesc(C.Structure):
 class PackJob(C.Structure):  # crnn_pack_job
     _fields_ = [("kind", C.c_int), ("out_f32", C.c_int), ("a", C.c_int), ("b", C.c_int), ("c", C.c_int),
                 ("d", C.c_int), ("e", C.c_int), ("pad_", C.c_int), ("start", C.c_long), ("src", vp),
-                ("src2", vp), ("perm", vp), ("dst", vp)]
+                ("src2", vp), ("perm", vp), ("dst", vp), ("dst2", vp)]
 
 
 # crnn_set_option keys (include/crnn_hip.h)
@@ -104,6 +104,8 @@ _SIGS = {
     "crnn_se_residual_fwd": ([i32, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, vp], i32),
     "crnn_se_bwd_reduce": ([i32, vp, vp, vp, vp, vp, vp, i32, i32, i32, vp], i32),
     "crnn_se_mlp_bwd": ([vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, vp], i32),
+    "crnn_se_mlp_bwd_partials": ([vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, vp],
+                                 i32),
     "crnn_hpool_fwd": ([i32, vp, vp, vp, vp, i32, i32, i32, i32, vp], i32),
     "crnn_hpool_bwd": ([i32, vp, vp, i32, i32, i32, i32, vp], i32),
     "crnn_gemm_nt": ([i32, vp, i32, vp, i32, vp, i32, vp, i32, i32, i32, i32, i32, vp], i32),

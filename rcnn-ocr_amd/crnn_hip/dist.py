@@ -94,6 +94,7 @@ class OverlappedAllReduce:
         self.active = dist.is_initialized() and dist.get_world_size() > 1
         self.issued = []
         self.last_issued = []
+        self.stream = None   # the collective stream (HIP tensors)
         self.reset()
 
     def reset(self):
@@ -118,8 +119,23 @@ class OverlappedAllReduce:
             self._issue(self.lo, self.hi)
 
     def _issue(self, lo, hi):
+        """all-reduce flat[lo:hi] on the collective stream, after the work the caller's (compute)
+        stream has enqueued so far: an explicit event edge, not the process group's notion of the
+        calling thread's current stream (the hooks run on the autograd thread; without the edge a
+        bucket was occasionally read before its last gradient kernel had finished,
+        tests/test_gpu_dp.py)"""
         self.issued.append((lo, hi))
-        self.works.append(dist.all_reduce(self.flat[lo:hi], async_op=True))
+        if self.flat.is_cuda:
+            cur = torch.cuda.current_stream(self.flat.device)
+            if self.stream is None:
+                self.stream = torch.cuda.Stream(self.flat.device)
+            ev = torch.cuda.Event()
+            ev.record(cur)
+            self.stream.wait_event(ev)
+            with torch.cuda.stream(self.stream):
+                self.works.append(dist.all_reduce(self.flat[lo:hi], async_op=True))
+        else:
+            self.works.append(dist.all_reduce(self.flat[lo:hi], async_op=True))
         self.hi = lo
 
     def finish(self):
@@ -131,5 +147,7 @@ class OverlappedAllReduce:
                     raise RuntimeError(f"finish(): gradients never reported final: {missing[:4]}")
                 self._issue(0, self.hi)
             for w in self.works:
-                w.wait()
+                w.wait()   # makes the collective stream wait for the collectives' completion
+            if self.stream is not None:   # and the caller's stream for the collective stream
+                torch.cuda.current_stream(self.flat.device).wait_stream(self.stream)
         self.reset()

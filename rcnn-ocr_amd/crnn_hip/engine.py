@@ -247,9 +247,13 @@ class CRNNEngine:
                 cat = torch.empty(n1 + ds.co * ds.kh * ds.kw * ds.ci, dtype=T, device=self.device)
                 self.packed[c1.name] = cat[:n1].view(c1.co, c1.kh, c1.kw, c1.ci)
                 self.packed[ds.name] = cat[n1:].view(ds.co, ds.kh, ds.kw, ds.ci)
-        # conv weights: their own launch, one block per output channel (crnn_pack_conv_batch)
+        # conv weights: their own launch, one block per output channel (crnn_pack_conv_batch); the
+        # convs with a transposed pack get their OHWI pack from that kernel's tiles (dst2, below)
+        tw = self.tw_convs()
         rows, slab = 0, 0
         for cs in self.convs():
+            if any(cs is t for t in tw):
+                continue
             out = self._pbuf(cs.name, (cs.co, cs.kh, cs.kw, cs.ci), T)
             job(L.PACK_CONV, self.p[cs.name], out, cs.co, cs.ci_real, cs.kh, cs.kw, cs.ci)
             jobs[-1].start = rows
@@ -261,11 +265,24 @@ class CRNNEngine:
         jobs.clear()
         # transposed, flipped kernels [Ci][KH][KW][Co] of the stride-1 convs (crnn_conv_dgrad_tw)
         tiles = 0
-        for cs in self.tw_convs():
+        for cs in tw:
             out = self._pbuf(cs.name + ".t", (cs.ci, cs.kh, cs.kw, cs.co), T)
             job(L.PACK_CONV_T, self.p[cs.name], out, cs.co, cs.ci, cs.kh, cs.kw)
+            jobs[-1].dst2 = ptr(self._pbuf(cs.name, (cs.co, cs.kh, cs.kw, cs.ci), T))
             jobs[-1].start = tiles
             tiles += L.lib().crnn_pack_conv_t_tiles(cs.co, cs.ci)
+        # the BiLSTM's W_hh'^T (BPTT B operand, K-contiguous): a gathered transpose on the same tiled
+        # kernel (KH = KW = 1, perm = the gate interleave) when its 16-B source rows allow, else an
+        # element gather in crnn_pack_batch (below)
+        whh_names = [f"enc_rnn.{l}.rnn.weight_hh_l0{sfx}" for l in range(self.nl) for sfx in ("", "_reverse")]
+        tiled_t = H % 16 == 0 and all(self.p[n].data_ptr() % 16 == 0 for n in whh_names)
+        for l in range(self.nl if tiled_t else 0):
+            pre = f"enc_rnn.{l}"
+            whh_t = self._pbuf(pre + ".whh_t", (2, H, 4 * H), T)
+            for d, sfx in enumerate(["", "_reverse"]):
+                job(L.PACK_CONV_T, self.p[pre + ".rnn.weight_hh_l0" + sfx], whh_t[d], 4 * H, H, 1, 1, perm=self.perm)
+                jobs[-1].start = tiles
+                tiles += L.lib().crnn_pack_conv_t_tiles(4 * H, H)
         if jobs:
             tarr = (L.PackJob * len(jobs))(*jobs)
             traw = torch.frombuffer(bytearray(bytes(tarr)), dtype=torch.uint8).to(self.device)
@@ -278,15 +295,16 @@ class CRNNEngine:
             ind = self.enc_dim if l == 0 else H
             wih = self._pbuf(pre + ".wih", (2, 4 * H, ind), T)
             whh = self._pbuf(pre + ".whh", (2, 4 * H, H), T)
-            whh_t = self._pbuf(pre + ".whh_t", (2, H, 4 * H), T)   # BPTT B operand, K-contiguous
             bias = self._pbuf(pre + ".bias", (2, 4 * H), torch.float32)
+            whh_t = self._pbuf(pre + ".whh_t", (2, H, 4 * H), T)
             for d, sfx in enumerate(["", "_reverse"]):
                 r = pre + ".rnn."
+                if not tiled_t:
+                    sizes.append(job(L.PACK_TRANSPOSE, self.p[r + "weight_hh_l0" + sfx], whh_t[d], 4 * H, 4 * H, H,
+                                     perm=self.perm))
                 sizes.append(job(L.PACK_ROWS, self.p[r + "weight_ih_l0" + sfx], wih[d], 4 * H, 4 * H, ind,
                                  perm=self.perm))
                 sizes.append(job(L.PACK_ROWS, self.p[r + "weight_hh_l0" + sfx], whh[d], 4 * H, 4 * H, H,
-                                 perm=self.perm))
-                sizes.append(job(L.PACK_TRANSPOSE, self.p[r + "weight_hh_l0" + sfx], whh_t[d], 4 * H, 4 * H, H,
                                  perm=self.perm))
                 sizes.append(job(L.PACK_ROWS_SUM, self.p[r + "bias_ih_l0" + sfx], bias[d], 4 * H, 4 * H, 1,
                                  out_f32=True, perm=self.perm, src2=self.p[r + "bias_hh_l0" + sfx]))
@@ -1071,14 +1089,18 @@ class CRNNEngine:
             dsig = ws.get(f"se.dsig{P}", (B, P), torch.float32)
             dhid = ws.get(f"se.dhid{P}", (B, Cr), torch.float32)
             dpool = ws.get(f"se.dpool{P}", (B, P), torch.float32)
-            call("crnn_se_mlp_bwd", ptr(ds), ptr(sb["pooled"]), ptr(sb["hid"]), ptr(sb["s"]),
+            # the SE MLP backward also writes BN2's per-sample backward sums (crnn_se_bn_partials' rows)
+            pg2 = ws.get("bnb.pg", (1024 * 512,), torch.float32)[: B * P]
+            pgx2 = ws.get("bnb.pgx", (1024 * 512,), torch.float32)[: B * P]
+            call("crnn_se_mlp_bwd_partials", ptr(ds), ptr(sb["pooled"]), ptr(sb["hid"]), ptr(sb["s"]),
                  ptr(self.p[blk.prefix + ".se.fc.0.weight"]), ptr(self.p[blk.prefix + ".se.fc.2.weight"]),
                  ptr(dsig), ptr(dhid), ptr(dpool), ptr(self._gview(blk.prefix + ".se.fc.0.weight")),
-                 ptr(self._gview(blk.prefix + ".se.fc.2.weight")), B, P, Cr, HW, acc, s)
+                 ptr(self._gview(blk.prefix + ".se.fc.2.weight")), ptr(abc), ptr(pg2), ptr(pgx2), B, P, Cr, HW, acc,
+                 s)
             dz2 = self._dz(f"b{bi}.c2", bufs[o1], Mo * P)
             self._bn_bwd(3, dyb, sb["z2"], (sb["m2"], sb["i2"], sb["sc2"], sb["sh2"]), blk.conv2.bn, Mo, P, HW=HW,
                          y=sb["y"], se=sb["s"], dpool=dpool, out=dz2, accumulate_params=accumulate,
-                         se_abc=(abc, B))
+                         sums=(pg2, pgx2, B))
             self._wgrad(blk.conv2, dz2, sb["a1"], B, ho, wo)
             da1 = bufs[o2][: Mo * P]
             d2 = blk.conv2.desc(B, ho, wo)

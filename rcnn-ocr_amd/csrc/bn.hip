@@ -514,14 +514,15 @@ template <typename T>
 __global__ void bn_relu_maxpool_kernel(const T* __restrict__ z, const float* __restrict__ sc, const float* __restrict__ sh,
                                        T* __restrict__ y, int B, int H, int W, int C) {
   const int Ho = H / 2, Wo = W / 2, cg = C / 8;
-  const long n = (long)B * Ho * Wo * cg;
+  const long n = (long)B * Ho * Wo * cg;   // < 2^31 (host check): 32-bit index arithmetic
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
-    int c8 = (int)(i % cg) * 8;
-    long p = i / cg;
-    int wo = (int)(p % Wo);
-    long q = p / Wo;
-    int ho = (int)(q % Ho);
-    int b = (int)(q / Ho);
+    const uint32_t iu = (uint32_t)i;
+    int c8 = (int)(iu % (uint32_t)cg) * 8;
+    const uint32_t p = iu / (uint32_t)cg;
+    int wo = (int)(p % (uint32_t)Wo);
+    const uint32_t q = p / (uint32_t)Wo;
+    int ho = (int)(q % (uint32_t)Ho);
+    int b = (int)(q / (uint32_t)Ho);
     float best[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) best[k] = -INFINITY;
@@ -705,7 +706,8 @@ __global__ __launch_bounds__(256) void se_mlp_bwd_kernel(const float* __restrict
                                                          const float* __restrict__ s, const float* __restrict__ w1,
                                                          const float* __restrict__ w2, float* __restrict__ dsig,
                                                          float* __restrict__ dhid, float* __restrict__ dpool, int B,
-                                                         float inv_hw) {
+                                                         float inv_hw, const float* __restrict__ abc,
+                                                         float* __restrict__ pg, float* __restrict__ pgx, int HW) {
   constexpr int Cr = C / 16;
   constexpr int G = Cr / 4, R = 64 / G;   // lanes per w2 row (16 B each), w2 rows per wave-instruction
   constexpr int CQ = C / 4, NI = CQ / R;  // channels per wave, load instructions per lane
@@ -773,7 +775,23 @@ __global__ __launch_bounds__(256) void se_mlp_bwd_kernel(const float* __restrict
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int r = 0; r < Cr; ++r) acc += dh[sb][r] * wv[r];
-      if (sb < nb) *reinterpret_cast<f32x4*>(dpool + (size_t)(b0 + sb) * C + c4) = acc * inv_hw;
+      const f32x4 dp = acc * inv_hw;
+      if (sb < nb) *reinterpret_cast<f32x4*>(dpool + (size_t)(b0 + sb) * C + c4) = dp;
+      if (abc != nullptr && sb < nb) {   // the CRNN_BNG_SE BatchNorm sums (se_bn_partials_kernel's rows)
+        const size_t b = (size_t)(b0 + sb);
+        const f32x4 sv = *reinterpret_cast<const f32x4*>(s + b * C + c4);
+        const f32x4 o0 = *reinterpret_cast<const f32x4*>(abc + b * 3 * C + c4);
+        const f32x4 o1 = *reinterpret_cast<const f32x4*>(abc + b * 3 * C + C + c4);
+        const f32x4 o2 = *reinterpret_cast<const f32x4*>(abc + b * 3 * C + 2 * C + c4);
+        f32x4 q0, q1;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          q0[e] = sv[e] * o0[e] + (float)HW * dp[e];
+          q1[e] = sv[e] * o1[e] + dp[e] * o2[e];
+        }
+        *reinterpret_cast<f32x4*>(pg + b * C + c4) = q0;
+        *reinterpret_cast<f32x4*>(pgx + b * C + c4) = q1;
+      }
     }
   }
 }
@@ -952,7 +970,112 @@ __global__ void pack_rows_kernel(const float* __restrict__ src, T* __restrict__ 
 }
 
 // all pack jobs in one launch: block b owns elements [b*chunk, (b+1)*chunk) of the concatenation
-// and walks the (start-sorted) job table from the job holding its first element
+// (chunk a multiple of 8) and walks the (start-sorted) job table from the job holding its first
+// element. Jobs whose start and size are multiples of 8 (every job the engine builds) go 8 output
+// elements per thread: 16-B stores, and for row gathers two 16-B source loads when the source is
+// 16-B aligned (parameters are views into the flat buffer at arbitrary offsets, so checked per job);
+// the transposed gathers (W_hh^T) read 8 rows of one column. Other jobs: one element per thread.
+template <typename T>
+__device__ __forceinline__ float pack_elem(const crnn_pack_job& jb, int i) {
+  if (jb.kind == CRNN_PACK_CONV) {
+    const int Ci = jb.b, KH = jb.c, KW = jb.d, Cip = jb.e;
+    const int ci = i % Cip;
+    int t = i / Cip;
+    const int kw = t % KW;
+    t /= KW;
+    const int kh = t % KH, co = t / KH;
+    return ci < Ci ? jb.src[(((size_t)co * Ci + ci) * KH + kh) * KW + kw] : 0.f;
+  }
+  if (jb.kind == CRNN_PACK_TRANSPOSE) {
+    const int rows = jb.a;
+    const int c = i / rows, r = i - c * rows;
+    const int sr = jb.perm ? jb.perm[r] : r;
+    return (r < jb.b && sr >= 0) ? jb.src[(size_t)sr * jb.c + c] : 0.f;
+  }
+  const int cols = jb.c;
+  const int r = i / cols, c = i - r * cols;
+  const int sr = jb.perm ? jb.perm[r] : r;
+  const bool ok = r < jb.b && sr >= 0;
+  float v = ok ? jb.src[(size_t)sr * cols + c] : 0.f;
+  if (jb.kind == CRNN_PACK_ROWS_SUM && ok) v += jb.src2[(size_t)sr * cols + c];
+  return v;
+}
+
+template <typename T>
+__device__ __forceinline__ void pack_store8(const crnn_pack_job& jb, int i, const float* v) {
+  if (jb.out_f32) {
+    f32x4* d = reinterpret_cast<f32x4*>((float*)jb.dst + i);
+    d[0] = f32x4{v[0], v[1], v[2], v[3]};
+    d[1] = f32x4{v[4], v[5], v[6], v[7]};
+  } else if constexpr (sizeof(T) == 2) {
+    *reinterpret_cast<bf16x8*>((T*)jb.dst + i) = pack8<T>(v);
+  } else {
+    f32x4* d = reinterpret_cast<f32x4*>((T*)jb.dst + i);
+    d[0] = f32x4{v[0], v[1], v[2], v[3]};
+    d[1] = f32x4{v[4], v[5], v[6], v[7]};
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ void pack_job8(const crnn_pack_job& jb, long a0, long a1) {
+  const int kind = jb.kind;
+  const bool rows = kind == CRNN_PACK_ROWS || kind == CRNN_PACK_ROWS_SUM;
+  const int cols = jb.c;
+  const bool vsrc = rows && cols % 8 == 0 && ((uintptr_t)jb.src & 15) == 0 &&
+                    (kind != CRNN_PACK_ROWS_SUM || ((uintptr_t)jb.src2 & 15) == 0);
+  for (long g = a0 + 8 * (long)threadIdx.x; g < a1; g += 8L * blockDim.x) {
+    const int i = (int)(g - jb.start);
+    float v[8];
+    if (rows && cols % 8 == 0) {   // 8 consecutive columns of one row
+      const int r = i / cols, c = i - r * cols;
+      const int sr = jb.perm ? jb.perm[r] : r;
+      const bool ok = r < jb.b && sr >= 0;
+      const size_t o = (size_t)(ok ? sr : 0) * cols + c;
+      if (vsrc) {
+        f32x4 x0 = *reinterpret_cast<const f32x4*>(jb.src + o), x1 = *reinterpret_cast<const f32x4*>(jb.src + o + 4);
+        if (kind == CRNN_PACK_ROWS_SUM) {
+          x0 += *reinterpret_cast<const f32x4*>(jb.src2 + o);
+          x1 += *reinterpret_cast<const f32x4*>(jb.src2 + o + 4);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          v[q] = ok ? x0[q] : 0.f;
+          v[4 + q] = ok ? x1[q] : 0.f;
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          float x = jb.src[o + q];
+          if (kind == CRNN_PACK_ROWS_SUM) x += jb.src2[o + q];
+          v[q] = ok ? x : 0.f;
+        }
+      }
+    } else if (rows) {                // cols == 1: 8 consecutive rows (bias vectors)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int r = i + q;
+        const int sr = jb.perm ? jb.perm[r] : r;
+        const bool ok = r < jb.b && sr >= 0;
+        float x = jb.src[ok ? sr : 0];
+        if (kind == CRNN_PACK_ROWS_SUM) x += jb.src2[ok ? sr : 0];
+        v[q] = ok ? x : 0.f;
+      }
+    } else {                          // transpose: 8 consecutive rows of one source column
+      const int R = jb.a;
+      const int c = i / R, r0 = i - c * R;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int r = r0 + q;
+        const int sr = jb.perm ? jb.perm[r] : r;
+        const bool ok = r < jb.b && sr >= 0;
+        const float x = jb.src[(size_t)(ok ? sr : 0) * jb.c + c];
+        v[q] = ok ? x : 0.f;
+      }
+    }
+    pack_store8<T>(jb, i, v);
+  }
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void pack_batch_kernel(const crnn_pack_job* __restrict__ jobs, int njobs, long total,
                                                          long chunk) {
@@ -972,32 +1095,18 @@ __global__ __launch_bounds__(256) void pack_batch_kernel(const crnn_pack_job* __
       if (jb.start >= e1) break;
       continue;
     }
+    const bool v8 = jb.start % 8 == 0 && jend % 8 == 0 && e0 % 8 == 0 && a1 % 8 == 0 &&
+                    ((jb.kind == CRNN_PACK_ROWS || jb.kind == CRNN_PACK_ROWS_SUM) ? (jb.c % 8 == 0 || jb.c == 1)
+                     : jb.kind == CRNN_PACK_TRANSPOSE ? jb.a % 8 == 0 : false);
+    if (v8) {
+      pack_job8<T>(jb, a0, a1);
+      continue;
+    }
     // element index inside a job fits 32 bits (the largest tensor is 2.4 M elements): 32-bit
     // divisions, not the 64-bit ones that dominated this kernel
     for (long g = a0 + threadIdx.x; g < a1; g += blockDim.x) {
       const int i = (int)(g - jb.start);
-      float v;
-      if (jb.kind == CRNN_PACK_CONV) {
-        const int Ci = jb.b, KH = jb.c, KW = jb.d, Cip = jb.e;
-        const int ci = i % Cip;
-        int t = i / Cip;
-        const int kw = t % KW;
-        t /= KW;
-        const int kh = t % KH, co = t / KH;
-        v = ci < Ci ? jb.src[(((size_t)co * Ci + ci) * KH + kh) * KW + kw] : 0.f;
-      } else if (jb.kind == CRNN_PACK_TRANSPOSE) {
-        const int rows = jb.a;
-        const int c = i / rows, r = i - c * rows;
-        const int sr = jb.perm ? jb.perm[r] : r;
-        v = (r < jb.b && sr >= 0) ? jb.src[(size_t)sr * jb.c + c] : 0.f;
-      } else {
-        const int cols = jb.c;
-        const int r = i / cols, c = i - r * cols;
-        const int sr = jb.perm ? jb.perm[r] : r;
-        const bool ok = r < jb.b && sr >= 0;
-        v = ok ? jb.src[(size_t)sr * cols + c] : 0.f;
-        if (jb.kind == CRNN_PACK_ROWS_SUM && ok) v += jb.src2[(size_t)sr * cols + c];
-      }
+      const float v = pack_elem<T>(jb, i);
       if (jb.out_f32) ((float*)jb.dst)[i] = v;
       else ((T*)jb.dst)[i] = fromf<T>(v);
     }
@@ -1007,7 +1116,11 @@ __global__ __launch_bounds__(256) void pack_batch_kernel(const crnn_pack_job* __
 // conv weights, one block per output channel co: the OIHW source slab [Ci][KH][KW] (contiguous) is
 // staged in LDS with coalesced reads, then written as the OHWI slab [KH][KW][Cip] (contiguous) —
 // both sides coalesced, unlike the per-element gather of pack_batch_kernel (stride KH*KW reads).
-// LDS reads at stride KH*KW words: conflict-free for 3x3 (9 is odd), 4-way at worst for 2x2.
+// A 16-B aligned slab (every conv but the 3-channel input one) is read as 16-B vectors with all of
+// a thread's loads in flight before its LDS stores (<= 5 per thread at Ci * KH * KW <= 5120), and
+// the OHWI row is written 8 channels (16 B) per store: the scalar load-store loop ran at the memory
+// latency (85 us per step for 42 M weights). LDS reads at stride KH*KW words: conflict-free for 3x3
+// (9 is odd), 4-way at worst for 2x2.
 template <typename T>
 __global__ __launch_bounds__(256) void pack_conv_kernel(const crnn_pack_job* __restrict__ jobs, int njobs) {
   extern __shared__ float slab[];
@@ -1020,18 +1133,51 @@ __global__ __launch_bounds__(256) void pack_conv_kernel(const crnn_pack_job* __r
   }
   const crnn_pack_job jb = jobs[lo];
   const int co = (int)(row - jb.start), Ci = jb.b, KHW = jb.c * jb.d, Cip = jb.e;
-  const float* src = jb.src + (size_t)co * Ci * KHW;
-  for (int i = threadIdx.x; i < Ci * KHW; i += blockDim.x) slab[i] = src[i];
+  const int n = Ci * KHW;
+  const float* src = jb.src + (size_t)co * n;
+  constexpr int PER = 5;
+  if (n % 4 == 0 && n <= 4 * 256 * PER && ((uintptr_t)src & 15) == 0) {
+    f32x4 v[PER];
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int k = threadIdx.x + 256 * u;
+      v[u] = *reinterpret_cast<const f32x4*>(src + 4 * (4 * k < n ? k : 0));   // clamped: unconditional
+    }
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int k = threadIdx.x + 256 * u;
+      if (4 * k < n) *reinterpret_cast<f32x4*>(&slab[4 * k]) = v[u];
+    }
+  } else {
+    for (int i = threadIdx.x; i < n; i += blockDim.x) slab[i] = src[i];
+  }
   __syncthreads();
   T* dst = (T*)jb.dst + (size_t)co * KHW * Cip;
-  for (int i = threadIdx.x; i < KHW * Cip; i += blockDim.x) {
-    const int t = i / Cip, ci = i - t * Cip;
-    dst[i] = fromf<T>(ci < Ci ? slab[ci * KHW + t] : 0.f);
+  if (Cip % 8 == 0) {
+    for (int i = 8 * threadIdx.x; i < KHW * Cip; i += 8 * blockDim.x) {
+      const int t = i / Cip, c0 = i - t * Cip;
+      float f[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) f[q] = c0 + q < Ci ? slab[(c0 + q) * KHW + t] : 0.f;
+      if constexpr (sizeof(T) == 2) {
+        *reinterpret_cast<bf16x8*>(dst + i) = pack8<T>(f);
+      } else {
+        *reinterpret_cast<f32x4*>(dst + i) = f32x4{f[0], f[1], f[2], f[3]};
+        *reinterpret_cast<f32x4*>(dst + i + 4) = f32x4{f[4], f[5], f[6], f[7]};
+      }
+    }
+  } else {
+    for (int i = threadIdx.x; i < KHW * Cip; i += blockDim.x) {
+      const int t = i / Cip, ci = i - t * Cip;
+      dst[i] = fromf<T>(ci < Ci ? slab[ci * KHW + t] : 0.f);
+    }
   }
 }
 
 // transposed, flipped conv kernel (crnn_conv_dgrad_tw's B operand): one workgroup per (64 co x 16 ci)
-// tile of a job. The source rows [co][ci0 .. ci0+15][KH*KW] are contiguous runs, read as 16-B vectors,
+// tile of a job. With KH = KW = 1 and a row permutation it is a plain tiled transpose of a gathered
+// matrix: the BiLSTM's W_hh'^T (perm = the gate interleave), whose per-element gather in
+// pack_batch_kernel read one source column per block (32x L2 traffic). The source rows [co][ci0 .. ci0+15][KH*KW] are contiguous runs, read as 16-B vectors,
 // all of a thread's loads in flight before its LDS stores (a load-store-load loop runs at the
 // memory latency); LDS row pitch 16*KHW + 1 words (the read-back's 64 consecutive co on distinct
 // banks); the destination rows [ci][tap'][co0 .. co0+63] are written as whole 128-B lines of
@@ -1050,7 +1196,8 @@ __device__ __forceinline__ void pack_conv_t_tile(const crnn_pack_job& jb, int tl
   for (int u = 0; u < PER; ++u) {
     const int k = threadIdx.x + 256 * u, r = k / V4, e = k - r * V4;
     const int rr = (k < NV && r < nco) ? r : 0;   // clamped: every load unconditional
-    v[u] = *reinterpret_cast<const f32x4*>(jb.src + ((size_t)(co0 + rr) * Ci + ci0) * KHW + 4 * e);
+    const int srow = jb.perm ? jb.perm[co0 + rr] : co0 + rr;   // row gather (BiLSTM gate order)
+    v[u] = *reinterpret_cast<const f32x4*>(jb.src + ((size_t)srow * Ci + ci0) * KHW + 4 * e);
   }
 #pragma unroll
   for (int u = 0; u < PER; ++u) {
@@ -1068,6 +1215,21 @@ __device__ __forceinline__ void pack_conv_t_tile(const crnn_pack_job& jb, int tl
     const int tp = rest % KHW, ci = rest / KHW;   // destination tap (flipped source tap KHW-1-tp)
     if (i < PT_CO * RUN && co < nco)
       dst[((size_t)(ci0 + ci) * KHW + tp) * Co + co0 + co] = fromf<T>(tile[co * P + ci * KHW + (KHW - 1 - tp)]);
+  }
+  if (jb.dst2) {   // the plain OHWI pack of the same tile: rows (co, tap) of 16 ci, two 8-channel pieces each
+    T* d2 = (T*)jb.dst2;
+    constexpr int NS = PT_CO * KHW * 2;
+#pragma unroll
+    for (int u = 0; u < (NS + 255) / 256; ++u) {
+      const int k = threadIdx.x + 256 * u;
+      const int hf = k & 1, rest = k >> 1, tp = rest % KHW, co = rest / KHW;
+      if (k < NS && co < nco) {
+        float f[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) f[q] = tile[co * P + (8 * hf + q) * KHW + tp];
+        st8<T>(d2 + ((size_t)(co0 + co) * KHW + tp) * Ci + ci0 + 8 * hf, pack8<T>(f));
+      }
+    }
   }
 }
 
@@ -1690,6 +1852,7 @@ int crnn_bn_act(int dtype, const void* z, const float* scale, const float* shift
 int crnn_bn_relu_maxpool(int dtype, const void* z, const float* scale, const float* shift, void* y, int B, int H,
                          int W, int C, void* stream) {
   long n = (long)B * (H / 2) * (W / 2) * (C / 8);
+  if (n >= (1L << 31)) return crnn_set_error(hipErrorInvalidValue, "bn_relu_maxpool: > 2^31 pooled 8-channel groups");
   DISPATCH(dtype, hipLaunchKernelGGL(bn_relu_maxpool_kernel<T>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream,
                                      (const T*)z, scale, shift, (T*)y, B, H, W, C));
   return (int)hipGetLastError();
@@ -1815,15 +1978,25 @@ int crnn_se_bwd_reduce(int dtype, const void* dy, const void* y, const void* z2,
 int crnn_se_mlp_bwd(const float* ds, const float* pooled, const float* hid, const float* s, const float* w1,
                     const float* w2, float* dsig, float* dhid, float* dpool, float* dw1, float* dw2, int B, int C,
                     int Cr, int HW, int accumulate, void* stream) {
+  return crnn_se_mlp_bwd_partials(ds, pooled, hid, s, w1, w2, dsig, dhid, dpool, dw1, dw2, nullptr, nullptr, nullptr,
+                                  B, C, Cr, HW, accumulate, stream);
+}
+
+int crnn_se_mlp_bwd_partials(const float* ds, const float* pooled, const float* hid, const float* s, const float* w1,
+                             const float* w2, float* dsig, float* dhid, float* dpool, float* dw1, float* dw2,
+                             const float* abc, float* pg, float* pgx, int B, int C, int Cr, int HW, int accumulate,
+                             void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if (Cr * 16 != C || (C != 256 && C != 512)) return crnn_set_error(hipErrorInvalidValue, "se_mlp: C in {256, 512}, Cr = C/16");
   const dim3 grid((B + SE_SB - 1) / SE_SB), wgrid(C / 64, Cr / 8);
   const float inv = 1.f / (float)HW;
   if (C == 256) {
-    hipLaunchKernelGGL(se_mlp_bwd_kernel<256>, grid, dim3(256), 0, st, ds, hid, s, w1, w2, dsig, dhid, dpool, B, inv);
+    hipLaunchKernelGGL(se_mlp_bwd_kernel<256>, grid, dim3(256), 0, st, ds, hid, s, w1, w2, dsig, dhid, dpool, B, inv,
+                       abc, pg, pgx, HW);
     hipLaunchKernelGGL(se_wgrad_kernel<256>, wgrid, dim3(256), 0, st, dsig, hid, dhid, pooled, dw1, dw2, B, accumulate);
   } else {
-    hipLaunchKernelGGL(se_mlp_bwd_kernel<512>, grid, dim3(256), 0, st, ds, hid, s, w1, w2, dsig, dhid, dpool, B, inv);
+    hipLaunchKernelGGL(se_mlp_bwd_kernel<512>, grid, dim3(256), 0, st, ds, hid, s, w1, w2, dsig, dhid, dpool, B, inv,
+                       abc, pg, pgx, HW);
     hipLaunchKernelGGL(se_wgrad_kernel<512>, wgrid, dim3(256), 0, st, dsig, hid, dhid, pooled, dw1, dw2, B, accumulate);
   }
   return (int)hipGetLastError();
@@ -1876,9 +2049,9 @@ int crnn_pack_batch(int dtype, const crnn_pack_job* jobs, int njobs, long total,
   if (njobs <= 0 || total <= 0) return 0;
   // ~4 elements per thread: the element loop is load-latency bound (one dependent load per
   // element, strided for the conv repack), so parallelism comes from many small blocks
-  long blocks = (total + 1023) / 1024;
+  long blocks = (total + 2047) / 2048;
   if (blocks > (1L << 20)) blocks = 1L << 20;
-  const long chunk = (total + blocks - 1) / blocks;
+  const long chunk = ((total + blocks - 1) / blocks + 7) / 8 * 8;   // whole 8-element groups per block
   DISPATCH(dtype, hipLaunchKernelGGL(pack_batch_kernel<T>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
                                      jobs, njobs, total, chunk));
   return (int)hipGetLastError();

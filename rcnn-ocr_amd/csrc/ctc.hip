@@ -22,7 +22,8 @@ __device__ __forceinline__ float lse2(float a, float b) {
 __global__ __launch_bounds__(256) void ctc_kernel(const float* __restrict__ logits, int ldc, int T, int C,
                                                   const int* __restrict__ targets, int Lmax,
                                                   const int* __restrict__ lengths, float* __restrict__ loss,
-                                                  float* __restrict__ dlogits, int zero_inf, float inv_B) {
+                                                  float* __restrict__ dlogits, int zero_inf, float inv_B,
+                                                  int stage) {
   extern __shared__ float sm[];
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nw = blockDim.x / 64;
   int L = lengths[b];
@@ -31,20 +32,41 @@ __global__ __launch_bounds__(256) void ctc_kernel(const float* __restrict__ logi
   const int S = 2 * L + 1;
   float* lse = sm;                    // [T]
   float* alpha = lse + T;             // [T][S]
-  float* bcur = alpha + (size_t)T * S;  // [S]
-  float* bnxt = bcur + S;             // [S]
-  float* grow = bnxt + S;             // [C]
-  float* evs = grow + C;              // [S] alpha*beta/p terms of the current frame
-  int* ext = (int*)(evs + S);         // [S]
+  float* beta = alpha + (size_t)T * S;  // [T][S]
+  float* grow = beta + (size_t)T * S;   // [nw][C] per-wave gradient row
+  float* evs = grow + (size_t)nw * C;   // [nw][S] per-wave alpha*beta/p terms of a frame
+  int* ext = (int*)(evs + (size_t)nw * S);  // [S]
   int* lnk = ext + S;                 // [S] next odd position with the same label | head flag
+  float* lgs = (float*)(lnk + S);     // [T][C] the sample's logits (stage != 0)
   const float* lg = logits + (size_t)b * T * ldc;
+  // stage: the sample's logits are copied to LDS once (8 loads in flight per thread), so the
+  // serial alpha / beta / gradient steps read log-probabilities from LDS; reading them from global
+  // memory put one dependent load round trip into every step (63-81 us per batch). Same values,
+  // same arithmetic: bit-identical results.
+  if (stage) {
+    const int TC = T * C;
+    for (int i0 = tid; i0 < TC; i0 += 8 * (int)blockDim.x) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = min(i0 + u * (int)blockDim.x, TC - 1);
+        const int t = i / C;
+        v[u] = lg[(size_t)t * ldc + (i - t * C)];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (i0 + u * (int)blockDim.x < TC) lgs[i0 + u * blockDim.x] = v[u];
+    }
+    __syncthreads();
+  }
+#define LG(t, c) (stage ? lgs[(size_t)(t) * C + (c)] : lg[(size_t)(t) * ldc + (c)])
 
   for (int t = wid; t < T; t += nw) {
     float m = -INFINITY;
-    for (int c = lane; c < C; c += 64) m = fmaxf(m, lg[(size_t)t * ldc + c]);
+    for (int c = lane; c < C; c += 64) m = fmaxf(m, LG(t, c));
     m = wave_max(m);
     float s = 0.f;
-    for (int c = lane; c < C; c += 64) s += __expf(lg[(size_t)t * ldc + c] - m);
+    for (int c = lane; c < C; c += 64) s += __expf(LG(t, c) - m);
     s = wave_sum(s);
     if (lane == 0) lse[t] = m + logf(s);
   }
@@ -66,16 +88,56 @@ __global__ __launch_bounds__(256) void ctc_kernel(const float* __restrict__ logi
     }
     lnk[s] = v;
   }
-#define LP(t, c) (lg[(size_t)(t) * ldc + (c)] - lse[(t)])
-  for (int s = tid; s < S; s += blockDim.x) alpha[s] = s < 2 ? LP(0, ext[s]) : -INFINITY;
-  for (int t = 1; t < T; ++t) {
-    __syncthreads();
-    for (int s = tid; s < S; s += blockDim.x) {
-      const float* ap = alpha + (size_t)(t - 1) * S;
-      float a = ap[s];
-      if (s >= 1) a = lse2(a, ap[s - 1]);
-      if (s >= 2 && ext[s] != 0 && ext[s] != ext[s - 2]) a = lse2(a, ap[s - 2]);
-      alpha[(size_t)t * S + s] = a + LP(t, ext[s]);
+#define LP(t, c) (LG(t, c) - lse[(t)])
+  // a wave's own LDS writes are seen by its later reads (in-order LDS per wave); the fence keeps
+  // the compiler from reordering them across lanes
+#define WAVE_LDS_SYNC()                                    \
+  do {                                                     \
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront"); \
+    __builtin_amdgcn_wave_barrier();                       \
+  } while (0)
+  // S <= 64 (labels up to 31): alpha on wave 0 and beta on wave 1 at the same time, each step
+  // synchronised within its wave only; longer label sets: all waves, a barrier per step
+  const bool one_wave = S <= 64;
+  if (one_wave) {
+    if (wid == 0) {
+      const int s = lane;
+      if (s < S) alpha[s] = s < 2 ? LP(0, ext[s]) : -INFINITY;
+      for (int t = 1; t < T; ++t) {
+        WAVE_LDS_SYNC();
+        if (s < S) {
+          const float* ap = alpha + (size_t)(t - 1) * S;
+          float a = ap[s];
+          if (s >= 1) a = lse2(a, ap[s - 1]);
+          if (s >= 2 && ext[s] != 0 && ext[s] != ext[s - 2]) a = lse2(a, ap[s - 2]);
+          alpha[(size_t)t * S + s] = a + LP(t, ext[s]);
+        }
+      }
+    } else if (wid == 1 && dlogits != nullptr) {
+      const int s = lane;
+      if (s < S) beta[(size_t)(T - 1) * S + s] = (s >= S - 2) ? LP(T - 1, ext[s]) : -INFINITY;
+      for (int t = T - 2; t >= 0; --t) {
+        WAVE_LDS_SYNC();
+        if (s < S) {
+          const float* bn = beta + (size_t)(t + 1) * S;
+          float v = bn[s];
+          if (s + 1 < S) v = lse2(v, bn[s + 1]);
+          if (s + 2 < S && ext[s] != 0 && ext[s] != ext[s + 2]) v = lse2(v, bn[s + 2]);
+          beta[(size_t)t * S + s] = v + LP(t, ext[s]);
+        }
+      }
+    }
+  } else {
+    for (int s = tid; s < S; s += blockDim.x) alpha[s] = s < 2 ? LP(0, ext[s]) : -INFINITY;
+    for (int t = 1; t < T; ++t) {
+      __syncthreads();
+      for (int s = tid; s < S; s += blockDim.x) {
+        const float* ap = alpha + (size_t)(t - 1) * S;
+        float a = ap[s];
+        if (s >= 1) a = lse2(a, ap[s - 1]);
+        if (s >= 2 && ext[s] != 0 && ext[s] != ext[s - 2]) a = lse2(a, ap[s - 2]);
+        alpha[(size_t)t * S + s] = a + LP(t, ext[s]);
+      }
     }
   }
   __syncthreads();
@@ -95,46 +157,55 @@ __global__ __launch_bounds__(256) void ctc_kernel(const float* __restrict__ logi
     for (int i = tid; i < T * ldc; i += blockDim.x) dl[i] = (i % ldc) < C ? fill : 0.f;
     return;
   }
-  for (int s = tid; s < S; s += blockDim.x) bnxt[s] = (s >= S - 2) ? LP(T - 1, ext[s]) : -INFINITY;
-  __syncthreads();
-  for (int t = T - 1; t >= 0; --t) {
-    // beta_t into bcur (bnxt holds beta_{t+1}; at t = T-1 it already is beta_{T-1})
-    for (int s = tid; s < S; s += blockDim.x) {
-      float v;
-      if (t == T - 1) {
-        v = bnxt[s];
-      } else {
-        v = bnxt[s];
-        if (s + 1 < S) v = lse2(v, bnxt[s + 1]);
-        if (s + 2 < S && ext[s] != 0 && ext[s] != ext[s + 2]) v = lse2(v, bnxt[s + 2]);
-        v += LP(t, ext[s]);
-      }
-      bcur[s] = v;
-      const float e = alpha[(size_t)t * S + s] + v - LP(t, ext[s]) - ll;
-      evs[s] = e > -INFINITY ? __expf(e) : 0.f;
-    }
-    for (int c = tid; c < C; c += blockDim.x) grow[c] = __expf(LP(t, c));
-    __syncthreads();
-    if (wid == 0) {   // class 0: every position whose symbol is the blank
-      float a = 0.f;
-      for (int s = lane; s < S; s += 64) a += ext[s] == 0 ? evs[s] : 0.f;
-      a = wave_sum(a);
-      if (lane == 0) grow[0] -= a;
-    }
-    for (int s = tid; s < S; s += blockDim.x) {
-      const int l = lnk[s];
-      if (l & HEAD) {
-        float a = evs[s];
-        for (int n = l & (HEAD - 1); n != 0; n = lnk[n] & (HEAD - 1)) a += evs[n];
-        grow[ext[s]] -= a;
+  // beta for every frame first (the serial part: one barrier per step), then the gradient of all
+  // frames in parallel, one frame per wave at a time: the per-frame exps, class sums and the row
+  // store used to sit inside the serial beta loop (three barriers per step). Same arithmetic and
+  // summation orders as before: bit-identical.
+  if (!one_wave) {   // (one_wave: wave 1 computed beta next to the alpha recursion)
+    for (int s = tid; s < S; s += blockDim.x)
+      beta[(size_t)(T - 1) * S + s] = (s >= S - 2) ? LP(T - 1, ext[s]) : -INFINITY;
+    for (int t = T - 2; t >= 0; --t) {
+      __syncthreads();
+      const float* bn = beta + (size_t)(t + 1) * S;
+      for (int s = tid; s < S; s += blockDim.x) {
+        float v = bn[s];
+        if (s + 1 < S) v = lse2(v, bn[s + 1]);
+        if (s + 2 < S && ext[s] != 0 && ext[s] != ext[s + 2]) v = lse2(v, bn[s + 2]);
+        beta[(size_t)t * S + s] = v + LP(t, ext[s]);
       }
     }
-    __syncthreads();
-    for (int c = tid; c < ldc; c += blockDim.x) dl[(size_t)t * ldc + c] = c < C ? grow[c] * scale : 0.f;
-    for (int s = tid; s < S; s += blockDim.x) bnxt[s] = bcur[s];
     __syncthreads();
   }
+  float* gr = grow + (size_t)wid * C;
+  float* ev = evs + (size_t)wid * S;
+  for (int t = wid; t < T; t += nw) {
+    for (int s = lane; s < S; s += 64) {
+      const float e = alpha[(size_t)t * S + s] + beta[(size_t)t * S + s] - LP(t, ext[s]) - ll;
+      ev[s] = e > -INFINITY ? __expf(e) : 0.f;
+    }
+    for (int c = lane; c < C; c += 64) gr[c] = __expf(LP(t, c));
+    WAVE_LDS_SYNC();
+    {   // class 0: every position whose symbol is the blank
+      float a = 0.f;
+      for (int s = lane; s < S; s += 64) a += ext[s] == 0 ? ev[s] : 0.f;
+      a = wave_sum(a);
+      if (lane == 0) gr[0] -= a;
+    }
+    for (int s = lane; s < S; s += 64) {
+      const int l = lnk[s];
+      if (l & HEAD) {
+        float a = ev[s];
+        for (int n = l & (HEAD - 1); n != 0; n = lnk[n] & (HEAD - 1)) a += ev[n];
+        gr[ext[s]] -= a;
+      }
+    }
+    WAVE_LDS_SYNC();
+    for (int c = lane; c < ldc; c += 64) dl[(size_t)t * ldc + c] = c < C ? gr[c] * scale : 0.f;
+    WAVE_LDS_SYNC();
+  }
+#undef WAVE_LDS_SYNC
 #undef LP
+#undef LG
 }
 
 __global__ void ctc_mean_kernel(const float* loss, const int* lengths, int B, float* out) {
@@ -299,15 +370,20 @@ extern "C" {
 int crnn_ctc_loss(const float* logits, int ldc, int B, int T, int C, const int* targets, int Lmax, const int* lengths,
                   float* loss, float* dlogits, int zero_inf, void* stream) {
   const int S = 2 * Lmax + 1;
-  size_t sm = ((size_t)T + (size_t)T * S + 3 * S + C) * sizeof(float) + 2 * S * sizeof(int);
+  constexpr int NW = 4;   // waves of the 256-thread workgroup
+  size_t sm = ((size_t)T + 2 * (size_t)T * S + NW * (size_t)(S + C)) * sizeof(float) + 2 * S * sizeof(int);
   if (sm > 160 * 1024) return crnn_set_error(hipErrorInvalidValue, "ctc_loss: T x (2*Lmax+1) too large for LDS");
+  // the sample's logits staged in LDS when they fit next to alpha (all the bench configs do)
+  const size_t staged = (size_t)T * C * sizeof(float);
+  const int stage = sm + staged <= 160 * 1024 ? 1 : 0;
+  if (stage) sm += staged;
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)ctc_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
   hipLaunchKernelGGL(ctc_kernel, dim3(B), dim3(256), sm, (hipStream_t)stream, logits, ldc, T, C, targets, Lmax, lengths,
-                     loss, dlogits, zero_inf, 1.f / (float)B);
+                     loss, dlogits, zero_inf, 1.f / (float)B, stage);
   return (int)hipGetLastError();
 }
 

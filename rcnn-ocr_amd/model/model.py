@@ -65,7 +65,9 @@ class _EncodeFn(torch.autograd.Function):
         eng.check_generation(ctx.gen)
         B, T, C = grad_logits.shape
         dl = eng.ws.get("autograd.dlogits", (B, T, eng.Cpad), torch.float32)
-        dl[:, :, C:].zero_()
+        if getattr(eng, "_dl_pad_ptr", None) != dl.data_ptr():   # pad columns: zeroed once per buffer
+            dl[:, :, C:].zero_()
+            eng._dl_pad_ptr = dl.data_ptr()
         dl[:, :, :C].copy_(grad_logits)
         grads, accumulate, attach = model._grad_views()
         eng.backward(dl, grads, accumulate=accumulate, stage_done=model.stage_done)

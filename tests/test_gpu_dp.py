@@ -74,13 +74,27 @@ def _worker(rank, world, port, q):
         ctc_loss(m(x), tg, tl).backward()
         red.finish()
         torch.cuda.synchronize()
-        got = m._flat_grad.detach().cpu()
+        got = m._flat_grad.detach().cpu().clone()
+        if os.environ.get("CRNN_DP_DIAG") == "1":   # a third, unhooked backward: local determinism under load
+            m.stage_done = None
+            opt.zero_grad()
+            ctc_loss(m(x), tg, tl).backward()
+            torch.cuda.synchronize()
+            loc = m._flat_grad.detach().cpu().clone()
+            dist.all_reduce(loc)
+            print(f"rank {rank}: 3rd backward vs 1st (both summed over ranks): max |diff| "
+                  f"{float((loc - want).abs().max()):.3e}; DP-reduced vs 1st {float((got - want).abs().max()):.3e}",
+                  flush=True)
         ok_seq = seq == CRNNEngine.backward_stages()
         spans = sorted(red.last_issued)
         n = m._flat_grad.numel()
         ok_tile = (len(spans) > 1 and spans[0][0] == 0 and spans[-1][1] == n
                    and all(a[1] == b[0] for a, b in zip(spans, spans[1:])))
         err = float((got - want).abs().max() / (want.abs().max() + 1e-30))
+        worst = sorted(((float((got[a:a + k] - want[a:a + k]).abs().max()), n)
+                        for n, (a, k) in m.flat_offsets().items()), reverse=True)[:4]
+        if err >= 1e-5:
+            print(f"rank {rank}: largest per-parameter differences {worst}", flush=True)
         opt.step(grad_scale=1.0 / world)
         torch.cuda.synchronize()
         c = m._flat_param.detach().double().sum().reshape(1).cpu()

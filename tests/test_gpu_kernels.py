@@ -1418,7 +1418,29 @@ def test_weight_pack_layouts(dtype):
         want[..., :cs.ci_real] = w.permute(0, 2, 3, 1)
         assert torch.equal(eng.packed[cs.name], want.to(dtype)), cs.name
         n += 1
+        wt = eng.packed.get(cs.name + ".t")   # crnn_conv_dgrad_tw's transposed, flipped kernel
+        if wt is not None:
+            assert torch.equal(wt, w.flip(2, 3).permute(1, 2, 3, 0).to(dtype)), cs.name + ".t"
     assert n == 28
+    # crnn_pack_batch: BiLSTM weights gate-interleaved (row 4j+q = reference row q*H+j), W_hh^T, the
+    # summed biases (fp32), the projection and the zero-padded CTC head
+    from crnn_hip.engine import gate_perm
+    H = 256
+    perm = torch.tensor(gate_perm(H), device=DEV)
+    for l in range(2):
+        pre = f"enc_rnn.{l}"
+        for d, sfx in enumerate(["", "_reverse"]):
+            r = pre + ".rnn."
+            wih, whh = eng.p[r + "weight_ih_l0" + sfx].detach(), eng.p[r + "weight_hh_l0" + sfx].detach()
+            assert torch.equal(eng.packed[pre + ".wih"][d], wih[perm].to(dtype))
+            assert torch.equal(eng.packed[pre + ".whh"][d], whh[perm].to(dtype))
+            assert torch.equal(eng.packed[pre + ".whh_t"][d], whh[perm].t().to(dtype))
+            b = (eng.p[r + "bias_ih_l0" + sfx].detach() + eng.p[r + "bias_hh_l0" + sfx].detach())[perm]
+            assert torch.equal(eng.packed[pre + ".bias"][d], b)
+        assert torch.equal(eng.packed[pre + ".lin"], eng.p[pre + ".linear.weight"].detach().to(dtype))
+    hw, hb = eng.packed["head.w"], eng.packed["head.b"]
+    assert torch.equal(hw[:194], eng.p["ctc_head.weight"].detach().to(dtype)) and not hw[194:].any()
+    assert torch.equal(hb[:194], eng.p["ctc_head.bias"].detach()) and not hb[194:].any()
 
 
 @pytest.mark.parametrize("BTH", [(256, 32, 512), (64, 20, 768), (32, 7, 256), (128, 9, 512), (16, 1, 256),

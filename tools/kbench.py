@@ -41,12 +41,16 @@ def main():
     ap.add_argument("--only", default=None)
     ap.add_argument("--layer", type=int, default=None)
     ap.add_argument("--opt", default=None, help="A/B a crnn_set_option key: KEY=V0,V1 (e.g. 0=0,1)")
+    ap.add_argument("--set", action="append", default=[], help="fixed crnn_set_option KEY=V for every variant")
     a = ap.parse_args()
     dev = torch.device("cuda")
     T = torch.bfloat16
     s = L.stream_ptr()
     tot = {}
     key, variants = None, [("", None)]
+    for kv in a.set:
+        k_, v_ = kv.split("=")
+        L.call("crnn_set_option", int(k_), int(v_))
     if a.opt:
         ks, vs = a.opt.split("=")
         key = int(ks)

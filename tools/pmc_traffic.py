@@ -17,8 +17,10 @@ def kind(name):
         return "lstm_fwd"
     if "lstm_seq_bwd" in name:
         return "lstm_bwd"
-    if ("gemm" in name and CONV.search(name)) or "halo3x3" in name:
+    if ("gemm" in name and CONV.search(name)) or "halo3x3" in name or "dgrad_cls_group" in name:
         return "conv"
+    if "wgrad_reduce" in name:   # the split-K slab reduce: part of its wgrad launch (bench.py times both)
+        return "conv_aux"
     return None
 
 
@@ -53,6 +55,10 @@ def main(p_fetch, p_write, p_mfma):
         if k:
             acc[k]["mfma_busy"] += cs.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0)
             acc[k]["gui_active"] += cs.get("GRBM_GUI_ACTIVE", 0.0)
+    aux = acc.pop("conv_aux", None)
+    if aux is not None and "conv" in acc:   # per conv launch as bench.py counts them (reduce included)
+        for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+            acc["conv"][ctr] += aux[ctr]
     for k, a in acc.items():
         n = max(1.0, a["n_FETCH_SIZE"])
         fetch = a["FETCH_SIZE"] / n
