@@ -36,12 +36,18 @@ def main():
             ctc_loss(m(x), tg, tl).backward()
             torch.cuda.synchronize()
             g = {k: p.grad.detach().clone() for k, p in m.named_parameters()}
+            # every engine workspace buffer's final state too: the first producer that differs
+            g.update({"ws:" + k: v.detach().clone() for k, v in m._engine.ws.bufs.items()
+                      if v.is_floating_point() and not k.startswith("rnn.seq_ws")})
             if ref is None:
                 ref = g
                 continue
-            bad = sorted(((float((g[k] - ref[k]).abs().max()), k) for k in g if not torch.equal(g[k], ref[k])),
-                         reverse=True)
-            print(f"step {i}: {len(bad)} parameters differ from step 0 {bad[:5]}", flush=True)
+            bad = sorted(((float((g[k].float() - ref[k].float()).abs().max()), k) for k in g
+                          if g[k].shape == ref[k].shape and not torch.equal(g[k], ref[k])), reverse=True)
+            wsb = [b for b in bad if b[1].startswith("ws:")]
+            pb = [b for b in bad if not b[1].startswith("ws:")]
+            print(f"step {i}: {len(pb)} parameters differ from step 0 {pb[:4]}; workspace buffers {wsb[:8]}",
+                  flush=True)
     finally:
         load.kill()
         load.wait()
