@@ -97,6 +97,18 @@ int crnn_cast_f32(int dtype, const float* src, void* dst, long n, void* stream);
  * function of (seed, i) only, so the backward is the same call on dy with the same seed. Not
  * torch's Philox stream: masks agree in distribution, not bit for bit. p in [0, 1). */
 int crnn_dropout(int dtype, const void* x, void* y, long n, float p, unsigned long long seed, void* stream);
+/* DropBlock2d, training mode (replaces torchvision.ops.DropBlock2d as SEBasicBlock uses it,
+   model/seresnet31.py:49-53 and :62; identity in eval or at p == 0, decided by the caller).
+   crnn_dropblock_mask: keep u8 [B][H][W][C] (1 = kept) and *kept = number of kept elements
+   (zeroed by the call); bs = min(block_size, H, W) must be odd (torchvision's mask for an even bs
+   is (H+2) x (W+2) and the reference's multiply raises) and gamma = p*H*W / (bs^2 (H-bs+1)(W-bs+1))
+   <= 1 (bernoulli_'s range). Seeds: drop_hash(seed, ((n*C + c)*(H-bs+1) + i)*(W-bs+1) + j) <
+   gamma * 2^32 (not torch's Philox stream; oracle dropblock_keep restates it).
+   crnn_dropblock_apply: y = x * keep * n / (1e-6 + *kept) (in place allowed; n % 8 == 0). */
+int crnn_dropblock_mask(unsigned char* keep, unsigned long long* kept, int B, int H, int W, int C, float p,
+                        int block_size, unsigned long long seed, void* stream);
+int crnn_dropblock_apply(int dtype, const void* x, void* y, const unsigned char* keep,
+                         const unsigned long long* kept, long n, void* stream);
 /* conv weight OIHW fp32 -> OHWI dtype with Ci zero-padded to Cip. */
 int crnn_pack_conv_weight(int dtype, const float* w, void* out, int Co, int Ci, int KH, int KW, int Cip, void* stream);
 /* row gather + cast: out[r][c] = src[perm[r]][c] (perm == NULL: identity), rows >= rows_src are zero.
@@ -286,6 +298,11 @@ int crnn_se_pool_mlp_fwd(const float* psum, int rows, long rows_per_partial, con
 /* y = relu((z2*scale+shift)*s[b][c] + idn'), idn' = idn*iscale+ishift if iscale else idn */
 int crnn_se_residual_fwd(int dtype, const void* z2, const float* scale, const float* shift, const float* s,
                          const void* idn, const float* iscale, const float* ishift, void* y, int B, int HW, int C, void* stream);
+/* crnn_se_residual_fwd with the block's DropBlock2d (model/seresnet31.py:61-62) between the SE gate
+   and the residual add: y = relu((z2*scale+shift) * s * keep * B*HW*C / (1e-6 + *kept) + idn'). */
+int crnn_se_residual_drop_fwd(int dtype, const void* z2, const float* scale, const float* shift, const float* s,
+                              const void* idn, const float* iscale, const float* ishift, void* y, int B, int HW,
+                              int C, const unsigned char* keep, const unsigned long long* kept, void* stream);
 /* ds[b][c] = sum_hw dy*(y>0)*(z2*scale+shift) */
 int crnn_se_bwd_reduce(int dtype, const void* dy, const void* y, const void* z2, const float* scale, const float* shift,
                        float* ds, int B, int HW, int C, void* stream);

@@ -112,12 +112,16 @@ def se_layer(x, p, prefix, ctx: Optional[Ctx] = None):
 
 
 def se_block(x, p, prefix, stride, has_ds, ctx):
-    """SEBasicBlock.forward, model/seresnet31.py:55-67 (dropblock = Identity at p=0)."""
+    """SEBasicBlock.forward, model/seresnet31.py:55-67 (dropblock: identity at p=0, else the
+    multiplier forced under "<prefix>.dropblock", see dropblock_keep)."""
     out = F.conv2d(x, p[prefix + ".conv1.weight"], stride=stride, padding=1)
     out = ctx.store(relu(ctx, prefix + ".bn1", batchnorm(out, p, prefix + ".bn1", ctx)))
     out = F.conv2d(out, p[prefix + ".conv2.weight"], stride=1, padding=1)
     out = batchnorm(out, p, prefix + ".bn2", ctx)
     out = se_layer(out, p, prefix + ".se", ctx)
+    drop = ctx.force.get(prefix + ".dropblock")   # DropBlock2d (:62) as keep * scale, dropblock_mult
+    if drop is not None:
+        out = out * drop.to(out.dtype)
     if has_ds:
         idn = F.conv2d(x, p[prefix + ".downsample.0.weight"], stride=stride)
         idn = batchnorm(idn, p, prefix + ".downsample.1", ctx)
@@ -291,6 +295,42 @@ def drop_keep_mask(seed: int, n: int, p: float) -> np.ndarray:
     t = p * 4294967296.0
     thr = 0xFFFFFFFF if t >= 4294967295.0 else int(t)
     return (h >= np.uint64(thr)).astype(np.float64) / (1.0 - p)
+
+
+def _splitmix_hash(seed: int, idx: np.ndarray) -> np.ndarray:
+    """csrc/common.hpp drop_hash: splitmix64's finalizer on seed ^ idx * golden, high 32 bits."""
+    with np.errstate(over="ignore"):
+        z = np.uint64(seed & 0xFFFFFFFFFFFFFFFF) ^ (idx.astype(np.uint64) * np.uint64(0x9E3779B97F4A7C15))
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return (z ^ (z >> np.uint64(31))) >> np.uint64(32)
+
+
+def dropblock_keep(seed: int, B: int, C: int, H: int, W: int, p: float, block_size: int) -> np.ndarray:
+    """torchvision.ops.drop_block2d (training) as SEBasicBlock applies it (model/seresnet31.py:49-53,
+    62), with the HIP path's seed draw -> keep [B, C, H, W] uint8 (1 = kept). The published algorithm:
+    bs = min(block_size, H, W); gamma = p*H*W / (bs^2 (H-bs+1)(W-bs+1)); seeds ~ Bernoulli(gamma) on
+    [B, C, H-bs+1, W-bs+1]; pad by bs//2; bs x bs stride-1 max-pool with padding bs//2; keep =
+    1 - pooled. Seed (n, c, i, j) = 1 iff drop_hash(seed, flat NCHW index) < gamma * 2^32 (torch's
+    Philox stream is not reproduced: masks agree in distribution, parity is checked against this)."""
+    bs = min(block_size, H, W)
+    if bs % 2 == 0:
+        raise ValueError("drop_block2d: the mask of an even block is (H+2) x (W+2) and does not broadcast")
+    Hs, Ws = H - bs + 1, W - bs + 1
+    gamma = p * H * W / (bs * bs * Hs * Ws)
+    t = gamma * 4294967296.0
+    thr = 0xFFFFFFFF if t >= 4294967295.0 else int(t)
+    seeds = (_splitmix_hash(seed, np.arange(B * C * Hs * Ws)) < np.uint64(thr)).astype(np.float32)
+    noise = F.pad(torch.from_numpy(seeds.reshape(B, C, Hs, Ws)), [bs // 2] * 4, value=0.0)
+    noise = F.max_pool2d(noise, stride=(1, 1), kernel_size=(bs, bs), padding=bs // 2)
+    return (1.0 - noise).numpy().astype(np.uint8)
+
+
+def dropblock_mult(keep: np.ndarray) -> torch.Tensor:
+    """keep * numel / (1e-6 + kept) in fp32 (drop_block2d's normalize_scale)"""
+    k = torch.from_numpy(keep.astype(np.float32))
+    scale = np.float32(k.numel()) / (np.float32(1e-6) + np.float32(int(keep.sum())))
+    return k * float(scale)
 
 
 def attn_drop_masks(seed: int, steps: int, B: int, T: int, p: float):

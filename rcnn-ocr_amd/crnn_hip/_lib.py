@@ -63,6 +63,8 @@ _SIGS = {
     "crnn_nchw_to_nhwc": ([i32, vp, vp, i32, i32, i32, i32, i32, vp], i32),
     "crnn_cast_f32": ([i32, vp, vp, i64, vp], i32),
     "crnn_dropout": ([i32, vp, vp, i64, f32, C.c_ulonglong, vp], i32),
+    "crnn_dropblock_mask": ([vp, vp, i32, i32, i32, i32, f32, i32, C.c_ulonglong, vp], i32),
+    "crnn_dropblock_apply": ([i32, vp, vp, vp, vp, i64, vp], i32),
     "crnn_pack_conv_weight": ([i32, vp, vp, i32, i32, i32, i32, i32, vp], i32),
     "crnn_pack_rows": ([i32, vp, vp, vp, i32, i32, i32, vp], i32),
     "crnn_conv_fwd": ([i32, C.POINTER(ConvDesc), vp, vp, vp, vp, vp, vp], i32),
@@ -102,6 +104,7 @@ _SIGS = {
     "crnn_se_mlp_fwd": ([vp, vp, vp, vp, vp, i32, i32, i32, vp], i32),
     "crnn_se_pool_mlp_fwd": ([vp, i32, i64, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, vp], i32),
     "crnn_se_residual_fwd": ([i32, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, vp], i32),
+    "crnn_se_residual_drop_fwd": ([i32, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, vp, vp, vp], i32),
     "crnn_se_bwd_reduce": ([i32, vp, vp, vp, vp, vp, vp, i32, i32, i32, vp], i32),
     "crnn_se_mlp_bwd": ([vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, vp], i32),
     "crnn_se_mlp_bwd_partials": ([vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, vp],

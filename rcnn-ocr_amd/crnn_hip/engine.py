@@ -575,11 +575,15 @@ class CRNNEngine:
 
     # ------------------------------------------------------------------ forward
     def forward(self, images: torch.Tensor, train: bool, update_running: bool = True,
-                save_for_backward: bool = False, dropout_p: float = 0.0) -> torch.Tensor:
+                save_for_backward: bool = False, dropout_p: float = 0.0, dropblock_p: float = 0.0,
+                dropblock_block_size: int = 5) -> torch.Tensor:
         """images [B,3,H,W] fp32 (reference NCHW input), or the encoder layout [B,H,W,8] in the
         compute dtype (crnn_hip.preprocess out="encoder") -> logits [B,T,C] fp32 (view).
         dropout_p: enc_dropout probability applied to the encoder output in training
-        (model/model.py:201,220); counter-based mask, regenerated in backward (crnn_dropout)."""
+        (model/model.py:201,220); counter-based mask, regenerated in backward (crnn_dropout).
+        dropblock_p / dropblock_block_size: every SE block's DropBlock2d in training
+        (model/seresnet31.py:49-53,62); keep bytes per block (crnn_dropblock_mask), applied inside
+        the SE-residual kernel and to the SE side of the block's gradient in backward."""
         L.require_device(images)
         self.pack()
         self.update_running = update_running
@@ -668,11 +672,24 @@ class CRNNEngine:
             else:
                 idn, isc, ish = x, None, None
             y = ws.get(tag + ".y", (B, ho, wo, P), T)
-            call("crnn_se_residual_fwd", dt, ptr(z2), ptr(bs2), ptr(bh2), ptr(se), ptr(idn), ptr(isc), ptr(ish),
-                 ptr(y), B, HW, P, s)
+            drop = None
+            if train and dropblock_p > 0.0:
+                # DropBlock2d between the SE gate and the residual add (model/seresnet31.py:61-62)
+                seed = ((self._drop_seed ^ 0xD1B54A32D192ED03)
+                        + 0x9E3779B97F4A7C15 * (self._drop_calls * 64 + bi + 1)) & 0xFFFFFFFFFFFFFFFF
+                keep = ws.get(tag + ".keep", (B, ho, wo, P), torch.uint8)
+                kept = ws.get(tag + ".kept", (1,), torch.int64)
+                call("crnn_dropblock_mask", ptr(keep), ptr(kept), B, ho, wo, P, float(dropblock_p),
+                     int(dropblock_block_size), seed, s)
+                call("crnn_se_residual_drop_fwd", dt, ptr(z2), ptr(bs2), ptr(bh2), ptr(se), ptr(idn), ptr(isc),
+                     ptr(ish), ptr(y), B, HW, P, ptr(keep), ptr(kept), s)
+                drop = dict(keep=keep, kept=kept, seed=seed)
+            else:
+                call("crnn_se_residual_fwd", dt, ptr(z2), ptr(bs2), ptr(bh2), ptr(se), ptr(idn), ptr(isc), ptr(ish),
+                     ptr(y), B, HW, P, s)
             blk_saved.append(dict(x=x, h=h, w=w, ho=ho, wo=wo, z1=z1b, m1=bm1, i1=bi1, sc1=bs1, sh1=bh1, a1=a1,
                                   z2=z2, m2=bm2, i2=bi2, sc2=bs2, sh2=bh2, pooled=pooled, hid=hid, s=se, ds=dsv,
-                                  y=y))
+                                  y=y, drop=drop))
             x, h, w = y, ho, wo
         sv["blocks"] = blk_saved
         # conv_out (model/seresnet31.py:129-136) + height collapse (model/model.py:191,216-218)
@@ -1080,11 +1097,18 @@ class CRNNEngine:
             dyb = bufs[cur][: Mo * P]
             if self.debug:
                 self.dbg[f"dy.b{bi}"] = dyb.clone().view(B, ho, wo, P)
+            # the SE side's gradient: through the block's DropBlock2d when it ran (the residual side
+            # below keeps dyb: the mask sits before the add, model/seresnet31.py:62-66)
+            dyse = dyb
+            if sb["drop"] is not None:
+                dyse = ws.get(f"dropblock.dy.{Mo * P}", (Mo * P,), dyb.dtype)
+                call("crnn_dropblock_apply", dt, ptr(dyb), ptr(dyse), ptr(sb["drop"]["keep"]),
+                     ptr(sb["drop"]["kept"]), Mo * P, s)
             ds = ws.get(f"se.ds{P}", (B, P), torch.float32)
             abc = ws.get(f"se.abc{P}", (B, 3, P), torch.float32)
             bn2 = blk.conv2.bn
             # one pass over (dy, y, z2) for the SE gate gradient AND the BN2 sums (crnn_hip.h)
-            call("crnn_se_bn_bwd_reduce", dt, ptr(dyb), ptr(sb["y"]), ptr(sb["z2"]), ptr(sb["m2"]), ptr(sb["i2"]),
+            call("crnn_se_bn_bwd_reduce", dt, ptr(dyse), ptr(sb["y"]), ptr(sb["z2"]), ptr(sb["m2"]), ptr(sb["i2"]),
                  ptr(self.p[bn2 + ".weight"]), ptr(self.p[bn2 + ".bias"]), ptr(ds), ptr(abc), B, HW, P, s)
             dsig = ws.get(f"se.dsig{P}", (B, P), torch.float32)
             dhid = ws.get(f"se.dhid{P}", (B, Cr), torch.float32)
@@ -1098,7 +1122,7 @@ class CRNNEngine:
                  ptr(self._gview(blk.prefix + ".se.fc.2.weight")), ptr(abc), ptr(pg2), ptr(pgx2), B, P, Cr, HW, acc,
                  s)
             dz2 = self._dz(f"b{bi}.c2", bufs[o1], Mo * P)
-            self._bn_bwd(3, dyb, sb["z2"], (sb["m2"], sb["i2"], sb["sc2"], sb["sh2"]), blk.conv2.bn, Mo, P, HW=HW,
+            self._bn_bwd(3, dyse, sb["z2"], (sb["m2"], sb["i2"], sb["sc2"], sb["sh2"]), blk.conv2.bn, Mo, P, HW=HW,
                          y=sb["y"], se=sb["s"], dpool=dpool, out=dz2, accumulate_params=accumulate,
                          sums=(pg2, pgx2, B))
             self._wgrad(blk.conv2, dz2, sb["a1"], B, ho, wo)

@@ -1263,6 +1263,63 @@ __global__ void dropout_kernel(const T* __restrict__ x, T* __restrict__ y, long 
     y[i] = fromf<T>(drop_hash(seed, (unsigned long long)i) >= thr ? tof(x[i]) * scale : 0.f);
 }
 
+// ------------------------------------------------------------ DropBlock2d (model/seresnet31.py:49-53,62)
+// torchvision.ops.drop_block2d in training mode, restated: bs = min(block_size, H, W); the seeds of
+// each (n, c) plane live on the (H-bs+1) x (W-bs+1) grid and are Bernoulli(gamma) with gamma =
+// p*H*W / (bs^2 (H-bs+1)(W-bs+1)); a seed at (i, j) zeroes rows i..i+bs-1, cols j..j+bs-1 (the
+// padded bs x bs stride-1 max-pool of the seed map); the kept elements are scaled by numel /
+// (1e-6 + kept). Seed (n, c, i, j) is drawn as drop_hash(seed, ((n*C + c)*Hs + i)*Ws + j) < thr:
+// counter based, so the backward reuses the stored keep bytes and a test regenerates the mask
+// (oracle: dropblock_keep); torch's Philox stream is not reproduced.
+// Thread = (pixel, 8-channel group) of the NHWC map; keep is u8 [B][H][W][C]; *kept counts the
+// kept elements (an integer sum: the total does not depend on the order of the adds).
+__global__ __launch_bounds__(256) void dropblock_mask_kernel(uint8_t* __restrict__ keep,
+                                                             unsigned long long* __restrict__ kept, int H, int W, int C,
+                                                             int bs, uint32_t thr, unsigned long long seed,
+                                                             long total8) {
+  const int C8 = C >> 3, Hs = H - bs + 1, Ws = W - bs + 1;
+  unsigned int nk = 0;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total8; e += (long)gridDim.x * blockDim.x) {
+    const long pix = e / C8;
+    const int c0 = (int)(e - pix * C8) * 8;
+    const int w = (int)(pix % W);
+    const long nh = pix / W;
+    const int h = (int)(nh % H);
+    const long n = nh / H;
+    const int i0 = max(0, h - bs + 1), i1 = min(h, Hs - 1), j0 = max(0, w - bs + 1), j1 = min(w, Ws - 1);
+    uint64_t kb = 0;
+    for (int k = 0; k < 8; ++k) {
+      const unsigned long long plane = (unsigned long long)(n * C + c0 + k) * Hs;
+      bool drop = false;
+      for (int i = i0; i <= i1 && !drop; ++i)
+        for (int j = j0; j <= j1 && !drop; ++j) drop = drop_hash(seed, (plane + i) * Ws + j) < thr;
+      if (!drop) {
+        kb |= 1ull << (8 * k);
+        ++nk;
+      }
+    }
+    *reinterpret_cast<uint64_t*>(keep + e * 8) = kb;
+  }
+  for (int off = 32; off > 0; off >>= 1) nk += __shfl_xor(nk, off);
+  if ((threadIdx.x & 63) == 0 && nk) atomicAdd(kept, (unsigned long long)nk);
+}
+
+// y = x * keep * numel / (1e-6 + kept), 8 elements per thread (the backward's SE-side gradient)
+template <typename T>
+__global__ __launch_bounds__(256) void dropblock_apply_kernel(const T* __restrict__ x, T* __restrict__ y,
+                                                              const uint8_t* __restrict__ keep,
+                                                              const unsigned long long* __restrict__ kept, long n8) {
+  const float scale = (float)(n8 * 8) / (1e-6f + (float)*kept);
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n8; e += (long)gridDim.x * blockDim.x) {
+    const uint64_t kb = *reinterpret_cast<const uint64_t*>(keep + e * 8);
+    float v[8];
+    unpack8<T>(ld8<T>(x + e * 8), v);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = ((kb >> (8 * i)) & 0xff) ? v[i] * scale : 0.f;
+    st8<T>(y + e * 8, pack8<T>(v));
+  }
+}
+
 // ------------------------------------------------------------ row-streaming elementwise kernels
 // Thread = (8-channel group c8, row lane r): the group is fixed for the thread's lifetime so
 // per-channel coefficients live in registers; a block streams a contiguous chunk of rows
@@ -1543,14 +1600,20 @@ __global__ __launch_bounds__(NT) void bnb_apply_kernel(crnn_bn_bwd_desc d, FastD
   }
 }
 
-template <typename T>
+// DROP: the block's DropBlock2d between the SE gate and the residual add (model/seresnet31.py:61-62):
+// the SE output is multiplied by keep * numel / (1e-6 + kept) (dropblock_mask_kernel below).
+template <typename T, bool DROP>
 __global__ __launch_bounds__(NT) void se_residual2_kernel(const T* __restrict__ z, const float* __restrict__ scp,
                                                           const float* __restrict__ shp, const float* __restrict__ s,
                                                           const T* __restrict__ idn, const float* __restrict__ iscp,
                                                           const float* __restrict__ ishp, T* __restrict__ y, long M,
-                                                          int C, FastDiv dHW, long rpb) {
+                                                          int C, FastDiv dHW, long rpb,
+                                                          const uint8_t* __restrict__ keep,
+                                                          const unsigned long long* __restrict__ kept) {
   const RowMap q = rowmap(C);
   float sc[8], sh[8], isc[8], ish[8], s8[8];
+  float dscale = 1.f;
+  if constexpr (DROP) dscale = (float)(M * C) / (1e-6f + (float)*kept);
   ld8f(scp + q.c8, sc);
   ld8f(shp + q.c8, sh);
   if (iscp) {
@@ -1575,8 +1638,16 @@ __global__ __launch_bounds__(NT) void se_residual2_kernel(const T* __restrict__ 
     float v[8], dd[8];
     unpack8<T>(ld8<T>(z + o), v);
     unpack8<T>(ld8<T>(idn + o), dd);
+    float km[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] = fmaxf((v[i] * sc[i] + sh[i]) * s8[i] + dd[i] * isc[i] + ish[i], 0.f);
+    for (int i = 0; i < 8; ++i) km[i] = s8[i];
+    if constexpr (DROP) {
+      const uint64_t kb = *reinterpret_cast<const uint64_t*>(keep + o);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) km[i] = ((kb >> (8 * i)) & 0xff) ? s8[i] * dscale : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = fmaxf((v[i] * sc[i] + sh[i]) * km[i] + dd[i] * isc[i] + ish[i], 0.f);
     st8<T>(y + o, pack8<T>(v));
   }
 }
@@ -1961,8 +2032,54 @@ int crnn_se_residual_fwd(int dtype, const void* z2, const float* scale, const fl
   int nb;
   long rpb;
   stream_grid(M, C, &nb, &rpb);
-  DISPATCH(dtype, hipLaunchKernelGGL(se_residual2_kernel<T>, dim3(nb), dim3(NT), 0, (hipStream_t)stream, (const T*)z2,
-                                     scale, shift, s, (const T*)idn, iscale, ishift, (T*)y, M, C, FastDiv(HW), rpb));
+  DISPATCH(dtype, hipLaunchKernelGGL((se_residual2_kernel<T, false>), dim3(nb), dim3(NT), 0, (hipStream_t)stream,
+                                     (const T*)z2, scale, shift, s, (const T*)idn, iscale, ishift, (T*)y, M, C,
+                                     FastDiv(HW), rpb, nullptr, nullptr));
+  return (int)hipGetLastError();
+}
+
+int crnn_se_residual_drop_fwd(int dtype, const void* z2, const float* scale, const float* shift, const float* s,
+                              const void* idn, const float* iscale, const float* ishift, void* y, int B, int HW,
+                              int C, const unsigned char* keep, const unsigned long long* kept, void* stream) {
+  if (!rowmap_ok(C)) return crnn_set_error(hipErrorInvalidValue, "se_residual: C/8 must divide 256");
+  if (!keep || !kept) return crnn_set_error(hipErrorInvalidValue, "se_residual_drop: keep / kept missing");
+  const long M = (long)B * HW;
+  int nb;
+  long rpb;
+  stream_grid(M, C, &nb, &rpb);
+  DISPATCH(dtype, hipLaunchKernelGGL((se_residual2_kernel<T, true>), dim3(nb), dim3(NT), 0, (hipStream_t)stream,
+                                     (const T*)z2, scale, shift, s, (const T*)idn, iscale, ishift, (T*)y, M, C,
+                                     FastDiv(HW), rpb, keep, kept));
+  return (int)hipGetLastError();
+}
+
+int crnn_dropblock_mask(unsigned char* keep, unsigned long long* kept, int B, int H, int W, int C, float p,
+                        int block_size, unsigned long long seed, void* stream) {
+  if (B <= 0 || H <= 0 || W <= 0 || C <= 0 || C % 8)
+    return crnn_set_error(hipErrorInvalidValue, "dropblock_mask: B, H, W > 0 and C % 8 == 0 required");
+  if (!(p >= 0.f && p <= 1.f)) return crnn_set_error(hipErrorInvalidValue, "dropblock_mask: p must be in [0, 1]");
+  const int hw = H < W ? H : W, bs = block_size < hw ? block_size : hw;
+  if (bs < 1 || bs % 2 == 0)
+    return crnn_set_error(hipErrorInvalidValue,
+                          "dropblock_mask: min(block_size, H, W) must be odd (drop_block2d's mask is "
+                          "(H+2) x (W+2) for an even block and does not broadcast against the input)");
+  const double gamma = (double)p * H * W / ((double)bs * bs * (double)(H - bs + 1) * (W - bs + 1));
+  if (gamma > 1.0) return crnn_set_error(hipErrorInvalidValue, "dropblock_mask: Bernoulli rate above 1");
+  const double t = gamma * 4294967296.0;
+  const uint32_t thr = t >= 4294967295.0 ? 0xffffffffu : (uint32_t)t;
+  hipError_t e = hipMemsetAsync(kept, 0, sizeof(unsigned long long), (hipStream_t)stream);
+  if (e != hipSuccess) return crnn_set_error(e, "dropblock_mask: memset");
+  const long total8 = (long)B * H * W * (C / 8);
+  hipLaunchKernelGGL(dropblock_mask_kernel, dim3(grid_for(total8)), dim3(256), 0, (hipStream_t)stream, keep, kept,
+                     H, W, C, bs, thr, seed, total8);
+  return (int)hipGetLastError();
+}
+
+int crnn_dropblock_apply(int dtype, const void* x, void* y, const unsigned char* keep,
+                         const unsigned long long* kept, long n, void* stream) {
+  if (n % 8) return crnn_set_error(hipErrorInvalidValue, "dropblock_apply: n % 8 != 0");
+  DISPATCH(dtype, hipLaunchKernelGGL(dropblock_apply_kernel<T>, dim3(grid_for(n / 8)), dim3(256), 0,
+                                     (hipStream_t)stream, (const T*)x, (T*)y, keep, kept, n / 8));
   return (int)hipGetLastError();
 }
 

@@ -23,7 +23,7 @@ import torch.nn as nn
 
 from crnn_hip import _lib as L
 from crnn_hip.engine import CRNNEngine, round8
-from model.seresnet31 import SEResNet31
+from model.seresnet31 import DropBlock2d, SEResNet31
 
 
 class BidirectionalLSTM(nn.Module):
@@ -52,8 +52,7 @@ class _EncodeFn(torch.autograd.Function):
     def forward(ctx, anchor, images, model, need_grad):
         eng = model._engine_for(images)
         logits = eng.forward(images, train=model.training, save_for_backward=need_grad,
-                             update_running=model.training,
-                             dropout_p=model.enc_dropout.p if model.training else 0.0)
+                             update_running=model.training, **model._drop_kwargs())
         ctx.model = model
         ctx.gen = eng.fwd_gen
         return logits.clone()
@@ -82,9 +81,9 @@ class _AttnTrainFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, anchor, images, text, model, steps):
         eng = model._engine_for(images)
-        p = model.enc_dropout.p if model.training else 0.0
-        eng.forward(images, train=model.training, save_for_backward=True, update_running=model.training,
-                    dropout_p=p)
+        kw = model._drop_kwargs()
+        p = kw["dropout_p"]
+        eng.forward(images, train=model.training, save_for_backward=True, update_running=model.training, **kw)
         key = "enc.drop" if p > 0.0 else f"r{model.num_rnn_layers - 1}.out"
         enc = eng.ws.bufs[key].float()
         dec = model._attn_decoder(enc.device)
@@ -164,6 +163,17 @@ class RCNN(nn.Module):
         # have become final (crnn_hip.dist.OverlappedAllReduce.ready), so the gradient all-reduce
         # overlaps the rest of the backward; None = single process
         self.stage_done = None
+        # the SE blocks' DropBlock2d (all blocks share p and block_size), kept out of the module tree
+        self._dropblock = [next((m for m in self.cnn.modules() if isinstance(m, DropBlock2d)), None)]
+
+    def _drop_kwargs(self) -> Dict[str, float]:
+        """the engine's training-mode regularisers: enc_dropout (model/model.py:201,220) and the SE
+        blocks' DropBlock2d (model/seresnet31.py:49-53,62); none in eval."""
+        if not self.training:
+            return dict(dropout_p=0.0)
+        db = self._dropblock[0]
+        return dict(dropout_p=self.enc_dropout.p, dropblock_p=db.p if db is not None else 0.0,
+                    dropblock_block_size=db.block_size if db is not None else 5)
 
     # ------------------------------------------------------------------ engine plumbing
     def _param_dict(self) -> Dict[str, torch.Tensor]:
@@ -289,9 +299,10 @@ class RCNN(nn.Module):
     def encode(self, x):
         """RCNN.encode (model/model.py:215-221): [B,3,H,W] -> [B, W/8, hidden] (inference)."""
         eng = self._engine_for(x)
-        p = self.enc_dropout.p if self.training else 0.0
+        kw = self._drop_kwargs()
+        p = kw["dropout_p"]
         with torch.no_grad():
-            eng.forward(x, train=self.training, save_for_backward=False, update_running=self.training, dropout_p=p)
+            eng.forward(x, train=self.training, save_for_backward=False, update_running=self.training, **kw)
         key = "enc.drop" if p > 0.0 else f"r{self.num_rnn_layers - 1}.out"   # after enc_dropout (model.py:220)
         return eng.ws.bufs[key].float().clone()
 

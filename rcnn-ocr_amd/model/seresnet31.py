@@ -24,14 +24,28 @@ class SELayer(nn.Module):
         raise NotImplementedError("SE blocks run inside the HIP engine; call RCNN.encode/forward")
 
 
+class DropBlock2d(nn.Module):
+    """torchvision.ops.DropBlock2d's attributes (p, block_size, inplace, eps) as SEBasicBlock holds
+    it (model/seresnet31.py:49-53). Parameter-free; in training the mask is drawn and applied inside
+    the HIP engine (crnn_dropblock_mask / crnn_se_residual_drop_fwd), identity in eval."""
+
+    def __init__(self, p: float, block_size: int, inplace: bool = False, eps: float = 1e-6):
+        super().__init__()
+        self.p, self.block_size, self.inplace, self.eps = p, block_size, inplace, eps
+
+    def forward(self, x):
+        raise NotImplementedError("DropBlock2d runs inside the HIP engine; call RCNN.encode/forward")
+
+    def extra_repr(self):
+        return f"p={self.p}, block_size={self.block_size}, inplace={self.inplace}"
+
+
 class SEBasicBlock(nn.Module):
     expansion = 1
 
     def __init__(self, inplanes, planes, stride=1, downsample=None, reduction=16, dropblock_p=0.0,
                  dropblock_block_size=5):
         super().__init__()
-        if dropblock_p > 0:
-            raise NotImplementedError("DropBlock2d (dropblock_p > 0) is not on the MI355X hot path")
         self.conv1 = nn.Conv2d(inplanes, planes, 3, stride=stride, padding=1, bias=False)
         self.bn1 = nn.BatchNorm2d(planes)
         self.relu = nn.ReLU(inplace=True)
@@ -39,7 +53,8 @@ class SEBasicBlock(nn.Module):
         self.bn2 = nn.BatchNorm2d(planes)
         self.se = SELayer(planes, reduction)
         self.downsample = downsample
-        self.dropblock = nn.Identity()
+        self.dropblock = DropBlock2d(p=dropblock_p, block_size=dropblock_block_size) if dropblock_p > 0 \
+            else nn.Identity()
         self.stride = stride
 
     def forward(self, x):

@@ -144,6 +144,9 @@ def hip_decisions(eng):
         f[blk.prefix + ".bn1"] = perm(cpu(sb["a1"]).reshape(B, sb["ho"], sb["wo"], -1) > 0)
         f[blk.prefix + ".se"] = cpu(sb["hid"]) > 0
         f[blk.prefix + ".out"] = perm(cpu(sb["y"]).reshape(B, sb["ho"], sb["wo"], -1) > 0)
+        if sb.get("drop") is not None:   # DropBlock2d's multiplier (crnn_oracle.se_block)
+            import crnn_oracle as O
+            f[blk.prefix + ".dropblock"] = O.dropblock_mult(perm(cpu(sb["drop"]["keep"])).numpy())
     co = sv["co"]
     f["cnn.conv_out.1"] = perm(cpu(co["a0"]).reshape(B, co["h2"], co["w2"], -1) > 0)
     zc = cpu(co["z1"]).reshape(B, co["h3"], co["w3"], -1)

@@ -21,11 +21,12 @@ def _gpu():
         pytest.skip("no HIP device")
 
 
-def build_model(sd, hidden, dtype, enc_dropout_p=0.0):
+def build_model(sd, hidden, dtype, enc_dropout_p=0.0, **kw):
     """enc_dropout_p = 0: the train-mode goldens were made with the reference's dropout off
     (tests/golden/make_goldens.py); test_enc_dropout_train covers p > 0."""
     from model.model import RCNN
-    m = RCNN(num_classes=194, hidden_size=hidden, blank_id=None, compute_dtype=dtype, enc_dropout_p=enc_dropout_p)
+    m = RCNN(num_classes=194, hidden_size=hidden, blank_id=None, compute_dtype=dtype, enc_dropout_p=enc_dropout_p,
+             **kw)
     missing, unexpected = m.load_state_dict(sd, strict=False)
     assert not unexpected, unexpected
     assert all(k.endswith("num_batches_tracked") for k in missing), missing
@@ -413,6 +414,45 @@ def test_enc_dropout_train():
     model.eval()
     with torch.no_grad():
         model(x)
+
+
+def test_dropblock_train_step_matches_forced_fp64():
+    """DropBlock2d in every SE block (model/seresnet31.py:49-53,62), training, block_size 3 on the
+    32x128 golden case: each block's keep mask is bit for bit crnn_oracle.dropblock_keep (the seed
+    draw is counter based, not torch's Philox), and EVERY parameter gradient of the HIP fp32 step is
+    within 1e-4 of the fp64 oracle that takes the HIP path's ReLU / max-pool decisions and these
+    masks (times numel / (1e-6 + kept), drop_block2d's scale). Eval applies none: logits equal a
+    dropblock-free model's. block_size 5 at this height raises, as the reference does (layer3's maps
+    are 4 rows, min(5, 4) = 4 is even and drop_block2d's mask does not broadcast)."""
+    from crnn_hip.ctc import ctc_loss
+    z = load("train_b4_32x128_h256.npz")
+    sd, hidden = case_params(z, with_running=False)
+    p, bs = 0.2, 3
+    model = build_model(sd, hidden, torch.float32, dropblock_p=p, dropblock_block_size=bs).train()
+    x = pixels_to_images(z["pixels"]).to(DEV)
+    logits = model(x)
+    ctc_loss(logits, torch.from_numpy(z["targets"]), torch.from_numpy(z["target_lengths"])).backward()
+    torch.cuda.synchronize()
+    eng = model._engine
+    B = x.shape[0]
+    for blk, sb in zip(eng.blocks, eng._saved["blocks"]):
+        d = sb["drop"]
+        assert d is not None, blk.prefix
+        ref = O.dropblock_keep(d["seed"], B, blk.planes, sb["ho"], sb["wo"], p, bs)
+        got = d["keep"].permute(0, 3, 1, 2).cpu().numpy()
+        assert np.array_equal(got, ref), blk.prefix
+        assert int(d["kept"].item()) == int(ref.sum())
+    _assert_vs_forced_fp64(model, sd, z)
+    plain = build_model(sd, hidden, torch.float32)
+    plain.load_state_dict(model.state_dict())   # the training step moved the BN running stats
+    plain.eval()
+    model.eval()
+    with torch.no_grad():
+        same = torch.equal(model(x), plain(x))
+    assert same
+    bad = build_model(sd, hidden, torch.float32, dropblock_p=p, dropblock_block_size=5).train()
+    with pytest.raises(RuntimeError):
+        bad(x)
 
 
 def test_attn_decoder_matches_reference():

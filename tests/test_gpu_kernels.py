@@ -567,6 +567,55 @@ def test_dropout_mask(dtype):
     assert torch.equal(k, ref)
 
 
+@pytest.mark.parametrize("geo", [(3, 8, 64, 32, 0.1, 5), (2, 5, 7, 16, 0.5, 5), (4, 3, 40, 8, 0.2, 5),
+                                 (2, 16, 128, 256, 0.15, 7), (1, 4, 9, 24, 0.3, 3)])
+def test_dropblock_mask(geo):
+    """crnn_dropblock_mask (DropBlock2d, model/seresnet31.py:49-53,62): the keep bytes are bit for bit
+    crnn_oracle.dropblock_keep (torchvision's drop_block2d with the HIP seed draw), NHWC, and *kept is
+    their exact sum; another seed gives another mask; crnn_dropblock_apply = x * keep * n / (1e-6 +
+    kept) in fp32 and bf16."""
+    import crnn_oracle as O
+    L = _L()
+    B, H, W, C, p, bs = geo
+    st = L.stream_ptr()
+    keep = torch.empty((B, H, W, C), dtype=torch.uint8, device=DEV)
+    kept = torch.full((1,), -1, dtype=torch.int64, device=DEV)
+    L.call("crnn_dropblock_mask", keep.data_ptr(), kept.data_ptr(), B, H, W, C, p, bs, 1234567, st)
+    ref = O.dropblock_keep(1234567, B, C, H, W, p, bs)
+    got = keep.permute(0, 3, 1, 2).cpu().numpy()
+    assert np.array_equal(got, ref), int((got != ref).sum())
+    assert int(kept.item()) == int(ref.sum())
+    assert 0 < int(ref.sum()) < ref.size
+    keep2 = torch.empty_like(keep)
+    L.call("crnn_dropblock_mask", keep2.data_ptr(), kept.data_ptr(), B, H, W, C, p, bs, 7654321, st)
+    assert not torch.equal(keep, keep2)
+    L.call("crnn_dropblock_mask", keep.data_ptr(), kept.data_ptr(), B, H, W, C, p, bs, 1234567, st)
+    mult = O.dropblock_mult(ref).permute(0, 2, 3, 1).contiguous()
+    for dtype, tol in ((torch.float32, 0.0), (torch.bfloat16, 8e-3)):
+        x = torch.randn((B, H, W, C), generator=torch.Generator().manual_seed(5)).to(DEV, dtype)
+        y = torch.empty_like(x)
+        L.call("crnn_dropblock_apply", L.dtype_code(dtype), x.data_ptr(), y.data_ptr(), keep.data_ptr(),
+               kept.data_ptr(), x.numel(), st)
+        want = (x.float().cpu() * mult).to(dtype).float()
+        if tol == 0.0:
+            assert torch.equal(y.float().cpu(), want)
+        else:
+            assert torch.allclose(y.float().cpu(), want, rtol=tol, atol=1e-6)
+
+
+def test_dropblock_mask_errors():
+    """the reference's failure modes: an even min(block_size, H, W) (torchvision's mask is (H+2) x
+    (W+2) and the multiply raises), p outside [0, 1], C % 8 != 0."""
+    L = _L()
+    keep = torch.empty(4 * 4 * 32 * 16, dtype=torch.uint8, device=DEV)
+    kept = torch.empty(1, dtype=torch.int64, device=DEV)
+    st = L.stream_ptr()
+    for args in ((2, 4, 32, 16, 0.1, 5), (2, 8, 32, 16, 0.1, 4), (2, 8, 32, 16, 1.5, 5), (2, 5, 5, 16, -0.1, 5),
+                 (2, 8, 32, 12, 0.1, 5)):
+        with pytest.raises(RuntimeError):
+            L.call("crnn_dropblock_mask", keep.data_ptr(), kept.data_ptr(), *args, 1, st)
+
+
 @pytest.mark.parametrize("BHWC", [(6, 40, 256), (5, 128, 512)])
 def test_se_bn_bwd_fused_reduce(BHWC):
     """crnn_se_bn_bwd_reduce + crnn_se_bn_partials == crnn_se_bwd_reduce + crnn_bn_bwd_reduce

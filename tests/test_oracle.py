@@ -143,3 +143,39 @@ def test_oracle_attn_decoder():
     assert np.array_equal(probs.argmax(-1).numpy(), z["greedy"])
     logits = O.attn_teacher(p, enc, text, steps, 3, V)
     np.testing.assert_allclose(logits.numpy(), z["logits"], rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("geo", [(2, 3, 8, 12, 0.3, 5), (3, 4, 5, 5, 0.5, 5), (2, 1, 3, 9, 0.4, 5), (1, 2, 6, 7, 0.2, 3)])
+def test_dropblock_keep_definition(geo):
+    """crnn_oracle.dropblock_keep (torchvision's drop_block2d structure: pad + bs x bs max-pool of the
+    seed map) against the direct definition: a seed at (i, j) of the (H-bs+1) x (W-bs+1) grid drops
+    rows i..i+bs-1, cols j..j+bs-1; seeds are the splitmix hash of the flat NCHW seed index below
+    gamma * 2^32."""
+    B, C, H, W, p, bsz = geo
+    seed = 99
+    keep = O.dropblock_keep(seed, B, C, H, W, p, bsz)
+    bs = min(bsz, H, W)
+    Hs, Ws = H - bs + 1, W - bs + 1
+    gamma = p * H * W / (bs * bs * Hs * Ws)
+    thr = int(gamma * 4294967296.0)
+    h = O._splitmix_hash(seed, np.arange(B * C * Hs * Ws)).reshape(B, C, Hs, Ws)
+    want = np.ones((B, C, H, W), np.uint8)
+    for n in range(B):
+        for c in range(C):
+            for i in range(Hs):
+                for j in range(Ws):
+                    if int(h[n, c, i, j]) < thr:
+                        want[n, c, i:i + bs, j:j + bs] = 0
+    assert np.array_equal(keep, want)
+    m = O.dropblock_mult(keep)
+    assert np.isclose(float(m.sum()), keep.size if keep.any() else 0.0, rtol=1e-5)
+
+
+def test_dropblock_keep_rate_and_even_block():
+    """the drop share is near p (gamma compensates for the block area; overlaps make it a little
+    lower), and an even effective block raises like the reference's broadcast failure."""
+    keep = O.dropblock_keep(5, 8, 16, 16, 64, 0.1, 5)
+    share = 1.0 - keep.mean()
+    assert 0.07 < share < 0.11, share
+    with pytest.raises(ValueError):
+        O.dropblock_keep(5, 2, 8, 4, 32, 0.1, 5)
