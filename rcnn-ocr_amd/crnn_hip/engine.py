@@ -598,6 +598,8 @@ class CRNNEngine:
             if Cin != 3:
                 raise ValueError("expected 3-channel crops")
         s = L.stream_ptr()
+        if train and (dropout_p > 0.0 or dropblock_p > 0.0):
+            self._drop_calls += 1   # one mask draw per training forward (enc_dropout, DropBlock2d)
         fuse = not train and not save_for_backward and self.eval_fuse   # eval inference fusions
         self._stat_cap = self._stat_capacity(B, H, W) if train or fuse else 0
         self._nbt = []
@@ -717,7 +719,6 @@ class CRNNEngine:
         # (crnn_dropout) whose seed is saved so the backward regenerates it
         sv["drop"] = None
         if train and dropout_p > 0.0:
-            self._drop_calls += 1
             seed = (self._drop_seed + 0x9E3779B97F4A7C15 * self._drop_calls) & 0xFFFFFFFFFFFFFFFF
             xdr = ws.get("enc.drop", (B, Tn, Hd), T)
             call("crnn_dropout", dt, ptr(xin), ptr(xdr), B * Tn * Hd, float(dropout_p), seed, s)

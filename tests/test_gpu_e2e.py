@@ -455,6 +455,50 @@ def test_dropblock_train_step_matches_forced_fp64():
         bad(x)
 
 
+def test_dropblock_bf16_train():
+    """DropBlock2d in the bf16 configuration: the masks are the fp32 path's (same seed stream), a new
+    mask is drawn every training forward, the bf16 gradient is no further from the fp32 path's (same
+    masks) than it is without DropBlock (random-init weights make both distances large: ReLU
+    decisions flip under bf16 storage), and a few AdamW steps descend."""
+    from crnn_hip.ctc import ctc_loss
+    from crnn_hip.optim import FusedAdamW
+    from crnn_hip.recipe import recipe_state_dict, synthetic_batch
+    sd = recipe_state_dict(O.param_shapes(256, 194), 5)
+    x, _, tg, tl = synthetic_batch(8, 32, 128, 16, 194, seed=9)
+    x = x.to(DEV)
+    flat, keeps = {}, {}
+    for p in (0.0, 0.1):
+        for dt in (torch.float32, torch.bfloat16):
+            m = build_model(sd, 256, dt, dropblock_p=p, dropblock_block_size=3).train()
+            ctc_loss(m(x), tg, tl).backward()
+            torch.cuda.synchronize()
+            flat[p, dt] = torch.cat([q.grad.reshape(-1).float() for _, q in sorted(m.named_parameters())])
+            if p > 0:
+                keeps[dt] = [sb["drop"]["keep"].clone() for sb in m._engine._saved["blocks"]]
+    assert all(torch.equal(a, b) for a, b in zip(keeps[torch.float32], keeps[torch.bfloat16]))
+    err = {p: float((flat[p, torch.bfloat16] - flat[p, torch.float32]).norm() / flat[p, torch.float32].norm())
+           for p in (0.0, 0.1)}
+    print("bf16 vs fp32 gradient distance: without DropBlock", err[0.0], "with (same masks)", err[0.1])
+    assert err[0.1] < 2 * err[0.0] + 1e-2
+    model = build_model(sd, 256, torch.bfloat16, dropblock_p=0.1, dropblock_block_size=3).train()
+    opt = FusedAdamW(model, lr=1e-3, weight_decay=0.0)
+    losses, first = [], None
+    for _ in range(6):
+        opt.zero_grad()
+        loss = ctc_loss(model(x), tg, tl)
+        k = model._engine._saved["blocks"][0]["drop"]["keep"].clone()
+        if first is None:
+            first = k
+        else:
+            assert not torch.equal(first, k)
+        loss.backward()
+        opt.step()
+        losses.append(float(loss))
+    print("losses", losses)
+    assert all(np.isfinite(losses))
+    assert losses[-1] < losses[0]
+
+
 def test_attn_decoder_matches_reference():
     """HIP attention decoder (crnn_hip/attn.py, csrc/attn.hip) vs the reference's own outputs
     (attn_decoder.npz, model/model.py:23-148): greedy-decode logits (blank masked) and the greedy
