@@ -50,6 +50,24 @@ def test_state_dict_contract_matches_reference_names():
     assert got == ref
 
 
+def test_dropblock_surface():
+    """dropblock_p > 0 builds the reference's module tree (model/seresnet31.py:49-53: a DropBlock2d
+    in each of the 11 SE blocks, Identity at p = 0) with the same state_dict (DropBlock2d has no
+    parameters); the engine gets (p, block_size) in training and nothing in eval."""
+    import crnn_oracle as O
+    from model.model import RCNN
+    from model.seresnet31 import DropBlock2d
+    m = RCNN(num_classes=194, hidden_size=512, dropblock_p=0.1, dropblock_block_size=3)
+    dbs = [mod for mod in m.modules() if isinstance(mod, DropBlock2d)]
+    assert len(dbs) == 11 and all(d.p == 0.1 and d.block_size == 3 and d.eps == 1e-6 for d in dbs)
+    assert [(k, tuple(v.shape)) for k, v in m.state_dict().items()] == O.param_shapes(512, 194)
+    assert m.train()._drop_kwargs() == dict(dropout_p=0.1, dropblock_p=0.1, dropblock_block_size=3)
+    assert m.eval()._drop_kwargs() == dict(dropout_p=0.0)
+    plain = RCNN(num_classes=194, hidden_size=64)
+    assert not any(isinstance(mod, DropBlock2d) for mod in plain.modules())
+    assert plain.train()._drop_kwargs()["dropblock_p"] == 0.0
+
+
 def test_refuses_cpu_tensors():
     from model.model import RCNN
     m = RCNN(num_classes=194, hidden_size=64)
