@@ -502,7 +502,8 @@ def main():
             "roofline_lstm": lstm_roofline(lstm, args, eng, tsteps),
             "final_loss": round(final_loss, 4),
             **({"options": opts} if opts else {}),
-            "dp": ({"allreduce": "RCCL sum of the flat fp32 gradient, bucketed and overlapped with the backward",
+            "dp": ({"allreduce": ("RCCL" if dist.get_backend() == "nccl" else dist.get_backend())
+                    + " sum of the flat fp32 gradient, bucketed and overlapped with the backward",
                     "param_checksum_spread": divergence} if world > 1 else None),
         }
         if world == 1 and not args.no_cpu_baseline:
