@@ -20,6 +20,13 @@ def main():
     from crnn_hip.ctc import ctc_loss
     from crnn_hip.recipe import recipe_state_dict, synthetic_batch
     from model.model import RCNN
+    from crnn_hip import _lib as L
+    # CRNN_DET_SET="KEY=V,KEY=V": library options for this process only (crnn_set_option), e.g. 0=0
+    # turns the 256-row GEMM's wave-half stagger off
+    for kv in filter(None, os.environ.get("CRNN_DET_SET", "").split(",")):
+        k, v = kv.split("=")
+        L.call("crnn_set_option", int(k), int(v))
+        print("option", k, "=", v, flush=True)
     load = subprocess.Popen([sys.executable, os.path.join(REPO, "bench.py"), "--no-cpu-baseline", "--steps", "3000",
                              "--warmup", "2", "--batch", "128"], stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
     try:
