@@ -813,6 +813,14 @@ __global__ __launch_bounds__(256) void se_wgrad_kernel(const float* __restrict__
   f32x4 a2[8], a1[8];   // a2[rr] = dw2[c4..c4+3][r0+rr], a1[rr] = dw1[r0+rr][c4..c4+3]
 #pragma unroll
   for (int rr = 0; rr < 8; ++rr) a2[rr] = a1[rr] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const __amdgpu_buffer_rsrc_t rds = mk_rsrc(dsig, (uint32_t)(B * C * 4)), rpo = mk_rsrc(pooled, (uint32_t)(B * C * 4));
+  const __amdgpu_buffer_rsrc_t rhi = mk_rsrc(hid, (uint32_t)(B * Cr * 4)), rdh = mk_rsrc(dhid, (uint32_t)(B * Cr * 4));
+  // device-scope (sc1) loads of the SE backward's small per-width buffers: with plain loads, a second
+  // process on the device made this kernel's se.fc gradients differ run to run while the buffers
+  // held identical values afterwards (tools/det_load.py)
+  auto ldc = [](__amdgpu_buffer_rsrc_t r, size_t e) {
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (uint32_t)(e * 4), 0, 16));
+  };
   for (int bb = bl; bb < B; bb += 64) {   // 4 samples per lane per batch, all loads first
     f32x4 dv[4], pv[4], hv[4][2], dhv[4][2];
     float mk[4];
@@ -820,12 +828,12 @@ __global__ __launch_bounds__(256) void se_wgrad_kernel(const float* __restrict__
     for (int j = 0; j < 4; ++j) {
       const int b = min(bb + 16 * j, B - 1);   // clamped: the value is masked below
       mk[j] = bb + 16 * j < B ? 1.f : 0.f;
-      dv[j] = *reinterpret_cast<const f32x4*>(dsig + (size_t)b * C + c4);
-      pv[j] = *reinterpret_cast<const f32x4*>(pooled + (size_t)b * C + c4);
+      dv[j] = ldc(rds, (size_t)b * C + c4);
+      pv[j] = ldc(rpo, (size_t)b * C + c4);
 #pragma unroll
       for (int hq = 0; hq < 2; ++hq) {
-        hv[j][hq] = *reinterpret_cast<const f32x4*>(hid + (size_t)b * Cr + r0 + 4 * hq);
-        dhv[j][hq] = *reinterpret_cast<const f32x4*>(dhid + (size_t)b * Cr + r0 + 4 * hq);
+        hv[j][hq] = ldc(rhi, (size_t)b * Cr + r0 + 4 * hq);
+        dhv[j][hq] = ldc(rdh, (size_t)b * Cr + r0 + 4 * hq);
       }
     }
 #pragma unroll

@@ -53,8 +53,10 @@ def main():
                           if g[k].shape == ref[k].shape and not torch.equal(g[k], ref[k])), reverse=True)
             wsb = [b for b in bad if b[1].startswith("ws:")]
             pb = [b for b in bad if not b[1].startswith("ws:")]
-            print(f"step {i}: {len(pb)} parameters differ from step 0 {pb[:4]}; workspace buffers {wsb[:8]}",
-                  flush=True)
+            order = {k: n for n, (k, _) in enumerate(m.named_parameters())}
+            deep = sorted((order[k], k) for _, k in pb)[-6:]   # the ones nearest the loss: the origin
+            print(f"step {i}: {len(pb)} parameters differ from step 0 {pb[:4]}; nearest the loss "
+                  f"{[k for _, k in deep]}; workspace buffers {wsb[:8]}", flush=True)
     finally:
         load.kill()
         load.wait()
