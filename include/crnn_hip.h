@@ -82,7 +82,10 @@ enum { CRNN_OPT_GEMM_STAGGER = 0,    /* 256-row conv GEMM: waves 4-7 one barrier
                                         skip their epilogue stores (the measured epilogue cost; results invalid) */
        CRNN_OPT_DGRAD_GROUP = 16,    /* strided conv dgrad on the 256-row kernel: 1 = all parity classes in ONE launch
                                         (grouped tile table, longest-K class first; default), 0 = a launch per class */
-       CRNN_OPT_COUNT = 17 };
+       CRNN_OPT_FIN_TICKET = 17,     /* BN finalize of <= 2048 partial rows: 0 = one launch with no inter-workgroup
+                                        hand-off (default), 1 = the r01-r03 ticketed chunk fold (sc1 hand-off that
+                                        is valid only at one workgroup per CU; kept for the under-load A/B) */
+       CRNN_OPT_COUNT = 18 };
 int crnn_set_option(int key, int value);
 /* current value of a tuning switch (0 for an unknown key) */
 int crnn_get_option(int key);

@@ -478,6 +478,105 @@ __global__ __launch_bounds__(256) void fin_fused_kernel(const float* __restrict_
   }
 }
 
+// One-launch finalize with NO inter-workgroup hand-off (r04, the default for <= FIN_FUSED_ROWS rows):
+// block = 8 channels; thread = (4-channel half h = tid & 1, row lane rl = tid >> 1 of 128). Each thread
+// folds rows rl, rl + 128, ... in double — forward: Chan's pairwise merge of the rows' (count, mean, M2);
+// backward: two plain sums — with 8 rows' 16-B loads in flight (out-of-range rows read 0 through the
+// buffer descriptor), then a fixed-order tree over the 128 row lanes in LDS. A block reads only what the
+// previous kernel wrote, so the launch boundary is the only hand-off. (fin_fused_kernel above handed
+// its chunk results to the group's last block by 4-B sc1 stores / loads + a ticket: a form the guide
+// measures valid only at one workgroup per CU; under load it read stale chunk results)
+constexpr int FIN1_RL = 128;
+template <bool CHAN, class A>
+__global__ __launch_bounds__(256) void fin_one_kernel(const float* __restrict__ p0, const float* __restrict__ p1,
+                                                      int rows, long rpp, int C, long count, A args) {
+  __shared__ double red[9][256];
+  const int tid = threadIdx.x, h = tid & 1, rl = tid >> 1;
+  const int c = blockIdx.x * 8 + 4 * h;
+  const uint32_t bytes = (uint32_t)((size_t)rows * C * sizeof(float));
+  const __amdgpu_buffer_rsrc_t r0s = mk_rsrc(p0, bytes), r1s = mk_rsrc(p1, bytes);
+  double n = 0.0, s[4] = {0.0, 0.0, 0.0, 0.0}, q[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int rb = rl; rb < rows; rb += 8 * FIN1_RL) {
+    f32x4 a[8], b[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int r = rb + u * FIN1_RL;
+      const uint32_t off = r < rows ? (uint32_t)(((size_t)r * C + c) * 4) : OOB;
+      a[u] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r0s, off, 0, 0));
+      b[u] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r1s, off, 0, 0));
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if constexpr (CHAN) {   // merge (nb, sum / nb, M2) of row r into (n, s = mean, q = M2)
+        const int r = rb + u * FIN1_RL;
+        const double nb = r < rows ? (double)span_rows(r, r + 1, rpp, count) : 0.0;
+        const double nn = n + nb;
+        const double w = nn > 0.0 ? nb / nn : 0.0, rnb = nb > 0.0 ? 1.0 / nb : 0.0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const double d = (double)a[u][i] * rnb - s[i];
+          s[i] += d * w;
+          q[i] += (double)b[u][i] + d * d * n * w;
+        }
+        n = nn;
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          s[i] += (double)a[u][i];
+          q[i] += (double)b[u][i];
+        }
+      }
+    }
+  }
+  // fixed-order tree over the row lanes: level st folds lane rl + st into lane rl (rl < st)
+  for (int st = FIN1_RL / 2; st >= 1; st >>= 1) {
+    if (rl >= st && rl < 2 * st) {
+      red[0][tid] = n;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        red[1 + i][tid] = s[i];
+        red[5 + i][tid] = q[i];
+      }
+    }
+    __syncthreads();
+    if (rl < st) {
+      const int o = tid + 2 * st;
+      if constexpr (CHAN) {
+        const double nb = red[0][o], nn = n + nb;
+        const double w = nn > 0.0 ? nb / nn : 0.0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const double d = red[1 + i][o] - s[i];
+          s[i] += d * w;
+          q[i] += red[5 + i][o] + d * d * n * w;
+        }
+        n = nn;
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          s[i] += red[1 + i][o];
+          q[i] += red[5 + i][o];
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (rl != 0) return;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if constexpr (CHAN) {
+      double var = q[i] / (double)count;
+      if (var < 0.0) var = 0.0;
+      write_affine(args, c + i, s[i], var, true, count);
+    } else {
+      if (args.dgamma) args.dgamma[c + i] = (float)(args.acc ? args.dgamma[c + i] + q[i] : q[i]);
+      if (args.dbeta) args.dbeta[c + i] = (float)(args.acc ? args.dbeta[c + i] + s[i] : s[i]);
+      args.mean_g[c + i] = (float)(s[i] / (double)count);
+      args.mean_gx[c + i] = (float)(q[i] / (double)count);
+    }
+  }
+}
+
 // eval mode: running statistics only
 __global__ void bn_eval_affine_kernel(int C, FinFwd a) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
@@ -487,6 +586,10 @@ __global__ void bn_eval_affine_kernel(int C, FinFwd a) {
 template <bool CHAN, class A>
 int launch_fin(const float* p0, const float* p1, int rows, long rpp, int C, long count, float* ws, const A& args,
                hipStream_t st) {
+  if (rows <= FIN_FUSED_ROWS && C % 8 == 0 && crnn_option(CRNN_OPT_FIN_TICKET) == 0) {
+    hipLaunchKernelGGL((fin_one_kernel<CHAN, A>), dim3(C / 8), dim3(256), 0, st, p0, p1, rows, rpp, C, count, args);
+    return (int)hipGetLastError();
+  }
   if (rows <= FIN_FUSED_ROWS && C <= FIN_CNT * 64) {  // one launch, ticket per 64-channel group
     int P = (rows + 15) / 16;
     if (P > FIN_PF) P = FIN_PF;

@@ -156,19 +156,50 @@ inline int tn_slab_splits(int M, int N, int K) {
   return eff_splits(K, (int)s);
 }
 
-// out[n] += sum over a row chunk; grid (ceil(N/64), row chunks)
+// out[n] (+)= sum_m X[m][n] (bias gradients), in a FIXED order: block = 16 columns; thread = (4-column
+// quarter q = tid & 3, row lane rl = tid >> 2 of 256) sums rows rl, rl + 256, ... with 8 rows' 4-column
+// loads in flight, then a fixed tree over the row lanes in LDS. One launch, no atomics: the r01-r03
+// version added row-chunk sums with fp32 atomics, whose last bits followed the arrival order.
+constexpr int CS_RL = 256;
 template <typename T>
-__global__ void colsum_kernel(const T* __restrict__ X, int ld, long M, int N, long rpc, float* __restrict__ out) {
-  __shared__ float red[4][64];
-  const int c = threadIdx.x & 63, r = threadIdx.x >> 6;
-  const int n = blockIdx.x * 64 + c;
-  const long m0 = blockIdx.y * rpc, m1 = min(M, m0 + rpc);
-  float s = 0.f;
-  if (n < N)
-    for (long m = m0 + r; m < m1; m += 4) s += tof(X[m * ld + n]);
-  red[r][c] = s;
+__global__ __launch_bounds__(1024) void colsum_kernel(const T* __restrict__ X, int ld, long M, int N,
+                                                      float* __restrict__ out, int accumulate, int vec) {
+  __shared__ f32x4 red[1024];
+  const int tid = threadIdx.x, q = tid & 3, rl = tid >> 2;
+  const int n = blockIdx.x * 16 + 4 * q;
+  const bool okn = n < N;   // vec (ld % 4 == 0, ld >= N): the quarter's 4 loads stay inside the row
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
+  for (long mb = rl; mb < M; mb += 8 * CS_RL) {
+    f32x4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const long m = mb + (long)u * CS_RL;
+      const bool ok = okn && m < M;
+      // clamped address, masked value: the loads stay unconditional (all 8 in flight)
+      const T* p = X + (size_t)(m < M ? m : M - 1) * ld + (okn ? n : 0);
+      if (vec) {
+        v[u] = ld4f<T>(p);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[u][e] = tof(p[n + e < N ? e : 0]);
+      }
+      if (!ok) v[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += v[u];
+  }
+  red[tid] = s;
   __syncthreads();
-  if (r == 0 && n < N) atomicAdd(out + n, red[0][c] + red[1][c] + red[2][c] + red[3][c]);
+  for (int st = CS_RL / 2; st >= 1; st >>= 1) {   // lane rl += lane rl + st, fixed order
+    if (rl < st) red[tid] = red[tid] + red[tid + 4 * st];
+    __syncthreads();
+  }
+  if (rl == 0 && okn) {
+    const f32x4 r = red[q];
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (n + e < N) out[n + e] = accumulate ? out[n + e] + r[e] : r[e];
+  }
 }
 
 }  // namespace
@@ -201,18 +232,15 @@ int crnn_gemm_tn(int dtype, const void* A, int lda, const void* B, int ldb, floa
 
 int crnn_colsum(int dtype, const void* X, int ld, long M, int N, float* out, int accumulate, int x_f32, void* stream) {
   hipStream_t st = (hipStream_t)stream;
-  if (!accumulate) {
-    hipError_t e = hipMemsetAsync(out, 0, (size_t)N * sizeof(float), st);
-    if (e != hipSuccess) return (int)e;
-  }
-  long chunks = (M + 255) / 256;
-  if (chunks > 512) chunks = 512;
-  long rpc = (M + chunks - 1) / chunks;
-  dim3 grid((N + 63) / 64, (unsigned)chunks);
+  if (ld < N || M < 0 || N < 0) return crnn_set_error(hipErrorInvalidValue, "colsum: ld >= N >= 0, M >= 0");
+  if (N == 0) return 0;
+  if (M == 0) return accumulate ? 0 : (int)hipMemsetAsync(out, 0, (size_t)N * sizeof(float), st);
+  const int vec = ld % 4 == 0 && ((uintptr_t)X % 16) == 0;
+  dim3 grid((N + 15) / 16);
   if (x_f32 || dtype != CRNN_BF16)
-    hipLaunchKernelGGL(colsum_kernel<float>, grid, dim3(256), 0, st, (const float*)X, ld, M, N, rpc, out);
+    hipLaunchKernelGGL(colsum_kernel<float>, grid, dim3(1024), 0, st, (const float*)X, ld, M, N, out, accumulate, vec);
   else
-    hipLaunchKernelGGL(colsum_kernel<bf16>, grid, dim3(256), 0, st, (const bf16*)X, ld, M, N, rpc, out);
+    hipLaunchKernelGGL(colsum_kernel<bf16>, grid, dim3(1024), 0, st, (const bf16*)X, ld, M, N, out, accumulate, vec);
   return (int)hipGetLastError();
 }
 

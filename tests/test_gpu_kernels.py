@@ -1303,12 +1303,21 @@ def test_bn_bwd_modes_ill_conditioned_channels(mode):
     assert err < 1e-4 and err_bad < 1e-3
 
 
-@pytest.mark.parametrize("rows,rpp,C", [(5000, 64, 64), (300, 128, 512), (1, 7, 24)])
-def test_bn_finalize_ticketed_combine(rows, rpp, C):
-    """crnn_bn_finalize / crnn_bn_bwd_finalize: one launch whose last block per channel block
-    combines up to 64 chunk partials (Chan, double). Twice on ONE workspace (ticket counters
-    re-armed by the kernel), vs fp64; a ragged last partial (count not a multiple of rpp)."""
+@pytest.mark.parametrize("ticket", [0, 1])
+@pytest.mark.parametrize("rows,rpp,C", [(5000, 64, 64), (300, 128, 512), (1, 7, 24), (2048, 16, 128)])
+def test_bn_finalize_combine(rows, rpp, C, ticket):
+    """crnn_bn_finalize / crnn_bn_bwd_finalize: <= 2048 partial rows in one launch (default: no
+    hand-off, Chan merges in double; CRNN_OPT_FIN_TICKET = 1: r03's ticketed chunk fold), more in two
+    launches. Twice on ONE workspace, vs fp64; a ragged last partial (count not a multiple of rpp)."""
     L = _L()
+    L.call("crnn_set_option", 17, ticket)
+    try:
+        _bn_finalize_combine(L, rows, rpp, C)
+    finally:
+        L.call("crnn_set_option", 17, 0)
+
+
+def _bn_finalize_combine(L, rows, rpp, C):
     g = torch.Generator().manual_seed(4)
     count = rows * rpp - (rpp // 3)
     x = (torch.randn(count, C, generator=g, dtype=torch.float64) * 0.01 + torch.randn(C, generator=g) * 50)
