@@ -847,13 +847,13 @@ class CRNNEngine:
         elif se_abc is not None:
             abc, B = se_abc
             rows = B
-            pg = ws.get("bnb.pg", (1024 * 512,), torch.float32)[: rows * C]
-            pgx = ws.get("bnb.pgx", (1024 * 512,), torch.float32)[: rows * C]
+            pg = self._bnb_ws("bnb.pg")[: rows * C]
+            pgx = self._bnb_ws("bnb.pgx")[: rows * C]
             call("crnn_se_bn_partials", ptr(abc), ptr(se), ptr(dpool), ptr(pg), ptr(pgx), B, HW, C, s)
         else:
             rows = L.lib().crnn_bn_rows(M)
-            pg = ws.get("bnb.pg", (1024 * 512,), torch.float32)[: rows * C]
-            pgx = ws.get("bnb.pgx", (1024 * 512,), torch.float32)[: rows * C]
+            pg = self._bnb_ws("bnb.pg")[: rows * C]
+            pgx = self._bnb_ws("bnb.pgx")[: rows * C]
             rd = d
             if reduce_y is not None:
                 rd = BnBwdDesc(ptr(dy), ptr(z), ptr(mean), ptr(inv), ptr(sc), ptr(sh), ptr(reduce_y), None, None,
@@ -865,6 +865,12 @@ class CRNNEngine:
              ptr(self.g[prefix + ".bias"]), ptr(mg), ptr(mgx), 1 if accumulate_params else 0, ptr(self._fin_ws()), s)
         call("crnn_bn_bwd_apply", self.dt, d, ptr(mg), ptr(mgx), ptr(out), s)
         return out
+
+    def _bnb_ws(self, name):
+        """the BN-backward per-channel partial rows (pg / pgx): room for 1024 rows of 512 channels
+        (the reduce and dgrad-epilogue row caps) and for the SE mode's one row per sample"""
+        B = self._saved["B"] if self._saved is not None else 0
+        return self.ws.get(name, (max(1024 * 512, B * 512),), torch.float32)
 
     def _dz(self, tag, scratch, n):
         """the BN-backward output that a conv's dgrad AND wgrad read: a view of the rotating scratch
@@ -1115,8 +1121,8 @@ class CRNNEngine:
             dhid = ws.get(f"se.dhid{P}", (B, Cr), torch.float32)
             dpool = ws.get(f"se.dpool{P}", (B, P), torch.float32)
             # the SE MLP backward also writes BN2's per-sample backward sums (crnn_se_bn_partials' rows)
-            pg2 = ws.get("bnb.pg", (1024 * 512,), torch.float32)[: B * P]
-            pgx2 = ws.get("bnb.pgx", (1024 * 512,), torch.float32)[: B * P]
+            pg2 = self._bnb_ws("bnb.pg")[: B * P]
+            pgx2 = self._bnb_ws("bnb.pgx")[: B * P]
             call("crnn_se_mlp_bwd_partials", ptr(ds), ptr(sb["pooled"]), ptr(sb["hid"]), ptr(sb["s"]),
                  ptr(self.p[blk.prefix + ".se.fc.0.weight"]), ptr(self.p[blk.prefix + ".se.fc.2.weight"]),
                  ptr(dsig), ptr(dhid), ptr(dpool), ptr(self._gview(blk.prefix + ".se.fc.0.weight")),
@@ -1138,8 +1144,8 @@ class CRNNEngine:
             sums = None
             if frows > 0 and frows * P <= 1024 * 512:
                 # dgrad + BN1's backward sums in the epilogue (no reduce pass over da1, z1)
-                pg = ws.get("bnb.pg", (1024 * 512,), torch.float32)[: frows * P]
-                pgx = ws.get("bnb.pgx", (1024 * 512,), torch.float32)[: frows * P]
+                pg = self._bnb_ws("bnb.pg")[: frows * P]
+                pgx = self._bnb_ws("bnb.pgx")[: frows * P]
                 self._conv_call("dgrad", self.conv_flops(blk.conv2, B, ho, wo), fname, dt, d2,
                                 ptr(dz2), ptr(fw), ptr(da1), ptr(sb["z1"]), ptr(sb["m1"]),
                                 ptr(sb["i1"]), ptr(sb["sc1"]), ptr(sb["sh1"]), ptr(pg), ptr(pgx), s)

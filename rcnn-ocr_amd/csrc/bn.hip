@@ -1535,8 +1535,12 @@ __device__ __forceinline__ void pool_window(const crnn_bn_bwd_desc& d, const Fas
 
 // CRNN_BNG_POOL_OUT: the pool-mode sums from the pooled output y and the pooled gradient dy (one row
 // per window): y > 0 means the window's first maximum got dy, and that maximum's z is (y - shift) /
-// scale. A channel with scale == 0 (all four values tie at relu(shift)) takes the first element's z
-// (the rare path reads it; the common path never touches the full-resolution tensor).
+// scale. That z carries y's bf16 rounding: an xhat error of 2^-8 |xhat + beta/gamma|, which grows with
+// |beta/gamma| as BN parameters train. A thread whose 8 channels include one with
+// |beta/gamma| > POOL_OUT_BG (or scale == 0: all four values tie at relu(shift)) takes the full
+// window from z instead (CRNN_BNG_POOL's arithmetic for those rows); the common path never touches
+// the full-resolution tensor.
+constexpr float POOL_OUT_BG = 4.f;
 template <typename T>
 __global__ __launch_bounds__(NT) void bnb_reduce_pool_out_kernel(crnn_bn_bwd_desc d, FastDiv dWo, long rpb,
                                                                  float* __restrict__ p0, float* __restrict__ p1) {
@@ -1548,32 +1552,42 @@ __global__ __launch_bounds__(NT) void bnb_reduce_pool_out_kernel(crnn_bn_bwd_des
   ld8f(d.invstd + q.c8, inv);
   ld8f(d.scale + q.c8, sc);
   ld8f(d.shift + q.c8, sh);
-  bool zero_sc = false;
+  bool wide = false;
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     a0[i] = a1[i] = 0.f;
-    zero_sc |= sc[i] == 0.f;
+    // beta / gamma = (shift + mean * scale) * invstd / scale
+    wide |= sc[i] == 0.f || fabsf((sh[i] + mean[i] * sc[i]) * inv[i]) > POOL_OUT_BG * fabsf(sc[i]);
     rsc[i] = sc[i] != 0.f ? 1.f / sc[i] : 0.f;
   }
   const long mend = d.M / 4;
   const long m0 = blockIdx.x * rpb, m1 = min(mend, m0 + rpb);
-  for (long m = m0 + q.r; m < m1; m += q.rl) {
-    const size_t o = (size_t)m * C + q.c8;
-    float y[8], dp[8];
-    unpack8<T>(ld8<T>((const T*)d.y + o), y);
-    unpack8<T>(ld8<T>((const T*)d.dy + o), dp);
-    float zf[8];
-    if (__builtin_expect(zero_sc, 0)) {   // first window element's z (full-res row 2*(m / Wo), col 2*(m % Wo))
-      uint32_t wo;
-      const uint32_t bho = dWo.divmod((uint32_t)m, wo);
-      unpack8<T>(ld8<T>((const T*)d.z + ((size_t)(2 * bho) * d.HW + 2 * wo) * C + q.c8), zf);
-    }
+  if (__builtin_expect(wide, 0)) {
+    for (long m = m0 + q.r; m < m1; m += q.rl) {
+      float z[4][8], g[4][8];
+      size_t o[4];
+      pool_window<T>(d, dWo, m, q.c8, sc, sh, z, g, o);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const float g = y[i] > 0.f ? dp[i] : 0.f;
-      const float z = sc[i] != 0.f ? (y[i] - sh[i]) * rsc[i] : zf[i];
-      a0[i] += g;
-      a1[i] += g * ((z - mean[i]) * inv[i]);
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          a0[i] += g[t][i];
+          a1[i] += g[t][i] * ((z[t][i] - mean[i]) * inv[i]);
+        }
+    }
+  } else {
+    for (long m = m0 + q.r; m < m1; m += q.rl) {
+      const size_t o = (size_t)m * C + q.c8;
+      float y[8], dp[8];
+      unpack8<T>(ld8<T>((const T*)d.y + o), y);
+      unpack8<T>(ld8<T>((const T*)d.dy + o), dp);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float g = y[i] > 0.f ? dp[i] : 0.f;
+        const float z = (y[i] - sh[i]) * rsc[i];
+        a0[i] += g;
+        a1[i] += g * ((z - mean[i]) * inv[i]);
+      }
     }
   }
 #pragma unroll

@@ -100,6 +100,8 @@ class _AttnTrainFn(torch.autograd.Function):
         grads, accumulate, attach = model._grad_views()
         attn_grads = {k[len("attn."):]: v for k, v in grads.items() if k.startswith("attn.")}
         denc = model._attn_dec.backward(grad_logits.contiguous(), attn_grads, accumulate)
+        if model.stage_done is not None:   # the decoder's gradients are final before the encoder's
+            model.stage_done(["attn."])
         model._engine.backward(None, grads, accumulate=accumulate, denc=denc, stage_done=model.stage_done)
         attach()
         return None, None, None, None, None

@@ -13,7 +13,17 @@ evaluation, resume from a checkpoint, and the scheduler step rules.
 
 New keys of this path (SURVEY §5 "Config"): `decoder` ("ctc", this path's default: CTC head +
 CTC loss; "attn": the reference's attention head + cross-entropy), `num_rnn_layers`
-(2), `dtype` ("bf16" | "fp32"), `enc_dropout_p` (0.1).
+(2), `dtype` ("bf16" | "fp32"), `enc_dropout_p` (0.1), `world_size` (data parallel).
+
+Data parallel (`world_size` > 1, one process per GPU under `torchrun --nproc-per-node N`): every
+rank builds the same model and takes rank 0's weights (broadcast of the flat parameter buffer);
+each epoch's batches (`batch_size` samples each, per rank) are dealt round-robin to the ranks, the
+same count to every rank (the remainder is dropped and logged); the backward's stage hooks drive the
+overlapped bucketed gradient all-reduce (crnn_hip.dist.OverlappedAllReduce, RCCL over xGMI) and the
+optimizer applies the rank mean. BatchNorm keeps per-rank batch statistics (the reference's plain
+BatchNorm2d); rank 0's running statistics are the ones saved. Validation batches are dealt the same
+way and the losses, references and hypotheses gathered, so every rank sees the same metrics and
+scheduler decisions; only rank 0 writes logs, metrics_epoch.csv and checkpoints.
 
 Each step: one HIP preprocess launch for the ragged batch (ResizeAndPadA + Normalize straight into
 the encoder layout) -> RCNN forward on the engine -> CTC (or cross-entropy) loss -> backward ->
@@ -169,17 +179,21 @@ def build_splits(cfg, stoi, img_h, img_w, max_len, encoding, val_size, seed):
     train_csvs, train_roots = cfg.train_csvs, cfg.train_roots
     val_csvs, val_roots = getattr(cfg, "val_csvs", None), getattr(cfg, "val_roots", None)
     train_sets, val_sets = [], []
+    any_val = bool(val_csvs and val_roots)
     for i, (c, r) in enumerate(zip(train_csvs, train_roots)):
-        sep = bool(val_csvs and val_roots and i < len(val_csvs) and i < len(val_roots)
+        sep = bool(any_val and i < len(val_csvs) and i < len(val_roots)
                    and val_csvs[i] is not None and val_roots[i] is not None)
-        kw = dict(img_height=img_h, img_max_width=img_w, encoding=encoding, max_len=max_len, strict_max_len=True)
+        if any_val:
+            kw = dict(img_height=img_h, img_max_width=img_w, encoding=encoding, max_len=max_len, strict_max_len=True)
+        else:   # split_train_val (:141-176): no max_len filter, long labels are cut by the collate
+            kw = dict(img_height=img_h, img_max_width=img_w, encoding=encoding)
         full = OCRDatasetAttn(c, r, stoi, **kw)
         if sep:
             train_sets.append(_Split(full, range(len(full))))
             vds = OCRDatasetAttn(val_csvs[i], val_roots[i], stoi, **kw)
             val_sets.append(_Split(vds, range(len(vds))))
             continue
-        n_val = min(val_size if val_size else 3000, len(full))
+        n_val = min(val_size if val_size else 3000, len(full)) if any_val else min(val_size, len(full))
         if len(full) - n_val <= 0:
             raise ValueError(f"dataset {c} has {len(full)} samples, not more than val_size {n_val}")
         tr, va = random_split_indices(len(full), n_val, seed + i)
@@ -188,20 +202,68 @@ def build_splits(cfg, stoi, img_h, img_w, max_len, encoding, val_size, seed):
     return train_sets, val_sets
 
 
-def run_training(cfg: Config, device: str = "cuda") -> Dict[str, object]:
-    seed = getattr(cfg, "seed", 42)
-    set_seed(seed)
-    exp_dir = getattr(cfg, "exp_dir", None)
-    os.makedirs(exp_dir, exist_ok=True)
-    logger = setup_logger(exp_dir)
-    logger.info(f"Start training | exp_dir={exp_dir} | seed={seed}")
-    try:
-        cfg.save()
-    except Exception as e:
-        logger.info(f"Config save skipped: {e}")
+def _null_logger() -> logging.Logger:
+    """ranks > 0: no console / file output"""
+    lg = logging.getLogger("crnn_hip.train.silent")
+    lg.propagate = False
+    if not lg.handlers:
+        lg.addHandler(logging.NullHandler())
+    return lg
+
+
+def _dp_setup(cfg, device: str):
+    """-> (world, rank, torch.device): torchrun's env when world_size (config or WORLD_SIZE) > 1"""
+    from crnn_hip import dist as D
+    world_env, rank, local = D.env_world()
+    want = getattr(cfg, "world_size", None)
+    world = int(want) if want is not None else world_env
+    if world < 1:
+        raise ValueError("world_size must be >= 1")
+    if world != world_env:
+        raise RuntimeError(f"world_size {world} needs one process per GPU: launch with torchrun --nproc-per-node "
+                           f"{world} (WORLD_SIZE is {world_env})")
     dev = torch.device(device)
     if dev.type != "cuda" or not torch.cuda.is_available():
         raise RuntimeError("run_training needs the HIP device (the CRNN path has no CPU fallback)")
+    if world > 1:
+        world, rank, local = D.init_from_env()
+        dev = torch.device("cuda", local)
+        torch.cuda.set_device(dev)
+    return world, rank, dev
+
+
+def ctc_infeasible(ids: torch.Tensor, lens: torch.Tensor, T: int) -> int:
+    """samples whose CTC alignment cannot exist at T frames: label length + repeated neighbours > T
+    (torch's ctc_loss gives +inf there and zero_infinity zeroes the sample's loss and gradient)"""
+    n = 0
+    for row, L in zip(ids.tolist(), lens.tolist()):
+        need = L + sum(1 for a, b in zip(row[:L], row[1:L]) if a == b)
+        n += need > T
+    return n
+
+
+def run_training(cfg: Config, device: str = "cuda") -> Dict[str, object]:
+    seed = getattr(cfg, "seed", 42)
+    set_seed(seed)
+    world, rank, dev = _dp_setup(cfg, device)
+    import torch.distributed as tdist
+    exp_dir = getattr(cfg, "exp_dir", None)
+    if world > 1:   # one experiment directory for the job: rank 0's
+        box = [exp_dir]
+        tdist.broadcast_object_list(box, src=0)
+        exp_dir = cfg.exp_dir = box[0]
+    lead = rank == 0
+    if lead:
+        os.makedirs(exp_dir, exist_ok=True)
+        logger = setup_logger(exp_dir)
+    else:
+        logger = _null_logger()
+    logger.info(f"Start training | exp_dir={exp_dir} | seed={seed} | world_size={world}")
+    if lead:
+        try:
+            cfg.save()
+        except Exception as e:
+            logger.info(f"Config save skipped: {e}")
 
     charset_path = cfg.charset_path
     encoding = getattr(cfg, "encoding", "utf-8")
@@ -232,14 +294,16 @@ def run_training(cfg: Config, device: str = "cuda") -> Dict[str, object]:
 
     if resume_path:
         exp_dir = os.path.dirname(resume_path)
-        os.makedirs(exp_dir, exist_ok=True)
-        logger = setup_logger(exp_dir)
+        if lead:
+            os.makedirs(exp_dir, exist_ok=True)
+            logger = setup_logger(exp_dir)
     log_dir = os.path.join(exp_dir, "logs")
-    os.makedirs(log_dir, exist_ok=True)
     metrics_csv_path = os.path.join(exp_dir, "metrics_epoch.csv")
-    if not os.path.exists(metrics_csv_path):
-        with open(metrics_csv_path, "w", newline="", encoding="utf-8") as f:
-            csv.writer(f).writerow(["epoch", "train_loss", "val_loss", "val_acc", "val_cer", "val_wer", "lr"])
+    if lead:
+        os.makedirs(log_dir, exist_ok=True)
+        if not os.path.exists(metrics_csv_path):
+            with open(metrics_csv_path, "w", newline="", encoding="utf-8") as f:
+                csv.writer(f).writerow(["epoch", "train_loss", "val_loss", "val_acc", "val_cer", "val_wer", "lr"])
     paths = {k: os.path.join(exp_dir, f"{k}_ckpt.pth") for k in ("best_loss", "best_acc", "last")}
     wpaths = {k: os.path.join(exp_dir, f"{k}_weights.pth") for k in ("best_loss", "best_acc", "last")}
 
@@ -250,6 +314,17 @@ def run_training(cfg: Config, device: str = "cuda") -> Dict[str, object]:
     model = RCNN(num_classes=len(itos), hidden_size=hidden_size, sos_id=SOS, eos_id=EOS, pad_id=PAD, blank_id=BLANK,
                  enc_dropout_p=enc_dropout_p, decoder=decoder, num_rnn_layers=num_rnn_layers,
                  compute_dtype=dtype).to(dev)
+    reducer = None
+    if world > 1:
+        from crnn_hip import dist as D
+        # one flat parameter buffer (the optimizer's and the all-reduce's unit), rank 0's values
+        model.flatten_parameters_()
+        D.broadcast_params(model._flat_param)
+        for b in model.buffers():
+            tdist.broadcast(b, 0)
+        model.mark_params_changed()
+        reducer = D.OverlappedAllReduce(model._flat_grad, model.flat_offsets())
+        model.stage_done = reducer.ready
     optimizer = make_optimizer(optimizer_name, model, lr, weight_decay, momentum)
     if scheduler_name == "ReduceLROnPlateau":
         scheduler = torch.optim.lr_scheduler.ReduceLROnPlateau(optimizer, mode="min", factor=0.5, patience=3,
@@ -284,10 +359,14 @@ def run_training(cfg: Config, device: str = "cuda") -> Dict[str, object]:
         ids, lens = ctc_targets(labels, stoi, max_len)
         return ids, lens, ["".join(itos[t] for t in row[:n]) for row, n in zip(ids.tolist(), lens.tolist())]
 
+    infeasible = [0]
+
     def train_loss(x, labels):
         if decoder == "ctc":
             ids, lens, _ = ctc_refs(labels)
-            return ctc_loss(model(x), ids, lens)
+            logits = model(x)
+            infeasible[0] += ctc_infeasible(ids, lens, logits.shape[1])
+            return ctc_loss(logits, ids, lens)
         from crnn_hip.attn import cross_entropy
         text_in, target_y, _ = pack_attention_targets(labels, stoi, max_len, drop_blank=True)
         logits = model(x, text=text_in.to(dev), is_train=True, batch_max_length=max_len)
@@ -314,7 +393,8 @@ def run_training(cfg: Config, device: str = "cuda") -> Dict[str, object]:
     start_epoch, global_step = 1, 0
     best_val_loss, best_val_acc = float("inf"), -1.0
     if resume_path and os.path.isfile(resume_path):
-        # the optimizer state is copied into the flat buffers at its first step (crnn_hip/optim.py)
+        # the optimizer state is copied into the flat buffers at its first step (crnn_hip/optim.py);
+        # every rank reads the same (rank 0's) checkpoint
         ck = load_checkpoint(resume_path, model, optimizer=optimizer, scheduler=scheduler, map_location=str(dev))
         start_epoch = int(ck.get("epoch", 0)) + 1
         global_step = int(ck.get("global_step", 0))
@@ -329,69 +409,116 @@ def run_training(cfg: Config, device: str = "cuda") -> Dict[str, object]:
                  "val_csvs": getattr(cfg, "val_csvs", None), "val_roots": getattr(cfg, "val_roots", None),
                  "hidden_size": hidden_size, "decoder": decoder, "num_rnn_layers": num_rnn_layers}
 
+    def deal(items):
+        """this rank's share: every world-th item from its rank, the same count on every rank"""
+        if world == 1:
+            return list(items)
+        n = len(items) // world
+        return [items[rank + world * k] for k in range(n)]
+
     for epoch in range(start_epoch, epochs + 1):
         model.train()
         total, nb = 0.0, 0
+        infeasible[0] = 0
         if train_proportions is not None:
             epoch_batches = list(iter(sampler))
         else:
             epoch_batches = [[flat[i] for i in b] for b in batches(range(len(flat)), batch_size, True, seed + epoch)]
-        for b in epoch_batches:
+        mine = deal(epoch_batches)
+        if world > 1 and len(epoch_batches) % world:
+            logger.info(f"epoch {epoch}: {len(epoch_batches) % world} of {len(epoch_batches)} batches dropped "
+                        f"(the same batch count on every rank)")
+        for b in mine:
             x, labels = load_batch([train_sets[d][i] for d, i in b])
             optimizer.zero_grad(set_to_none=True)
             loss = train_loss(x, labels)
             loss.backward()
-            optimizer.step()
+            if reducer is not None:
+                reducer.finish()
+                optimizer.step(grad_scale=1.0 / world)
+            else:
+                optimizer.step()
             total += float(loss.item())
             nb += 1
             global_step += 1
+        if world > 1:   # the job's mean train loss and infeasible count
+            t = torch.tensor([total, float(nb), float(infeasible[0])], dtype=torch.float64, device=dev)
+            tdist.all_reduce(t)
+            total, nb, infeasible[0] = float(t[0]), int(t[1]), int(t[2])
         avg_train_loss = total / max(1, nb)
+        if infeasible[0]:
+            logger.info(f"epoch {epoch}: {infeasible[0]} training samples have no CTC alignment at the model's "
+                        f"frame count (label + repeats > T); zero_infinity zeroed their loss and gradient")
         should_eval = ((epoch - start_epoch) % eval_every == 0) or (epoch == epochs)
         avg_val_loss = val_acc = val_cer = val_wer = None
         if should_eval:
             model.eval()
             tot_loss, tot_batches, refs_all, hyps_all = 0.0, 0, [], []
-            for vs in val_sets:
-                for b in batches(range(len(vs)), batch_size, False, 0):
-                    x, labels = load_batch([vs[i] for i in b])
-                    l, refs, hyps = val_batch(x, labels)
-                    tot_loss += l
-                    tot_batches += 1
-                    refs_all += refs
-                    hyps_all += hyps
+            vb = [(vs, b) for vs in val_sets for b in batches(range(len(vs)), batch_size, False, 0)]
+            if world > 1:   # every batch once: round-robin over the ranks (no drop)
+                vb = vb[rank::world]
+            for vs, b in vb:
+                x, labels = load_batch([vs[i] for i in b])
+                l, refs, hyps = val_batch(x, labels)
+                tot_loss += l
+                tot_batches += 1
+                refs_all += refs
+                hyps_all += hyps
+            if world > 1:
+                box = [None] * world
+                tdist.all_gather_object(box, (tot_loss, tot_batches, refs_all, hyps_all))
+                tot_loss = sum(v[0] for v in box)
+                tot_batches = sum(v[1] for v in box)
+                refs_all = [r for v in box for r in v[2]]
+                hyps_all = [h for v in box for h in v[3]]
             n = max(1, len(refs_all))
             avg_val_loss = tot_loss / max(1, tot_batches)
             val_acc = compute_accuracy(refs_all, hyps_all)
             val_cer = sum(character_error_rate(r, h) for r, h in zip(refs_all, hyps_all)) / n
             val_wer = sum(word_error_rate(r, h) for r, h in zip(refs_all, hyps_all)) / n
+        if world > 1:   # the replicas must hold the same weights: report the spread of their checksums
+            c = model._flat_param.detach().double().sum().reshape(1)
+            cmax, cmin = c.clone(), c.clone()
+            tdist.all_reduce(cmax, op=tdist.ReduceOp.MAX)
+            tdist.all_reduce(cmin, op=tdist.ReduceOp.MIN)
+            logger.info(f"epoch {epoch}: replica parameter checksum spread {float(cmax - cmin):.3e}")
         lr_now = optimizer.param_groups[0]["lr"]
-        with open(metrics_csv_path, "a", newline="", encoding="utf-8") as f:
-            row = ([f"{avg_val_loss:.6f}", f"{val_acc:.6f}", f"{val_cer:.6f}", f"{val_wer:.6f}"] if should_eval
-                   else ["skipped"] * 4)
-            csv.writer(f).writerow([epoch, f"{avg_train_loss:.6f}"] + row + [f"{lr_now:.6e}"])
+        if lead:
+            with open(metrics_csv_path, "a", newline="", encoding="utf-8") as f:
+                row = ([f"{avg_val_loss:.6f}", f"{val_acc:.6f}", f"{val_cer:.6f}", f"{val_wer:.6f}"] if should_eval
+                       else ["skipped"] * 4)
+                csv.writer(f).writerow([epoch, f"{avg_train_loss:.6f}"] + row + [f"{lr_now:.6e}"])
         msg = f"Epoch {epoch:03d}/{epochs} | train_loss={avg_train_loss:.4f}"
         if should_eval:
             msg += f" | val_loss={avg_val_loss:.4f} | acc={val_acc:.4f} | CER={val_cer:.4f} | WER={val_wer:.4f}"
         logger.info(msg + f" | lr={lr_now:.2e}")
         if should_eval:
             def ck(path, vl, va):
-                save_checkpoint(path, model, optimizer, scheduler, None, epoch, global_step, vl, va, itos, stoi,
-                                ck_config, log_dir)
+                if lead:
+                    save_checkpoint(path, model, optimizer, scheduler, None, epoch, global_step, vl, va, itos, stoi,
+                                    ck_config, log_dir)
+
+            def sw(path):
+                if lead:
+                    save_weights(path, model)
             ck(paths["last"], avg_val_loss, val_acc)
-            save_weights(wpaths["last"], model)
+            sw(wpaths["last"])
             if avg_val_loss < best_val_loss:
                 best_val_loss = avg_val_loss
                 ck(paths["best_loss"], best_val_loss, val_acc)
-                save_weights(wpaths["best_loss"], model)
+                sw(wpaths["best_loss"])
             if val_acc >= best_val_acc:
                 best_val_acc = val_acc
                 ck(paths["best_acc"], best_val_loss, best_val_acc)
-                save_weights(wpaths["best_acc"], model)
+                sw(wpaths["best_acc"])
         if scheduler is not None:
             if isinstance(scheduler, torch.optim.lr_scheduler.ReduceLROnPlateau):
                 if should_eval and avg_val_loss is not None:
                     scheduler.step(avg_val_loss)
             else:
                 scheduler.step()
+    if reducer is not None:
+        model.stage_done = None
+        tdist.barrier()   # rank 0's checkpoints are on disk before any rank returns
     logger.info("Training finished.")
     return {"val_acc": best_val_acc, "val_loss": best_val_loss, "exp_dir": exp_dir}

@@ -6,9 +6,11 @@ stage_done sequence driving crnn_hip.dist.OverlappedAllReduce (RCNN.stage_done),
 
 Checked: the stage sequence equals CRNNEngine.backward_stages(); the issued buckets tile the flat
 buffer exactly once; the reduced buffer equals, bit for bit, the rank sum of each bucket's local
-gradient at the moment it was issued (the overlap's contract), and the sum of a separate
-unhooked backward up to the run-to-run fp32 noise the SE-weight / stem reductions show when two
-processes share the device; after the optimizer step both replicas hold bit-identical weights.
+gradient at the moment it was issued (the overlap's contract), and EXACTLY the sum of a separate
+unhooked backward although the two processes share the device (r04: the BN finalize without an
+inter-workgroup hand-off and the fixed-order bias sums made the backward deterministic under that
+load; r03 had to relax this bar to 1e-2); after the optimizer step both replicas hold bit-identical
+weights.
 RCCL itself runs only on the driver's 8-GPU node."""
 import os
 import socket
@@ -28,7 +30,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, geom=(64, 16, 128)):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank), CRNN_SHARE_DEVICE="1", CRNN_LSTM_PER_STEP="1",
                       HSA_ENABLE_IPC_MODE_LEGACY="0")
@@ -48,11 +50,12 @@ def _worker(rank, world, port, q):
         world_, rank_, local = D.init_from_env("gloo")
         dev = torch.device("cuda", local)
         torch.cuda.set_device(dev)
-        m = RCNN(num_classes=194, hidden_size=64, blank_id=None, compute_dtype=torch.bfloat16, enc_dropout_p=0.0)
+        hid, B, W = geom
+        m = RCNN(num_classes=194, hidden_size=hid, blank_id=None, compute_dtype=torch.bfloat16, enc_dropout_p=0.0)
         # rank 1 starts from different weights: the broadcast must replace them
-        m.load_state_dict(recipe_state_dict(O.param_shapes(64, 194), 5 + rank), strict=False)
+        m.load_state_dict(recipe_state_dict(O.param_shapes(hid, 194), 5 + rank), strict=False)
         m = m.to(dev).train()
-        x, _, tg, tl = synthetic_batch(16, 32, 128, 16, 194, seed=100 + rank)
+        x, _, tg, tl = synthetic_batch(B, 32, W, W // 8, 194, seed=100 + rank)
         x = x.to(dev)
         m(x)                                   # builds the engine and the flat buffers
         D.broadcast_params(m._flat_param)
@@ -102,8 +105,9 @@ def _worker(rank, world, port, q):
         ok_tile = (len(spans) > 1 and spans[0][0] == 0 and spans[-1][1] == n
                    and all(a[1] == b[0] for a, b in zip(spans, spans[1:])))
         # the reduced buffer must equal the rank sum of the issued snapshots exactly (gloo sums two
-        # fp32 values: order-free), and the first backward's summed gradient up to the run-to-run
-        # noise of the fp32 SE-weight / stem reductions under the two-process load (tools/det_load.py)
+        # fp32 values: order-free), and — the backward being deterministic under the two-process load
+        # (fixed-order reductions, no inter-workgroup hand-off outside the BiLSTM sweeps) — exactly
+        # the first, unhooked backward's summed gradient
         local = torch.zeros_like(got)
         for (lo, hi), v in snaps.items():
             local[lo:hi] = v.cpu()
@@ -112,7 +116,7 @@ def _worker(rank, world, port, q):
         err = float((got - want).abs().max() / (want.abs().max() + 1e-30))
         worst = sorted(((float((got[a:a + k] - want[a:a + k]).abs().max()), n)
                         for n, (a, k) in m.flat_offsets().items()), reverse=True)[:4]
-        if err >= 1e-5:
+        if err > 0.0:
             print(f"rank {rank}: largest per-parameter differences {worst}", flush=True)
         opt.step(grad_scale=1.0 / world)
         torch.cuda.synchronize()
@@ -129,16 +133,19 @@ def _worker(rank, world, port, q):
             dist.destroy_process_group()
 
 
-def test_dp_world2_on_one_device_overlapped_allreduce():
+@pytest.mark.parametrize("geom", [(64, 16, 128), (512, 128, 256)], ids=["h64_b16", "h512_b128_bench_kernels"])
+def test_dp_world2_on_one_device_overlapped_allreduce(geom):
+    """geom = (hidden, per-rank batch, width): the second runs the bench's kernel selection (256-row
+    conv GEMMs, halo stem, stride-2 class-group dgrads, hidden 512) under the DP hooks"""
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, q, geom)) for r in range(2)]
     for p in ps:
         p.start()
-    res = sorted(q.get(timeout=100) for _ in ps)
+    res = sorted(q.get(timeout=200) for _ in ps)
     for p in ps:
         p.join(timeout=30)
     print("dp world 2:", [r[:6] for r in res])
@@ -148,5 +155,5 @@ def test_dp_world2_on_one_device_overlapped_allreduce():
         assert ok_seq, "stage_done sequence differs from CRNNEngine.backward_stages()"
         assert ok_tile, "issued buckets do not tile the flat buffer"
         assert exact == 0.0, exact
-        assert err < 1e-2, err
+        assert err == 0.0, err
         assert spread == 0.0, spread

@@ -1428,10 +1428,12 @@ def test_bn_bwd_pool_mode_matches_maxpool_then_relu_mode(dtype, shape):
     yp = torch.empty(B, H // 2, W // 2, C, dtype=dtype, device=DEV)
     L.call("crnn_bn_relu_maxpool", dt, zd.data_ptr(), scd.data_ptr(), shd.data_ptr(), yp.data_ptr(), B, H, W, C, st)
     out = []
-    for zero in (False, True):
+    for zero in (False, True, "wide"):
         scz, shz = scd.clone(), shd.clone()
-        if zero:
+        if zero is True:
             scz[3], shz[3] = 0.0, 0.7
+        elif zero == "wide":   # |beta/gamma| = 6 on channels 8..15: that 8-channel group reads z's windows
+            shz[8:16] += 6.0 * scz[8:16] / invd[8:16]
         ypz = torch.empty_like(yp)
         L.call("crnn_bn_relu_maxpool", dt, zd.data_ptr(), scz.data_ptr(), shz.data_ptr(), ypz.data_ptr(), B, H, W, C,
                st)
@@ -1447,6 +1449,9 @@ def test_bn_bwd_pool_mode_matches_maxpool_then_relu_mode(dtype, shape):
     for (s4, x4), (s5, x5) in out:
         assert relerr(s5, s4) < 1e-6          # the same g: exactly the pooled gradients where y > 0
         assert relerr(x5, x4) < (1e-5 if dtype == torch.float32 else 2e-2)   # xhat from y vs from z
+    # the wide group takes CRNN_BNG_POOL's arithmetic over the same rows: equal sums
+    (s4, x4), (s5, x5) = out[2]
+    assert torch.equal(s5[8:16], s4[8:16]) and torch.equal(x5[8:16], x4[8:16])
     # fused == unfused up to the order of the fp32 partial sums
     assert relerr(dbet_p, dbet_u) < 1e-5 and relerr(dgam_p, dgam_u) < 1e-5
     assert relerr(dz_p, dz_u) < (1e-5 if dtype == torch.float32 else 1e-2)
