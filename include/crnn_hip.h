@@ -217,6 +217,13 @@ int crnn_conv_dgrad_bnrelu_tw(int dtype, const crnn_conv_desc* d, const void* dy
 /* dw_oihw (fp32, reference layout) = beta*dw + wgrad(dy, x); ws = split-K slabs. */
 int crnn_conv_wgrad(int dtype, const crnn_conv_desc* d, const void* dy, const void* x, float* dw_oihw, float* ws, size_t ws_bytes, float beta, void* stream);
 size_t crnn_conv_wgrad_workspace(int dtype, const crnn_conv_desc* d);
+/* the two halves of crnn_conv_wgrad, so that the slab reduce can run on another stream (ordered by the
+ * caller after the GEMM; the slab workspace must not be reused before the reduce has read it):
+ * _gemm writes the split-K fp32 slabs into ws, _reduce sums them into dw_oihw (beta as above). */
+int crnn_conv_wgrad_gemm(int dtype, const crnn_conv_desc* d, const void* dy, const void* x, float* ws, size_t ws_bytes,
+                         void* stream);
+int crnn_conv_wgrad_reduce(int dtype, const crnn_conv_desc* d, float* dw_oihw, const float* ws, size_t ws_bytes,
+                           float beta, void* stream);
 /* fwd tile (BM x BN) the library picks for (dtype, d): bf16 GEMM-sized convs run the 256-row
  * deep-pipelined kernel, fp32 (parity mode) and small ones the 128/64 kernels */
 void crnn_conv_fwd_tile(int dtype, const crnn_conv_desc* d, int* bm, int* bn);

@@ -87,6 +87,8 @@ _SIGS = {
     "crnn_conv_dgrad_bnrelu": ([i32, C.POINTER(ConvDesc), vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp], i32),
     "crnn_conv_wgrad": ([i32, C.POINTER(ConvDesc), vp, vp, vp, vp, sz, f32, vp], i32),
     "crnn_conv_wgrad_workspace": ([i32, C.POINTER(ConvDesc)], sz),
+    "crnn_conv_wgrad_gemm": ([i32, C.POINTER(ConvDesc), vp, vp, vp, sz, vp], i32),
+    "crnn_conv_wgrad_reduce": ([i32, C.POINTER(ConvDesc), vp, vp, sz, f32, vp], i32),
     "crnn_bn_finalize": ([vp, vp, i32, i64, i32, i64, vp, vp, vp, vp, f32, f32, i32, vp, vp, vp, vp, vp, vp], i32),
     "crnn_bn_finalize_workspace": ([i32], sz),
     "crnn_channel_stats": ([i32, vp, i64, i32, vp, vp, i32, vp], i32),

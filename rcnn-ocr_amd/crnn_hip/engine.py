@@ -165,6 +165,8 @@ class CRNNEngine:
         self._cur_ver = None
         self._eval_affine: Dict[str, tuple] = {}   # BN tag -> version key of its cached eval affine
         self._side = None           # side stream of the running backward (wgrad_stream)
+        self._rside = None          # ... or of its conv wgrad slab reduces (wgrad_reduce_stream)
+        self._slab_i, self._slab_ev = 0, [None, None]
         self._side_stream = None
         self.debug = False      # when set, backward keeps copies of block-boundary gradients
         self._last_partials = None  # (psum, rows, rows_per_partial) of the latest training-mode conv
@@ -398,6 +400,12 @@ class CRNNEngine:
     # backward() returns. Measured (profiles/r02t_wgrad_side_stream_ab.log): the two streams
     # time-share the CUs, the wgrad launches take twice as long, and the step gains 0.4 %, so off.
     wgrad_stream = os.environ.get("CRNN_WGRAD_STREAM", "0") == "1"
+    # only the conv wgrads' split-K slab REDUCES on a second stream (CRNN_WGRAD_REDUCE_STREAM, default 1):
+    # a memory-bound pass whose output (the fp32 weight gradient) nothing reads before the optimizer, so it
+    # runs beside the next dgrad GEMM (MFMA / LDS-bound, one 512-thread block per CU, room for more waves)
+    # instead of in the chain; the slabs alternate between two buffers, and a GEMM waits only for the
+    # reduce that last read its buffer
+    wgrad_reduce_stream = os.environ.get("CRNN_WGRAD_REDUCE_STREAM", "1") == "1"
     # forward without saved activations: eval conv -> BN -> ReLU pairs as one conv launch with the
     # running-stat affine + ReLU in the epilogue, and the BiLSTM sweeps store no gates / cell
     # states (CRNN_EVAL_FUSE, default 1)
@@ -881,6 +889,8 @@ class CRNNEngine:
         return self.ws.get("g.dz." + tag, (n,), self.dtype)
 
     def _wgrad(self, cs: ConvSpec, dz, x, b, h, w):
+        if self._rside is not None:
+            return self._wgrad_split(cs, dz, x, b, h, w)
         if self._side is not None:
             # ordered after everything the compute stream has enqueued so far (dz's producer)
             self._side.wait_stream(torch.cuda.current_stream(self.device))
@@ -897,6 +907,32 @@ class CRNNEngine:
         beta = 1.0 if self.accumulate else 0.0
         self._conv_call("wgrad", self.conv_flops(cs, b, h, w), "crnn_conv_wgrad", self.dt, d, ptr(dz), ptr(x),
                         ptr(self.g[cs.name]), ptr(wsb), wsb.numel() * 4, beta, L.stream_ptr())
+
+    def _wgrad_split(self, cs: ConvSpec, dz, x, b, h, w):
+        """the split-K GEMM on the compute stream, its slab reduce on the reduce stream"""
+        d = cs.desc(b, h, w)
+        need = L.lib().crnn_conv_wgrad_workspace(self.dt, d)
+        i = self._slab_i
+        self._slab_i ^= 1
+        wsb = self.ws.get(f"wgrad.ws{i}", (self._wg_cap,), torch.float32)
+        if need > wsb.numel() * 4:
+            raise RuntimeError("wgrad workspace too small")
+        cur = torch.cuda.current_stream(self.device)
+        if self._slab_ev[i] is not None:       # the reduce that last read this buffer
+            cur.wait_event(self._slab_ev[i])
+        self._conv_call("wgrad", self.conv_flops(cs, b, h, w), "crnn_conv_wgrad_gemm", self.dt, d, ptr(dz), ptr(x),
+                        ptr(wsb), wsb.numel() * 4, L.stream_ptr())
+        ev = torch.cuda.Event()
+        ev.record(cur)
+        self._rside.wait_event(ev)
+        with torch.cuda.stream(self._rside):
+            t0 = self._mark()
+            call("crnn_conv_wgrad_reduce", self.dt, d, ptr(self.g[cs.name]), ptr(wsb), wsb.numel() * 4,
+                 1.0 if self.accumulate else 0.0, L.stream_ptr())
+            self._record("wgrad", 0.0, t0)
+            done = torch.cuda.Event()
+            done.record(self._rside)
+        self._slab_ev[i] = done
 
     def _wgrad_capacity(self, B, H, W):
         lib = L.lib()
@@ -940,21 +976,28 @@ class CRNNEngine:
         unless accumulating)."""
         sv = self._saved
         self._side = None
+        self._rside = None
         if self.wgrad_stream:
             if self._side_stream is None:
                 self._side_stream = torch.cuda.Stream(self.device)
             self._side = self._side_stream
+        elif self.wgrad_reduce_stream:
+            if self._side_stream is None:
+                self._side_stream = torch.cuda.Stream(self.device)
+            self._rside = self._side_stream
+            self._slab_i, self._slab_ev = 0, [None, None]
+        side = self._side if self._side is not None else self._rside
         if stage_done is None:
             done = lambda prefixes: None  # noqa: E731
-        elif self._side is None:
+        elif side is None:
             done = stage_done
         else:
             def done(prefixes):
                 # the stage's weight gradients come from the side stream, its BN / SE ones from
                 # the compute stream: issue the hook (an all-reduce orders itself after the
                 # caller's current stream) on the side stream once it has caught up with both
-                self._side.wait_stream(torch.cuda.current_stream(self.device))
-                with torch.cuda.stream(self._side):
+                side.wait_stream(torch.cuda.current_stream(self.device))
+                with torch.cuda.stream(side):
                     stage_done(prefixes)
         if sv is None:
             raise RuntimeError("forward(save_for_backward=True) must precede backward")
@@ -982,9 +1025,10 @@ class CRNNEngine:
         try:
             self._backward_encoder(dx, grads, acc, done)
         finally:
-            if self._side is not None:
-                torch.cuda.current_stream(self.device).wait_stream(self._side)
+            if side is not None:
+                torch.cuda.current_stream(self.device).wait_stream(side)
                 self._side = None
+                self._rside = None
         self.poll_status()
 
     def _head_backward(self, dlogits, grads, acc, dx):

@@ -1065,8 +1065,10 @@ int conv_dgrad_tw_launch(const crnn_conv_desc* d, const void* dy, const void* wt
   return launch256<256, 128>(la, lb, ep, M, N, K, st);
 }
 
+// phases: bit 0 = the split-K GEMM into the fp32 slabs, bit 1 = the slab reduce into the OIHW gradient
+// (crnn_conv_wgrad_gemm / _reduce run them apart, so the reduce can go to another stream)
 template <typename T> int conv_wgrad_t(const crnn_conv_desc* d, const void* dy, const void* x, float* dw,
-                                       float* ws, size_t ws_bytes, float beta, hipStream_t st) {
+                                       float* ws, size_t ws_bytes, float beta, hipStream_t st, int phases = 3) {
   Geo g = geo(d);
   int Mp = g.B * g.Ho * g.Wo, Kp = g.KH * g.KW * g.Ci;
   int bm, bn, splits;
@@ -1074,7 +1076,8 @@ template <typename T> int conv_wgrad_t(const crnn_conv_desc* d, const void* dy, 
   size_t need = (size_t)splits * g.Co * Kp * sizeof(float);
   if (ws_bytes < need) return crnn_set_error(hipErrorInvalidValue, "conv_wgrad: workspace too small");
   int rc = 0;
-  if (bm == 0) {  // halo-tiled direct kernel (plan: bm = bn = 0), one slab per workgroup
+  if (!(phases & 1)) {
+  } else if (bm == 0) {  // halo-tiled direct kernel (plan: bm = bn = 0), one slab per workgroup
     rc = conv_halo_wgrad(d, dy, x, ws, st);
   } else {
   WgradA<T> la{(const T*)dy, g.Co, Mp, nbytes((long)Mp * g.Co, sizeof(T))};
@@ -1100,7 +1103,7 @@ template <typename T> int conv_wgrad_t(const crnn_conv_desc* d, const void* dy, 
   } else if (bm == 128) rc = launch<T, 128, 128>(la, lb, ep, g.Co, Kp, Mp, splits, st);
   else rc = launch<T, 64, 64>(la, lb, ep, g.Co, Kp, Mp, splits, st);
   }
-  if (rc) return rc;
+  if (rc || !(phases & 2)) return rc;
   int ci_real = d->Ci_real > 0 ? d->Ci_real : g.Ci;
   long total = (long)g.Co * Kp;
   if (crnn_option(CRNN_OPT_WGRAD_REDUCE) != 0 && g.KH * g.KW <= 16 && g.Ci % 8 == 0) {
@@ -1314,6 +1317,22 @@ int crnn_conv_wgrad(int dtype, const crnn_conv_desc* d, const void* dy, const vo
   if (d->Ci % 8 || d->Co % 8) return crnn_set_error(hipErrorInvalidValue, "conv_wgrad: channels must be multiples of 8");
   return dtype == CRNN_BF16 ? conv_wgrad_t<bf16>(d, dy, x, dw_oihw, ws, ws_bytes, beta, st)
                             : conv_wgrad_t<float>(d, dy, x, dw_oihw, ws, ws_bytes, beta, st);
+}
+
+int crnn_conv_wgrad_gemm(int dtype, const crnn_conv_desc* d, const void* dy, const void* x, float* ws,
+                         size_t ws_bytes, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (d->Ci % 8 || d->Co % 8) return crnn_set_error(hipErrorInvalidValue, "conv_wgrad: channels must be multiples of 8");
+  return dtype == CRNN_BF16 ? conv_wgrad_t<bf16>(d, dy, x, nullptr, ws, ws_bytes, 0.f, st, 1)
+                            : conv_wgrad_t<float>(d, dy, x, nullptr, ws, ws_bytes, 0.f, st, 1);
+}
+
+int crnn_conv_wgrad_reduce(int dtype, const crnn_conv_desc* d, float* dw_oihw, const float* ws, size_t ws_bytes,
+                           float beta, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (d->Ci % 8 || d->Co % 8) return crnn_set_error(hipErrorInvalidValue, "conv_wgrad: channels must be multiples of 8");
+  return dtype == CRNN_BF16 ? conv_wgrad_t<bf16>(d, nullptr, nullptr, dw_oihw, (float*)ws, ws_bytes, beta, st, 2)
+                            : conv_wgrad_t<float>(d, nullptr, nullptr, dw_oihw, (float*)ws, ws_bytes, beta, st, 2);
 }
 
 }  // extern "C"

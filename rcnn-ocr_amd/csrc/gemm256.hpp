@@ -286,6 +286,15 @@ __device__ __forceinline__ void gemm_stamp_ids() {
 #define GEMM_STAMP(p)
 #endif
 
+// Diagnostic build only (-DCRNN_DIAG_A_ONCE=n, tools/build_variant.sh; results invalid): the A operand's
+// LDS-DMA is issued for the first n K-tiles only, the later ones reuse whatever the buffers hold — the
+// upper bound of a kernel that stages each conv input pixel once per channel chunk (halo tile) instead of
+// once per tap
+#ifndef CRNN_DIAG_A_ONCE
+#define CRNN_DIAG_A_ONCE 0
+#endif
+__device__ __forceinline__ bool diag_a_issue(int t) { return CRNN_DIAG_A_ONCE == 0 || t < CRNN_DIAG_A_ONCE; }
+
 // One work item of the grid kernel: tile (m_tile, n_tile), K range [kz*klen, min(K, (kz+1)*klen)).
 template <int BM, int BN, int SKIP, class LA, class LB, class EPI>
 __device__ __forceinline__ void gemm256_item(LA la, LB lb, EPI epi, int M, int K, int klen, int m_tile, int n_tile,
@@ -373,7 +382,7 @@ __device__ __forceinline__ void gemm256_item(LA la, LB lb, EPI epi, int M, int K
     // ---- P1: quadrant (0,0)
     oa.template load<0, MQ, FM>(af, As, lA, wr * WM, lane);
     ob.template load<0, NQ>(*reinterpret_cast<bf16x8(*)[NQ][2]>(&bfr[0]), Bs, lB, wc * WN, lane);
-    if (n1) oa.issue(la, ra, sA0 + (b ^ 1) * STAGE, 1, pa1);
+    if (n1 && diag_a_issue(t + 1)) oa.issue(la, ra, sA0 + (b ^ 1) * STAGE, 1, pa1);
     lds_wait_all();
     raw_barrier();
     __builtin_amdgcn_s_setprio(1);
@@ -388,7 +397,7 @@ __device__ __forceinline__ void gemm256_item(LA la, LB lb, EPI epi, int M, int K
     raw_barrier();
     // ---- P2: quadrant (0,1)
     ob.template load<1, NQ>(*reinterpret_cast<bf16x8(*)[NQ][2]>(&bfr[NQ]), Bs, lB, wc * WN, lane);
-    if (n2) oa.issue(la, ra, sA0 + b * STAGE, 0, pa2);
+    if (n2 && diag_a_issue(t + 2)) oa.issue(la, ra, sA0 + b * STAGE, 0, pa2);
     lds_wait_all();
     raw_barrier();
     __builtin_amdgcn_s_setprio(1);

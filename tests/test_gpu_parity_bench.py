@@ -129,13 +129,17 @@ def _kernel_selection(eng, B, H, W):
     assert bm.value == 256, "layer4 must run on the 256-row GEMM"
 
 
-def test_train_step_bf16_b128_bench_selection():
-    """configs[2]'s train step in bf16 at B=128 (the smallest batch that takes every kernel of the
-    B=256 bench: persistent BiLSTM fwd + BPTT, 256-row conv fwd / dgrad / wgrad, halo stem): logits,
-    loss and d logits against the fp32 oracle within the bf16-storage bar; parameter gradients
-    reported against the same bar (median over parameters)."""
+GRAD_FLOOR = 2e-3   # per-parameter slack: two bf16 roundings' worth (2^-8) of independent noise
+
+
+def test_train_step_bf16_b256_bench_selection():
+    """configs[2]'s train step in bf16 at the bench's B=256 (persistent BiLSTM fwd + BPTT, 256-row
+    conv fwd / dgrad / wgrad, halo stem, stride-2 class-group dgrads): logits, loss and d logits
+    against the fp32 oracle within the bf16-storage bar, and EVERY parameter's gradient within twice
+    its own bf16-storage-model error plus GRAD_FLOOR (a single broken gradient — an SE weight, a BN
+    scale — fails the test; r03 bounded only the median)."""
     from crnn_hip.ctc import ctc_loss
-    B, H, W, hid = 128, 32, 256, 512
+    B, H, W, hid = 256, 32, 256, 512
     sd = recipe_state_dict(O.param_shapes(hid, C), 41, head_gain=HEAD_GAIN)
     x, _, tg, tl = synthetic_batch(B, H, W, W // 8, C, seed=42)
     m = hip_model(sd, hid, torch.bfloat16).train()
@@ -148,7 +152,7 @@ def test_train_step_bf16_b128_bench_selection():
     ref_lg, ref_loss, ref_dl, ref_g = oracle_logits(sd, x, True, grads=True, targets=(tg, tl))
     emu_lg, emu_loss, emu_dl, emu_g = oracle_logits(sd, x, True, store=bf16, grads=True, targets=(tg, tl))
     hip_lg = logits.detach().float().cpu()
-    assert_within_bar("train B=128 logits", hip_lg, emu_lg, ref_lg)
+    assert_within_bar("train B=256 logits", hip_lg, emu_lg, ref_lg)
     e_l, e_le = abs(float(loss) - ref_loss) / abs(ref_loss), abs(emu_loss - ref_loss) / abs(ref_loss)
     print(f"loss rel err hip {e_l:.2e} vs bf16-model {e_le:.2e}")
     assert e_l <= 1.5 * e_le + 1e-4
@@ -161,7 +165,12 @@ def test_train_step_bf16_b128_bench_selection():
     mh, me = float(np.median(list(eh.values()))), float(np.median(list(ee.values())))
     worst = sorted(eh.items(), key=lambda kv: -kv[1])[:3]
     print(f"param grads vs fp32 oracle: median rel err hip {mh:.3e} vs bf16-model {me:.3e}; worst hip {worst}")
-    assert mh <= 2.0 * me + 1e-3, (mh, me)
+    ratio = sorted(((eh[k] / (2.0 * ee[k] + GRAD_FLOOR), k, eh[k], ee[k]) for k in eh), reverse=True)
+    print("tightest parameters (hip / bar, hip err, model err):", [(k, round(r, 3), f"{a:.2e}", f"{b:.2e}")
+                                                                  for r, k, a, b in ratio[:6]])
+    bad = [(k, a, b) for r, k, a, b in ratio if r > 1.0]
+    assert not bad, f"{len(bad)} parameter gradients outside 2x their bf16-model error + {GRAD_FLOOR}: {bad[:6]}"
+    assert len(eh) == len(dict(m.named_parameters())), "every parameter must have an oracle gradient"
 
 
 def test_inference_bf16_b256_bench_selection():

@@ -1,0 +1,113 @@
+"""Word accuracy pinned to the reference's OWN trained model (north_star:
+"word-accuracy within 0.1 % of reference").
+
+tests/golden/make_refmodel.py trained the reference RCNN (attention head; its CNN the seed recipe,
+frozen; its BiLSTM encoder and decoder trained with the reference's modules and CE step on CPU) and
+recorded the reference's own greedy predictions on 1000 held-out rendered lines. Here the same
+weights go through the reference's checkpoint format into this path's reference API —
+training.utils.load_crnn and inference.OCRInference.predict (HIP preprocess -> engine -> HIP
+attention decoder -> decode_tokens) — and must give:
+  * fp32: the reference's strings, line for line;
+  * bf16 (the performance mode): exact-match accuracy within 0.1 % of the reference's (1 line in
+    1000), and the same strings on at least 99 % of the lines.
+Reference: inference.py:126-195, training/utils.py:70-119, model/model.py:166-227."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from helpers import GOLDEN
+
+pytestmark = pytest.mark.gpu
+CHARSET = os.path.join(GOLDEN, "charset.txt")
+
+
+def dequantize(q, s):
+    q2 = q.reshape(q.shape[0], -1) if q.dim() > 1 else q.reshape(1, -1)
+    return (q2.float() * s.reshape(-1, 1)).reshape(q.shape)
+
+
+@pytest.fixture(scope="module")
+def refmodel(tmp_path_factory):
+    """(checkpoint path in the reference's save_checkpoint format, val images, truth, reference
+    predictions, reference accuracy, max_len, (img_h, img_w))"""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from crnn_hip.recipe import recipe_state_dict
+    from model.model import RCNN
+    z = np.load(os.path.join(GOLDEN, "refmodel_attn.npz"))
+    hid, seed = int(z["hidden"]), int(z["seed"])
+    m = RCNN(num_classes=194, hidden_size=hid, blank_id=None, decoder="attn")
+    shapes = [(k, tuple(v.shape)) for k, v in m.state_dict().items() if not k.startswith("attn.")]
+    sd = dict(m.state_dict())                      # every key of the reference's attention model
+    sd.update(recipe_state_dict(shapes, seed))     # the CNN (and the BiLSTM, overwritten below): the recipe
+    for k in z.files:
+        if k.startswith("bn::"):
+            sd[k[4:]] = torch.from_numpy(z[k])
+        elif k.startswith("q::"):
+            name = k[3:]
+            sd[name] = dequantize(torch.from_numpy(z[k]), torch.from_numpy(z["s::" + name]))
+    assert all(("q::" + k) in z.files for k in sd if k.startswith("attn.") or k.startswith("enc_rnn."))
+    from data.transforms import load_charset
+    itos, stoi = load_charset(CHARSET)
+    ck = {"epoch": 1, "global_step": 0, "model_state": sd, "optimizer_state": None, "scheduler_state": None,
+          "itos": itos, "stoi": stoi,
+          "scaler_state": None, "best_val_loss": 0.0, "best_val_acc": float(z["ref_accuracy"]),
+          "config": {"hidden_size": hid, "img_h": int(z["img_h"]), "img_w": int(z["img_w"]),
+                     "max_len": int(z["max_len"])}}
+    path = str(tmp_path_factory.mktemp("refmodel") / "ref_ckpt.pth")
+    torch.save(ck, path)
+    widths, flat = z["val_widths"], z["val_pixels"]
+    H = int(z["img_h"])
+    imgs, off = [], 0
+    for w in widths.tolist():
+        n = H * w * 3
+        imgs.append(flat[off:off + n].reshape(H, w, 3))
+        off += n
+    assert off == flat.size
+    return (path, imgs, [str(s) for s in z["val_truth"]], [str(s) for s in z["ref_pred"]],
+            float(z["ref_accuracy"]), int(z["max_len"]), (H, int(z["img_w"])))
+
+
+def _predict(refmodel, dtype):
+    from inference import OCRInference
+    path, imgs, _, _, _, max_len, (H, W) = refmodel
+    ocr = OCRInference(path, CHARSET, device="cuda", img_h=H, img_w=W, compute_dtype=dtype)
+    assert ocr.model.decoder == "attn"
+    return ocr.predict(imgs, max_length=max_len, batch_size=256)
+
+
+def test_refmodel_fp32_reproduces_reference_strings(refmodel):
+    _, _, truth, ref, ref_acc, _, _ = refmodel
+    got = _predict(refmodel, torch.float32)
+    diff = [(i, r, g) for i, (r, g) in enumerate(zip(ref, got)) if r != g]
+    acc = float(np.mean([g == t for g, t in zip(got, truth)]))
+    print(f"fp32: {len(diff)} of {len(ref)} strings differ from the reference's; accuracy {acc:.4f} "
+          f"(reference {ref_acc:.4f}); first differences {diff[:5]}")
+    assert not diff
+    assert acc == ref_acc
+
+
+def test_refmodel_bf16_accuracy_within_0p1pct(refmodel):
+    _, _, truth, ref, ref_acc, _, _ = refmodel
+    got = _predict(refmodel, torch.bfloat16)
+    same = float(np.mean([g == r for g, r in zip(got, ref)]))
+    acc = float(np.mean([g == t for g, t in zip(got, truth)]))
+    print(f"bf16: exact-match accuracy {acc:.4f} vs reference {ref_acc:.4f}; same string as the reference on "
+          f"{same:.4f} of the lines")
+    assert abs(acc - ref_acc) <= 0.001 + 1e-9
+    assert same >= 0.99
+
+
+def test_refmodel_load_crnn(refmodel):
+    """training.utils.load_crnn (training/utils.py:70-119) on the same checkpoint: the attention
+    model with the checkpoint's weights, eval mode"""
+    from training.utils import load_crnn
+    path = refmodel[0]
+    m = load_crnn(path, hidden_size=256, device="cuda")
+    assert m.decoder == "attn" and not m.training
+    sd = torch.load(path, map_location="cpu", weights_only=True)["model_state"]
+    got = m.state_dict()
+    for k in ("attn.generator.weight", "enc_rnn.1.rnn.weight_hh_l0", "cnn.layer4.2.bn2.running_var"):
+        assert torch.equal(got[k].cpu(), sd[k]), k
