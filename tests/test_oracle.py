@@ -179,3 +179,48 @@ def test_dropblock_keep_rate_and_even_block():
     assert 0.07 < share < 0.11, share
     with pytest.raises(ValueError):
         O.dropblock_keep(5, 2, 8, 4, 32, 0.1, 5)
+
+
+def test_oracle_reads_like_the_trained_reference_model():
+    """tests/golden/refmodel_attn.npz (make_refmodel.py: the reference RCNN with a trained BiLSTM +
+    attention decoder and its own greedy predictions): the oracle's eval encode + attention greedy
+    decode, on the preprocess restatement's input, gives the reference's strings on a sample of the
+    fitted and the held-out lines (the fixture and the oracle pin each other; the GPU test
+    tests/test_gpu_refmodel.py runs all 2 x 1000 lines on the HIP path)."""
+    import preprocess_oracle as P
+    from crnn_hip.recipe import recipe_state_dict
+    z = np.load(os.path.join(GOLDEN, "refmodel_attn.npz"))
+    hid, seed, H, W, L = (int(z[k]) for k in ("hidden", "seed", "img_h", "img_w", "max_len"))
+    with open(os.path.join(GOLDEN, "charset.txt"), encoding="utf-8") as f:
+        itos = [l.rstrip("\n") for l in f if l.rstrip("\n") != ""]
+    stoi = {s: i for i, s in enumerate(itos)}
+    enc_shapes = [(k, s) for k, s in O.param_shapes(hid, len(itos)) if not k.startswith("ctc_head")]
+    p = recipe_state_dict(enc_shapes, seed)
+    for k in z.files:
+        if k.startswith("bn::"):
+            p[k[4:]] = torch.from_numpy(z[k])
+        elif k.startswith("q::"):
+            q, s = torch.from_numpy(z[k]), torch.from_numpy(z["s::" + k[3:]])
+            q2 = q.reshape(q.shape[0], -1) if q.dim() > 1 else q.reshape(1, -1)
+            p[k[3:] if not k[3:].startswith("attn.") else k[3 + 5:]] = (q2.float() * s.reshape(-1, 1)).reshape(q.shape)
+    for name in ("fit", "val"):
+        widths, flat = z[f"{name}_widths"], z[f"{name}_pixels"]
+        imgs, off = [], 0
+        for w in widths.tolist()[:24]:
+            imgs.append(flat[off:off + H * w * 3].reshape(H, w, 3))
+            off += H * w * 3
+        x = torch.from_numpy(np.stack([P.preprocess(im, H, W)[1] for im in imgs]))
+        with torch.no_grad():
+            enc = O.encode(x, p, O.Ctx(train=False))
+            lg = O.attn_greedy(p, enc, L + 1, stoi["<SOS>"], None, len(itos))
+        got = []
+        for row in lg.argmax(-1):
+            s = ""
+            for t in row.tolist():
+                if t == stoi["<EOS>"]:
+                    break
+                if t != stoi["<PAD>"]:
+                    s += itos[t]
+            got.append(s)
+        ref = [str(t) for t in z[f"{name}_ref_pred"][:24]]
+        assert got == ref, (name, [(g, r) for g, r in zip(got, ref) if g != r][:4])

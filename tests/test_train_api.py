@@ -154,3 +154,28 @@ def test_run_training_end_to_end(tmp_path, decoder):
     assert r["samples"] == 8 and 0.0 <= r["accuracy"] <= 1.0 and r["cer"] >= 0.0
     rows = list(csv.reader(open(r["report"], encoding="utf-8")))
     assert rows[0] == ["image_path", "true_text", "predicted_text", "cer", "wer", "exact_match"] and len(rows) == 9
+
+
+def test_ctc_infeasible_count():
+    """label + repeated neighbours > T has no CTC alignment (zero_infinity zeroes it): counted"""
+    from training.train import ctc_infeasible
+    ids = torch.tensor([[5, 5, 6, 0], [5, 6, 7, 8], [9, 9, 9, 0]])
+    lens = torch.tensor([3, 4, 3])
+    # needs: 3 + 1 = 4, 4 + 0 = 4, 3 + 2 = 5
+    assert ctc_infeasible(ids, lens, 4) == 1
+    assert ctc_infeasible(ids, lens, 3) == 3
+    assert ctc_infeasible(ids, lens, 5) == 0
+
+
+def test_split_without_val_csvs_keeps_long_labels(tmp_path):
+    """no val_csvs / val_roots at all: the reference's split_train_val (training/train.py:141-176)
+    builds the datasets WITHOUT max_len (no too-long filter) and takes min(val_size, n) for val"""
+    from training.train import build_splits
+    stoi = _stoi()
+    root = os.path.join(LINES, "a")
+    cfg = type("C", (), {"train_csvs": [os.path.join(root, "labels.csv")], "train_roots": [root]})()
+    tr, va = build_splits(cfg, stoi, 32, 128, 2, "utf-8", 5, 7)   # max_len 2 would drop every label
+    assert len(tr[0]) + len(va[0]) == 40 and len(va[0]) == 5
+    cfg.val_csvs, cfg.val_roots = [None], [None]
+    with pytest.raises(ValueError):       # with a val list given, max_len filters (train.py:356-366)
+        build_splits(cfg, stoi, 32, 128, 2, "utf-8", 5, 7)

@@ -9,3 +9,4 @@ for o in 1 0; do
 done
 step dp timeout -k 10 500 python -u -m pytest -v --timeout 300 --timeout-method thread tests/test_gpu_dp.py tests/test_train_dp.py
 step pool timeout -k 10 200 python -u -m pytest -v --timeout 120 --timeout-method thread tests/test_gpu_kernels.py -k "pool_mode or colsum or finalize"
+step refmodel timeout -k 10 300 python -u -m pytest -v --timeout 200 --timeout-method thread tests/test_gpu_refmodel.py tests/test_gpu_parity_bench.py -k "refmodel or train_step"
