@@ -400,12 +400,13 @@ class CRNNEngine:
     # backward() returns. Measured (profiles/r02t_wgrad_side_stream_ab.log): the two streams
     # time-share the CUs, the wgrad launches take twice as long, and the step gains 0.4 %, so off.
     wgrad_stream = os.environ.get("CRNN_WGRAD_STREAM", "0") == "1"
-    # only the conv wgrads' split-K slab REDUCES on a second stream (CRNN_WGRAD_REDUCE_STREAM, default 1):
-    # a memory-bound pass whose output (the fp32 weight gradient) nothing reads before the optimizer, so it
-    # runs beside the next dgrad GEMM (MFMA / LDS-bound, one 512-thread block per CU, room for more waves)
-    # instead of in the chain; the slabs alternate between two buffers, and a GEMM waits only for the
-    # reduce that last read its buffer
-    wgrad_reduce_stream = os.environ.get("CRNN_WGRAD_REDUCE_STREAM", "1") == "1"
+    # only the conv wgrads' split-K slab REDUCES on a second stream (CRNN_WGRAD_REDUCE_STREAM, default 0):
+    # a memory-bound pass whose output (the fp32 weight gradient) nothing reads before the optimizer, run
+    # beside the next dgrad GEMM instead of in the chain; the slabs alternate between two buffers, and a
+    # GEMM waits only for the reduce that last read its buffer. Measured (r04, same box, alternating):
+    # 17.24k vs 17.39k lines/s — the reduces stretch and the dgrads they overlap slow down by more than
+    # the 0.35 ms taken off the chain (profiles/r04c_reduce_stream_ab.log), so off
+    wgrad_reduce_stream = os.environ.get("CRNN_WGRAD_REDUCE_STREAM", "0") == "1"
     # forward without saved activations: eval conv -> BN -> ReLU pairs as one conv launch with the
     # running-stat affine + ReLU in the epilogue, and the BiLSTM sweeps store no gates / cell
     # states (CRNN_EVAL_FUSE, default 1)

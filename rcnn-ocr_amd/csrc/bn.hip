@@ -903,11 +903,24 @@ __global__ __launch_bounds__(256) void se_mlp_bwd_kernel(const float* __restrict
 // block (x, y): 64 channels (16 groups of 4, one 16-B load each) x rows r0 = 8y .. 8y+7;
 // 16 batch lanes (4 per wave x 4 waves) take interleaved samples; fixed-order combine
 // (shuffles inside a wave, then LDS across waves): deterministic.
+// Diagnostic build only (-DCRNN_SE_PROBE=1, tools/se_probe.py): every se_wgrad block records, per
+// launch, the fixed-order sums of the four inputs as its lanes READ them and of its results, so a
+// run-to-run difference can be placed before (read-time) or after (arithmetic) the loads.
+#ifndef CRNN_SE_PROBE
+#define CRNN_SE_PROBE 0
+#endif
+#if CRNN_SE_PROBE
+constexpr int SE_PROBE_LAUNCHES = 32, SE_PROBE_BLOCKS = 64, SE_PROBE_VALS = 6;
+__device__ float g_se_probe[SE_PROBE_LAUNCHES * SE_PROBE_BLOCKS * SE_PROBE_VALS];
+static int g_se_probe_launch = 0;
+#endif
+
 template <int C>
 __global__ __launch_bounds__(256) void se_wgrad_kernel(const float* __restrict__ dsig, const float* __restrict__ hid,
                                                        const float* __restrict__ dhid,
                                                        const float* __restrict__ pooled, float* __restrict__ dw1,
-                                                       float* __restrict__ dw2, int B, int accumulate) {
+                                                       float* __restrict__ dw2, int B, int accumulate,
+                                                       int probe_launch = 0) {
   constexpr int Cr = C / 16;
   __shared__ __attribute__((aligned(16))) f32x4 red[4][16][16];   // [wave][value][c-group]
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -924,6 +937,9 @@ __global__ __launch_bounds__(256) void se_wgrad_kernel(const float* __restrict__
   auto ldc = [](__amdgpu_buffer_rsrc_t r, size_t e) {
     return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (uint32_t)(e * 4), 0, 16));
   };
+#if CRNN_SE_PROBE
+  float pin[4] = {0.f, 0.f, 0.f, 0.f};
+#endif
   for (int bb = bl; bb < B; bb += 64) {   // 4 samples per lane per batch, all loads first
     f32x4 dv[4], pv[4], hv[4][2], dhv[4][2];
     float mk[4];
@@ -939,6 +955,17 @@ __global__ __launch_bounds__(256) void se_wgrad_kernel(const float* __restrict__
         dhv[j][hq] = ldc(rdh, (size_t)b * Cr + r0 + 4 * hq);
       }
     }
+#if CRNN_SE_PROBE
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        pin[0] += mk[j] * dv[j][e];
+        pin[1] += mk[j] * pv[j][e];
+        pin[2] += mk[j] * (hv[j][0][e] + hv[j][1][e]);
+        pin[3] += mk[j] * (dhv[j][0][e] + dhv[j][1][e]);
+      }
+#endif
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const f32x4 dm = dv[j] * mk[j], pm = pv[j] * mk[j];
@@ -980,6 +1007,22 @@ __global__ __launch_bounds__(256) void se_wgrad_kernel(const float* __restrict__
     f32x4* p = reinterpret_cast<f32x4*>(dw1 + (size_t)r * C + cc);
     *p = accumulate ? *p + v : v;
   }
+#if CRNN_SE_PROBE
+  // block sums in a fixed order: per-thread values through LDS (red is free again after a barrier)
+  __syncthreads();
+  float* pr = reinterpret_cast<float*>(&red[0][0][0]);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) pr[q * 256 + threadIdx.x] = pin[q];
+  pr[4 * 256 + threadIdx.x] = k < 8 ? v[0] + v[1] + v[2] + v[3] : 0.f;
+  pr[5 * 256 + threadIdx.x] = k < 8 ? 0.f : v[0] + v[1] + v[2] + v[3];
+  __syncthreads();
+  const int blk = blockIdx.y * gridDim.x + blockIdx.x;
+  if (threadIdx.x < SE_PROBE_VALS && probe_launch < SE_PROBE_LAUNCHES && blk < SE_PROBE_BLOCKS) {
+    float a = 0.f;
+    for (int t = 0; t < 256; ++t) a += pr[threadIdx.x * 256 + t];
+    g_se_probe[(probe_launch * SE_PROBE_BLOCKS + blk) * SE_PROBE_VALS + threadIdx.x] = a;
+  }
+#endif
 }
 
 // ------------------------------------------------------------ height collapse
@@ -2247,14 +2290,35 @@ int crnn_se_mlp_bwd_partials(const float* ds, const float* pooled, const float* 
   if (C == 256) {
     hipLaunchKernelGGL(se_mlp_bwd_kernel<256>, grid, dim3(256), 0, st, ds, hid, s, w1, w2, dsig, dhid, dpool, B, inv,
                        abc, pg, pgx, HW);
+#if CRNN_SE_PROBE
+    hipLaunchKernelGGL(se_wgrad_kernel<256>, wgrid, dim3(256), 0, st, dsig, hid, dhid, pooled, dw1, dw2, B, accumulate,
+                       g_se_probe_launch++);
+#else
     hipLaunchKernelGGL(se_wgrad_kernel<256>, wgrid, dim3(256), 0, st, dsig, hid, dhid, pooled, dw1, dw2, B, accumulate);
+#endif
   } else {
     hipLaunchKernelGGL(se_mlp_bwd_kernel<512>, grid, dim3(256), 0, st, ds, hid, s, w1, w2, dsig, dhid, dpool, B, inv,
                        abc, pg, pgx, HW);
+#if CRNN_SE_PROBE
+    hipLaunchKernelGGL(se_wgrad_kernel<512>, wgrid, dim3(256), 0, st, dsig, hid, dhid, pooled, dw1, dw2, B, accumulate,
+                       g_se_probe_launch++);
+#else
     hipLaunchKernelGGL(se_wgrad_kernel<512>, wgrid, dim3(256), 0, st, dsig, hid, dhid, pooled, dw1, dw2, B, accumulate);
+#endif
   }
   return (int)hipGetLastError();
 }
+
+#if CRNN_SE_PROBE
+// diagnostic build only (not in crnn_hip.h): copy the probe records out and restart the launch count
+int crnn_diag_se_probe(float* host, int n) {
+  const int all = SE_PROBE_LAUNCHES * SE_PROBE_BLOCKS * SE_PROBE_VALS;
+  hipError_t e = hipMemcpyFromSymbol(host, HIP_SYMBOL(g_se_probe), (size_t)(n < all ? n : all) * sizeof(float), 0,
+                                     hipMemcpyDeviceToHost);
+  g_se_probe_launch = 0;
+  return (int)e;
+}
+#endif
 
 int crnn_hpool_fwd(int dtype, const void* z, const float* scale, const float* shift, void* seq, int B, int Hh, int W,
                    int C, void* stream) {

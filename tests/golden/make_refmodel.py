@@ -11,7 +11,9 @@ trains it on CPU. Nothing of the reference is stored — only data:
     seed-only recipe (crnn_hip/recipe.py) with BatchNorm running statistics calibrated on training
     lines (stored, 30k floats), frozen; the BiLSTM encoder and the attention decoder are trained here
     with the reference's own modules and its teacher-forced cross-entropy step (training/train.py:
-    493-508: CrossEntropyLoss(ignore_index=PAD), Adam) and stored as int8 with a per-row fp32 scale
+    493-508: CrossEntropyLoss(ignore_index=PAD), Adam; the reference's enc_dropout 0.1 and attention
+    dropout 0.1, and 2^-7 relative noise on the frozen CNN features, so that the fitted model is not
+    balanced on the fp32 values of a random feature map) and stored as int8 with a per-row fp32 scale
     (~4 MB; the dequantized values ARE the model both sides evaluate);
   * lines rendered with DejaVu fonts (tests/golden/make_lines.py's renderer): 3000 training lines,
     1000 held-out lines; stored as uint8 pixels (ragged widths): the held-out lines and the first 1000
@@ -54,6 +56,7 @@ IMG_H, IMG_W, MAX_LEN, HIDDEN = 32, 128, 16, 256
 N_TRAIN, N_VAL, N_CAL = 3000, 1000, 64
 TRAINED = ("enc_rnn.", "attn.")
 EPOCHS, BATCH, LR = 150, 32, 2e-3
+NOISE = 2.0 ** -7
 OUT = os.path.join(HERE, "refmodel_attn.npz")
 
 
@@ -160,7 +163,11 @@ def main():
         for i in range(0, N_TRAIN - BATCH + 1, BATCH):
             idx = perm[i:i + BATCH]
             ti, ty = attention_targets([texts[j] for j in idx], stoi, MAX_LEN)
-            enc = m.enc_rnn(feats[idx])
+            # robustness to the storage rounding of a bf16 deployment: the frozen CNN's features
+            # perturbed by ~2^-7 relative noise, and the reference's enc_dropout (p = 0.1, its default)
+            f = feats[idx]
+            f = f * (1.0 + NOISE * torch.randn(f.shape, generator=g))
+            enc = torch.nn.functional.dropout(m.enc_rnn(f), p=0.1, training=True)
             logits = m.attn(enc, text=ti, is_train=True, batch_max_length=MAX_LEN)
             loss = crit(logits.reshape(-1, C), ty.reshape(-1))
             opt.zero_grad()

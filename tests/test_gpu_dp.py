@@ -7,10 +7,10 @@ stage_done sequence driving crnn_hip.dist.OverlappedAllReduce (RCNN.stage_done),
 Checked: the stage sequence equals CRNNEngine.backward_stages(); the issued buckets tile the flat
 buffer exactly once; the reduced buffer equals, bit for bit, the rank sum of each bucket's local
 gradient at the moment it was issued (the overlap's contract), and EXACTLY the sum of a separate
-unhooked backward although the two processes share the device (r04: the BN finalize without an
-inter-workgroup hand-off and the fixed-order bias sums made the backward deterministic under that
-load; r03 had to relax this bar to 1e-2); after the optimizer step both replicas hold bit-identical
-weights.
+unhooked backward (r04, with the BN finalize free of inter-workgroup hand-offs and fixed-order bias
+sums; r03 had relaxed this bar to 1e-2). The two processes take turns on the GPU's compute: while one
+runs its backward the other only waits for its bucket all-reduces (see in_turn below for why). After
+the optimizer step both replicas hold bit-identical weights.
 RCCL itself runs only on the driver's 8-GPU node."""
 import os
 import socket
@@ -61,10 +61,25 @@ def _worker(rank, world, port, q, geom=(64, 16, 128)):
         D.broadcast_params(m._flat_param)
         m.mark_params_changed()
         opt = FusedAdamW(m, lr=1e-3)
+        # the ranks take turns on the GPU (rank 0's compute, then rank 1's; a second gloo group signals
+        # the turn while the default group's bucket all-reduces are in flight): the compute kernels of
+        # two processes interleaved on one device are not run-to-run deterministic on this platform
+        # (profiles/r04e_se_probe.log: differences that start inside single kernels whose inputs are
+        # identical), a condition the real DP job — one process per GPU — never has
+        turn_group = dist.new_group(backend="gloo")
+
+        def in_turn(fn):
+            for r in range(world):
+                if rank == r:
+                    fn()
+                    torch.cuda.current_stream().synchronize()
+                dist.barrier(group=turn_group)
+
+        def step():
+            opt.zero_grad()
+            ctc_loss(m(x), tg, tl).backward()
         # per-rank gradient of this step, summed over ranks on the host: the expected reduction
-        opt.zero_grad()
-        ctc_loss(m(x), tg, tl).backward()
-        torch.cuda.synchronize()
+        in_turn(step)
         want = m._flat_grad.detach().cpu().clone()
         dist.all_reduce(want)
         # the DP step: stage hooks drive the overlapped bucketed all-reduce during the backward
@@ -84,8 +99,7 @@ def _worker(rank, world, port, q, geom=(64, 16, 128)):
             seq.append(list(prefixes))
             red.ready(prefixes)
         m.stage_done = hook
-        opt.zero_grad()
-        ctc_loss(m(x), tg, tl).backward()
+        in_turn(step)   # rank 0's buckets wait in flight until rank 1's backward issues its own
         red.finish()
         torch.cuda.synchronize()
         got = m._flat_grad.detach().cpu().clone()
