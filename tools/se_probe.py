@@ -33,10 +33,18 @@ def main():
     buf = np.zeros(NL * NB * NV, dtype=np.float32)
     env = dict(os.environ)
     env.pop("CRNN_HIP_LIB", None)   # the load process runs the default library
-    load = subprocess.Popen([sys.executable, os.path.join(REPO, "bench.py"), "--no-cpu-baseline", "--steps", "3000",
-                             "--warmup", "2", "--batch", "128"], stdout=subprocess.DEVNULL,
-                            stderr=subprocess.DEVNULL, env=env)
+    if os.environ.get("SE_PROBE_LOAD") == "matmul":   # a load process with no kernel of this library
+        cmd = [sys.executable, "-c", "import torch\na=torch.randn(4096,4096,device='cuda',dtype=torch.bfloat16)\n"
+               "while True:\n  b=a@a\n  torch.cuda.synchronize()"]
+    else:
+        cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--no-cpu-baseline", "--steps", "3000", "--warmup", "2",
+               "--batch", "128"]
+    load = subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, env=env)
     try:
+        if os.environ.get("SE_PROBE_SHIFT") == "1":
+            # this process's device allocations at different virtual addresses from the load process's
+            # (the two run the same allocation sequence otherwise): a test for cross-process aliasing
+            pad = torch.empty((37 << 20) + 4096 * 7, dtype=torch.uint8, device="cuda")   # noqa: F841
         m = RCNN(num_classes=194, hidden_size=hid, blank_id=None, compute_dtype=torch.bfloat16, enc_dropout_p=0.0)
         m.load_state_dict(recipe_state_dict(O.param_shapes(hid, 194), 5), strict=False)
         m = m.cuda().train()
@@ -65,8 +73,10 @@ def main():
             dout = sorted({int(l) for l, _ in zip(*np.nonzero((p[:, :, 4:] != refp[:, :, 4:]).any(-1)))})
             if bad or din or dout:
                 nbad += 1
-            print(f"step {i}: {len(bad)} gradients differ {bad[:4]}; se_wgrad launches with different INPUTS "
-                  f"{din}, different OUTPUTS {dout}", flush=True)
+            order = {k: n for n, (k, _) in enumerate(m.named_parameters())}
+            near = sorted(bad, key=lambda k: order[k])[-4:]   # the differing parameters nearest the loss
+            print(f"step {i}: {len(bad)} gradients differ, nearest the loss {near}; se_wgrad launches with "
+                  f"different INPUTS {din}, different OUTPUTS {dout}", flush=True)
         print(f"{nbad} of {steps - 1} steps differ", flush=True)
     finally:
         load.kill()
