@@ -39,6 +39,8 @@ def main():
     else:
         cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--no-cpu-baseline", "--steps", "3000", "--warmup", "2",
                "--batch", "128"]
+        if os.environ.get("SE_PROBE_LOAD") == "fp32":   # this library, but no LDS-DMA GEMM (fp32 kernels)
+            cmd += ["--dtype", "fp32"]
     load = subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, env=env)
     try:
         if os.environ.get("SE_PROBE_SHIFT") == "1":
