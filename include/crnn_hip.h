@@ -416,6 +416,10 @@ int crnn_lstm_seq_config(int B, int H, int bwd, int* S, int* U);
 /* diagnostics: record per-phase s_memrealtime stamps of the following persistent launches into a
  * device buffer of (grid * T * 8) u64 (NULL: off) */
 int crnn_lstm_seq_debug_stamps(unsigned long long* buf);
+/* measurement: record the two hipEvent_t right before and right after the NEXT persistent sweep's
+ * kernel on its stream (not around the counter memset and the status kernel the call also
+ * enqueues); one-shot, NULL pairs are ignored */
+int crnn_lstm_seq_time_next(void* ev_start, void* ev_end);
 size_t crnn_lstm_seq_workspace(int B);
 /* gsv / csv: the gates and cell states BPTT reads, or both NULL (inference: not stored) */
 int crnn_lstm_seq_fwd(const void* xg, const void* whh, void* hseq, void* gsv, float* csv, unsigned* ws, int B, int T,

@@ -128,6 +128,7 @@ _SIGS = {
     "crnn_lstm_dbias_workspace": ([i32], sz),
     "crnn_lstm_seq_supported": ([i32, i32, i32], i32),
     "crnn_lstm_seq_workspace": ([i32], sz),
+    "crnn_lstm_seq_time_next": ([vp, vp], i32),
     "crnn_lstm_seq_status_offset": ([i32], sz),
     "crnn_lstm_seq_config": ([i32, i32, i32, vp, vp], i32),
     "crnn_lstm_seq_debug_stamps": ([vp], i32),

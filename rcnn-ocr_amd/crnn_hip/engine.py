@@ -344,6 +344,17 @@ class CRNNEngine:
         a.record()
         return a
 
+    def _seq_marks(self):
+        """(start, end) events the library records around the next persistent BiLSTM kernel alone
+        (crnn_lstm_seq_time_next), when timing is on; else None"""
+        if getattr(self, "timers", None) is None:
+            return None
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()   # creates the HIP events; the library re-records both on the launch stream
+        b.record()
+        call("crnn_lstm_seq_time_next", a.cuda_event, b.cuda_event)
+        return a, b
+
     def _record(self, kind, work, start):
         if start is None:
             return
@@ -764,16 +775,19 @@ class CRNNEngine:
             gsv = ws.get(f"r{l}.gates", (2, Tn, B, 4 * Hd), T)
             csv = ws.get(f"r{l}.c", (2, Tn, B, Hd), torch.float32)
             whh = self.packed[pre + ".whh"]
-            t0 = self._mark()
             if self._seq_ok(B):
+                ev = self._seq_marks()
                 # without saved activations the sweep stores no gates / cell states (inference)
                 keep = save_for_backward or not self.eval_fuse
                 call("crnn_lstm_seq_fwd", ptr(xg), ptr(whh), ptr(hseq), ptr(gsv) if keep else None,
                      ptr(csv) if keep else None, ptr(self._seq_ws(B)), B, Tn, Hd, s)
+                if ev is not None:
+                    self.timers.append(("lstm_fwd", Tn * self.lstm_step_bytes(B, Hd, T), ev[0], ev[1]))
             else:
+                t0 = self._mark()
                 for st in range(Tn):
                     call("crnn_lstm_step_fwd", dt, ptr(xg), ptr(whh), ptr(hseq), ptr(gsv), ptr(csv), B, Tn, Hd, st, s)
-            self._record("lstm_fwd", Tn * self.lstm_step_bytes(B, Hd, T), t0)
+                self._record("lstm_fwd", Tn * self.lstm_step_bytes(B, Hd, T), t0)
             out = ws.get(f"r{l}.out", (B, Tn, Hd), T)
             call("crnn_gemm_nt", dt, ptr(hseq), 2 * Hd, ptr(self.packed[pre + ".lin"]), 2 * Hd, ptr(out), Hd,
                  ptr(self.p[pre + ".linear.bias"]), B * Tn, Hd, 2 * Hd, 0, 0, s)
@@ -1065,16 +1079,19 @@ class CRNNEngine:
             dg = ws.get("rnn.dgates", (2, Tn, B, 4 * Hd), T)
             dc = ws.get("rnn.dc", (2, B, Hd), torch.float32)
             whh, whh_t = self.packed[pre + ".whh"], self.packed[pre + ".whh_t"]
-            t0 = self._mark()
             if self._seq_ok(B):
+                ev = self._seq_marks()
                 call("crnn_lstm_seq_bwd", ptr(dh), ptr(whh_t), ptr(r["gates"]), ptr(r["c"]), ptr(dg),
                      ptr(self._seq_ws(B)), B, Tn, Hd, s)
+                if ev is not None:
+                    self.timers.append(("lstm_bwd", Tn * self.lstm_bptt_step_bytes(B, Hd, T), ev[0], ev[1]))
             else:
+                t0 = self._mark()
                 bws = ws.get("rnn.bptt_ws", (L.lib().crnn_lstm_bptt_workspace(B, Hd) // 4,), torch.float32)
                 for stp in range(Tn):
                     call("crnn_lstm_step_bwd", dt, ptr(dh), ptr(whh), ptr(whh_t), ptr(r["gates"]), ptr(r["c"]),
                          ptr(dg), ptr(dc), ptr(bws), B, Tn, Hd, stp, s)
-            self._record("lstm_bwd", Tn * self.lstm_bptt_step_bytes(B, Hd, T), t0)
+                self._record("lstm_bwd", Tn * self.lstm_bptt_step_bytes(B, Hd, T), t0)
             rr = pre + ".rnn."
             gq = lambda n: ptr(self._gview(rr + n))  # noqa: E731
             # gradients straight into the parameters' .grad views (reference row order)

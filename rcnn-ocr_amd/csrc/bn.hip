@@ -480,99 +480,110 @@ __global__ __launch_bounds__(256) void fin_fused_kernel(const float* __restrict_
 
 // One-launch finalize with NO inter-workgroup hand-off (r04, the default for <= FIN_FUSED_ROWS rows):
 // block = 8 channels; thread = (4-channel half h = tid & 1, row lane rl = tid >> 1 of 128). Each thread
-// folds rows rl, rl + 128, ... in double — forward: Chan's pairwise merge of the rows' (count, mean, M2);
-// backward: two plain sums — with 8 rows' 16-B loads in flight (out-of-range rows read 0 through the
-// buffer descriptor), then a fixed-order tree over the 128 row lanes in LDS. A block reads only what the
-// previous kernel wrote, so the launch boundary is the only hand-off. (fin_fused_kernel above handed
-// its chunk results to the group's last block by 4-B sc1 stores / loads + a ticket: a form the guide
-// measures valid only at one workgroup per CU; under load it read stale chunk results)
+// holds its NR rows (rl, rl + 128, ...; 16-B buffer loads all in flight, out-of-range rows read 0) in
+// registers. Backward: the two sums in double. Forward (CHAN): two passes over the registers, no
+// per-row division — the batch mean from the row sums, then M2 = sum_r (M2_r + n_r (mean_r - mean)^2)
+// (every row holds rpp samples except at most the one at count / rpp). Block sums: an xor butterfly
+// over the wave's 32 row lanes (commutative adds: every lane ends with the same bits), then the four
+// waves' values from LDS in a fixed order. A block reads only what the previous kernel wrote, so the
+// launch boundary is the only hand-off. (fin_fused_kernel above handed its chunk results to the
+// group's last block by 4-B sc1 stores / loads + a ticket: a form the guide measures valid only at one
+// workgroup per CU; under load it read stale chunk results)
 constexpr int FIN1_RL = 128;
-template <bool CHAN, class A>
+
+template <int K>
+__device__ __forceinline__ void fin1_block_sum(double (&v)[K], double (*sh)[2][K], int wv, int h, int rl) {
+#pragma unroll
+  for (int o = 2; o < 64; o <<= 1)
+#pragma unroll
+    for (int k = 0; k < K; ++k) v[k] += __shfl_xor(v[k], o);
+  if ((rl & 31) == 0)
+#pragma unroll
+    for (int k = 0; k < K; ++k) sh[wv][h][k] = v[k];
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < K; ++k) v[k] = ((sh[0][h][k] + sh[1][h][k]) + sh[2][h][k]) + sh[3][h][k];
+}
+
+template <bool CHAN, int NR, class A>
 __global__ __launch_bounds__(256) void fin_one_kernel(const float* __restrict__ p0, const float* __restrict__ p1,
                                                       int rows, long rpp, int C, long count, A args) {
-  __shared__ double red[9][256];
-  const int tid = threadIdx.x, h = tid & 1, rl = tid >> 1;
+  __shared__ double sh1[4][2][8], sh2[4][2][4];
+  const int tid = threadIdx.x, h = tid & 1, rl = tid >> 1, wv = tid >> 6;
   const int c = blockIdx.x * 8 + 4 * h;
   const uint32_t bytes = (uint32_t)((size_t)rows * C * sizeof(float));
   const __amdgpu_buffer_rsrc_t r0s = mk_rsrc(p0, bytes), r1s = mk_rsrc(p1, bytes);
-  double n = 0.0, s[4] = {0.0, 0.0, 0.0, 0.0}, q[4] = {0.0, 0.0, 0.0, 0.0};
-  for (int rb = rl; rb < rows; rb += 8 * FIN1_RL) {
-    f32x4 a[8], b[8];
+  f32x4 a[NR], b[NR];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int r = rb + u * FIN1_RL;
-      const uint32_t off = r < rows ? (uint32_t)(((size_t)r * C + c) * 4) : OOB;
-      a[u] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r0s, off, 0, 0));
-      b[u] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r1s, off, 0, 0));
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      if constexpr (CHAN) {   // merge (nb, sum / nb, M2) of row r into (n, s = mean, q = M2)
-        const int r = rb + u * FIN1_RL;
-        const double nb = r < rows ? (double)span_rows(r, r + 1, rpp, count) : 0.0;
-        const double nn = n + nb;
-        const double w = nn > 0.0 ? nb / nn : 0.0, rnb = nb > 0.0 ? 1.0 / nb : 0.0;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const double d = (double)a[u][i] * rnb - s[i];
-          s[i] += d * w;
-          q[i] += (double)b[u][i] + d * d * n * w;
-        }
-        n = nn;
-      } else {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          s[i] += (double)a[u][i];
-          q[i] += (double)b[u][i];
-        }
-      }
-    }
+  for (int u = 0; u < NR; ++u) {
+    const int r = rl + u * FIN1_RL;
+    const uint32_t off = r < rows ? (uint32_t)(((size_t)r * C + c) * 4) : OOB;
+    a[u] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r0s, off, 0, 0));
+    b[u] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r1s, off, 0, 0));
   }
-  // fixed-order tree over the row lanes: level st folds lane rl + st into lane rl (rl < st)
-  for (int st = FIN1_RL / 2; st >= 1; st >>= 1) {
-    if (rl >= st && rl < 2 * st) {
-      red[0][tid] = n;
+  if constexpr (CHAN) {
+    double v[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int u = 0; u < NR; ++u)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] += (double)a[u][i];
+    fin1_block_sum<4>(v, (double(*)[2][4])sh2, wv, h, rl);
+    double mean[4], q[4];
+    const double rc = 1.0 / (double)count;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      mean[i] = v[i] * rc;
+      q[i] = 0.0;
+    }
+    // row r holds nb(r) = rpp samples for r < rfull, count % rpp at r == rfull, none beyond
+    const long rfull = count / rpp;
+    const double npart = (double)(count - rfull * rpp), rr = 1.0 / (double)rpp;
+    const double rpart = npart > 0.0 ? 1.0 / npart : 0.0;
+#pragma unroll
+    for (int u = 0; u < NR; ++u) {
+      const long r = rl + u * FIN1_RL;
+      const double nb = r < rfull ? (double)rpp : (r == rfull ? npart : 0.0);
+      const double rnb = r < rfull ? rr : (r == rfull ? rpart : 0.0);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        red[1 + i][tid] = s[i];
-        red[5 + i][tid] = q[i];
+        const double d = (double)a[u][i] * rnb - mean[i];
+        q[i] += nb > 0.0 ? (double)b[u][i] + nb * d * d : 0.0;
       }
     }
-    __syncthreads();
-    if (rl < st) {
-      const int o = tid + 2 * st;
-      if constexpr (CHAN) {
-        const double nb = red[0][o], nn = n + nb;
-        const double w = nn > 0.0 ? nb / nn : 0.0;
+    double w[8];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const double d = red[1 + i][o] - s[i];
-          s[i] += d * w;
-          q[i] += red[5 + i][o] + d * d * n * w;
-        }
-        n = nn;
-      } else {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          s[i] += red[1 + i][o];
-          q[i] += red[5 + i][o];
-        }
-      }
+    for (int i = 0; i < 4; ++i) {
+      w[i] = q[i];
+      w[4 + i] = 0.0;
     }
-    __syncthreads();
-  }
-  if (rl != 0) return;
+    fin1_block_sum<8>(w, sh1, wv, h, rl);
+    if (rl != 0) return;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    if constexpr (CHAN) {
-      double var = q[i] / (double)count;
+    for (int i = 0; i < 4; ++i) {
+      double var = w[i] * rc;
       if (var < 0.0) var = 0.0;
-      write_affine(args, c + i, s[i], var, true, count);
-    } else {
-      if (args.dgamma) args.dgamma[c + i] = (float)(args.acc ? args.dgamma[c + i] + q[i] : q[i]);
-      if (args.dbeta) args.dbeta[c + i] = (float)(args.acc ? args.dbeta[c + i] + s[i] : s[i]);
-      args.mean_g[c + i] = (float)(s[i] / (double)count);
-      args.mean_gx[c + i] = (float)(q[i] / (double)count);
+      write_affine(args, c + i, mean[i], var, true, count);
+    }
+  } else {
+    double v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = 0.0;
+#pragma unroll
+    for (int u = 0; u < NR; ++u)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        v[i] += (double)a[u][i];
+        v[4 + i] += (double)b[u][i];
+      }
+    fin1_block_sum<8>(v, sh1, wv, h, rl);
+    if (rl != 0) return;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const double s = v[i], q = v[4 + i];
+      if (args.dgamma) args.dgamma[c + i] = (float)(args.acc ? args.dgamma[c + i] + q : q);
+      if (args.dbeta) args.dbeta[c + i] = (float)(args.acc ? args.dbeta[c + i] + s : s);
+      args.mean_g[c + i] = (float)(s / (double)count);
+      args.mean_gx[c + i] = (float)(q / (double)count);
     }
   }
 }
@@ -587,7 +598,15 @@ template <bool CHAN, class A>
 int launch_fin(const float* p0, const float* p1, int rows, long rpp, int C, long count, float* ws, const A& args,
                hipStream_t st) {
   if (rows <= FIN_FUSED_ROWS && C % 8 == 0 && crnn_option(CRNN_OPT_FIN_TICKET) == 0) {
-    hipLaunchKernelGGL((fin_one_kernel<CHAN, A>), dim3(C / 8), dim3(256), 0, st, p0, p1, rows, rpp, C, count, args);
+    const dim3 g(C / 8), t(256);
+    if (rows <= 2 * FIN1_RL)
+      hipLaunchKernelGGL((fin_one_kernel<CHAN, 2, A>), g, t, 0, st, p0, p1, rows, rpp, C, count, args);
+    else if (rows <= 4 * FIN1_RL)
+      hipLaunchKernelGGL((fin_one_kernel<CHAN, 4, A>), g, t, 0, st, p0, p1, rows, rpp, C, count, args);
+    else if (rows <= 8 * FIN1_RL)
+      hipLaunchKernelGGL((fin_one_kernel<CHAN, 8, A>), g, t, 0, st, p0, p1, rows, rpp, C, count, args);
+    else
+      hipLaunchKernelGGL((fin_one_kernel<CHAN, 16, A>), g, t, 0, st, p0, p1, rows, rpp, C, count, args);
     return (int)hipGetLastError();
   }
   if (rows <= FIN_FUSED_ROWS && C <= FIN_CNT * 64) {  // one launch, ticket per 64-channel group

@@ -814,11 +814,26 @@ static size_t seq_ring_bytes(int B) {
 size_t crnn_lstm_seq_status_offset(int B) { return seq_ring_offset(B) + seq_ring_bytes(B); }
 size_t crnn_lstm_seq_workspace(int B) { return crnn_lstm_seq_status_offset(B) + 256; }
 
+// crnn_lstm_seq_time_next: events recorded right before / after the NEXT sweep's kernel, so a caller's
+// kernel time excludes the counter memset in front of it and the status kernel behind it
+static hipEvent_t g_seq_ev[2] = {nullptr, nullptr};
+static void seq_time_mark(hipStream_t st, int end) {
+  if (g_seq_ev[end] == nullptr) return;
+  hipEventRecord(g_seq_ev[end], st);
+  g_seq_ev[end] = nullptr;
+}
+
 static int seq_accum_status(unsigned* ws, int B, hipStream_t st, int rc) {
   if (rc != 0) return rc;
   hipLaunchKernelGGL(seq_status_accum_kernel, dim3(1), dim3(64), 0, st, ws + 2 * (B / 16 + 1),
                      (unsigned*)((char*)ws + crnn_lstm_seq_status_offset(B)));
   return (int)hipGetLastError();
+}
+
+int crnn_lstm_seq_time_next(void* ev_start, void* ev_end) {
+  g_seq_ev[0] = (hipEvent_t)ev_start;
+  g_seq_ev[1] = (hipEvent_t)ev_end;
+  return 0;
 }
 
 int crnn_lstm_seq_fwd(const void* xg, const void* whh, void* hseq, void* gsv, float* csv, unsigned* ws, int B, int T,
@@ -842,9 +857,11 @@ int crnn_lstm_seq_fwd(const void* xg, const void* whh, void* hseq, void* gsv, fl
   unsigned* xtab = crnn_option(CRNN_OPT_LSTM_L2_HANDOFF) > 1 ? (unsigned*)((char*)ws + seq_tab_offset(B)) : nullptr;
   const bf16 *x = (const bf16*)xg, *w = (const bf16*)whh;
   int rc;
+  seq_time_mark(st, 0);
   if (H == 256) rc = launch_fwd<256>(S, U, grid, st, x, w, (bf16*)hseq, (bf16*)gsv, csv, cnt, err, ring, B, T, xtab);
   else if (H == 512) rc = launch_fwd<512>(S, U, grid, st, x, w, (bf16*)hseq, (bf16*)gsv, csv, cnt, err, ring, B, T, xtab);
   else rc = launch_fwd<768>(S, U, grid, st, x, w, (bf16*)hseq, (bf16*)gsv, csv, cnt, err, ring, B, T, xtab);
+  seq_time_mark(st, 1);
   return seq_accum_status(ws, B, st, rc);
 }
 
@@ -865,9 +882,11 @@ int crnn_lstm_seq_bwd(const void* dhseq, const void* whh_t, const void* gsv, con
   unsigned* xtab = crnn_option(CRNN_OPT_LSTM_L2_HANDOFF) ? (unsigned*)((char*)ws + seq_tab_offset(B)) : nullptr;
   const bf16 *dh = (const bf16*)dhseq, *wt = (const bf16*)whh_t, *gv = (const bf16*)gsv;
   int rc;
+  seq_time_mark(st, 0);
   if (H == 256) rc = launch_bwd<256>(S, U, grid, st, dh, wt, gv, csv, (bf16*)dgates, cnt, err, ring, B, T, xtab);
   else if (H == 512) rc = launch_bwd<512>(S, U, grid, st, dh, wt, gv, csv, (bf16*)dgates, cnt, err, ring, B, T, xtab);
   else rc = launch_bwd<768>(S, U, grid, st, dh, wt, gv, csv, (bf16*)dgates, cnt, err, ring, B, T, xtab);
+  seq_time_mark(st, 1);
   return seq_accum_status(ws, B, st, rc);
 }
 

@@ -29,7 +29,8 @@ def main():
     x = torch.randn(512, device=dev)
     y = torch.empty(512, dtype=torch.bfloat16, device=dev)
     print(f"trivial launch        {timeit(lambda: L.call('crnn_cast_f32', L.BF16, x.data_ptr(), y.data_ptr(), 512, st)):7.2f} us")
-    for C, rows, rpp in [(512, 256, 128), (256, 1024, 128), (64, 16384, 128), (128, 16384, 128)]:
+    for C, rows, rpp in [(512, 256, 128), (512, 512, 128), (256, 1024, 128), (256, 2048, 128), (128, 2048, 128),
+                         (64, 16384, 128), (128, 16384, 128)]:
         ps, pq = torch.rand(rows, C, device=dev), torch.rand(rows, C, device=dev)
         gm, bt = torch.ones(C, device=dev), torch.zeros(C, device=dev)
         rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
