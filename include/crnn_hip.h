@@ -85,7 +85,11 @@ enum { CRNN_OPT_GEMM_STAGGER = 0,    /* 256-row conv GEMM: waves 4-7 one barrier
        CRNN_OPT_FIN_TICKET = 17,     /* BN finalize of <= 2048 partial rows: 0 = one launch with no inter-workgroup
                                         hand-off (default), 1 = the r01-r03 ticketed chunk fold (sc1 hand-off that
                                         is valid only at one workgroup per CU; kept for the under-load A/B) */
-       CRNN_OPT_COUNT = 18 };
+       CRNN_OPT_CONV_HALO_W = 18,    /* 3x3 / stride-1 conv fwd and stride-1 dgrad (forward path) over maps of a
+                                        power-of-two width 32..256 on the 256-row kernel: 1 = one W-halo A image per
+                                        (kernel row, 64-channel block) serves the three kw K-tiles (gemm256hw.hpp;
+                                        default), 0 = an A image per K-tile (gemm256.hpp) */
+       CRNN_OPT_COUNT = 19 };
 int crnn_set_option(int key, int value);
 /* current value of a tuning switch (0 for an unknown key) */
 int crnn_get_option(int key);

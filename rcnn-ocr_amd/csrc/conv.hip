@@ -12,6 +12,7 @@
 // accumulators for training-mode BatchNorm (two rows per 128-row M tile).
 #include "gemm.hpp"
 #include "gemm256.hpp"
+#include "gemm256hw.hpp"
 #include "crnn_internal.hpp"
 
 using namespace gemm;
@@ -741,6 +742,39 @@ inline bool pad_skip_ok(const Geo& g, int rows, int cols) {
          g.pw == 1 && rows == 4 && rows * cols == 128;
 }
 
+// the W-halo A image kernel (gemm256hw.hpp) for this forward-form geometry, or -1
+inline int halo_w_lwo(const Geo& g) {
+  if (!crnn_option(CRNN_OPT_CONV_HALO_W)) return -1;
+  if (g.KH != 3 || g.KW != 3 || g.sh != 1 || g.sw != 1 || g.ph != 1 || g.pw != 1) return -1;
+  if (g.Hi != g.Ho || g.Wi != g.Wo || g.Ci % 64) return -1;
+  return gemm::halo_w_log2(g.Wo);
+}
+
+// the 256-row launch of a forward-form conv (FwdA loader, K-contiguous weights [N][K]): the W-halo kernel
+// when the geometry takes it, else gemm256 (with the padding-row skip on 4-row maps)
+template <class EPI>
+int launch_fwd256(const Geo& g, const FwdA<bf16, true>& la, const RowMajorK<bf16>& lb, const EPI& ep, int M, int N,
+                  int K, int bn, hipStream_t st) {
+  const bool skip = pad_skip_ok(g, g.Ho, g.Wo);
+  const int lwo = halo_w_lwo(g);
+  if (lwo >= 0 && la.bytes < (1u << 30)) {   // (the image contexts pack element offsets in 29 bits)
+    const gemm::HaloWDesc a{la.x, la.bytes, g.B, g.Ho, g.Wo, g.Ci, lwo, g.Ci / 64};
+    if (skip) {
+      if (bn == 256) return gemm::launch256hw<256, 1>(a, lb, ep, M, N, st);
+      return gemm::launch256hw<128, 1>(a, lb, ep, M, N, st);
+    }
+    if (bn == 256) return gemm::launch256hw<256, 0>(a, lb, ep, M, N, st);
+    return gemm::launch256hw<128, 0>(a, lb, ep, M, N, st);
+  }
+  if (skip) {
+    const int ktk = g.KW * g.Ci / 64;
+    if (bn == 256) return launch256<256, 256, 1>(la, lb, ep, M, N, K, st, 1, 1, ktk);
+    return launch256<256, 128, 1>(la, lb, ep, M, N, K, st, 1, 1, ktk);
+  }
+  if (bn == 256) return launch256<256, 256>(la, lb, ep, M, N, K, st);
+  return launch256<256, 128>(la, lb, ep, M, N, K, st);
+}
+
 
 template <typename T, bool UT>
 int conv_fwd_tt(const Geo& g, const crnn_conv_desc* d, const void* x, const void* w, void* y, float* psum,
@@ -753,13 +787,7 @@ int conv_fwd_tt(const Geo& g, const crnn_conv_desc* d, const void* x, const void
   int bm, bn;
   crnn_conv_fwd_tile(sizeof(T) == 2 ? CRNN_BF16 : CRNN_F32, d, &bm, &bn);
   if constexpr (sizeof(T) == 2 && UT) {
-    if (bm == 256 && pad_skip_ok(g, g.Ho, g.Wo)) {
-      const int ktk = g.KW * g.Ci / 64;
-      if (bn == 256) return launch256<256, 256, 1>(la, lb, ep, M, N, K, st, 1, 1, ktk);
-      return launch256<256, 128, 1>(la, lb, ep, M, N, K, st, 1, 1, ktk);
-    }
-    if (bm == 256 && bn == 256) return launch256<256, 256>(la, lb, ep, M, N, K, st);
-    if (bm == 256 && bn == 128) return launch256<256, 128>(la, lb, ep, M, N, K, st);
+    if (bm == 256 && (bn == 256 || bn == 128)) return launch_fwd256(g, la, lb, ep, M, N, K, bn, st);
   }
   if (bm == 128 && bn == 128) return launch<T, 128, 128>(la, lb, ep, M, N, K, 1, st);
   if (bm == 128 && bn == 64) return launch<T, 128, 64>(la, lb, ep, M, N, K, 1, st);
@@ -1056,13 +1084,7 @@ int conv_dgrad_tw_launch(const crnn_conv_desc* d, const void* dy, const void* wt
   int bm, bn;
   crnn_conv_fwd_tile(CRNN_BF16, &t, &bm, &bn);
   if (bm != 256) return crnn_set_error(hipErrorInvalidValue, "conv_dgrad_tw: geometry not on the 256-row path");
-  if (pad_skip_ok(g, g.Ho, g.Wo)) {
-    const int ktk = g.KW * g.Ci / 64;
-    if (bn == 256) return launch256<256, 256, 1>(la, lb, ep, M, N, K, st, 1, 1, ktk);
-    return launch256<256, 128, 1>(la, lb, ep, M, N, K, st, 1, 1, ktk);
-  }
-  if (bn == 256) return launch256<256, 256>(la, lb, ep, M, N, K, st);
-  return launch256<256, 128>(la, lb, ep, M, N, K, st);
+  return launch_fwd256(g, la, lb, ep, M, N, K, bn, st);
 }
 
 // phases: bit 0 = the split-K GEMM into the fp32 slabs, bit 1 = the slab reduce into the OIHW gradient

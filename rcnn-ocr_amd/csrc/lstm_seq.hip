@@ -819,7 +819,7 @@ size_t crnn_lstm_seq_workspace(int B) { return crnn_lstm_seq_status_offset(B) + 
 static hipEvent_t g_seq_ev[2] = {nullptr, nullptr};
 static void seq_time_mark(hipStream_t st, int end) {
   if (g_seq_ev[end] == nullptr) return;
-  hipEventRecord(g_seq_ev[end], st);
+  (void)hipEventRecord(g_seq_ev[end], st);
   g_seq_ev[end] = nullptr;
 }
 
