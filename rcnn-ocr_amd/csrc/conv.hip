@@ -754,10 +754,13 @@ inline int halo_w_lwo(const Geo& g) {
 // when the geometry takes it, else gemm256 (with the padding-row skip on 4-row maps)
 template <class EPI>
 int launch_fwd256(const Geo& g, const FwdA<bf16, true>& la, const RowMajorK<bf16>& lb, const EPI& ep, int M, int N,
-                  int K, int bn, hipStream_t st) {
+                  int K, int bn, hipStream_t st, bool dgrad = false) {
   const bool skip = pad_skip_ok(g, g.Ho, g.Wo);
   const int lwo = halo_w_lwo(g);
-  if (lwo >= 0 && la.bytes < (1u << 30)) {   // (the image contexts pack element offsets in 29 bits)
+  // (the image contexts pack element offsets in 29 bits; the padding-skip form with the BN-backward tile
+  // hook at BN = 256 exceeds the 256-register budget inside the K loop, so the stride-1 dgrads of 4-row maps
+  // at BN = 256 — with or without the hook, so that both forms sum in one order — keep the K-tile images)
+  if (lwo >= 0 && la.bytes < (1u << 30) && !(dgrad && skip && bn == 256)) {
     const gemm::HaloWDesc a{la.x, la.bytes, g.B, g.Ho, g.Wo, g.Ci, lwo, g.Ci / 64};
     if (skip) {
       if (bn == 256) return gemm::launch256hw<256, 1>(a, lb, ep, M, N, st);
@@ -1084,7 +1087,7 @@ int conv_dgrad_tw_launch(const crnn_conv_desc* d, const void* dy, const void* wt
   int bm, bn;
   crnn_conv_fwd_tile(CRNN_BF16, &t, &bm, &bn);
   if (bm != 256) return crnn_set_error(hipErrorInvalidValue, "conv_dgrad_tw: geometry not on the 256-row path");
-  return launch_fwd256(g, la, lb, ep, M, N, K, bn, st);
+  return launch_fwd256(g, la, lb, ep, M, N, K, bn, st, true);
 }
 
 // phases: bit 0 = the split-K GEMM into the fp32 slabs, bit 1 = the slab reduce into the OIHW gradient

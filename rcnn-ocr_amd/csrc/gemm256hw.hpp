@@ -8,21 +8,24 @@
 // pieces a workgroup issues. Here the K-tiles run in (kh, channel block, kw) order, and ONE image per
 // (kh, channel block) serves its three kw K-tiles: the tile's 256/Wo output rows, each widened by
 // one pixel on both sides (Wo + 2 image rows per output row, zero where the column is padding), so
-// output row r at tap kw reads image row r + 2 (r / Wo) + kw. Image pieces per K-tile: 40/3 instead
-// of 32 (a 3x3 output row of 64 pixels needs 66 image rows; IA = 5 pieces per wave, rows past the
-// image read zeros). The B operand's K order follows by remapping the K-tile's first k in prep().
+// output row r at tap kw reads image row r + 2 (r / Wo) + kw. The B operand's K order follows by
+// remapping the K-tile's first k.
 //
-// LDS: two image buffers (40 KB each: image u+1 is filled while the three K-tiles of image u read
-// the other) + the two B stages of gemm256_item (32 KB each at BN = 256) = 144 KB.
-// Image swizzle: logical 16-B chunk c of image row j sits at physical chunk c ^ (j & 7). Unlike the
-// (j >> 1) & 7 of the K-tile images, this keeps every ds_read_b128 lane group on distinct banks at
-// ANY row offset (the kw shift and the 2-row gap per output row move the fragment's first row):
-// bank = 32 (j & 1) + 4 (c ^ (j & 7)), and the two 8-lane row runs of a lane group differ in c's
-// low bit, so (j & 1, physical chunk) is a bijection over the group's 16 lanes.
+// Image layout: rows of 10 16-B slots (pitch 160 B; slots 8 and 9 are padding). A fragment read is then
+// a per-lane base (row c16, chunk g4) plus a wave-uniform offset (first row, kw, buffer): one VALU add
+// per fragment. With pitch 160 the 16 lanes of every ds_read_b128 lane group land on distinct banks at
+// ANY first row (enumerated). An XOR-swizzled 128-B pitch needs ~5 VALU per fragment to rebuild the
+// swizzle for each kw shift, which cost more than the DMA it saved (+24 % VALU, +7 % busy cycles,
+// profiles/r04m_*). A DMA wave-instruction fills 64 consecutive slots (6.4 rows); its lanes on padding
+// slots read zeros. <= 43 pieces per image (8 output rows of 32 + 2 columns = 272 rows); IA = 6 per
+// wave, pieces past the image go to a dummy KB.
+//
+// LDS: two image buffers (43 KB each: image u+1 is filled while the three K-tiles of image u read the
+// other), the dummy KB, and the two B stages of gemm256_item (32 KB each at BN = 256) = 151 KB.
 //
 // DMA schedule (per wave; vmcnt retires in issue order):
 //   K-tile 3u   : P1 image u+1 pieces 0, 1; P2 piece 2     P3 / P4: B of K-tile t+2 (as gemm256_item)
-//   K-tile 3u+1 : P1 piece 3;           P2 piece 4         P3 / P4: B of t+2
+//   K-tile 3u+1 : P1 pieces 3, 4;       P2 piece 5         P3 / P4: B of t+2
 //   K-tile 3u+2 : -                                       P3 / P4: B of t+2
 // The image buffer of u+1 was last read in P3 of K-tile 3u-1 (the distance gemm256_item keeps between
 // a half-tile's last read and its re-fill). The P4 wait of K-tile t leaves outstanding only what was
@@ -51,10 +54,12 @@ __global__ __launch_bounds__(512) void gemm256hw_kernel(HaloWDesc a, LB lb, EPI 
   constexpr int MQ = MI / 2, NQ = NI / 2;
   constexpr int QN = WN / 2;
   using OB = Op256<LB, BN, QN>;
-  constexpr int IA = 5;                    // image pieces (8 rows, 1 KB) per wave
-  constexpr int AIMG = IA * 8 * 1024;      // one image buffer: 320 rows of 128 B
+  constexpr int IA = 6;                    // image pieces (64 slots of 16 B) per wave
+  constexpr int NPMAX = 43;                // pieces of the largest image (272 rows x 10 slots)
+  constexpr int AIMG = NPMAX * 1024;       // one image buffer
+  constexpr int PITCH = 160;               // image row pitch (10 slots)
   constexpr int VB = 2 * OB::I;            // B DMA instructions of one K-tile
-  __shared__ __attribute__((aligned(1024))) char smem[2 * AIMG + 2 * OB::TB];
+  __shared__ __attribute__((aligned(1024))) char smem[2 * AIMG + 1024 + 2 * OB::TB];
 
   // ---- work item (as gemm256_kernel: XCD remap, grouped tile order)
   const int nwg = tiles_m * tiles_n;
@@ -77,34 +82,38 @@ __global__ __launch_bounds__(512) void gemm256hw_kernel(HaloWDesc a, LB lb, EPI 
   const __amdgpu_buffer_rsrc_t rb = lb.rsrc();
   const __amdgpu_buffer_rsrc_t ra = mk_rsrc(a.x, a.bytes);
   char* const sA = smem;
-  char* const sB = smem + 2 * AIMG;
+  char* const sDummy = smem + 2 * AIMG;   // destination of the pieces past the image (zeros)
+  char* const sB = smem + 2 * AIMG + 1024;
 
-  // ---- image DMA contexts: piece i of this wave fills image rows j = 8 (IA wid + i) + lane / 8
+  // ---- image DMA contexts: lane l of piece q = IA wid + i fills slot 64 q + l = (row j, chunk c)
   const int W2 = a.Wo + 2, Wi = a.Wo, Hi = a.Ho;
   const int IR = (BM >> a.lwo) * W2;       // image rows in use
+  const int NP = (IR * 10 + 63) >> 6;      // pieces in use (<= NPMAX)
   const int orow0 = m0 >> a.lwo;           // the tile's first output row (b Ho + ho)
-  // per piece: element offset of (b, ho, wcol, lane's chunk) in bits 0-28 (host: x < 2^30 bytes),
-  // bit 29 + kh set when the input row ho + kh - 1 exists (one register per piece)
+  // per piece: element offset of (b, ho, wcol, chunk c) in bits 0-28 (host: x < 2^30 bytes), bit 29 + kh
+  // set when that input row exists and the slot is a real chunk of a real column (one register per piece)
   uint32_t actx[IA];
 #pragma unroll
   for (int i = 0; i < IA; ++i) {
-    const int j = (wid * IA + i) * 8 + (lane >> 3);
+    const int sl = (wid * IA + i) * 64 + lane;
+    const int j = (sl * 0xCCCD) >> 19, c = sl - 10 * j;   // sl / 10 (sl < 2^14)
     const int q = j / W2, wcol = j - q * W2 - 1, orow = orow0 + q;
     const int b = orow / a.Ho, ho = orow - b * a.Ho;
-    const bool ok = j < IR && orow < a.B * a.Ho && wcol >= 0 && wcol < Wi;
+    const bool ok = c < 8 && j < IR && orow < a.B * a.Ho && wcol >= 0 && wcol < Wi;
     uint32_t mk = 0;
 #pragma unroll
     for (int kh = 0; kh < 3; ++kh)
       if (ok && (unsigned)(ho + kh - 1) < (unsigned)Hi) mk |= 1u << (29 + kh);
-    // offset of the kh = 1 row (b, ho, wcol): non-negative whenever a row bit is set (wcol >= 0)
-    actx[i] = mk | ((uint32_t)(((b * Hi + ho) * Wi + wcol) * a.Ci + (((lane & 7) ^ (j & 7)) << 3)) & 0x1fffffffu);
+    // the kh = 1 row's offset: non-negative whenever a row bit is set
+    actx[i] = mk | ((uint32_t)(((b * Hi + ho) * Wi + wcol) * a.Ci + c * 8) & 0x1fffffffu);
   }
   const int rowstride = Wi * a.Ci;
   auto issue_a = [&](int i, int buf, int kh, int cb) __attribute__((always_inline)) {
-    const uint32_t c = actx[i];
-    const uint32_t voff = ((c >> (29 + kh)) & 1u)
-                              ? (uint32_t)((int)(c & 0x1fffffffu) + (kh - 1) * rowstride + cb * 64) * 2u : OOB;
-    dma16(ra, sA + buf * AIMG + (wid * IA + i) * 1024, voff);
+    const uint32_t cx = actx[i];
+    const uint32_t voff = ((cx >> (29 + kh)) & 1u)
+                              ? (uint32_t)((int)(cx & 0x1fffffffu) + (kh - 1) * rowstride + cb * 64) * 2u : OOB;
+    const int pq = wid * IA + i;
+    dma16(ra, pq < NP ? sA + buf * AIMG + pq * 1024 : sDummy, voff);
   };
 
   f32x4 acc[MI][NI];
@@ -128,24 +137,21 @@ __global__ __launch_bounds__(512) void gemm256hw_kernel(HaloWDesc a, LB lb, EPI 
   if (stagger && wr == 1) raw_barrier();
 
   bf16x8 af[MQ][2], bfr[NI][2];
-  const int c16 = lane & 15, g4 = lane >> 4;
+  const uint32_t lbase = (uint32_t)((lane & 15) * PITCH + (lane >> 4) * 16);   // row c16, chunk g4
   // A fragments of quadrant H (rows wr*128 + H*64 + 16f + c16) at tap kw from image buffer ib
   auto read_a = [&](auto hc, auto fmc, int ib, int kw) __attribute__((always_inline)) {
     constexpr int H = decltype(hc)::value;
     constexpr uint32_t FM = decltype(fmc)::value;
-    const char* img = sA + ib * AIMG;
 #pragma unroll
     for (int f = 0; f < MQ; ++f)
       if ((FM >> (H * MQ + f)) & 1u) {
         const int rbf = wr * WM + H * (WM / 2) + f * 16;
-        // the fragment's first image row: wave-uniform, recomputed here (opaque to hoisting: 24
-        // loop-invariant lane addresses would not fit the register budget next to the accumulators)
-        int j0 = __builtin_amdgcn_readfirstlane(rbf + ((rbf >> a.lwo) << 1) + kw);
-        asm volatile("" : "+s"(j0));
-        const int j = j0 + c16;
-        const uint32_t ad = (uint32_t)j * 128u + ((uint32_t)(g4 ^ (j & 7)) << 4);
-        af[f][0] = *reinterpret_cast<const bf16x8*>(img + ad);
-        af[f][1] = *reinterpret_cast<const bf16x8*>(img + (ad ^ 64u));
+        // wave-uniform byte offset of the fragment's first row (opaque: not hoisted out of the K loop)
+        int u0 = ib * AIMG + (rbf + ((rbf >> a.lwo) << 1) + kw) * PITCH;
+        asm volatile("" : "+s"(u0));
+        const char* p = sA + lbase + u0;
+        af[f][0] = *reinterpret_cast<const bf16x8*>(p);
+        af[f][1] = *reinterpret_cast<const bf16x8*>(p + 64);
       }
   };
 
@@ -169,7 +175,10 @@ __global__ __launch_bounds__(512) void gemm256hw_kernel(HaloWDesc a, LB lb, EPI 
         issue_a(1, ib ^ 1, khn, cbn);
       }
     } else if constexpr (P == 1) {
-      if (nu) issue_a(3, ib ^ 1, khn, cbn);
+      if (nu) {
+        issue_a(3, ib ^ 1, khn, cbn);
+        issue_a(4, ib ^ 1, khn, cbn);
+      }
     }
     lds_wait_all();
     raw_barrier();
@@ -188,7 +197,7 @@ __global__ __launch_bounds__(512) void gemm256hw_kernel(HaloWDesc a, LB lb, EPI 
     if constexpr (P == 0) {
       if (nu) issue_a(2, ib ^ 1, khn, cbn);
     } else if constexpr (P == 1) {
-      if (nu) issue_a(4, ib ^ 1, khn, cbn);
+      if (nu) issue_a(5, ib ^ 1, khn, cbn);
     }
     lds_wait_all();
     raw_barrier();
@@ -224,7 +233,7 @@ __global__ __launch_bounds__(512) void gemm256hw_kernel(HaloWDesc a, LB lb, EPI 
         if (nu) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(VB + 3) : "memory");
         else asm volatile("s_waitcnt vmcnt(%0)" ::"i"(VB) : "memory");
       } else if constexpr (P == 1) {
-        if (nu) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(VB + 2) : "memory");
+        if (nu) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(VB + 3) : "memory");
         else asm volatile("s_waitcnt vmcnt(%0)" ::"i"(VB) : "memory");
       } else {
         asm volatile("s_waitcnt vmcnt(%0)" ::"i"(VB) : "memory");
@@ -293,7 +302,7 @@ __global__ __launch_bounds__(512) void gemm256hw_kernel(HaloWDesc a, LB lb, EPI 
 }
 
 // the W-halo kernel takes a 3x3 / stride-1 / pad-1 geometry with Ci % 64 == 0 and Wo a power of two in
-// [32, 256] (then 256 output rows are whole output rows and the image fits IA pieces per wave)
+// [32, 256] (then 256 output rows are whole output rows and the image fits NPMAX pieces)
 inline int halo_w_log2(int Wo) {
   for (int l = 5; l <= 8; ++l)
     if (Wo == (1 << l)) return l;

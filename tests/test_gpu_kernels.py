@@ -309,6 +309,7 @@ def test_conv_fwd_dgrad_wgrad(cfg, dtype):
         # M = 8448 per class vs 16896 for the full dgrad) — so those agree to fp32 summation order
         # (bf16 outputs within one rounding step). The row-class and skip comparisons hold the
         # quantization rule off.
+        halo_w = k == (3, 3) and s == (1, 1) and p == (1, 1) and Ci % 64 == 0 and W in (32, 64, 128, 256)
         for key in (L.OPT_ROW_CLASS, L.OPT_PAD_SKIP, L.OPT_QUANT_TILE):
             outs = []
             for v in (1, 0):
@@ -328,7 +329,13 @@ def test_conv_fwd_dgrad_wgrad(cfg, dtype):
                 finally:
                     L.call("crnn_set_option", key, 1)
                     L.call("crnn_set_option", L.OPT_QUANT_TILE, 1)
-            assert torch.equal(outs[0][0], outs[1][0])
+            if key == L.OPT_QUANT_TILE and halo_w:
+                # the W-halo kernel (gemm256hw.hpp) sums K in (kh, channel block, kw) order, the 128-row
+                # kernel the rule may pick in (kh, kw, channel) order: fp32 summation order apart
+                a, b = outs[0][0].float(), outs[1][0].float()
+                assert float((a - b).abs().max()) <= 2 ** -7 * float(b.abs().max()) and relerr(a, b) < 2e-3, key
+            else:
+                assert torch.equal(outs[0][0], outs[1][0]), key
             if key == L.OPT_PAD_SKIP:
                 assert torch.equal(outs[0][1], outs[1][1])
             else:

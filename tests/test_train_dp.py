@@ -1,11 +1,13 @@
 """run_training with world_size 2 (SURVEY §5 "Config" world_size, §8e): two
 processes on the box's one GPU (gloo over device tensors, per-step BiLSTM launches: the persistent
 sweeps need the whole chip), launched the way torchrun would (RANK / WORLD_SIZE / MASTER_* in the
-env). Checked against a single-process emulation of the same job: the same batches dealt to the two
-"ranks", each step's two shard gradients accumulated in one process and applied as their mean. BN
-keeps per-shard batch statistics in both, so the emulation is the DP step's definition; only the
-order of fp32 additions differs (bf16 noise in the weights). Reference: training/train.py:179-235,
-:493-518."""
+env). With CRNN_SHARE_DEVICE=1 run_training gives the ranks the device in turn for their forward /
+backward and optimizer step (kernels of two processes sharing one GPU are not bit-reproducible,
+DESIGN.md §6); the overlapped all-reduce still runs as in deployment. Checked against a single-process
+emulation of the same job: the same batches dealt to the two "ranks", each step's two shard gradients
+accumulated in one process and applied as their mean. BN keeps per-shard batch statistics in both, so
+the emulation is the DP step's definition: measured |dp - emulation| / |update| = 1.5e-10 after two
+epochs (profiles/r04o_dp.log). Reference: training/train.py:179-235, :493-518."""
 import json
 import os
 import socket
@@ -133,4 +135,4 @@ def test_run_training_world2_matches_single_process_emulation(tmp_path):
     upd = float((em - p0.cpu()).norm())
     rel = float((dp - em).norm()) / upd
     print(f"DP vs emulation: |dp - emu| / |update| = {rel:.3e} (update norm {upd:.3e})")
-    assert upd > 0 and rel < 2e-2, rel
+    assert upd > 0 and rel < 1e-6, rel
