@@ -758,9 +758,10 @@ int launch_fwd256(const Geo& g, const FwdA<bf16, true>& la, const RowMajorK<bf16
   const bool skip = pad_skip_ok(g, g.Ho, g.Wo);
   const int lwo = halo_w_lwo(g);
   // (the image contexts pack element offsets in 29 bits; the padding-skip form with the BN-backward tile
-  // hook at BN = 256 exceeds the 256-register budget inside the K loop, so the stride-1 dgrads of 4-row maps
-  // at BN = 256 — with or without the hook, so that both forms sum in one order — keep the K-tile images)
-  if (lwo >= 0 && la.bytes < (1u << 30) && !(dgrad && skip && bn == 256)) {
+  // hook at BN = 256 exceeds the 256-register budget inside the K loop: the K-tile images there, so on
+  // 4-row maps the dgrad's plain and BN-ReLU forms sum K in different orders)
+  (void)dgrad;
+  if (lwo >= 0 && la.bytes < (1u << 30) && !(gemm::has_tile_hook<EPI>::value && skip && bn == 256)) {
     const gemm::HaloWDesc a{la.x, la.bytes, g.B, g.Ho, g.Wo, g.Ci, lwo, g.Ci / 64};
     if (skip) {
       if (bn == 256) return gemm::launch256hw<256, 1>(a, lb, ep, M, N, st);

@@ -142,11 +142,15 @@ __global__ __launch_bounds__(512) void gemm256hw_kernel(HaloWDesc a, LB lb, EPI 
   auto read_a = [&](auto hc, auto fmc, int ib, int kw) __attribute__((always_inline)) {
     constexpr int H = decltype(hc)::value;
     constexpr uint32_t FM = decltype(fmc)::value;
+    // the wave's row base, opaque here: every uniform offset below is rebuilt per call by a few SALU
+    // ops instead of 24 loop-invariant SGPRs (which spill, through VGPR lanes, next to the accumulators)
+    int wbase = wr * WM;
+    asm volatile("" : "+s"(wbase));
 #pragma unroll
     for (int f = 0; f < MQ; ++f)
       if ((FM >> (H * MQ + f)) & 1u) {
-        const int rbf = wr * WM + H * (WM / 2) + f * 16;
-        // wave-uniform byte offset of the fragment's first row (opaque: not hoisted out of the K loop)
+        const int rbf = wbase + H * (WM / 2) + f * 16;
+        // wave-uniform byte offset of the fragment's first row
         int u0 = ib * AIMG + (rbf + ((rbf >> a.lwo) << 1) + kw) * PITCH;
         asm volatile("" : "+s"(u0));
         const char* p = sA + lbase + u0;
@@ -286,6 +290,9 @@ __global__ __launch_bounds__(512) void gemm256hw_kernel(HaloWDesc a, LB lb, EPI 
     row(std::integral_constant<uint32_t, M2>{}, 2);
   }
   if (stagger && wr == 0) raw_barrier();
+  // nothing of the epilogue (per-column BN constants of the tile hooks) is computed before this point
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
 
   // ---- epilogue (as gemm256_item)
   const int mr = lane & 15, nq = 4 * (lane >> 4);
