@@ -1324,11 +1324,11 @@ def test_bn_finalize_combine(rows, rpp, C, ticket):
     hand-off, Chan merges in double; CRNN_OPT_FIN_TICKET = 1: r03's ticketed chunk fold), more in two
     launches. Twice on ONE workspace, vs fp64; a ragged last partial (count not a multiple of rpp)."""
     L = _L()
-    L.call("crnn_set_option", 17, ticket)
+    L.call("crnn_set_option", L.OPT_FIN_TICKET, ticket)
     try:
         _bn_finalize_combine(L, rows, rpp, C)
     finally:
-        L.call("crnn_set_option", 17, 0)
+        L.call("crnn_set_option", L.OPT_FIN_TICKET, 0)
 
 
 def _bn_finalize_combine(L, rows, rpp, C):
