@@ -4,7 +4,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
-T=${TAG:-r04z}
+T=${TAG:-r04zz}
 mkdir -p gpurun_out
 if [ "$PART" != "bench" ]; then
 timeout -k 10 1000 python -u -m pytest tests -m gpu -q --timeout 240 --timeout-method thread > gpurun_out/${T}_pytest.log 2>&1
