@@ -477,6 +477,75 @@ TW_CONVS = [
 ]
 
 
+# W-halo A image kernel (gemm256hw.hpp) geometries beyond the model's: output width 256 / 32 / 64 / 128,
+# 4-row maps with a ragged last tile (BN = 128), tiles that span a sample boundary mid-sample (Ho = 6),
+# Ci = 64 / 128 / 256 (1 / 2 / 4 channel blocks per image)
+HALO_W_CONVS = [
+    # B, Ci, H, W, Co
+    (48, 64, 8, 256, 128),
+    (40, 128, 8, 32, 256),
+    (131, 256, 4, 32, 128),
+    (44, 64, 6, 64, 64),
+    (20, 128, 16, 128, 128),
+]
+
+
+@pytest.mark.parametrize("geo", HALO_W_CONVS)
+def test_conv_halo_w_kernel(geo):
+    """3x3 / stride-1 / pad-1 conv forward (with the BN partial sums) and the stride-1 input gradient on
+    the forward path, with the W-halo kernel (CRNN_OPT_CONV_HALO_W = 1) against the K-tile-image kernel
+    (0) and torch fp32: the two kernels sum K in different orders, so they agree to fp32 summation order
+    (bf16 outputs within one rounding step); both within bf16 rounding of torch."""
+    L = _L()
+    B, Ci, H, W, Co = geo
+    g = torch.Generator().manual_seed(B + Ci + W)
+    x = torch.randn(B, Ci, H, W, generator=g).bfloat16().float()
+    w = (torch.randn(Co, Ci, 3, 3, generator=g) / math.sqrt(Ci * 9)).bfloat16().float()
+    dy = torch.randn(B, Co, H, W, generator=g).bfloat16().float()
+    xr = x.clone().requires_grad_(True)
+    y_ref = F.conv2d(xr, w, padding=1)
+    (y_ref * dy).sum().backward()
+    y_ref = y_ref.detach().permute(0, 2, 3, 1).contiguous()
+    dx_ref = xr.grad.permute(0, 2, 3, 1).contiguous()
+    dt, st = L.BF16, L.stream_ptr()
+    d = L.ConvDesc(B, H, W, Ci, H, W, Co, 3, 3, 1, 1, 1, 1, Ci)
+    xd = to_nhwc(x, None, torch.bfloat16)
+    dyd = to_nhwc(dy, None, torch.bfloat16)
+    wdev = w.to(DEV).contiguous()
+    wd = torch.empty(Co, 3, 3, Ci, dtype=torch.bfloat16, device=DEV)
+    L.call("crnn_pack_conv_weight", dt, wdev.data_ptr(), wd.data_ptr(), Co, Ci, 3, 3, Ci, st)
+    job = L.PackJob(L.PACK_CONV_T, 0, Co, Ci, 3, 3, 0, 0, 0, wdev.data_ptr(), None, None, 0)
+    wt = torch.empty(Ci, 3, 3, Co, dtype=torch.bfloat16, device=DEV)
+    job.dst = wt.data_ptr()
+    tab = torch.frombuffer(bytearray(bytes(job)), dtype=torch.uint8).to(DEV)
+    L.call("crnn_pack_conv_t_batch", dt, tab.data_ptr(), 1, L.lib().crnn_pack_conv_t_tiles(Co, Ci), st)
+    rows = L.lib().crnn_conv_stat_rows(dt, d)
+    outs = {}
+    for v in (0, 1):
+        L.call("crnn_set_option", L.OPT_CONV_HALO_W, v)
+        try:
+            y = torch.empty(B, H, W, Co, dtype=torch.bfloat16, device=DEV)
+            ps, pq = torch.zeros(rows, Co, device=DEV), torch.zeros(rows, Co, device=DEV)
+            L.call("crnn_conv_fwd", dt, d, xd.data_ptr(), wd.data_ptr(), y.data_ptr(), ps.data_ptr(), pq.data_ptr(), st)
+            dx = torch.empty(B, H, W, Ci, dtype=torch.bfloat16, device=DEV)
+            if L.lib().crnn_conv_dgrad_tw_rows(dt, d) > 0:
+                L.call("crnn_conv_dgrad_tw", dt, d, dyd.data_ptr(), wt.data_ptr(), dx.data_ptr(), None, None, 0, st)
+            else:
+                L.call("crnn_conv_dgrad", dt, d, dyd.data_ptr(), wd.data_ptr(), dx.data_ptr(), None, None, 0, st)
+            torch.cuda.synchronize()
+            outs[v] = (y.float().cpu(), ps.sum(0).cpu(), dx.float().cpu())
+        finally:
+            L.call("crnn_set_option", L.OPT_CONV_HALO_W, 1)
+    for v in (0, 1):
+        y, s, dx = outs[v]
+        assert relerr(y, y_ref) < 1e-2, (v, relerr(y, y_ref))
+        assert relerr(s, y_ref.reshape(-1, Co).sum(0)) < 1e-2
+        assert relerr(dx, dx_ref) < 1e-2, (v, relerr(dx, dx_ref))
+    for i in (0, 2):
+        a_, b_ = outs[1][i], outs[0][i]
+        assert float((a_ - b_).abs().max()) <= 2 ** -7 * float(b_.abs().max()) and relerr(a_, b_) < 2e-3, i
+
+
 @pytest.mark.parametrize("geo", TW_CONVS)
 def test_conv_dgrad_tw_forward_path(geo):
     """stride-1 dgrad on the forward conv path (crnn_conv_dgrad_tw / _bnrelu_tw) with the transposed,
