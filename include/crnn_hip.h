@@ -543,6 +543,17 @@ int crnn_sgd_step(float* p, const float* g, float* momentum_buf, long n, float l
 int crnn_adamw(float* p, const float* g, float* m, float* v, long n, float lr, float beta1, float beta2, float eps,
                float weight_decay, int step, float grad_scale, void* stream);
 
+/* ------------------------------------------------------------------ diagnostics (not on any model path)
+ * LDS sentinel: `blocks` workgroups of 256 threads, each filling lds_bytes of dynamic LDS with a
+ * known pattern and re-checking it `iters` times (sleep x 127*64 cycles between checks), so that a
+ * kernel running concurrently on another stream can be checked for LDS writes outside its own
+ * allocation. out (crnn_diag_lds_sentinel_words() u32, zeroed by the caller): [0] mismatching
+ * words, [1] records taken, [2] waves that saw one, [3] checks done; then records of 8 words
+ * {index, got, expected, HW_ID, LDS_ALLOC, XCC_ID, check, block}. */
+int crnn_diag_lds_sentinel(unsigned* out, int blocks, int lds_bytes, int iters, unsigned seed, int sleep,
+                           void* stream);
+int crnn_diag_lds_sentinel_words(void);
+
 #ifdef __cplusplus
 }
 #endif

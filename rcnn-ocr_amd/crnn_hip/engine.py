@@ -36,6 +36,17 @@ STAGES = [("layer1", 1, 2, 128, 256), ("layer2", 2, 1, 256, 256),
           ("layer3", 5, 2, 256, 512), ("layer4", 3, 1, 512, 512)]
 
 
+def dropout_seed(base: int) -> int:
+    """the engine's dropout mask stream seed: torch's initial seed, with the data-parallel rank mixed in
+    when a process group of more than one rank is up (run_training seeds every rank alike, so without the
+    rank the replicas would draw identical masks, unlike independent per-replica dropout)"""
+    seed = base & 0xFFFFFFFFFFFFFFFF
+    import torch.distributed as tdist
+    if tdist.is_available() and tdist.is_initialized() and tdist.get_world_size() > 1:
+        seed ^= ((tdist.get_rank() + 1) * 0x94D049BB133111EB) & 0xFFFFFFFFFFFFFFFF
+    return seed
+
+
 def round8(n: int) -> int:
     return (n + 7) // 8 * 8
 
@@ -170,7 +181,7 @@ class CRNNEngine:
         self._side_stream = None
         self.debug = False      # when set, backward keeps copies of block-boundary gradients
         self._last_partials = None  # (psum, rows, rows_per_partial) of the latest training-mode conv
-        self._drop_seed = int(torch.initial_seed()) & 0xFFFFFFFFFFFFFFFF  # enc_dropout mask stream
+        self._drop_seed = dropout_seed(int(torch.initial_seed()))  # enc_dropout mask stream (per replica)
         self._drop_calls = 0
         self.dbg: Dict[str, torch.Tensor] = {}
 
@@ -1179,6 +1190,10 @@ class CRNNEngine:
             # one pass over (dy, y, z2) for the SE gate gradient AND the BN2 sums (crnn_hip.h)
             call("crnn_se_bn_bwd_reduce", dt, ptr(dyse), ptr(sb["y"]), ptr(sb["z2"]), ptr(sb["m2"]), ptr(sb["i2"]),
                  ptr(self.p[bn2 + ".weight"]), ptr(self.p[bn2 + ".bias"]), ptr(ds), ptr(abc), B, HW, P, s)
+            if self.debug:   # the SE chain kernel by kernel (tools/cohab_model.py localises differences)
+                for k, v in (("y", sb["y"]), ("z2", sb["z2"]), ("m2", sb["m2"]), ("i2", sb["i2"]), ("s", sb["s"]),
+                             ("hid", sb["hid"]), ("pooled", sb["pooled"]), ("1_ds", ds), ("1_abc", abc)):
+                    self.dbg[f"se.b{bi}.{k}"] = v.clone()
             dsig = ws.get(f"se.dsig{P}", (B, P), torch.float32)
             dhid = ws.get(f"se.dhid{P}", (B, Cr), torch.float32)
             dpool = ws.get(f"se.dpool{P}", (B, P), torch.float32)
@@ -1190,10 +1205,20 @@ class CRNNEngine:
                  ptr(dsig), ptr(dhid), ptr(dpool), ptr(self._gview(blk.prefix + ".se.fc.0.weight")),
                  ptr(self._gview(blk.prefix + ".se.fc.2.weight")), ptr(abc), ptr(pg2), ptr(pgx2), B, P, Cr, HW, acc,
                  s)
+            if self.debug:
+                for k, v in (("2_dsig", dsig), ("2_dhid", dhid), ("2_dpool", dpool), ("2_pg", pg2), ("2_pgx", pgx2),
+                             ("2_dw1", self._gview(blk.prefix + ".se.fc.0.weight")),
+                             ("2_dw2", self._gview(blk.prefix + ".se.fc.2.weight"))):
+                    self.dbg[f"se.b{bi}.{k}"] = v.clone()
             dz2 = self._dz(f"b{bi}.c2", bufs[o1], Mo * P)
             self._bn_bwd(3, dyse, sb["z2"], (sb["m2"], sb["i2"], sb["sc2"], sb["sh2"]), blk.conv2.bn, Mo, P, HW=HW,
                          y=sb["y"], se=sb["s"], dpool=dpool, out=dz2, accumulate_params=accumulate,
                          sums=(pg2, pgx2, B))
+            if self.debug:
+                for k, v in (("3_mg", ws.get("bnb.mg", (512,), torch.float32)),
+                             ("3_mgx", ws.get("bnb.mgx", (512,), torch.float32)),
+                             ("3_dgamma", self.g[bn2 + ".weight"]), ("3_dz2", dz2)):
+                    self.dbg[f"se.b{bi}.{k}"] = v.clone()
             self._wgrad(blk.conv2, dz2, sb["a1"], B, ho, wo)
             da1 = bufs[o2][: Mo * P]
             d2 = blk.conv2.desc(B, ho, wo)
