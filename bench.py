@@ -39,6 +39,9 @@ def parse():
     ap.add_argument("--layers", type=int, default=2)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-sub", action="store_true",
+                    help="default train line only: skip the configs[1] inference and configs[4] long-line "
+                         "sub-measurements that a 1-GPU run attaches as sub_measurements")
     ap.add_argument("--cpu-sample", type=int, default=None,
                     help="batch of the CPU baseline sample (default: the bench batch, B=256, as BASELINE.md)")
     ap.add_argument("--cpu-steps", type=int, default=1, help="timed CPU steps (after one warm-up at B=32)")
@@ -305,7 +308,37 @@ def main():
     torch.cuda.set_device(dev)
     if args.mode == "preprocess":
         return bench_preprocess(args, world, rank, dev)
+    out = measure(args, world, rank, dev)
+    if rank == 0 and world == 1 and args.mode == "train" and args.config is None and not args.no_sub:
+        # BASELINE configs[1] (inference) and configs[4] (long lines) as sub-measurements of the default line,
+        # so that the driver's own run observes them; each with its own rooflines and a
+        # bounded CPU-oracle sample
+        import copy
+        subs = {}
+        for key, mode, cfg, steps, cpu_b in (("configs1_infer", "infer", None, 20, 256),
+                                              ("configs4_long", "train", "long", 10, 8)):
+            a = copy.copy(args)
+            a.mode, a.config, a.steps, a.warmup, a.cpu_sample = mode, cfg, steps, 3, cpu_b
+            if cfg == "long":
+                a.width, a.hidden, a.layers, a.batch = 1024, 768, 4, 64
+            t0 = time.perf_counter()
+            r = measure(a, world, rank, dev)
+            r["wall_s"] = round(time.perf_counter() - t0, 1)
+            subs[key] = {k: r[k] for k in ("metric", "value", "unit", "ms_per_step", "steps", "warmup", "dtype",
+                                           "config", "roofline", "roofline_lstm", "cpu_baseline", "wall_s")
+                         if k in r}
+            torch.cuda.empty_cache()
+        out["sub_measurements"] = subs
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
+
+def measure(args, world, rank, dev):
+    """build the model for args, time args.steps steps after args.warmup (barrier + synchronize around the
+    timed region, max over ranks) -> the bench line's dict on rank 0 (None on the other ranks)"""
+    from crnn_hip import dist as D
     from crnn_hip.ctc import ctc_loss
     from crnn_hip.optim import FusedAdamW
     from crnn_hip.recipe import recipe_state_dict, synthetic_batch
@@ -334,7 +367,7 @@ def main():
     inv_world = 1.0 / world
     # DP: bucketed RCCL all-reduce of the flat gradient, issued stage by stage during the backward
     # (head / BiLSTM first, stem last) so it overlaps the remaining backward kernels
-    reducer = D.OverlappedAllReduce(model._flat_grad, model.flat_offsets()) if world > 1 else None
+    reducer = D.OverlappedAllReduce(model._flat_grad, model.flat_offsets(), timing=True) if world > 1 else None
     model.stage_done = reducer.ready if reducer is not None else None   # the API path's backward hook
 
     ids = torch.empty(args.batch, T, dtype=torch.int32, device=dev)
@@ -399,6 +432,8 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    if reducer is not None:
+        reducer.wait_events.clear()   # the exposed-wait events of the timed steps only
     eng.enable_timing(args.kernel_timing == "all")
     t0 = time.perf_counter()
     for i in range(args.steps):
@@ -424,6 +459,17 @@ def main():
         dist.all_reduce(cmax, op=dist.ReduceOp.MAX)
         dist.all_reduce(cmin, op=dist.ReduceOp.MIN)
         divergence = float((cmax - cmin).item())
+    dp_overlap = None
+    if reducer is not None:   # per-step exposed all-reduce wait of the compute stream, max over ranks
+        ex = torch.tensor([reducer.exposed_ms_per_step()], dtype=torch.float64, device=dev)
+        dist.all_reduce(ex, op=dist.ReduceOp.MAX)
+        nb, nbytes = reducer.buckets_per_step()
+        dp_overlap = {"exposed_allreduce_ms_per_step_max_rank": round(float(ex.item()), 4),
+                      "buckets_per_step": nb, "allreduce_bytes_per_step": nbytes,
+                      "bucket_mb": [round(b / 2 ** 20, 2) for b in reducer.last_bucket_bytes()],
+                      "exposed_note": "HIP events on the compute stream around finish()'s wait for the collective "
+                                      "stream (the all-reduce time NOT hidden under the backward), mean over the "
+                                      "timed steps"}
     lines = args.batch * world * args.steps
     value = lines / elapsed
     final_loss = float(loss.float().mean().item()) if args.mode in ("train", "attn_train") else 0.0
@@ -504,7 +550,7 @@ def main():
             **({"options": opts} if opts else {}),
             "dp": ({"allreduce": ("RCCL" if dist.get_backend() == "nccl" else dist.get_backend())
                     + " sum of the flat fp32 gradient, bucketed and overlapped with the backward",
-                    "param_checksum_spread": divergence} if world > 1 else None),
+                    "param_checksum_spread": divergence, **(dp_overlap or {})} if world > 1 else None),
         }
         if world == 1 and not args.no_cpu_baseline:
             try:
@@ -514,9 +560,8 @@ def main():
                 out["cpu_baseline"] = cpu_baseline(args, threads, shapes, ap_cpu)
             except Exception as e:  # report, never fake
                 out["cpu_baseline"] = {"value": None, "error": repr(e)}
-        print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+        return out
+    return None
 
 
 if __name__ == "__main__":

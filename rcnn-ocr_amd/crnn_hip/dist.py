@@ -77,8 +77,10 @@ class OverlappedAllReduce:
     that finishes out of layout order just waits until everything after it is final). Each issued
     bucket is recorded in `issued` as (lo, hi) for tests."""
 
-    def __init__(self, flat_grad: torch.Tensor, offsets, min_bucket_bytes: int = 8 << 20):
-        """offsets: {param name: (start, numel)} into flat_grad (the model's flat layout)."""
+    def __init__(self, flat_grad: torch.Tensor, offsets, min_bucket_bytes: int = 8 << 20, timing: bool = False):
+        """offsets: {param name: (start, numel)} into flat_grad (the model's flat layout).
+        timing: finish() brackets the compute stream's wait for the collectives with HIP events
+        (exposed_ms_per_step(): the all-reduce time the backward did not hide)."""
         self.flat = flat_grad
         self.offsets = offsets
         spans = sorted((s, s + n, k) for k, (s, n) in offsets.items())
@@ -95,6 +97,8 @@ class OverlappedAllReduce:
         self.issued = []
         self.last_issued = []
         self.stream = None   # the collective stream (HIP tensors)
+        self.timing = timing and flat_grad.is_cuda
+        self.wait_events = []   # (start, end) per finish() with timing
         self.reset()
 
     def reset(self):
@@ -146,8 +150,30 @@ class OverlappedAllReduce:
                 if missing:
                     raise RuntimeError(f"finish(): gradients never reported final: {missing[:4]}")
                 self._issue(0, self.hi)
+            ev = None
+            if self.timing:   # before the waits: a wait() may already order the caller's stream
+                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                ev[0].record(torch.cuda.current_stream(self.flat.device))
             for w in self.works:
                 w.wait()   # makes the collective stream wait for the collectives' completion
             if self.stream is not None:   # and the caller's stream for the collective stream
                 torch.cuda.current_stream(self.flat.device).wait_stream(self.stream)
+            if ev is not None:
+                ev[1].record(torch.cuda.current_stream(self.flat.device))
+                self.wait_events.append(ev)
         self.reset()
+
+    def exposed_ms_per_step(self) -> float:
+        """mean over the recorded finish() calls of the compute stream's wait for the collectives (ms);
+        synchronise first"""
+        if not self.wait_events:
+            return 0.0
+        return sum(a.elapsed_time(b) for a, b in self.wait_events) / len(self.wait_events)
+
+    def last_bucket_bytes(self):
+        return [(hi - lo) * self.flat.element_size() for lo, hi in self.last_issued]
+
+    def buckets_per_step(self):
+        """(bucket count, bytes) of the last completed step"""
+        b = self.last_bucket_bytes()
+        return len(b), sum(b)

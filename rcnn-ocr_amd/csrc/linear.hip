@@ -167,7 +167,10 @@ __global__ __launch_bounds__(1024) void colsum_kernel(const T* __restrict__ X, i
   __shared__ f32x4 red[1024];
   const int tid = threadIdx.x, q = tid & 3, rl = tid >> 2;
   const int n = blockIdx.x * 16 + 4 * q;
-  const bool okn = n < N;   // vec (ld % 4 == 0, ld >= N): the quarter's 4 loads stay inside the row
+  const bool okn = n < N;
+  // 16-B loads only for a quarter whose 4 columns are all < N (vec: ld % 4 == 0, 16-B aligned X): the
+  // last row of a strided view may end at column N, so a ragged last quarter loads element-wise
+  const bool vq = vec && n + 4 <= N;
   f32x4 s = {0.f, 0.f, 0.f, 0.f};
   for (long mb = rl; mb < M; mb += 8 * CS_RL) {
     f32x4 v[8];
@@ -177,7 +180,7 @@ __global__ __launch_bounds__(1024) void colsum_kernel(const T* __restrict__ X, i
       const bool ok = okn && m < M;
       // clamped address, masked value: the loads stay unconditional (all 8 in flight)
       const T* p = X + (size_t)(m < M ? m : M - 1) * ld + (okn ? n : 0);
-      if (vec) {
+      if (vq) {
         v[u] = ld4f<T>(p);
       } else {
 #pragma unroll

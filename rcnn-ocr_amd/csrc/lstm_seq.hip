@@ -830,6 +830,12 @@ static int seq_accum_status(unsigned* ws, int B, hipStream_t st, int rc) {
   return (int)hipGetLastError();
 }
 
+// clears the one-shot events on every path out of a sweep call: an early return (validation, memset failure)
+// must not leave handles armed that the caller may destroy before the next sweep records them
+struct SeqEvGuard {
+  ~SeqEvGuard() { g_seq_ev[0] = g_seq_ev[1] = nullptr; }
+};
+
 int crnn_lstm_seq_time_next(void* ev_start, void* ev_end) {
   g_seq_ev[0] = (hipEvent_t)ev_start;
   g_seq_ev[1] = (hipEvent_t)ev_end;
@@ -838,6 +844,7 @@ int crnn_lstm_seq_time_next(void* ev_start, void* ev_end) {
 
 int crnn_lstm_seq_fwd(const void* xg, const void* whh, void* hseq, void* gsv, float* csv, unsigned* ws, int B, int T,
                       int H, void* stream) {
+  const SeqEvGuard ev_guard;
   hipStream_t st = (hipStream_t)stream;
   int S, U;
   if (!seq_config(B, H, false, S, U)) return crnn_set_error(hipErrorInvalidValue, "lstm_seq: unsupported shape");
@@ -867,6 +874,7 @@ int crnn_lstm_seq_fwd(const void* xg, const void* whh, void* hseq, void* gsv, fl
 
 int crnn_lstm_seq_bwd(const void* dhseq, const void* whh_t, const void* gsv, const float* csv, void* dgates,
                       unsigned* ws, int B, int T, int H, void* stream) {
+  const SeqEvGuard ev_guard;
   hipStream_t st = (hipStream_t)stream;
   int S, U;
   if (!seq_config(B, H, true, S, U)) return crnn_set_error(hipErrorInvalidValue, "lstm_seq: unsupported shape");

@@ -232,14 +232,42 @@ def _dp_setup(cfg, device: str):
     return world, rank, dev
 
 
+_BN_STATS = ("running_mean", "running_var")
+
+
+def sync_bn_stats(model, world: int) -> None:
+    """data parallel: every rank normalises with its own batch statistics (BatchNorm2d, no SyncBN), so the
+    ranks' running_mean / running_var drift apart while the replicas' weights stay identical. Before eval
+    and checkpointing they are replaced by their mean over the ranks (all-reduce in fp64), so every rank
+    evaluates the same model and rank 0 saves the job's statistics."""
+    if world <= 1:
+        return
+    import torch.distributed as tdist
+    bufs = [b for n, b in model.named_buffers() if n.endswith(_BN_STATS)]
+    if not bufs:
+        return
+    flat = torch.cat([b.detach().reshape(-1).double() for b in bufs])
+    tdist.all_reduce(flat)
+    flat /= world
+    off = 0
+    with torch.no_grad():
+        for b in bufs:
+            n = b.numel()
+            b.copy_(flat[off:off + n].view_as(b).to(b.dtype))
+            off += n
+
+
 def ctc_infeasible(ids: torch.Tensor, lens: torch.Tensor, T: int) -> int:
     """samples whose CTC alignment cannot exist at T frames: label length + repeated neighbours > T
-    (torch's ctc_loss gives +inf there and zero_infinity zeroes the sample's loss and gradient)"""
-    n = 0
-    for row, L in zip(ids.tolist(), lens.tolist()):
-        need = L + sum(1 for a, b in zip(row[:L], row[1:L]) if a == b)
-        n += need > T
-    return n
+    (torch's ctc_loss gives +inf there and zero_infinity zeroes the sample's loss and gradient).
+    Vectorised: equal neighbours (k, k+1) counted where k + 1 < len."""
+    ids = torch.as_tensor(ids)
+    lens = torch.as_tensor(lens).reshape(-1).to(ids.device)
+    if ids.ndim != 2 or ids.shape[1] < 2:
+        return int((lens > T).sum())
+    k = torch.arange(1, ids.shape[1], device=ids.device)
+    rep = ((ids[:, 1:] == ids[:, :-1]) & (k[None, :] < lens[:, None])).sum(1)
+    return int(((lens + rep) > T).sum())
 
 
 def run_training(cfg: Config, device: str = "cuda") -> Dict[str, object]:
@@ -363,7 +391,7 @@ def run_training(cfg: Config, device: str = "cuda") -> Dict[str, object]:
 
     def train_loss(x, labels):
         if decoder == "ctc":
-            ids, lens, _ = ctc_refs(labels)
+            ids, lens = ctc_targets(labels, stoi, max_len)
             logits = model(x)
             infeasible[0] += ctc_infeasible(ids, lens, logits.shape[1])
             return ctc_loss(logits, ids, lens)
@@ -472,6 +500,7 @@ def run_training(cfg: Config, device: str = "cuda") -> Dict[str, object]:
         if infeasible[0]:
             logger.info(f"epoch {epoch}: {infeasible[0]} training samples have no CTC alignment at the model's "
                         f"frame count (label + repeats > T); zero_infinity zeroed their loss and gradient")
+        sync_bn_stats(model, world)   # before eval / checkpoints: one set of running statistics for the job
         should_eval = ((epoch - start_epoch) % eval_every == 0) or (epoch == epochs)
         avg_val_loss = val_acc = val_cer = val_wer = None
         if should_eval:
@@ -500,7 +529,8 @@ def run_training(cfg: Config, device: str = "cuda") -> Dict[str, object]:
             val_cer = sum(character_error_rate(r, h) for r, h in zip(refs_all, hyps_all)) / n
             val_wer = sum(word_error_rate(r, h) for r, h in zip(refs_all, hyps_all)) / n
         if world > 1:   # the replicas must hold the same weights: report the spread of their checksums
-            c = model._flat_param.detach().double().sum().reshape(1)
+            c = (model._flat_param.detach().double().sum() + sum(
+                b.detach().double().sum() for n, b in model.named_buffers() if n.endswith(_BN_STATS))).reshape(1)
             cmax, cmin = c.clone(), c.clone()
             tdist.all_reduce(cmax, op=tdist.ReduceOp.MAX)
             tdist.all_reduce(cmin, op=tdist.ReduceOp.MIN)

@@ -1,4 +1,4 @@
-"""world_size-2 gloo tests of the data-parallel glue (crnn_hip/dist.py) on CPU.
+"""world_size-2 and -4 gloo tests of the data-parallel glue (crnn_hip/dist.py) on CPU.
 
 The HIP compute path has no CPU fallback, so these exercise what DP adds on top of it:
 the bucketed gradient all-reduce and the parameter broadcast, and check the DP identity on
@@ -32,9 +32,10 @@ def _worker(rank, world, port, q):
     D.init_from_env("gloo")
     try:
         # bucketed all-reduce: tiny buckets force many collectives in flight
+        tri = world * (world + 1) // 2   # sum over ranks of (rank + 1)
         g = torch.arange(1000, dtype=torch.float32) * (rank + 1)
         D.allreduce_grads(g, bucket_bytes=4 * 37)
-        ok_sum = torch.allclose(g, torch.arange(1000, dtype=torch.float32) * 3)
+        ok_sum = torch.allclose(g, torch.arange(1000, dtype=torch.float32) * tri)
         # broadcast from rank 0
         p = torch.full((17,), float(rank + 5))
         D.broadcast_params(p)
@@ -46,9 +47,9 @@ def _worker(rank, world, port, q):
         shapes = [(k, s) for k, s in O.param_shapes(16, 10, 1, enc_dim=24) if k.startswith(("enc_rnn", "ctc_head"))]
         sd = recipe_state_dict(shapes, 7)
         gen = torch.Generator().manual_seed(3)
-        x = torch.randn(4, 6, 24, generator=gen)
-        tg = torch.randint(1, 10, (4, 3), generator=gen)
-        tl = torch.tensor([3, 2, 1, 3])
+        x = torch.randn(2 * world, 6, 24, generator=gen)
+        tg = torch.randint(1, 10, (2 * world, 3), generator=gen)
+        tl = torch.tensor([3, 2, 1, 3] * ((world + 1) // 2))[: 2 * world]
 
         def grads(xs, ts, ls):
             p = {k: v.clone().requires_grad_(True) for k, v in sd.items()}
@@ -72,7 +73,7 @@ def _worker(rank, world, port, q):
             for pre in (["ctc_head.", "enc_rnn."], ["cnn.conv_out."], ["cnn.layer1.0."], ["cnn.conv0."]):
                 red.ready(pre)
             red.finish()
-            ok_ov = ok_ov and torch.allclose(g2, torch.arange(1000, dtype=torch.float32) * 3)
+            ok_ov = ok_ov and torch.allclose(g2, torch.arange(1000, dtype=torch.float32) * tri)
         # the REAL layout and stage order: RCNN.flat_offsets() and CRNNEngine.backward_stages() (the
         # sequence backward() reports), in order and shuffled; buckets must tile the buffer exactly
         # once, each issued only once all of its parameters were reported final
@@ -100,17 +101,25 @@ def _worker(rank, world, port, q):
                 spans = sorted(red.last_issued)
                 ok_real = ok_real and spans[0][0] == 0 and spans[-1][1] == n and all(
                     a[1] == b[0] for a, b in zip(spans, spans[1:]))
-                ok_real = ok_real and bool((g3 == 3).all())
-        q.put((rank, ok_sum, ok_bc, ok_dp and ok_ov and ok_real))
+                ok_real = ok_real and bool((g3 == tri).all())
+        # per-replica dropout streams: the engine's mask seed differs across ranks for the same torch seed
+        from crnn_hip.engine import dropout_seed
+        seeds = [None] * world
+        dist.all_gather_object(seeds, dropout_seed(1234))
+        ok_drop = len(set(seeds)) == world
+        q.put((rank, ok_sum, ok_bc, ok_dp and ok_ov and ok_real and ok_drop))
     finally:
         dist.destroy_process_group()
 
 
-def test_gloo_world2_allreduce_broadcast_and_dp_identity():
+@pytest.mark.parametrize("world", [2, 4])
+def test_gloo_allreduce_broadcast_and_dp_identity(world):
+    """world 2 and world 4: bucketed sum, broadcast, the DP identity on the oracle's
+    BiLSTM + head, and the overlapped reducer's bucket tiling on the model's real layout and stage order"""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in ps:
         p.start()
     res = [q.get(timeout=240) for _ in ps]
@@ -124,3 +133,10 @@ def test_buckets_cover_buffer():
     bs = buckets(1003, 4, 40)
     assert bs[0] == slice(0, 10) and bs[-1].stop == 1003
     assert sum(s.stop - s.start for s in bs) == 1003
+
+
+def test_dropout_seed_single_process_is_torch_seed():
+    """without a process group the enc_dropout mask seed is torch's initial seed (masks unchanged)"""
+    from crnn_hip.engine import dropout_seed
+    assert dropout_seed(1234) == 1234
+    assert dropout_seed(-1) == 0xFFFFFFFFFFFFFFFF

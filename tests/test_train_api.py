@@ -165,6 +165,9 @@ def test_ctc_infeasible_count():
     assert ctc_infeasible(ids, lens, 4) == 1
     assert ctc_infeasible(ids, lens, 3) == 3
     assert ctc_infeasible(ids, lens, 5) == 0
+    # repeats past the label length do not count
+    assert ctc_infeasible(torch.tensor([[5, 6, 6, 6]]), torch.tensor([2]), 2) == 0
+    assert ctc_infeasible(torch.tensor([[5, 6, 6, 6]]), torch.tensor([4]), 5) == 1
 
 
 def test_split_without_val_csvs_keeps_long_labels(tmp_path):
