@@ -89,7 +89,10 @@ enum { CRNN_OPT_GEMM_STAGGER = 0,    /* 256-row conv GEMM: waves 4-7 one barrier
                                         power-of-two width 32..256 on the 256-row kernel: 1 = one W-halo A image per
                                         (kernel row, 64-channel block) serves the three kw K-tiles (gemm256hw.hpp;
                                         default), 0 = an A image per K-tile (gemm256.hpp) */
-       CRNN_OPT_COUNT = 19 };
+       CRNN_OPT_LSTM_PIPE = 19,      /* persistent BiLSTM: bit 0 = forward sweep as two pipelined 16-sample groups x
+                                        32 units per workgroup (a group's hand-off travels while the workgroup
+                                        computes the other group), bit 1 = the same for the BPTT */
+       CRNN_OPT_COUNT = 20 };
 int crnn_set_option(int key, int value);
 /* current value of a tuning switch (0 for an unknown key) */
 int crnn_get_option(int key);
@@ -545,13 +548,15 @@ int crnn_adamw(float* p, const float* g, float* m, float* v, long n, float lr, f
 
 /* ------------------------------------------------------------------ diagnostics (not on any model path)
  * LDS sentinel: `blocks` workgroups of 256 threads, each filling lds_bytes of dynamic LDS with a
- * known pattern and re-checking it `iters` times (sleep x 127*64 cycles between checks), so that a
+ * known pattern and re-checking it `iters` times (sleep x 127*64 cycles between checks; mode bit 0:
+ * each check rewrites the allocation with a new pattern first, bit 1: each check also verifies a
+ * wave-wide __shfl_xor sum), so that a
  * kernel running concurrently on another stream can be checked for LDS writes outside its own
  * allocation. out (crnn_diag_lds_sentinel_words() u32, zeroed by the caller): [0] mismatching
  * words, [1] records taken, [2] waves that saw one, [3] checks done; then records of 8 words
  * {index, got, expected, HW_ID, LDS_ALLOC, XCC_ID, check, block}. */
 int crnn_diag_lds_sentinel(unsigned* out, int blocks, int lds_bytes, int iters, unsigned seed, int sleep,
-                           void* stream);
+                           int mode, void* stream);
 int crnn_diag_lds_sentinel_words(void);
 
 #ifdef __cplusplus

@@ -48,7 +48,7 @@ class PackJob(C.Structure):  # crnn_pack_job
 (OPT_GEMM_STAGGER, OPT_GEMM_PERSISTENT, OPT_DEEP_LINEAR, OPT_WGRAD_TILE, OPT_LSTM_TILE, OPT_HALO_CONV, OPT_LSTM_HANDOFF,
  OPT_WGRAD_REDUCE, OPT_WGRAD_FAST, OPT_ROW_CLASS, OPT_QUANT_TILE, OPT_PAD_SKIP, OPT_LSTM_BWD_PART,
  OPT_LSTM_L2_HANDOFF, OPT_GEMM4W, OPT_DIAG, OPT_DGRAD_GROUP, OPT_FIN_TICKET,
- OPT_CONV_HALO_W) = range(19)
+ OPT_CONV_HALO_W, OPT_LSTM_PIPE) = range(20)
 
 PACK_CONV, PACK_ROWS, PACK_ROWS_SUM, PACK_TRANSPOSE, PACK_CONV_T = 0, 1, 2, 3, 4
 
@@ -155,7 +155,7 @@ _SIGS = {
     "crnn_adamw": ([vp, vp, vp, vp, i64, f32, f32, f32, f32, f32, i32, f32, vp], i32),
     "crnn_adam_step": ([vp, vp, vp, vp, i64, f32, f32, f32, f32, f32, i32, f32, i32, vp, vp], i32),
     "crnn_sgd_step": ([vp, vp, vp, i64, f32, f32, f32, f32, i32, vp, vp], i32),
-    "crnn_diag_lds_sentinel": ([vp, i32, i32, i32, C.c_uint, i32, vp], i32),
+    "crnn_diag_lds_sentinel": ([vp, i32, i32, i32, C.c_uint, i32, i32, vp], i32),
     "crnn_diag_lds_sentinel_words": ([], i32),
 }
 

@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "crnn_internal.hpp"
+#include "common.hpp"
 
 namespace {
 
@@ -21,8 +22,12 @@ __device__ __forceinline__ uint32_t sentinel_word(uint32_t seed, uint32_t blk, u
 
 // out: [0] mismatching words seen (summed over checks), [1] records taken, [2] waves that saw one,
 //      [3] checks done; records from word 8: {index, got, expected, HW_ID, LDS_ALLOC, XCC_ID, check, block}
+// mode bit 0: every check first REWRITES the whole allocation with a pattern of its own (16-B stores),
+// barriers, then reads it back — a write lost or altered while other kernels' LDS traffic (LDS-DMA
+// landings, transposing reads) shares the CU shows as a mismatch; bit 1: every check also folds a
+// known per-lane value over the wave with __shfl_xor (ds_bpermute) and checks the sum
 __global__ __launch_bounds__(256) void lds_sentinel_kernel(uint32_t* out, int words, int iters, uint32_t seed,
-                                                           int sleep) {
+                                                           int sleep, int mode) {
   extern __shared__ uint32_t lds[];
   const uint32_t blk = blockIdx.x;
   for (int i = threadIdx.x; i < words; i += 256) lds[i] = sentinel_word(seed, blk, (uint32_t)i);
@@ -34,8 +39,31 @@ __global__ __launch_bounds__(256) void lds_sentinel_kernel(uint32_t* out, int wo
   uint32_t seen = 0;
   for (int it = 0; it < iters; ++it) {
     for (int s = 0; s < sleep; ++s) __builtin_amdgcn_s_sleep(127);
+    const uint32_t sd = (mode & 1) ? seed + 0x1000193u * (uint32_t)(it + 1) : seed;
+    if (mode & 1) {
+      __syncthreads();   // every wave's reads of the previous pattern are done
+      for (int i = 4 * threadIdx.x; i + 3 < words; i += 1024) {
+        u32x4 v;
+        for (int e = 0; e < 4; ++e) v[e] = sentinel_word(sd, blk, (uint32_t)(i + e));
+        *reinterpret_cast<u32x4*>(lds + i) = v;
+      }
+      __syncthreads();
+    }
+    if (mode & 2) {
+      float x = (float)((threadIdx.x & 63) + 1);
+      for (int o = 1; o < 64; o <<= 1) x += __shfl_xor(x, o, 64);
+      if (x != 2080.f) {   // 1 + ... + 64
+        ++seen;
+        const uint32_t slot = atomicAdd(out + 1, 1u);
+        if (slot < (uint32_t)SENT_REC) {
+          uint32_t* r = out + 8 + slot * SENT_REC_WORDS;
+          r[0] = 0xFFFFFFFFu; r[1] = __float_as_uint(x); r[2] = __float_as_uint(2080.f); r[3] = hw;
+          r[4] = la; r[5] = xcc; r[6] = (uint32_t)it; r[7] = blk;
+        }
+      }
+    }
     for (int i = threadIdx.x; i < words; i += 256) {
-      const uint32_t want = sentinel_word(seed, blk, (uint32_t)i);
+      const uint32_t want = sentinel_word(sd, blk, (uint32_t)i);
       const uint32_t got = lds[i];
       if (got != want) {
         ++seen;
@@ -60,7 +88,7 @@ __global__ __launch_bounds__(256) void lds_sentinel_kernel(uint32_t* out, int wo
 }  // namespace
 
 extern "C" int crnn_diag_lds_sentinel(unsigned* out, int blocks, int lds_bytes, int iters, unsigned seed, int sleep,
-                                      void* stream) {
+                                      int mode, void* stream) {
   if (!out || blocks <= 0 || lds_bytes < 1024 || lds_bytes > 160 * 1024 || (lds_bytes & 3) || iters < 0 || sleep < 0)
     return crnn_set_error((int)hipErrorInvalidValue, "crnn_diag_lds_sentinel: bad arguments");
   static bool attr = false;
@@ -69,7 +97,7 @@ extern "C" int crnn_diag_lds_sentinel(unsigned* out, int blocks, int lds_bytes, 
     attr = true;
   }
   hipLaunchKernelGGL(lds_sentinel_kernel, dim3(blocks), dim3(256), lds_bytes, (hipStream_t)stream, (uint32_t*)out,
-                     lds_bytes / 4, iters, (uint32_t)seed, sleep);
+                     lds_bytes / 4, iters, (uint32_t)seed, sleep, mode);
   return (int)hipGetLastError();
 }
 

@@ -1715,3 +1715,95 @@ def test_lstm_seq_l2_handoff_identical(BTH):
     for x, y in zip(outs[2], outs[0]):
         assert torch.isfinite(x.float()).all()
         assert torch.equal(x, y), BTH
+
+
+@pytest.mark.parametrize("BTH", [(128, 9, 512), (64, 20, 768), (32, 7, 256), (256, 32, 512)])
+def test_lstm_seq_fwd_pipelined_groups(BTH):
+    """Persistent BiLSTM forward with two pipelined 16-sample groups per workgroup (CRNN_OPT_LSTM_PIPE
+    bit 0, lstm_seq_fwd_pipe_kernel): per group the same loads, MFMA order and partial-sum order as the
+    one-group 16 x 32 tile (where that tile fits the chip: B = 128, H = 512; B = 64, H = 768; B = 32,
+    H = 256) and as the default tile at the bench's B = 256; the cell's fused multiply-adds are the
+    compiler's per kernel, so the comparison is to bf16 rounding carried through the recurrence (first
+    GPU run: not bit-identical). No timed-out wait, the counters complete ((H/32) * T per (direction,
+    32-sample slice))."""
+    L = _L()
+    B, T, H = BTH
+    g = torch.Generator().manual_seed(21)
+    xg = (torch.randn(B, T, 2, 4 * H, generator=g) * 0.7).to(DEV, torch.bfloat16)
+    whh = (torch.randn(2, 4 * H, H, generator=g) / H ** 0.5).to(DEV, torch.bfloat16)
+    st = L.stream_ptr()
+    outs = {}
+    try:
+        for pipe, force in ((1, 0), (0, 2), (0, 0)):
+            L.call("crnn_set_option", L.OPT_LSTM_PIPE, pipe)
+            L.call("crnn_set_option", L.OPT_LSTM_TILE, force)
+            if not L.lib().crnn_lstm_seq_supported(L.dtype_code(torch.bfloat16), B, H):
+                continue
+            S, U = seq_tile(B, H)
+            if pipe:
+                assert (S, U) == (32, 32)
+            elif force == 2 and (S, U) != (16, 32):
+                continue
+            hseq = torch.full((B, T, 2 * H), 3.0, dtype=torch.bfloat16, device=DEV)
+            gsv = torch.full((2, T, B, 4 * H), 3.0, dtype=torch.bfloat16, device=DEV)
+            csv = torch.full((2, T, B, H), 3.0, device=DEV)
+            ws = torch.full((L.lib().crnn_lstm_seq_workspace(B) // 4,), 7, dtype=torch.int32, device=DEV)
+            L.call("crnn_lstm_seq_fwd", xg.data_ptr(), whh.data_ptr(), hseq.data_ptr(), gsv.data_ptr(),
+                   csv.data_ptr(), ws.data_ptr(), B, T, H, st)
+            torch.cuda.synchronize()
+            assert int(ws[2 * (B // 16 + 1)].item()) == 0      # error word: no timed-out wait
+            assert int(ws[: 2 * (B // S)].min().item()) == H // U * T
+            outs[(pipe, force)] = (hseq, gsv, csv)
+    finally:
+        L.call("crnn_set_option", L.OPT_LSTM_PIPE, 0)
+        L.call("crnn_set_option", L.OPT_LSTM_TILE, 0)
+    p = outs[(1, 0)]
+    for x in p:
+        assert torch.isfinite(x.float()).all()
+    for key in ((0, 2), (0, 0)):
+        if key not in outs:
+            continue
+        for name, x, y in zip(("h", "gates", "cell"), p, outs[key]):
+            e = relerr(x.float().cpu(), y.float().cpu())
+            same = float((x == y).float().mean())
+            print(f"{BTH} pipe vs tile {key}: {name} relerr {e:.2e}, identical {same:.4f}")
+            assert e < 1e-2, (BTH, key, name, e)
+
+
+@pytest.mark.parametrize("BTH", [(128, 9, 512), (64, 20, 768), (256, 32, 512)])
+def test_lstm_seq_bwd_pipelined_groups(BTH):
+    """Persistent BPTT with two pipelined 16-sample groups per workgroup (CRNN_OPT_LSTM_PIPE bit 1,
+    lstm_seq_bwd_pipe_kernel; one step counter per group) against the one-group kernel: the same
+    arithmetic per group (fused multiply-adds the compiler's), dgates to bf16 rounding carried through the
+    steps; finite, no timed-out wait, every group's counter complete ((H/32) * T)."""
+    L = _L()
+    B, T, H = BTH
+    g = torch.Generator().manual_seed(22)
+    whh = (torch.randn(2, 4 * H, H, generator=g) / H ** 0.5).to(DEV, torch.bfloat16)
+    whh_t = whh.transpose(1, 2).contiguous()
+    gsv = torch.rand(2, T, B, 4 * H, generator=g).to(DEV, torch.bfloat16)
+    csv = (torch.randn(2, T, B, H, generator=g) * 0.5).to(DEV)
+    dh = (torch.randn(B, T, 2 * H, generator=g) * 0.5).to(DEV, torch.bfloat16)
+    st = L.stream_ptr()
+    outs = {}
+    try:
+        for pipe in (2, 0):
+            L.call("crnn_set_option", L.OPT_LSTM_PIPE, pipe)
+            if not L.lib().crnn_lstm_seq_supported(L.dtype_code(torch.bfloat16), B, H):
+                pytest.skip("persistent sweep unsupported at this shape")
+            S, U = seq_tile(B, H, 1)
+            dg = torch.full((2, T, B, 4 * H), 3.0, dtype=torch.bfloat16, device=DEV)
+            ws = torch.full((L.lib().crnn_lstm_seq_workspace(B) // 4,), 7, dtype=torch.int32, device=DEV)
+            L.call("crnn_lstm_seq_bwd", dh.data_ptr(), whh_t.data_ptr(), gsv.data_ptr(), csv.data_ptr(),
+                   dg.data_ptr(), ws.data_ptr(), B, T, H, st)
+            torch.cuda.synchronize()
+            assert int(ws[2 * (B // 16 + 1)].item()) == 0
+            ncnt = 2 * (B // 32) * 2 if pipe else 2 * (B // S)
+            assert int(ws[:ncnt].min().item()) == H // U * T, (pipe, S, U)
+            assert torch.isfinite(dg.float()).all()
+            outs[pipe] = dg.float().cpu()
+    finally:
+        L.call("crnn_set_option", L.OPT_LSTM_PIPE, 0)
+    e = relerr(outs[2], outs[0])
+    print(f"{BTH} BPTT pipe vs one-group: dgates relerr {e:.2e}, identical {float((outs[2] == outs[0]).float().mean()):.4f}")
+    assert e < 1e-2, (BTH, e)

@@ -85,7 +85,7 @@ def main():
     if kind.startswith("hog"):
         _, hb, hl, hi = kind.split(":")
         hout = torch.zeros(L.lib().crnn_diag_lds_sentinel_words(), dtype=torch.int32, device="cuda")
-        hog = lambda st: L.call("crnn_diag_lds_sentinel", hout.data_ptr(), int(hb), int(hl), int(hi), 7, 1, st)  # noqa
+        hog = lambda st: L.call("crnn_diag_lds_sentinel", hout.data_ptr(), int(hb), int(hl), int(hi), 7, 1, 0, st)  # noqa
     vm, vx, vtg, vtl = make(5, 256, victim_seq)
     am, ax, atg, atl = make(6, 256, aggr_seq)
     probe = os.environ.get("COHAB_PROBE") == "1"

@@ -91,6 +91,7 @@ def main():
     ap.add_argument("--sleep", type=int, default=1)
     ap.add_argument("--launches", type=int, default=4, help="aggressor launches per round")
     ap.add_argument("--only", default=None)
+    ap.add_argument("--mode", type=int, default=0, help="sentinel mode bits: 1 rewrite per check, 2 shuffle check")
     a = ap.parse_args()
     torch.cuda.init()
     main_s = torch.cuda.current_stream()
@@ -115,7 +116,7 @@ def main():
                 side.wait_stream(main_s)
                 with torch.cuda.stream(side):
                     L.call("crnn_diag_lds_sentinel", out.data_ptr(), a.blocks, lds, a.iters, 1234 + r, a.sleep,
-                           side.cuda_stream)
+                           a.mode, side.cuda_stream)
                 for _ in range(a.launches - (a.launches // 2 if r % 2 == 0 else 0)):
                     fn()
                 torch.cuda.synchronize()
