@@ -437,24 +437,6 @@ def run_training(cfg: Config, device: str = "cuda") -> Dict[str, object]:
                  "val_csvs": getattr(cfg, "val_csvs", None), "val_roots": getattr(cfg, "val_roots", None),
                  "hidden_size": hidden_size, "decoder": decoder, "num_rnn_layers": num_rnn_layers}
 
-    turns = None
-    if world > 1 and os.environ.get("CRNN_SHARE_DEVICE") == "1":
-        # rehearsal with every rank on one device (crnn_hip/dist.py): the ranks' training compute runs in
-        # turn. Kernels of two processes that share a GPU are not bit-reproducible; one
-        # process per GPU, the deployment, never shares one.
-        turns = tdist.new_group(backend="gloo")
-
-    def in_turn(fn):
-        if turns is None:
-            return fn()
-        out = None
-        for r in range(world):
-            if r == rank:
-                out = fn()
-                torch.cuda.current_stream(dev).synchronize()
-            tdist.barrier(group=turns)
-        return out
-
     def deal(items):
         """this rank's share: every world-th item from its rank, the same count on every rank"""
         if world == 1:
@@ -483,10 +465,10 @@ def run_training(cfg: Config, device: str = "cuda") -> Dict[str, object]:
                 lo.backward()
                 return lo
 
-            loss = in_turn(fwd_bwd)
+            loss = fwd_bwd()
             if reducer is not None:
                 reducer.finish()
-                in_turn(lambda: optimizer.step(grad_scale=1.0 / world))
+                optimizer.step(grad_scale=1.0 / world)
             else:
                 optimizer.step()
             total += float(loss.item())

@@ -154,3 +154,56 @@ def test_train_step_gradients_bit_identical_under_load(persistent_lstm):
             continue
         bad = sorted(k for k in g if not torch.equal(g[k], ref[k]))
         assert not bad, f"step {i}: {len(bad)} gradients differ from step 0, e.g. {bad[:6]}"
+
+
+def _bench_model(seed, use_seq):
+    import crnn_oracle as O
+    from crnn_hip.recipe import recipe_state_dict, synthetic_batch
+    from model.model import RCNN
+    m = RCNN(num_classes=194, hidden_size=512, blank_id=None, compute_dtype=torch.bfloat16, enc_dropout_p=0.0)
+    m.load_state_dict(recipe_state_dict(O.param_shapes(512, 194), seed), strict=False)
+    m = m.cuda().train()
+    x, _, tg, tl = synthetic_batch(256, 32, 256, 32, 194, seed=100 + seed)
+    x = x.cuda()
+    m(x)
+    m._engine.use_seq = use_seq
+    return m, x, tg, tl
+
+
+def _grads(m, x, tg, tl):
+    from crnn_hip.ctc import ctc_loss
+    m.zero_grad(set_to_none=True)
+    ctc_loss(m(x), tg, tl).backward()
+
+
+@pytest.mark.parametrize("victim_seq", [False, True])
+def test_train_steps_bit_identical_beside_this_librarys_step(victim_seq):
+    """the side load is THIS library's own bf16 train step (a second model with its
+    own engine and batch: the 256-row LDS-DMA conv GEMMs, the W-halo and halo stem convs, the BN / SE
+    chain, the per-step BiLSTM) on a side stream, overlapping a victim model's step at the bench
+    configuration (B = 256, 32x256, hidden 512). Both models' every gradient must be bit-identical to the
+    one each computed on an idle device, over 40 overlapped iterations.
+    Found with this set-up (tools/cohab_model.py, profiles/r05*_cohab*): the SE chain's small reductions
+    (se_wgrad, the SE-MLP backward's dpool) returned different outputs from identical inputs in 4-25 % of
+    the iterations — single low halves of packed fp32 pairs (the v_pk_add_f32 / v_pk_fma_f32 results) — and
+    in none of 200 with the device code built without packed fp32 VALU ops (csrc/Makefile NOPK)."""
+    vm, vx, vtg, vtl = _bench_model(5, victim_seq)
+    am, ax, atg, atl = _bench_model(6, False)   # the persistent sweeps need the whole chip: one at a time
+    _grads(vm, vx, vtg, vtl)
+    torch.cuda.synchronize()
+    vref = {k: p.grad.detach().clone() for k, p in vm.named_parameters()}
+    _grads(am, ax, atg, atl)
+    torch.cuda.synchronize()
+    aref = {k: p.grad.detach().clone() for k, p in am.named_parameters()}
+    side = torch.cuda.Stream()
+    for i in range(40):
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(2):
+                _grads(am, ax, atg, atl)
+        _grads(vm, vx, vtg, vtl)
+        torch.cuda.synchronize()
+        vbad = [k for k, p in vm.named_parameters() if not torch.equal(p.grad, vref[k])]
+        abad = [k for k, p in am.named_parameters() if not torch.equal(p.grad, aref[k])]
+        assert not vbad and not abad, (f"iteration {i}: victim {len(vbad)} gradients differ {vbad[-3:]}, "
+                                       f"side model {len(abad)} {abad[-3:]}")

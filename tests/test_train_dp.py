@@ -1,9 +1,8 @@
 """run_training with world_size 2 (SURVEY §5 "Config" world_size, §8e): two
 processes on the box's one GPU (gloo over device tensors, per-step BiLSTM launches: the persistent
 sweeps need the whole chip), launched the way torchrun would (RANK / WORLD_SIZE / MASTER_* in the
-env). With CRNN_SHARE_DEVICE=1 run_training gives the ranks the device in turn for their forward /
-backward and optimizer step (kernels of two processes sharing one GPU are not bit-reproducible,
-DESIGN.md §6); the overlapped all-reduce still runs as in deployment. Checked against a single-process
+env). With CRNN_SHARE_DEVICE=1 every rank uses device 0; the two ranks compute concurrently (r05: no
+turn-taking) and the overlapped all-reduce runs as in deployment. Checked against a single-process
 emulation of the same job: the same batches dealt to the two "ranks", each step's two shard gradients
 accumulated in one process and applied as their mean. BN keeps per-shard batch statistics in both, so
 the emulation is the DP step's definition: measured |dp - emulation| / |update| = 1.5e-10 after two
