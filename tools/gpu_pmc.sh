@@ -3,7 +3,7 @@
 # FETCH_SIZE, WRITE_SIZE, MFMA busy + GUI active, over a short bench run.
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-ARGS="bench.py --steps 3 --warmup 1 --no-cpu-baseline"
+ARGS="bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-sub"
 i=0
 for C in "FETCH_SIZE" "WRITE_SIZE" "SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE"; do
   i=$((i+1))
