@@ -148,6 +148,20 @@ __global__ __launch_bounds__(256) void lstm_seq_fwd_kernel(const bf16* __restric
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int b0 = bs * S, n0 = ns * GR;
   unsigned* mycnt = cnt + d * nbs + bs;
+  if (stamps && threadIdx.x == 0) stamps[(size_t)blockIdx.x * Tn * 8 + 7] = __builtin_amdgcn_s_memrealtime();
+
+  // step 0's input rows first: vmcnt retires in order, so issued ahead of the 64 W_hh loads below
+  // they let step 0 (no recurrent term) compute and publish while the slice is still arriving
+  bf16x4 xv[QB];  // raw prefetch: converted at the step's use, not at the load
+  auto load_xg = [&](int t) {
+#pragma unroll
+    for (int q = 0; q < QB; ++q) {
+      const int bi = w * QB + q, i = bi / NJ, j = bi % NJ;
+      const int b = b0 + 16 * i + c, n = n0 + 16 * j + 4 * g;
+      xv[q] = *reinterpret_cast<const bf16x4*>(xg + ((size_t)b * Tn + t) * 2 * H4 + d * H4 + n);
+    }
+  };
+  load_xg(d == 0 ? 0 : Tn - 1);
 
   // W_hh' slice fragments: rows n0 + 16j + c, k = w*KW + 32kc + 8g; register slot kk holds K-chunk
   // kc = (kk + rot) % KK: the workgroups of a (d, bs) group read the handed-off h in rotated chunk
@@ -170,16 +184,6 @@ __global__ __launch_bounds__(256) void lstm_seq_fwd_kernel(const bf16* __restric
   float cst[QB];
 #pragma unroll
   for (int q = 0; q < QB; ++q) cst[q] = 0.f;
-  bf16x4 xv[QB];  // raw prefetch: converted at the step's use, not at the load
-  auto load_xg = [&](int t) {
-#pragma unroll
-    for (int q = 0; q < QB; ++q) {
-      const int bi = w * QB + q, i = bi / NJ, j = bi % NJ;
-      const int b = b0 + 16 * i + c, n = n0 + 16 * j + 4 * g;
-      xv[q] = *reinterpret_cast<const bf16x4*>(xg + ((size_t)b * Tn + t) * 2 * H4 + d * H4 + n);
-    }
-  };
-  load_xg(d == 0 ? 0 : Tn - 1);
 
   for (int s = 0; s < Tn; ++s) {
     const int t = d == 0 ? s : Tn - 1 - s;
@@ -678,23 +682,7 @@ __global__ __launch_bounds__(256) void lstm_seq_bwd_kernel(const bf16* __restric
   const int b0 = bs * S, u0 = ns * U;
   unsigned* mycnt = cnt + d * nbs + bs;
 
-  // W_hh'^T slice fragments: rows u0 + 16j + c of whh_t[d] ([H][4H]), k = w*KW + 32kc + 8g
-  const int rot = (ns * KK / nsl) % KK;   // rotated K-chunk order, as in the forward kernel
-  bf16x8 wf[NU][KK];
-  {
-    const bf16* wb = whh_t + (size_t)d * H * H4;
-#pragma unroll
-    for (int j = 0; j < NU; ++j)
-#pragma unroll
-      for (int kk = 0; kk < KK; ++kk) {
-        const int kc = kk + rot < KK ? kk + rot : kk + rot - KK;
-        wf[j][kk] = *reinterpret_cast<const bf16x8*>(wb + (size_t)(u0 + 16 * j + c) * H4 + w * KW + 32 * kc + 8 * g);
-      }
-  }
-  const __amdgpu_buffer_rsrc_t rg = rsrc_of(dgates);
-  // dgates payload: plain stores + the drained counter when the group is on one XCD (the
-  // consumers' sc1 loads then hit the shared L2), sc1 stores otherwise (seq_group_local)
-  const bool l2_handoff = xtab && seq_group_local(xtab, (d * nbs + bs) * nsl, nsl, ns, err);
+  if (stamps && threadIdx.x == 0) stamps[(size_t)blockIdx.x * Tn * 8 + 7] = __builtin_amdgcn_s_memrealtime();
   const bool fin = w < NBLK;
   const int fi = fin ? w % MI : 0, fj = fin ? w / MI : 0;
   const int bl = 16 * fi + c, b = b0 + bl;
@@ -718,7 +706,25 @@ __global__ __launch_bounds__(256) void lstm_seq_bwd_kernel(const bf16* __restric
     has_prev_f = has_prev ? 1.f : 0.f;
     dhv = ld4f<bf16>(dhseq + ((size_t)b * Tn + t) * 2 * H + d * H + u);
   };
-  load_in(d == 0 ? Tn - 1 : 0);
+  load_in(d == 0 ? Tn - 1 : 0);   // ahead of the W_hh slice loads (forward sweep)
+
+  // W_hh'^T slice fragments: rows u0 + 16j + c of whh_t[d] ([H][4H]), k = w*KW + 32kc + 8g
+  const int rot = (ns * KK / nsl) % KK;   // rotated K-chunk order, as in the forward kernel
+  bf16x8 wf[NU][KK];
+  {
+    const bf16* wb = whh_t + (size_t)d * H * H4;
+#pragma unroll
+    for (int j = 0; j < NU; ++j)
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk) {
+        const int kc = kk + rot < KK ? kk + rot : kk + rot - KK;
+        wf[j][kk] = *reinterpret_cast<const bf16x8*>(wb + (size_t)(u0 + 16 * j + c) * H4 + w * KW + 32 * kc + 8 * g);
+      }
+  }
+  const __amdgpu_buffer_rsrc_t rg = rsrc_of(dgates);
+  // dgates payload: plain stores + the drained counter when the group is on one XCD (the
+  // consumers' sc1 loads then hit the shared L2), sc1 stores otherwise (seq_group_local)
+  const bool l2_handoff = xtab && seq_group_local(xtab, (d * nbs + bs) * nsl, nsl, ns, err);
 
   for (int s = 0; s < Tn; ++s) {
     const int t = d == 0 ? Tn - 1 - s : s;

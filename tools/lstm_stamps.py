@@ -16,7 +16,7 @@ from crnn_hip import _lib as L  # noqa: E402
 PH = ["start", "waited", "mfma+part", "reduced", "epilogue", "stored", "published"]
 
 
-def run(kind, B, T, H):
+def run(kind, B, T, H, save=True):
     dev = torch.device("cuda")
     st = L.stream_ptr()
     g = torch.Generator(device="cpu").manual_seed(0)
@@ -36,14 +36,16 @@ def run(kind, B, T, H):
     stamps = torch.zeros(grid * T * 8, dtype=torch.int64, device=dev)
 
     def fwd():
-        L.call("crnn_lstm_seq_fwd", xg.data_ptr(), whh.data_ptr(), hseq.data_ptr(), gsv.data_ptr(), csv.data_ptr(),
-               ws.data_ptr(), B, T, H, st)
+        L.call("crnn_lstm_seq_fwd", xg.data_ptr(), whh.data_ptr(), hseq.data_ptr(), gsv.data_ptr() if save else None,
+               csv.data_ptr() if save else None, ws.data_ptr(), B, T, H, st)
 
     def bwd():
         L.call("crnn_lstm_seq_bwd", hseq.data_ptr(), whh_t.data_ptr(), gsv.data_ptr(), csv.data_ptr(), dg.data_ptr(),
                ws.data_ptr(), B, T, H, st)
 
+    save0, save = save, True
     fwd()
+    save = save0
     fn = fwd if kind == "fwd" else bwd
     for _ in range(3):
         fn()
@@ -61,7 +63,7 @@ def run(kind, B, T, H):
     s = stamps.view(grid, T, 8).cpu().numpy().astype(np.int64)
     ho = "granule" if HANDOFF else "counter"
     print(f"{kind}: B={B} T={T} H={H} tile {S}x{U} grid={grid} hand-off {ho if kind == 'fwd' else 'counter'}: "
-          f"{us:.1f} us/sweep = {us / T:.2f} us/step (no stamps)")
+          f"{'' if save else '(inference, nothing saved) '}{us:.1f} us/sweep = {us / T:.2f} us/step (no stamps)")
     steps = slice(2, T - 1)
     d = s[:, steps, :]
     for p in range(1, 7):
@@ -78,6 +80,15 @@ def run(kind, B, T, H):
     wait_done = s[:, 1:, 1]
     lat = (wait_done - last_pub[None, :]) * 10 / 1e3
     print(f"  last publish (any block, step s-1) -> waited (step s): median {np.median(lat):.3f} us")
+    # launch ramp and prologue: slot 7 of step 0 = the workgroup's entry stamp
+    ent = s[:, 0, 7]
+    if (ent > 0).all():
+        t0 = ent.min()
+        us_ = lambda v: (v - t0) * 10 / 1e3
+        print(f"  entry spread (first -> last workgroup) {us_(ent.max()):.2f} us; entry -> step-0 start median "
+              f"{np.median((s[:, 0, 0] - ent) * 10 / 1e3):.2f} us max {np.max((s[:, 0, 0] - ent) * 10 / 1e3):.2f}; "
+              f"first entry -> last step-0 publish {us_(s[:, 0, 6].max()):.2f} us; first entry -> last step end "
+              f"{us_(s[:, -1, 6].max()):.2f} us; steps 1..T-1 {(s[:, -1, 6].max() - s[:, 0, 6].max()) * 10 / 1e3 / (T - 1):.3f} us each")
 
 
 HANDOFF = 1
@@ -85,6 +96,13 @@ HANDOFF = 1
 if __name__ == "__main__":
     # forward under both hand-off forms (CRNN_OPT_LSTM_HANDOFF), each tile, in one process
     B, T, H = (int(a) for a in sys.argv[1:4]) if len(sys.argv) > 3 else (256, 32, 512)
+    if os.environ.get("STAMPS_SAVE_AB"):
+        # default tile and hand-off: saved-forward stores on / off (the BPTT operands' cost per step),
+        # then the default BPTT
+        for save in (True, False, True):
+            run("fwd", B, T, H, save)
+        run("bwd", B, T, H)
+        sys.exit(0)
     for force in (1, 2, 3):
         L.call("crnn_set_option", L.OPT_LSTM_TILE, force)
         for HANDOFF in (1, 0, 1):
