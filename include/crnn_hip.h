@@ -92,7 +92,9 @@ enum { CRNN_OPT_GEMM_STAGGER = 0,    /* 256-row conv GEMM: waves 4-7 one barrier
        CRNN_OPT_LSTM_PIPE = 19,      /* persistent BiLSTM: bit 0 = forward sweep as two pipelined 16-sample groups x
                                         32 units per workgroup (a group's hand-off travels while the workgroup
                                         computes the other group), bit 1 = the same for the BPTT */
-       CRNN_OPT_COUNT = 20 };
+       CRNN_OPT_LINEAR_ROW8 = 20,    /* bf16 crnn_gemm_nt / nn on the 256-row kernel: 1 = 16-B row stores through the
+                                        wave's LDS (8 columns per lane; default), 0 = 8-B stores from the MFMA layout */
+       CRNN_OPT_COUNT = 21 };
 int crnn_set_option(int key, int value);
 /* current value of a tuning switch (0 for an unknown key) */
 int crnn_get_option(int key);

@@ -9,8 +9,11 @@ using namespace gemm;
 
 namespace {
 
-template <typename T> struct OutEpi {
+template <typename T, bool ROW8 = false> struct OutEpi {
   static constexpr bool kStats = false;
+  // ROW8 (CRNN_OPT_LINEAR_ROW8, 256-row kernel only): the accumulators go through the wave's LDS and a lane
+  // stores 8 consecutive columns (one 16-B bf16 store, gemm256.hpp row8_epilogue) instead of 4
+  static constexpr bool kRow8 = ROW8;
   void* c;
   int ldc, M, N, c_f32, accumulate, atomic;
   const float* bias;
@@ -49,6 +52,36 @@ template <typename T> struct OutEpi {
       }
     }
   }
+  // 8 consecutive columns n..n+7 of row m (the same per-element arithmetic as two store() calls)
+  __device__ __forceinline__ void store8(int m, int n, f32x4 lo, f32x4 hi, int kz) const {
+    if constexpr (sizeof(T) == 2) {
+      if (!c_f32 && !atomic && n + 8 <= N && (ldc % 8) == 0) {
+        if (m >= M) return;
+        if (bias) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            lo[r] += bias[n + r];
+            hi[r] += bias[n + 4 + r];
+          }
+        }
+        T* p = (T*)c + (size_t)m * ldc + n;
+        if (accumulate) {
+          lo += ld4f<T>(p);
+          hi += ld4f<T>(p + 4);
+        }
+        bf16x8 v;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          v[r] = (bf16)lo[r];
+          v[4 + r] = (bf16)hi[r];
+        }
+        *reinterpret_cast<bf16x8*>(p) = v;
+        return;
+      }
+    }
+    store(m, n, lo, kz);
+    store(m, n + 4, hi, kz);
+  }
   __device__ __forceinline__ void stats(int, int, f32x4, f32x4) const {}
 };
 
@@ -61,8 +94,12 @@ int run(const LA& la, const LB& lb, const OutEpi<T>& ep, int M, int N, int K, in
     if (crnn_option(CRNN_OPT_DEEP_LINEAR) && splits == 1 && K >= 256) {
       const long t256 = (long)((M + 255) / 256) * ((N + 255) / 256);
       const long t128 = (long)((M + 255) / 256) * ((N + 127) / 128);
-      if (N >= 256 && t256 * 4 >= cu * 3) return launch256<256, 256>(la, lb, ep, M, N, K, st);
-      if (N >= 128 && t128 * 4 >= cu * 3) return launch256<256, 128>(la, lb, ep, M, N, K, st);
+      const OutEpi<T, true> ep8{ep.c, ep.ldc, ep.M, ep.N, ep.c_f32, ep.accumulate, ep.atomic, ep.bias};
+      const bool row8 = crnn_option(CRNN_OPT_LINEAR_ROW8) != 0;
+      if (N >= 256 && t256 * 4 >= cu * 3)
+        return row8 ? launch256<256, 256>(la, lb, ep8, M, N, K, st) : launch256<256, 256>(la, lb, ep, M, N, K, st);
+      if (N >= 128 && t128 * 4 >= cu * 3)
+        return row8 ? launch256<256, 128>(la, lb, ep8, M, N, K, st) : launch256<256, 128>(la, lb, ep, M, N, K, st);
     }
   }
   if (M >= 128 && N >= 128 && work >= 128L * 128 * 128) return launch<T, 128, 128>(la, lb, ep, M, N, K, splits, st);

@@ -778,6 +778,38 @@ def test_se_pool_from_partials(hw):
     assert relerr(p1, p0) < 2e-3
 
 
+@pytest.mark.parametrize("mnk", [(8192, 4096, 512), (1000, 1032, 1024), (2048, 512, 1024)])
+def test_gemm_nt_row8_epilogue_bit_identical(mnk):
+    """crnn_gemm_nt / crnn_gemm_nn (bf16 out, bias, overwrite and accumulate) with the 16-B row stores
+    (CRNN_OPT_LINEAR_ROW8 = 1) and the 8-B MFMA-layout stores (0): the same fp32 value per element before
+    the one bf16 rounding, so bit-identical; ragged M and an N that is not a multiple of 256 included"""
+    L = _L()
+    M, N, K = mnk
+    g = torch.Generator().manual_seed(21)
+    A = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16)
+    Bm = (torch.randn(N, K, generator=g) * 0.05).to(DEV, torch.bfloat16)
+    Bk = (torch.randn(K, N, generator=g) * 0.05).to(DEV, torch.bfloat16)
+    bias = torch.randn(N, generator=g).to(DEV)
+    st = L.stream_ptr()
+    outs = {}
+    try:
+        for opt in (0, 1):
+            L.call("crnn_set_option", L.OPT_LINEAR_ROW8, opt)
+            C = torch.full((M, N), 5.0, dtype=torch.bfloat16, device=DEV)
+            L.call("crnn_gemm_nt", L.BF16, A.data_ptr(), K, Bm.data_ptr(), K, C.data_ptr(), N, bias.data_ptr(), M, N,
+                   K, 0, 0, st)
+            C2 = torch.full((M, N), 0.5, dtype=torch.bfloat16, device=DEV)
+            L.call("crnn_gemm_nn", L.BF16, A.data_ptr(), K, Bk.data_ptr(), N, C2.data_ptr(), N, M, N, K, 0, 1, st)
+            torch.cuda.synchronize()
+            outs[opt] = (C, C2)
+    finally:
+        L.call("crnn_set_option", L.OPT_LINEAR_ROW8, 1)
+    ref = (A.float() @ Bm.float().t() + bias).cpu()
+    assert relerr(outs[1][0].float().cpu(), ref) < 1e-2
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("mnk", [(37, 50, 64), (256, 194, 512), (304, 1024, 256), (8, 16, 8), (200, 512, 8192),
                                  (512, 1024, 4096)])

@@ -6,7 +6,8 @@ turn-taking) and the overlapped all-reduce runs as in deplo
 emulation of the same job: the same batches dealt to the two "ranks", each step's two shard gradients
 accumulated in one process and applied as their mean. BN keeps per-shard batch statistics in both, so
 the emulation is the DP step's definition: measured |dp - emulation| / |update| = 1.5e-10 after two
-epochs (profiles/r04o_dp.log). Reference: training/train.py:179-235, :493-518."""
+epochs (profiles/r04o_dp.log). The emulation also keeps one copy of the BN running statistics per rank and
+averages them at each epoch end, as sync_bn_stats does; rank 0's checkpoint must hold that average. Reference: training/train.py:179-235, :493-518."""
 import json
 import os
 import socket
@@ -82,18 +83,40 @@ def _emulate(cfg, world):
     opt = make_optimizer(cfg.optimizer, model, cfg.lr, cfg.weight_decay, cfg.momentum)
     train_sets, _ = build_splits(cfg, stoi, cfg.img_h, cfg.img_w, cfg.max_len, "utf-8", cfg.val_size, cfg.seed)
     flat = [(d, i) for d, s in enumerate(train_sets) for i in range(len(s))]
+    # BN running statistics: one copy per "rank", updated only by that rank's shards, replaced by their
+    # fp64 mean at the end of every epoch (training/train.py sync_bn_stats, before eval and checkpoint)
+    bufs = {n: b for n, b in model.named_buffers() if n.endswith(("running_mean", "running_var"))}
+    per_rank = [{n: b.detach().clone() for n, b in bufs.items()} for _ in range(world)]
     model.train()
+
+    @torch.no_grad()
+    def load(r):
+        for n, b in bufs.items():
+            b.copy_(per_rank[r][n])
+
+    @torch.no_grad()
+    def save(r):
+        for n, b in bufs.items():
+            per_rank[r][n].copy_(b)
     for epoch in range(1, cfg.epochs + 1):
         eb = [[flat[i] for i in b] for b in batches(range(len(flat)), cfg.batch_size, True, cfg.seed + epoch)]
         for k in range(len(eb) // world):
             opt.zero_grad(set_to_none=True)
             for r in range(world):
+                load(r)
                 crops, labels = zip(*[train_sets[d][i] for d, i in eb[r + world * k]])
                 x = preprocess_batch(list(crops), cfg.img_h, cfg.img_w, out="encoder", dtype=torch.bfloat16,
                                      device=dev)
                 ids, lens = ctc_targets(list(labels), stoi, cfg.max_len)
                 ctc_loss(model(x), ids, lens).backward()
+                save(r)
             opt.step(grad_scale=1.0 / world)
+        with torch.no_grad():
+            for n, b in bufs.items():
+                m = sum(per_rank[r][n].double() for r in range(world)) / world
+                for r in range(world):
+                    per_rank[r][n].copy_(m.to(b.dtype))
+        load(0)
     torch.cuda.synchronize()
     return p0, model
 
@@ -135,3 +158,14 @@ def test_run_training_world2_matches_single_process_emulation(tmp_path):
     rel = float((dp - em).norm()) / upd
     print(f"DP vs emulation: |dp - emu| / |update| = {rel:.3e} (update norm {upd:.3e})")
     assert upd > 0 and rel < 1e-6, rel
+    # BN running statistics: rank 0 saves the ranks' mean, as the emulation computes it. Each rank's
+    # statistics come from its own shards' forward passes; the weights they see differ from the emulation's by
+    # the rel above, so the buffers agree to a tolerance of the same kind
+    names = [n for n, _ in model.named_buffers() if n.endswith(("running_mean", "running_var"))]
+    assert names
+    worst = 0.0
+    for n in names:
+        a, b = sd[n].float(), dict(model.named_buffers())[n].detach().float().cpu()
+        worst = max(worst, float((a - b).abs().max()) / (float(b.abs().max()) + 1e-12))
+    print(f"BN running statistics: max relative |dp - emu| = {worst:.3e} over {len(names)} buffers")
+    assert worst < 1e-4, worst

@@ -68,8 +68,32 @@ def main():
                                                  dW4[3].data_ptr(), wgw.data_ptr(), need, B, T, H, In, 0, st),
         "lstm dx": lambda: L.call("crnn_lstm_dx", L.BF16, dg.data_ptr(), wih.data_ptr(), dxl.data_ptr(), B, T, H, In, st),
     }
+    # the same products through torch.matmul (hipBLASLt), bf16 in and out: the vendor reference per shape
+    dgf = dg.permute(0, 2, 1, 3).reshape(2, M, 4 * H)       # [d][b*T + t][4H] (layout irrelevant for timing)
+    xb = x.view(M, In)
+    hb = hseq.view(M, 2 * H)
+    vendor = {
+        "xg nt 8192x4096x512": lambda: torch.addmm(bias.to(bf), xb, wih.t()),
+        "lin fwd nt 8192x512x1024": lambda: hb @ lin.t(),
+        "lin bwd nn 8192x1024x512": lambda: dx @ lin,
+        "lin wgrad tn 512x1024x8192": lambda: dx.t() @ hb,
+        "dwhh (2 dirs)": lambda: torch.bmm(dgf.transpose(1, 2), hb[:, :H].unsqueeze(0).expand(2, M, H)),
+        "dwih (2 dirs)": lambda: torch.bmm(dgf.transpose(1, 2), xb.unsqueeze(0).expand(2, M, In)),
+        "lstm dx": lambda: dgf.transpose(0, 1).reshape(M, 8 * H) @ wih,
+    }
     for name, fn in ops.items():
         line = f"{name:28s}"
+        if os.environ.get("GEMMBENCH_VENDOR") and name in vendor:
+            vf = vendor[name]
+            for _ in range(3):
+                vf()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(20):
+                vf()
+            e1.record()
+            torch.cuda.synchronize()
+            line += f" | hipBLASLt: {e0.elapsed_time(e1) / 20 * 1e3:8.1f} us"
         for v in vals:
             L.call("crnn_set_option", key, v)
             for _ in range(3):
