@@ -94,7 +94,12 @@ enum { CRNN_OPT_GEMM_STAGGER = 0,    /* 256-row conv GEMM: waves 4-7 one barrier
                                         computes the other group), bit 1 = the same for the BPTT */
        CRNN_OPT_LINEAR_ROW8 = 20,    /* bf16 crnn_gemm_nt / nn on the 256-row kernel: 1 = 16-B row stores through the
                                         wave's LDS (8 columns per lane; default), 0 = 8-B stores from the MFMA layout */
-       CRNN_OPT_COUNT = 21 };
+       CRNN_OPT_HALO_ROW16 = 21,     /* the stem's input conv (3 -> 64, halo kernel): 1 = the output tile staged in LDS
+                                        and stored as full 128-B lines (16 B per lane; default), 0 = 8-B stores from
+                                        the MFMA layout */
+       CRNN_OPT_POOL2 = 22,          /* stem BN -> ReLU -> 2x2 max-pool (crnn_bn_relu_maxpool): 1 = a thread's channels
+                                        fixed, two pooled pixels per iteration, no integer division; 0 = the r01 form */
+       CRNN_OPT_COUNT = 23 };
 int crnn_set_option(int key, int value);
 /* current value of a tuning switch (0 for an unknown key) */
 int crnn_get_option(int key);

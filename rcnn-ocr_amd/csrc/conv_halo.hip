@@ -41,7 +41,13 @@ template <int CI> struct Ring {
 // FLIP = false: y = conv(x, W), W packed [CO][3][3][CI] (conv.hip's OHWI pack).
 // FLIP = true : dx = conv(dy, W'), W'[o][t][c] = W[c][8 - t][o], read from the forward pack
 //               [CI][3][3][CO] (CI = forward Co, CO = forward Ci).
-template <int CI, int CO, bool FLIP, bool POOL = false>
+// ROW16 (CRNN_OPT_HALO_ROW16, not with POOL): the output tile (128 pixels x CO, contiguous in NHWC) goes
+// through LDS, so each lane stores whole 16-B chunks and a wave instruction covers full 128-B lines, instead of
+// 8-B pieces of 16 pixels from the MFMA layout; staged in the ring slot the finished row frees when it is
+// large enough, else in an array of its own. Used for the 3 (8) -> 64 input conv, whose rows are
+// store-bound (130 -> 100 us at B = 256, profiles/r05u/); the 64 -> 128 forward spills with it (+2.5 %) and
+// the input gradient does not move, so those keep the direct stores.
+template <int CI, int CO, bool FLIP, bool POOL = false, bool ROW16 = false>
 __global__ __launch_bounds__(512) void halo3x3_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wp,
                                                       bf16* __restrict__ y, float* __restrict__ psum,
                                                       float* __restrict__ psq, int H, int W, int RB, uint32_t xbytes,
@@ -144,6 +150,10 @@ __global__ __launch_bounds__(512) void halo3x3_kernel(const bf16* __restrict__ x
   // POOL: the even row's activations (bf16: rounding is monotonic, so max and rounding commute) in
   // this lane's slice of LDS, max-combined with the odd row's (same lane: no barrier)
   __shared__ __attribute__((aligned(16))) bf16 keep[POOL ? 512 * MI * NJ * 4 : 4];
+  static_assert(!(ROW16 && POOL) && (!ROW16 || CO % 64 == 0), "row stores: CO multiple of 64, no pool");
+  constexpr int STG = TW * CO * 2;                 // the staged output tile, bytes
+  constexpr bool STG_IN_RING = STG <= R::SLOT;
+  __shared__ __attribute__((aligned(16))) char stg_own[ROW16 && !STG_IN_RING ? STG : 16];
   for (int yy = r0; yy < r0 + RB; ++yy) {
     load_row(yy + 2);  // lands while this row computes; stored to the free slot below
     f32x4 acc[MI][NJ];
@@ -224,6 +234,26 @@ __global__ __launch_bounds__(512) void halo3x3_kernel(const bf16* __restrict__ x
             if ((c & 1) == 0)
               st4<bf16>(y + (p0 + ((pw * 64 + 16 * i + c) >> 1)) * CO + cw * CW + 16 * j + 4 * g, v);
           }
+      }
+    } else if constexpr (ROW16) {
+      // [128 pixels][CO] bf16, 16-B chunk q of pixel p at chunk q ^ (p & 7)
+      char* sg = STG_IN_RING ? ring + (yy & 3) * R::SLOT : stg_own;   // ring: the slot of row yy - 1
+      if constexpr (STG_IN_RING) __syncthreads();   // every wave is done reading row yy - 1
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const int px = pw * 64 + 16 * i + c, ch = cw * CW + 16 * j + 4 * g;
+          const bf16x4 v = {(bf16)acc[i][j][0], (bf16)acc[i][j][1], (bf16)acc[i][j][2], (bf16)acc[i][j][3]};
+          *reinterpret_cast<bf16x4*>(sg + px * (CO * 2) + (((ch >> 3) ^ (px & 7)) << 4) + ((ch >> 2) & 1) * 8) = v;
+        }
+      __syncthreads();
+      constexpr int QN = CO / 8;   // 16-B chunks per pixel
+#pragma unroll
+      for (int k = 0; k < TW * QN / 512; ++k) {
+        const int e = threadIdx.x + 512 * k, px = e / QN, q = e % QN;
+        const u32x4 v = *reinterpret_cast<const u32x4*>(sg + px * (CO * 2) + ((q ^ (px & 7)) << 4));
+        *reinterpret_cast<u32x4*>(y + (m0 + px) * CO + 8 * q) = v;
       }
     } else {
 #pragma unroll
@@ -452,7 +482,11 @@ int conv_halo_fwd(const crnn_conv_desc* d, const void* x, const void* w, void* y
   const int rb = band_rows(d->Hi, d->Ci);
   const dim3 grid(d->B * (d->Wi / TW) * (d->Hi / rb));
   const uint32_t xbytes = (uint32_t)((size_t)d->B * d->Hi * d->Wi * d->Ci * 2);
-  if (d->Ci == 8)
+  const bool row16 = crnn_option(CRNN_OPT_HALO_ROW16) != 0;
+  if (d->Ci == 8 && row16)
+    hipLaunchKernelGGL((halo3x3_kernel<8, 64, false, false, true>), grid, dim3(512), 0, st, (const bf16*)x,
+                       (const bf16*)w, (bf16*)y, psum, psq, d->Hi, d->Wi, rb, xbytes, esc, esh);
+  else if (d->Ci == 8)
     hipLaunchKernelGGL((halo3x3_kernel<8, 64, false>), grid, dim3(512), 0, st, (const bf16*)x, (const bf16*)w,
                        (bf16*)y, psum, psq, d->Hi, d->Wi, rb, xbytes, esc, esh);
   else

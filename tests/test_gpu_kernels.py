@@ -415,6 +415,47 @@ def test_conv_halo_vs_gemm():
     assert relerr(w1, w0) < 1e-5   # fp32 accumulation both ways (beta = 1 keeps the 0.25 start)
 
 
+@pytest.mark.parametrize("ci_co", [(8, 64), (64, 128)])
+def test_conv_halo_row16_stores_bit_identical(ci_co):
+    """The stem halo convs under CRNN_OPT_HALO_ROW16 = 1 (the input conv's output tile staged through LDS and
+    stored as full lines) and 0 (8-B stores from the MFMA layout): the same bf16 values, so y, the BN partial
+    statistics and (64 -> 128) dx are bit-identical."""
+    L = _L()
+    Ci, Co = ci_co
+    B, H, W = 4, 32, 256
+    g = torch.Generator().manual_seed(17)
+    x = torch.randn(B, H, W, Ci, generator=g).to(DEV, torch.bfloat16)
+    w = (torch.randn(Co, Ci, 3, 3, generator=g) / 24).to(DEV)
+    dy = torch.randn(B, H, W, Co, generator=g).to(DEV, torch.bfloat16)
+    dt = L.BF16
+    st = L.stream_ptr()
+    d = L.ConvDesc(B, H, W, Ci, H, W, Co, 3, 3, 1, 1, 1, 1, Ci)
+    wd = torch.empty(Co, 3, 3, Ci, dtype=torch.bfloat16, device=DEV)
+    L.call("crnn_pack_conv_weight", dt, w.data_ptr(), wd.data_ptr(), Co, Ci, 3, 3, Ci, st)
+    rows = L.lib().crnn_conv_stat_rows(dt, d)
+    out = {}
+    try:
+        for opt in (0, 1):
+            L.call("crnn_set_option", L.OPT_HALO_ROW16, opt)
+            y = torch.full((B, H, W, Co), 9.0, dtype=torch.bfloat16, device=DEV)
+            ps = torch.full((rows, Co), 9.0, device=DEV)
+            pq = torch.full((rows, Co), 9.0, device=DEV)
+            L.call("crnn_conv_fwd", dt, d, x.data_ptr(), wd.data_ptr(), y.data_ptr(), ps.data_ptr(), pq.data_ptr(), st)
+            res = [y, ps, pq]
+            if Ci == 64:
+                dx = torch.full((B, H, W, Ci), 9.0, dtype=torch.bfloat16, device=DEV)
+                L.call("crnn_conv_dgrad", dt, d, dy.data_ptr(), wd.data_ptr(), dx.data_ptr(), None, None, 0, st)
+                res.append(dx)
+            torch.cuda.synchronize()
+            out[opt] = res
+    finally:
+        L.call("crnn_set_option", L.OPT_HALO_ROW16, 1)
+    ref = torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2), w.to(torch.bfloat16).float(), padding=1)
+    assert relerr(out[1][0].float().permute(0, 3, 1, 2), ref) < 1e-2
+    for a, b in zip(out[0], out[1]):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("geo", [(128, 256, 8, 64, 256), (256, 512, 4, 32, 512), (131, 256, 8, 62, 256)])
 def test_dgrad_bnrelu_fused(geo):
     """crnn_conv_dgrad_bnrelu == crnn_conv_dgrad + crnn_bn_bwd_reduce (CRNN_BNG_RELU) through
@@ -1346,6 +1387,33 @@ def test_maxpool_relu_bn(dtype):
     pre = z * sc[None, :, None, None] + sh[None, :, None, None]
     dz = dfull.float().permute(0, 3, 1, 2).cpu() * (pre > 0).float() * sc[None, :, None, None]
     assert relerr(dz, zr.grad) < tol
+
+
+@pytest.mark.parametrize("shape", [(4, 128, 32, 256), (3, 64, 6, 10), (1, 16, 2, 2), (5, 24, 8, 12)])
+def test_bn_relu_maxpool_forms_bit_identical(shape):
+    """crnn_bn_relu_maxpool under CRNN_OPT_POOL2 = 1 (fixed channels per thread, two pooled pixels per
+    iteration; C / 8 must divide 256, else the r01 kernel runs) and 0: bit-identical, and equal to torch"""
+    L = _L()
+    B, C, H, W = shape
+    g = torch.Generator().manual_seed(9)
+    z = torch.randn(B, H, W, C, generator=g).to(DEV, torch.bfloat16)
+    sc = (torch.rand(C, generator=g) + 0.5).to(DEV)
+    sh = (torch.randn(C, generator=g) * 0.2).to(DEV)
+    st = L.stream_ptr()
+    outs = {}
+    try:
+        for opt in (0, 1):
+            L.call("crnn_set_option", L.OPT_POOL2, opt)
+            y = torch.full((B, H // 2, W // 2, C), 5.0, dtype=torch.bfloat16, device=DEV)
+            L.call("crnn_bn_relu_maxpool", L.BF16, z.data_ptr(), sc.data_ptr(), sh.data_ptr(), y.data_ptr(), B, H, W, C,
+                   st)
+            torch.cuda.synchronize()
+            outs[opt] = y
+    finally:
+        L.call("crnn_set_option", L.OPT_POOL2, 1)
+    ref = F.max_pool2d(torch.relu(z.float().permute(0, 3, 1, 2) * sc[None, :, None, None] + sh[None, :, None, None]), 2, 2)
+    assert relerr(outs[1].float().permute(0, 3, 1, 2), ref) < 1e-2
+    assert torch.equal(outs[0], outs[1])
 
 
 @pytest.mark.parametrize("mode", [0, 1, 2, 3])
