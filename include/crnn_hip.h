@@ -97,8 +97,8 @@ enum { CRNN_OPT_GEMM_STAGGER = 0,    /* 256-row conv GEMM: waves 4-7 one barrier
        CRNN_OPT_HALO_ROW16 = 21,     /* the stem's input conv (3 -> 64, halo kernel): 1 = the output tile staged in LDS
                                         and stored as full 128-B lines (16 B per lane; default), 0 = 8-B stores from
                                         the MFMA layout */
-       CRNN_OPT_POOL2 = 22,          /* stem BN -> ReLU -> 2x2 max-pool (crnn_bn_relu_maxpool): 1 = a thread's channels
-                                        fixed, two pooled pixels per iteration, no integer division; 0 = the r01 form */
+       CRNN_OPT_HALO_WG2 = 22,       /* the stem input conv's weight gradient (halo kernel, streaming): 1 = one workgroup
+                                        per band (two per CU, one slab each; default), 0 = min(bands, CUs) workgroups */
        CRNN_OPT_COUNT = 23 };
 int crnn_set_option(int key, int value);
 /* current value of a tuning switch (0 for an unknown key) */

@@ -664,56 +664,6 @@ __global__ void bn_relu_maxpool_kernel(const T* __restrict__ z, const float* __r
   }
 }
 
-// the same with a thread's 8 channels fixed (C / 8 divides the 256-thread block: scale / shift loaded once),
-// two output pixels per iteration (8 window loads of 16 B in flight per thread) and no integer division
-template <typename T>
-__global__ __launch_bounds__(256) void bn_relu_maxpool2_kernel(const T* __restrict__ z, const float* __restrict__ sc,
-                                                               const float* __restrict__ sh, T* __restrict__ y, int H,
-                                                               int W, int C, uint32_t npix, FastDiv dWo, FastDiv dHo) {
-  const int cg = C / 8, per = 256 / cg;
-  const int c8 = (int)(threadIdx.x % (uint32_t)cg) * 8;
-  float a[8], h[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    a[k] = sc[c8 + k];
-    h[k] = sh[c8 + k];
-  }
-  const int Ho = H / 2, Wo = W / 2;
-  const uint32_t stride = gridDim.x * (uint32_t)per;
-  for (uint32_t p = blockIdx.x * (uint32_t)per + threadIdx.x / (uint32_t)cg; p < npix; p += 2 * stride) {
-    const uint32_t p2 = p + stride < npix ? p + stride : p;
-    typename VT<T>::v8 v[2][4];
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      uint32_t wo, ho;
-      const uint32_t q = dWo.divmod(u ? p2 : p, wo);
-      const uint32_t b = dHo.divmod(q, ho);
-      const T* base = z + (((size_t)b * H + 2 * ho) * W + 2 * wo) * C + c8;
-#pragma unroll
-      for (int dh = 0; dh < 2; ++dh)
-#pragma unroll
-        for (int dw = 0; dw < 2; ++dw) v[u][2 * dh + dw] = ld8<T>(base + ((size_t)dh * W + dw) * C);
-    }
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      float best[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) best[k] = -INFINITY;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float f[8];
-        unpack8<T>(v[u][e], f);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const float r = fmaxf(f[k] * a[k] + h[k], 0.f);
-          best[k] = r > best[k] ? r : best[k];
-        }
-      }
-      if (u == 0 || p2 != p) st8<T>(y + (size_t)(u ? p2 : p) * C + c8, pack8<T>(best));
-    }
-  }
-}
-
 // route d(pool) to the first maximum (scan order h, w — torch's max_pool2d index)
 template <typename T>
 __global__ void maxpool_bwd_kernel(const T* __restrict__ z, const float* __restrict__ sc, const float* __restrict__ sh,
@@ -2173,15 +2123,6 @@ int crnn_bn_relu_maxpool(int dtype, const void* z, const float* scale, const flo
                          int W, int C, void* stream) {
   long n = (long)B * (H / 2) * (W / 2) * (C / 8);
   if (n >= (1L << 31)) return crnn_set_error(hipErrorInvalidValue, "bn_relu_maxpool: > 2^31 pooled 8-channel groups");
-  const long npix = (long)B * (H / 2) * (W / 2);
-  if (crnn_option(CRNN_OPT_POOL2) && C % 8 == 0 && 256 % (C / 8) == 0 && npix < (1L << 30)) {
-    const int per = 256 / (C / 8);
-    const FastDiv dWo((uint32_t)(W / 2)), dHo((uint32_t)(H / 2));
-    DISPATCH(dtype, hipLaunchKernelGGL(bn_relu_maxpool2_kernel<T>, dim3(grid_for((npix + 1) / 2, per)), dim3(256), 0,
-                                       (hipStream_t)stream, (const T*)z, scale, shift, (T*)y, H, W, C,
-                                       (uint32_t)npix, dWo, dHo));
-    return (int)hipGetLastError();
-  }
   DISPATCH(dtype, hipLaunchKernelGGL(bn_relu_maxpool_kernel<T>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream,
                                      (const T*)z, scale, shift, (T*)y, B, H, W, C));
   return (int)hipGetLastError();

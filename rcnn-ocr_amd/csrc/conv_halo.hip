@@ -519,12 +519,15 @@ int conv_halo_dgrad(const crnn_conv_desc* d, const void* dy, const void* w, void
   return (int)hipGetLastError();
 }
 
-// stem wgrad on the halo kernel: grid = slabs = min(bands, CUs)
+// stem wgrad on the halo kernel: grid = slabs = min(bands, CUs). The input conv's (CI = 8: 12 accumulator
+// registers, 41 KB of LDS) streams dy with one row in flight per workgroup; CRNN_OPT_HALO_WG2 gives it one
+// workgroup per band, up to two per CU, for twice the bytes in flight
 int conv_halo_wgrad_slabs(const crnn_conv_desc* d) {
   const int bands = d->B * (d->Wi / TW);
   int ncu = crnn_cu_count();
   if (ncu <= 0) ncu = 256;
-  return bands < ncu ? bands : ncu;
+  const int cap = d->Ci == 8 && crnn_option(CRNN_OPT_HALO_WG2) ? 2 * ncu : ncu;
+  return bands < cap ? bands : cap;
 }
 
 int conv_halo_wgrad(const crnn_conv_desc* d, const void* dy, const void* x, float* ws, hipStream_t st) {

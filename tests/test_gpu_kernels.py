@@ -456,6 +456,37 @@ def test_conv_halo_row16_stores_bit_identical(ci_co):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("B", [8, 1])
+def test_conv_halo_input_wgrad_two_per_cu(B):
+    """The stem input conv's weight gradient (3 -> 64 padded to 8 channels, halo kernel) with one workgroup
+    per band (CRNN_OPT_HALO_WG2 = 1) and with min(bands, CUs) (0): the same sums grouped into other slabs,
+    so equal to fp32 rounding, and both equal to torch's fp64 weight gradient."""
+    L = _L()
+    Ci, H, W, Co = 8, 32, 256, 64
+    g = torch.Generator().manual_seed(19)
+    x = torch.randn(B, H, W, Ci, generator=g).to(DEV, torch.bfloat16)
+    dy = torch.randn(B, H, W, Co, generator=g).to(DEV, torch.bfloat16)
+    st = L.stream_ptr()
+    d = L.ConvDesc(B, H, W, Ci, H, W, Co, 3, 3, 1, 1, 1, 1, Ci)
+    out = {}
+    try:
+        for opt in (0, 1):
+            L.call("crnn_set_option", L.OPT_HALO_WG2, opt)
+            need = L.lib().crnn_conv_wgrad_workspace(L.BF16, d)
+            wsb = torch.empty(need // 4 + 1, device=DEV)
+            dw = torch.zeros(Co, Ci, 3, 3, device=DEV)
+            L.call("crnn_conv_wgrad", L.BF16, d, dy.data_ptr(), x.data_ptr(), dw.data_ptr(), wsb.data_ptr(), need, 0.0, st)
+            torch.cuda.synchronize()
+            out[opt] = dw.clone()
+    finally:
+        L.call("crnn_set_option", L.OPT_HALO_WG2, 1)
+    xr = x.double().permute(0, 3, 1, 2).requires_grad_(False)
+    ref = torch.nn.grad.conv2d_weight(xr, (Co, Ci, 3, 3), dy.double().permute(0, 3, 1, 2), padding=1)
+    for opt in (0, 1):
+        assert relerr(out[opt].double().cpu(), ref.cpu()) < 1e-5, opt
+    assert relerr(out[1], out[0]) < 1e-5
+
+
 @pytest.mark.parametrize("geo", [(128, 256, 8, 64, 256), (256, 512, 4, 32, 512), (131, 256, 8, 62, 256)])
 def test_dgrad_bnrelu_fused(geo):
     """crnn_conv_dgrad_bnrelu == crnn_conv_dgrad + crnn_bn_bwd_reduce (CRNN_BNG_RELU) through
@@ -1387,33 +1418,6 @@ def test_maxpool_relu_bn(dtype):
     pre = z * sc[None, :, None, None] + sh[None, :, None, None]
     dz = dfull.float().permute(0, 3, 1, 2).cpu() * (pre > 0).float() * sc[None, :, None, None]
     assert relerr(dz, zr.grad) < tol
-
-
-@pytest.mark.parametrize("shape", [(4, 128, 32, 256), (3, 64, 6, 10), (1, 16, 2, 2), (5, 24, 8, 12)])
-def test_bn_relu_maxpool_forms_bit_identical(shape):
-    """crnn_bn_relu_maxpool under CRNN_OPT_POOL2 = 1 (fixed channels per thread, two pooled pixels per
-    iteration; C / 8 must divide 256, else the r01 kernel runs) and 0: bit-identical, and equal to torch"""
-    L = _L()
-    B, C, H, W = shape
-    g = torch.Generator().manual_seed(9)
-    z = torch.randn(B, H, W, C, generator=g).to(DEV, torch.bfloat16)
-    sc = (torch.rand(C, generator=g) + 0.5).to(DEV)
-    sh = (torch.randn(C, generator=g) * 0.2).to(DEV)
-    st = L.stream_ptr()
-    outs = {}
-    try:
-        for opt in (0, 1):
-            L.call("crnn_set_option", L.OPT_POOL2, opt)
-            y = torch.full((B, H // 2, W // 2, C), 5.0, dtype=torch.bfloat16, device=DEV)
-            L.call("crnn_bn_relu_maxpool", L.BF16, z.data_ptr(), sc.data_ptr(), sh.data_ptr(), y.data_ptr(), B, H, W, C,
-                   st)
-            torch.cuda.synchronize()
-            outs[opt] = y
-    finally:
-        L.call("crnn_set_option", L.OPT_POOL2, 1)
-    ref = F.max_pool2d(torch.relu(z.float().permute(0, 3, 1, 2) * sc[None, :, None, None] + sh[None, :, None, None]), 2, 2)
-    assert relerr(outs[1].float().permute(0, 3, 1, 2), ref) < 1e-2
-    assert torch.equal(outs[0], outs[1])
 
 
 @pytest.mark.parametrize("mode", [0, 1, 2, 3])

@@ -31,6 +31,12 @@ def main():
         keep = (x, w, dy, d, wd, y, ps, pq)
         cases[f"fwd {Ci}->{Co}"] = (keep, lambda k=keep: L.call("crnn_conv_fwd", L.BF16, k[3], k[0].data_ptr(), k[4].data_ptr(),
                                                                   k[5].data_ptr(), k[6].data_ptr(), k[7].data_ptr(), st))
+        wsb = torch.empty(2 * 512 * Co * Ci * 9 + 16, device=dev)      # room for one slab per band
+        dw = torch.empty(Co, Ci, 3, 3, device=dev)
+        keep3 = keep + (wsb, dw)
+        cases[f"wgrad {Ci}->{Co}"] = (keep3, lambda k=keep3: L.call("crnn_conv_wgrad", L.BF16, k[3], k[2].data_ptr(),
+                                                                      k[0].data_ptr(), k[9].data_ptr(), k[8].data_ptr(),
+                                                                      k[8].numel() * 4, 0.0, st))
         if Ci == 64:
             dx = torch.empty(B, H, W, Ci, dtype=torch.bfloat16, device=dev)
             keep2 = keep + (dx,)
