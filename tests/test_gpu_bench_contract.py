@@ -1,0 +1,51 @@
+"""bench.py's output contract (the driver parses this line): one JSON object on stdout with the metric,
+the whole-job value, the step timing, the run shape, the roofline object of the dominant kernel family,
+the BiLSTM roofline and the CPU baseline (the oracle on a bounded sample, port kind), at a small batch
+so the test takes seconds. Reference metric: BASELINE.json (text-lines/sec, train step)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(*args):
+    env = dict(os.environ)
+    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), *args], cwd=REPO, env=env,
+                       capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [l for l in p.stdout.splitlines() if l.strip().startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+def test_bench_line_contract():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    d = _run("--steps", "2", "--warmup", "1", "--batch", "32", "--cpu-sample", "2", "--no-sub")
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config", "roofline", "roofline_lstm", "cpu_baseline"):
+        assert k in d, k
+    assert d["n_gpus"] == 1 and d["steps"] == 2 and d["warmup"] == 1
+    assert d["higher_is_better"] is True and d["scaling"] == "weak" and d["dtype"] == "bf16"
+    assert d["value"] > 0 and d["ms_per_step"] > 0
+    # whole-job throughput = lines per step / step time
+    assert abs(d["value"] - 32 / (d["ms_per_step"] / 1e3)) <= 0.02 * d["value"]
+    assert "workload" in d["config"] and "model" not in d["config"]
+    r = d["roofline"]
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
+        assert k in r, k
+    assert r["bound"] in ("hbm", "mfma") and r["unit"] in ("GB/s", "TFLOP/s")
+    assert 0 < r["frac"] < 1 and abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
+    for part in ("lstm_fwd", "lstm_bwd"):
+        lr = d["roofline_lstm"][part]
+        assert lr["bound"] == "hbm" and 0 < lr["frac"] < 1
+    c = d["cpu_baseline"]
+    for k in ("value", "unit", "cores", "kind", "sample"):
+        assert k in c, k
+    assert c["kind"] in ("port", "reference") and c["value"] > 0 and c["cores"] >= 1
