@@ -648,6 +648,7 @@ template <typename T> struct DgradBnEpi {
 
 struct SlabEpi {
   static constexpr bool kStats = false;
+  static constexpr bool kPrefer4W = true;
   float* ws;  // [nsplit][Mrows][N]
   int M, N;
   __device__ __forceinline__ void store(int m, int n, f32x4 v, int kz) const {
@@ -1193,7 +1194,9 @@ void crnn_conv_wgrad_plan(int dtype, const crnn_conv_desc* d, int* bm, int* bn, 
     // (twice the tiles, about half the split-K slabs), 2.. = target grid of 128 * value blocks
     const int opt = crnn_option(CRNN_OPT_WGRAD_TILE);
     *bm = 256;
-    *bn = (Kp % 256 == 0 && opt != 1) ? 256 : 128;
+    // Kp = 256 (the 1x1 downsample of 256 channels): 256 x 128 tiles, twice the tiles and half the split-K
+    // slabs (30.9 -> 25.2 us, profiles/r05y/kbench_opt3)
+    *bn = (Kp % 256 == 0 && Kp > 256 && opt != 1) ? 256 : 128;
     long tiles = (long)(d->Co / 256) * (Kp / *bn);
     const long target = opt >= 2 ? 128L * opt : CRNN_WGRAD_BLOCKS;
     long want = target / tiles;                 // whole rounds of 1-block-per-CU waves

@@ -343,10 +343,11 @@ def test_conv_fwd_dgrad_wgrad(cfg, dtype):
                 assert float((a - b).abs().max()) <= 2 ** -7 * float(b.abs().max()) and relerr(a, b) < 2e-3
             # BN partials: the partial grouping may change with the tile (sums agree to fp32 order)
             assert relerr(outs[0][2], outs[1][2]) < 1e-5
-        # the 4-wave form of the 256-row GEMM (CRNN_OPT_GEMM4W): the same fragments, K order, split-K
-        # and per-wave statistic rows as the 8-wave form, so the same bits
+        # the 4-wave form of the 256-row GEMM (CRNN_OPT_GEMM4W; 2 = the weight gradients only): the same
+        # fragments, K order, split-K and per-wave statistic rows as the 8-wave form, so the same bits
         outs = []
-        for v in (1, 0):
+        f4 = L.lib().crnn_get_option(L.OPT_GEMM4W)
+        for v in (1, 2, 0):
             L.call("crnn_set_option", L.OPT_GEMM4W, v)
             try:
                 y2 = torch.empty_like(yd)
@@ -362,9 +363,10 @@ def test_conv_fwd_dgrad_wgrad(cfg, dtype):
                 torch.cuda.synchronize()
                 outs.append((y2, dx2, dw2, ps2, pq2))
             finally:
-                L.call("crnn_set_option", L.OPT_GEMM4W, 0)
-        for a, b in zip(*outs):
-            assert torch.equal(a, b), d
+                L.call("crnn_set_option", L.OPT_GEMM4W, f4)
+        for o in outs[1:]:
+            for a, b in zip(outs[0], o):
+                assert torch.equal(a, b), d
 
 
 def test_conv_halo_vs_gemm():
