@@ -593,6 +593,7 @@ template <typename T> struct DgradEpi {
 template <typename T> struct DgradBnEpi {
   static constexpr bool kStats = false;
   static constexpr bool kTileHook = true;
+  static constexpr int kPrefer4W = 4;
   T* dx;
   int M, N;
   const T* z;
@@ -648,7 +649,7 @@ template <typename T> struct DgradBnEpi {
 
 struct SlabEpi {
   static constexpr bool kStats = false;
-  static constexpr bool kPrefer4W = true;
+  static constexpr int kPrefer4W = 2;
   float* ws;  // [nsplit][Mrows][N]
   int M, N;
   __device__ __forceinline__ void store(int m, int n, f32x4 v, int kz) const {

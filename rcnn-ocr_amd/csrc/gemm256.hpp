@@ -87,10 +87,12 @@ template <class E> struct has_tile_hook<E, std::void_t<decltype(E::kTileHook)>> 
 // MFMA layout gives a lane 4 columns of a row): a wave-instruction then stores whole 128-B row
 // pieces with half the store instructions — the epilogue's store tail is issue-bound
 // (MI355X_MICROARCH.md, epilogue store tail).
-// an EPI with `static constexpr bool kPrefer4W = true` (the conv weight-gradient slabs) runs on the 4-wave
-// form when CRNN_OPT_GEMM4W = 2 (per-layer kbench, profiles/r05y/: the wgrads gain, the forwards lose)
-template <class E, class = void> struct prefers_4w : std::false_type {};
-template <class E> struct prefers_4w<E, std::void_t<decltype(E::kPrefer4W)>> : std::bool_constant<E::kPrefer4W> {};
+// an EPI with `static constexpr int kPrefer4W = bit` runs on the 4-wave form when CRNN_OPT_GEMM4W has that bit
+// (2: the conv weight-gradient slabs, 4: the BN-fused conv input gradients, 8: the BiLSTM weight-gradient
+// slabs; per-layer kbench, profiles/r05y/: the conv wgrads gain, the forwards lose); CRNN_OPT_GEMM4W = 1:
+// every launch
+template <class E, class = void> struct prefers_4w : std::integral_constant<int, 0> {};
+template <class E> struct prefers_4w<E, std::void_t<decltype(E::kPrefer4W)>> : std::integral_constant<int, E::kPrefer4W> {};
 
 template <class E, class = void> struct has_row8 : std::false_type {};
 template <class E> struct has_row8<E, std::void_t<decltype(E::kRow8)>> : std::bool_constant<E::kRow8> {};
@@ -981,7 +983,7 @@ inline int launch256(const LA& la, const LB& lb, const EPI& epi, int M, int N, i
   const int ncu = crnn_cu_count();
   const int popt = crnn_option(CRNN_OPT_GEMM_PERSISTENT);   // 1: when items > CUs, 2: always
   const int f4 = crnn_option(CRNN_OPT_GEMM4W);
-  if (f4 == 1 || (f4 == 2 && prefers_4w<EPI>::value)) {
+  if (f4 == 1 || (f4 & ~1 & prefers_4w<EPI>::value) != 0) {
     hipLaunchKernelGGL((gemm4w_kernel<BM, BN, SKIP, LA, LB, EPI>), dim3(items), dim3(256), 0, st, la, lb, epi, M, N, K,
                        klen, tm, tn, nsplit, nbatch, ktk);
     return (int)hipGetLastError();

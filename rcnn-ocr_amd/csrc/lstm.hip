@@ -418,6 +418,7 @@ template <typename T> struct GateWB {   // B rows n, k = t*B + b: x[b][t][n] (ki
 
 struct BatchSlabEpi {
   static constexpr bool kStats = false;
+  static constexpr int kPrefer4W = 8;
   float* ws;  // [NB][nsplit][M][N]
   int M, N, nsplit, bz;
   __device__ __forceinline__ void set_batch(int b) { bz = b; }

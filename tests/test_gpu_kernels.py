@@ -347,7 +347,7 @@ def test_conv_fwd_dgrad_wgrad(cfg, dtype):
         # fragments, K order, split-K and per-wave statistic rows as the 8-wave form, so the same bits
         outs = []
         f4 = L.lib().crnn_get_option(L.OPT_GEMM4W)
-        for v in (1, 2, 0):
+        for v in (1, 2, 6, 0):
             L.call("crnn_set_option", L.OPT_GEMM4W, v)
             try:
                 y2 = torch.empty_like(yd)
@@ -538,6 +538,24 @@ def test_dgrad_bnrelu_fused(geo):
     assert torch.equal(out[0][0], out[1][0])
     for a, b in zip(out[0][1:], out[1][1:]):
         assert relerr(b, a) < 5e-3   # fp32 accumulators vs the bf16-rounded dx of the unfused pass
+    # the fused dgrad on the 4-wave GEMM form (CRNN_OPT_GEMM4W bit 4): dx bit for bit, the BN partial sums
+    # equal per channel (their grouping into partial rows may follow the wave layout)
+    f4 = L.lib().crnn_get_option(L.OPT_GEMM4W)
+    res = []
+    try:
+        for v in (2, 6):
+            L.call("crnn_set_option", L.OPT_GEMM4W, v)
+            dx = torch.empty(M, Ci, dtype=T, device=DEV)
+            pg, pgx = torch.empty(rows, Ci, device=DEV), torch.empty(rows, Ci, device=DEV)
+            L.call("crnn_conv_dgrad_bnrelu", dt, d, dy.data_ptr(), wd.data_ptr(), dx.data_ptr(), z.data_ptr(),
+                   mean.data_ptr(), inv.data_ptr(), sc.data_ptr(), sh.data_ptr(), pg.data_ptr(), pgx.data_ptr(), st)
+            torch.cuda.synchronize()
+            res.append((dx, pg, pgx))
+    finally:
+        L.call("crnn_set_option", L.OPT_GEMM4W, f4)
+    assert torch.equal(res[0][0], res[1][0])
+    for i in (1, 2):
+        assert relerr(res[1][i].double().sum(0), res[0][i].double().sum(0)) < 1e-5
 
 
 TW_CONVS = [
@@ -1066,6 +1084,21 @@ def _bilstm_case(L, BTHI, dtype, oneshot):
                    w2[2].data_ptr(), w2[3].data_ptr(), wgw.data_ptr(), need, B, T, H, In, accm, st)
         for got, ref in zip(w2, [dwih[0], dwih[1], dwhh[0], dwhh[1]]):
             assert relerr(got.cpu(), 2 * ref.cpu()) < 1e-5
+        # on the 4-wave GEMM form (CRNN_OPT_GEMM4W bit 8): the same bits
+        f4 = L.lib().crnn_get_option(L.OPT_GEMM4W)
+        res = []
+        try:
+            for v in (2, 10):
+                L.call("crnn_set_option", L.OPT_GEMM4W, v)
+                w4 = [torch.zeros_like(t) for t in w2]
+                L.call("crnn_lstm_wgrad", dg.data_ptr(), xd.data_ptr(), hseq.data_ptr(), w4[0].data_ptr(),
+                       w4[1].data_ptr(), w4[2].data_ptr(), w4[3].data_ptr(), wgw.data_ptr(), need, B, T, H, In, 0, st)
+                torch.cuda.synchronize()
+                res.append(w4)
+        finally:
+            L.call("crnn_set_option", L.OPT_GEMM4W, f4)
+        for a, b in zip(*res):
+            assert torch.equal(a, b)
     db2 = torch.full((2, 4 * H), 3.0, device=DEV)
     dbws = torch.empty(L.lib().crnn_lstm_dbias_workspace(H) // 4, device=DEV)
     L.call("crnn_lstm_dbias", dt, dg.data_ptr(), db[0].data_ptr(), db2[0].data_ptr(), db[1].data_ptr(), None,
