@@ -79,8 +79,8 @@ enum { CRNN_OPT_GEMM_STAGGER = 0,    /* 256-row conv GEMM: waves 4-7 one barrier
        CRNN_OPT_GEMM4W = 14,         /* 256-row GEMM family: 1 = the 4-wave form (one wave per SIMD, 128 x BN/2
                                         per wave, fragments double-buffered in registers), 0 = the 8-wave form;
                                         otherwise a mask of the families that take the 4-wave form: 2 = the conv
-                                        weight gradients (default: 2), 4 = the BN-fused conv input gradients,
-                                        8 = the BiLSTM weight gradients */
+                                        weight gradients, 4 = the BN-fused conv input gradients, 8 = the BiLSTM
+                                        weight gradients (default 0: see DESIGN.md r05 on co-scheduling) */
        CRNN_OPT_DIAG = 15,           /* diagnostics only (default 0): bit 0 = conv fwd / plain dgrad / wgrad GEMMs
                                         skip their epilogue stores (the measured epilogue cost; results invalid) */
        CRNN_OPT_DGRAD_GROUP = 16,    /* strided conv dgrad on the 256-row kernel: 1 = all parity classes in ONE launch

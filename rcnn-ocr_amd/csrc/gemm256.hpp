@@ -90,7 +90,7 @@ template <class E> struct has_tile_hook<E, std::void_t<decltype(E::kTileHook)>> 
 // an EPI with `static constexpr int kPrefer4W = bit` runs on the 4-wave form when CRNN_OPT_GEMM4W has that bit
 // (2: the conv weight-gradient slabs, 4: the BN-fused conv input gradients, 8: the BiLSTM weight-gradient
 // slabs; per-layer kbench, profiles/r05y/: the conv wgrads gain, the forwards lose); CRNN_OPT_GEMM4W = 1:
-// every launch
+// every launch. Off by default: one unreproduced co-scheduled determinism failure with bit 2 on
 template <class E, class = void> struct prefers_4w : std::integral_constant<int, 0> {};
 template <class E> struct prefers_4w<E, std::void_t<decltype(E::kPrefer4W)>> : std::integral_constant<int, E::kPrefer4W> {};
 
