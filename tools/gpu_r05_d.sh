@@ -3,5 +3,5 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
-timeout -k 10 500 python -u tools/det_opt.py 14 0,2,0,2 60 > gpurun_out/r05d2_det_gemm4w.log 2>&1; rc=$?
-grep -v amdgpu.ids gpurun_out/r05d2_det_gemm4w.log | tail -8; exit $rc
+timeout -k 10 600 python -u tools/det_opt.py 14 0,2,0,2 300 > gpurun_out/r05d3_det_gemm4w.log 2>&1; rc=$?
+grep -v amdgpu.ids gpurun_out/r05d3_det_gemm4w.log | tail -8; exit $rc
