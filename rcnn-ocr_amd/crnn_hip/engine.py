@@ -342,6 +342,14 @@ class CRNNEngine:
         on the launch stream; conv_time_ms() sums them after a synchronize."""
         self.timers = [] if on else None
 
+    def enable_lstm_timing(self, on: bool = True):
+        """record the persistent BiLSTM sweeps' kernel-only events in every step, also when the conv events
+        are off (four event pairs per step: the per-sweep mean over many steps, comparable to a profiler's)"""
+        self.lstm_timers = [] if on else None
+
+    def _timer_list(self):
+        return self.timers if getattr(self, "timers", None) is not None else self.lstm_timers
+
     def _conv_call(self, kind, flops, name, *args):
         t0 = self._mark()
         call(name, *args)
@@ -358,7 +366,7 @@ class CRNNEngine:
     def _seq_marks(self):
         """(start, end) events the library records around the next persistent BiLSTM kernel alone
         (crnn_lstm_seq_time_next), when timing is on; else None"""
-        if getattr(self, "timers", None) is None:
+        if getattr(self, "timers", None) is None and getattr(self, "lstm_timers", None) is None:
             return None
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record()   # creates the HIP events; the library re-records both on the launch stream
@@ -392,11 +400,14 @@ class CRNNEngine:
         conv fwd / dgrad / wgrad (work = FLOP) and lstm_fwd / lstm_bwd (recurrence sweeps, work =
         algorithmic bytes)."""
         out = {}
-        for kind, flops, a, b in self.timers or []:
+        lt = getattr(self, "lstm_timers", None)
+        for kind, flops, a, b in (self.timers or []) + (lt or []):
             n, ms, fl = out.get(kind, (0, 0.0, 0.0))
             out[kind] = (n + 1, ms + a.elapsed_time(b), fl + flops)
         if self.timers is not None:
             self.timers.clear()
+        if lt is not None:
+            lt.clear()
         return out
 
     @staticmethod
@@ -793,7 +804,7 @@ class CRNNEngine:
                 call("crnn_lstm_seq_fwd", ptr(xg), ptr(whh), ptr(hseq), ptr(gsv) if keep else None,
                      ptr(csv) if keep else None, ptr(self._seq_ws(B)), B, Tn, Hd, s)
                 if ev is not None:
-                    self.timers.append(("lstm_fwd", Tn * self.lstm_step_bytes(B, Hd, T), ev[0], ev[1]))
+                    self._timer_list().append(("lstm_fwd", Tn * self.lstm_step_bytes(B, Hd, T), ev[0], ev[1]))
             else:
                 t0 = self._mark()
                 for st in range(Tn):
@@ -1095,7 +1106,7 @@ class CRNNEngine:
                 call("crnn_lstm_seq_bwd", ptr(dh), ptr(whh_t), ptr(r["gates"]), ptr(r["c"]), ptr(dg),
                      ptr(self._seq_ws(B)), B, Tn, Hd, s)
                 if ev is not None:
-                    self.timers.append(("lstm_bwd", Tn * self.lstm_bptt_step_bytes(B, Hd, T), ev[0], ev[1]))
+                    self._timer_list().append(("lstm_bwd", Tn * self.lstm_bptt_step_bytes(B, Hd, T), ev[0], ev[1]))
             else:
                 t0 = self._mark()
                 bws = ws.get("rnn.bptt_ws", (L.lib().crnn_lstm_bptt_workspace(B, Hd) // 4,), torch.float32)
