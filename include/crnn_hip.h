@@ -84,7 +84,8 @@ enum { CRNN_OPT_GEMM_STAGGER = 0,    /* 256-row conv GEMM: waves 4-7 one barrier
        CRNN_OPT_DIAG = 15,           /* diagnostics only (default 0): bit 0 = conv fwd / plain dgrad / wgrad GEMMs
                                         skip their epilogue stores (the measured epilogue cost; results invalid) */
        CRNN_OPT_DGRAD_GROUP = 16,    /* strided conv dgrad on the 256-row kernel: 1 = all parity classes in ONE launch
-                                        (grouped tile table, longest-K class first; default), 0 = a launch per class */
+                                        (grouped tile table, longest-K class first), 0 = a launch per class,
+                                        2 = grouped with 256 x 256 tiles when Ci % 256 == 0 (default) */
        CRNN_OPT_FIN_TICKET = 17,     /* BN finalize of <= 2048 partial rows: 0 = one launch with no inter-workgroup
                                         hand-off (default), 1 = the r01-r03 ticketed chunk fold (sc1 hand-off that
                                         is valid only at one workgroup per CU; kept for the under-load A/B) */

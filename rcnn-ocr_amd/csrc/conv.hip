@@ -965,7 +965,10 @@ int conv_dgrad_strided(const Geo& g, const void* dy, const void* w, void* dx, co
       for (int i = 1; i < nrec; ++i)
         for (int j = i; j > 0 && recs[j].K > recs[j - 1].K; --j) std::swap(recs[j], recs[j - 1]);
       ClsGroup<T> G{};
-      const int tn = g.Ci / 128;
+      // CRNN_OPT_DGRAD_GROUP = 2: 256 x 256 tiles when Ci allows (half the tiles, each A row gathered once
+      // for 256 output channels instead of twice)
+      const int bn = crnn_option(CRNN_OPT_DGRAD_GROUP) == 2 && g.Ci % 256 == 0 ? 256 : 128;
+      const int tn = g.Ci / bn;
       int total = 0;
       for (int i = 0; i < nrec; ++i) {
         recs[i].start = total;
@@ -982,8 +985,12 @@ int conv_dgrad_strided(const Geo& g, const void* dy, const void* w, void* dx, co
       G.tn = tn;
       G.total = total;
       if constexpr (sizeof(T) == 2) {
-        hipLaunchKernelGGL((dgrad_cls_group_kernel<T, 128>), dim3(total), dim3(512), 0, st, G,
-                           crnn_option(CRNN_OPT_GEMM_STAGGER));
+        if (bn == 256)
+          hipLaunchKernelGGL((dgrad_cls_group_kernel<T, 256>), dim3(total), dim3(512), 0, st, G,
+                             crnn_option(CRNN_OPT_GEMM_STAGGER));
+        else
+          hipLaunchKernelGGL((dgrad_cls_group_kernel<T, 128>), dim3(total), dim3(512), 0, st, G,
+                             crnn_option(CRNN_OPT_GEMM_STAGGER));
         return (int)hipGetLastError();
       }
     }

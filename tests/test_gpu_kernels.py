@@ -197,7 +197,7 @@ def test_dgrad_class_group(geo):
     dycat[m:].copy_(to_nhwc(dyd, None, torch.bfloat16).reshape(-1))
     outs = {}
     try:
-        for grouped in (1, 0):
+        for grouped in (1, 0, 2):
             L.lib().crnn_set_option(L.OPT_DGRAD_GROUP, grouped)
             dx = torch.full((B, H, W, Ci), float("nan"), dtype=torch.bfloat16, device=DEV)
             if with_ds:
@@ -207,13 +207,15 @@ def test_dgrad_class_group(geo):
             torch.cuda.synchronize()
             outs[grouped] = dx.float().permute(0, 3, 1, 2).cpu()
     finally:
-        L.lib().crnn_set_option(L.OPT_DGRAD_GROUP, 1)
+        L.lib().crnn_set_option(L.OPT_DGRAD_GROUP, 2)
     e1, e0 = relerr(outs[1], ref), relerr(outs[0], ref)
     print(f"dgrad class group {geo}: grouped rel err {e1:.3e}, per class {e0:.3e}")
     assert torch.isfinite(outs[1]).all()
     assert e1 < 1e-2 and e1 <= e0 * 1.05 + 1e-6
     if B == 256:
         assert torch.equal(outs[1], outs[0]), "grouped launch differs from the per-class launches"
+    # 256 x 256 group tiles (CRNN_OPT_DGRAD_GROUP = 2, Ci % 256 == 0): the same K-tiles per element
+    assert torch.equal(outs[2], outs[1]), "256-wide group tiles differ from the 128-wide ones"
 
 
 @pytest.mark.parametrize("dtype,cfg", [(dt, c) for c in CONVS for dt in (torch.float32, torch.bfloat16)]
