@@ -5,6 +5,8 @@ AdamW) in bf16 at B=256 per GPU on 32x256 synthetic crops — BASELINE.json conf
     python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
     torchrun --nproc-per-node N bench.py --gpus N ...      (one process per GPU)
 
+`python bench.py --gpus N` (N > 1) with no launcher env starts the N ranks itself (a torch.distributed.run
+child, before any GPU call in this process). A run whose rank count differs from --gpus exits non-zero.
 Rank 0 prints ONE JSON line (metric/value/...); value = lines/s over all ranks.
 """
 import argparse
@@ -300,9 +302,38 @@ def bench_preprocess(args, world, rank, dev):
         dist.destroy_process_group()
 
 
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n):
+    """`python bench.py --gpus N` without a launcher: start N fresh ranks (one process per GPU) under
+    torch.distributed.run as a CHILD process and return its exit code. This process has not touched the
+    GPU (no HIP call before this point), and it never execs: it only waits and relays (rank 0 prints the
+    JSON line straight to the inherited stdout)."""
+    import subprocess
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env["CRNN_BENCH_SPAWNED"] = "1"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     args = parse()
+    if args.gpus < 1:
+        sys.exit("bench.py: --gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
     from crnn_hip import dist as D
+    world = D.env_world()[0]
+    if world != args.gpus:   # never report an N-GPU line measured on another rank count
+        sys.exit(f"bench.py: --gpus {args.gpus} but the launcher started {world} rank(s) (WORLD_SIZE); refusing to "
+                 f"report a line whose n_gpus differs from --gpus")
     world, rank, local = D.init_from_env()
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)

@@ -49,9 +49,8 @@ int crnn_version(void);
 const char* crnn_last_error_string(void);
 /* tuning switches, process-wide (benchmark A/B only; defaults are the measured-best settings) */
 enum { CRNN_OPT_GEMM_STAGGER = 0,    /* 256-row conv GEMM: waves 4-7 one barrier behind waves 0-3 */
-       CRNN_OPT_GEMM_PERSISTENT = 1, /* 256-row GEMM: <= 1 block per CU looping over tiles, one continuous
-                                        LDS-DMA pipeline across tile boundaries; 0 (default) off, 1 when
-                                        tiles > CUs, 2 always */
+       CRNN_OPT_GEMM_PERSISTENT = 1, /* retired in r06 (the persistent 256-row GEMM measured 20-50 % slower and
+                                        was removed); the key is kept so option numbers stay stable: no effect */
        CRNN_OPT_DEEP_LINEAR = 2,     /* bf16 crnn_gemm_nt/nn on the 256-row kernel when its grid fills the chip (default 1) */
        CRNN_OPT_WGRAD_TILE = 3,      /* conv wgrad plan: 0 = 256x256, 1 = 256x128 tiles, n >= 2: ~128n blocks */
        CRNN_OPT_LSTM_TILE = 4,       /* persistent BiLSTM workgroup tile: 0 = auto, 1 = 32 samples x 32 units,
@@ -59,8 +58,12 @@ enum { CRNN_OPT_GEMM_STAGGER = 0,    /* 256-row conv GEMM: waves 4-7 one barrier
        CRNN_OPT_HALO_CONV = 5,       /* full-resolution 3x3 stride-1 convs (the stem's 64 -> 128) on the
                                         halo-tiled direct kernel (conv_halo.hip): 1 = on (default), 0 = GEMM,
                                         n >= 2: on, with n-row bands for the MFMA-bound instances */
-       CRNN_OPT_LSTM_HANDOFF = 6,    /* persistent BiLSTM forward: 1 = data-tagged granule ring (default),
-                                        0 = write-through payload + step counter */
+       CRNN_OPT_LSTM_HANDOFF = 6,    /* persistent BiLSTM forward: 1 = K-split waves, data-tagged granule ring,
+                                        0 = K-split waves, write-through payload + step counter, 2 = unit-complete
+                                        waves (each wave owns whole units over the full K; h staged once per
+                                        workgroup in LDS; granules published from registers), 3 (default) = the
+                                        same with 8 waves of 8 units where the tile has 64 units (H <= 512),
+                                        form 1 on the 32-unit tiles */
        CRNN_OPT_WGRAD_REDUCE = 7,    /* conv wgrad split-K slab reduce: 1 = (co, 64-channel) tiles transposed
                                         through LDS, coalesced OIHW stores (default), 0 = flat, scattered stores */
        CRNN_OPT_WGRAD_FAST = 8,      /* conv wgrad on the 256-row kernel: 1 = per-tile scalar pixel decode for
@@ -80,22 +83,20 @@ enum { CRNN_OPT_GEMM_STAGGER = 0,    /* 256-row conv GEMM: waves 4-7 one barrier
                                         per wave, fragments double-buffered in registers), 0 = the 8-wave form;
                                         otherwise a mask of the families that take the 4-wave form: 2 = the conv
                                         weight gradients, 4 = the BN-fused conv input gradients, 8 = the BiLSTM
-                                        weight gradients (default 0: see DESIGN.md r05 on co-scheduling) */
+                                        weight gradients (default 2 since r06, when the asm-load register reuse
+                                        behind r05's co-scheduled mismatch was found and fixed) */
        CRNN_OPT_DIAG = 15,           /* diagnostics only (default 0): bit 0 = conv fwd / plain dgrad / wgrad GEMMs
                                         skip their epilogue stores (the measured epilogue cost; results invalid) */
        CRNN_OPT_DGRAD_GROUP = 16,    /* strided conv dgrad on the 256-row kernel: 1 = all parity classes in ONE launch
                                         (grouped tile table, longest-K class first), 0 = a launch per class,
                                         2 = grouped with 256 x 256 tiles when Ci % 256 == 0 (default) */
-       CRNN_OPT_FIN_TICKET = 17,     /* BN finalize of <= 2048 partial rows: 0 = one launch with no inter-workgroup
-                                        hand-off (default), 1 = the r01-r03 ticketed chunk fold (sc1 hand-off that
-                                        is valid only at one workgroup per CU; kept for the under-load A/B) */
+       CRNN_OPT_FIN_TICKET = 17,     /* retired in r06 (the r01-r03 ticketed BN finalize was removed): no effect */
        CRNN_OPT_CONV_HALO_W = 18,    /* 3x3 / stride-1 conv fwd and stride-1 dgrad (forward path) over maps of a
                                         power-of-two width 32..256 on the 256-row kernel: 1 = one W-halo A image per
                                         (kernel row, 64-channel block) serves the three kw K-tiles (gemm256hw.hpp;
                                         default), 0 = an A image per K-tile (gemm256.hpp) */
-       CRNN_OPT_LSTM_PIPE = 19,      /* persistent BiLSTM: bit 0 = forward sweep as two pipelined 16-sample groups x
-                                        32 units per workgroup (a group's hand-off travels while the workgroup
-                                        computes the other group), bit 1 = the same for the BPTT */
+       CRNN_OPT_LSTM_PIPE = 19,      /* retired in r06 (the pipelined two-group BiLSTM sweeps measured slower and
+                                        were removed): no effect */
        CRNN_OPT_LINEAR_ROW8 = 20,    /* bf16 crnn_gemm_nt / nn on the 256-row kernel: 1 = 16-B row stores through the
                                         wave's LDS (8 columns per lane; default), 0 = 8-B stores from the MFMA layout */
        CRNN_OPT_HALO_ROW16 = 21,     /* the stem's input conv (3 -> 64, halo kernel): 1 = the output tile staged in LDS
@@ -556,19 +557,6 @@ int crnn_sgd_step(float* p, const float* g, float* momentum_buf, long n, float l
 /* AdamW without a status guard: crnn_adam_step(..., coupled = 0, skip = null) */
 int crnn_adamw(float* p, const float* g, float* m, float* v, long n, float lr, float beta1, float beta2, float eps,
                float weight_decay, int step, float grad_scale, void* stream);
-
-/* ------------------------------------------------------------------ diagnostics (not on any model path)
- * LDS sentinel: `blocks` workgroups of 256 threads, each filling lds_bytes of dynamic LDS with a
- * known pattern and re-checking it `iters` times (sleep x 127*64 cycles between checks; mode bit 0:
- * each check rewrites the allocation with a new pattern first, bit 1: each check also verifies a
- * wave-wide __shfl_xor sum), so that a
- * kernel running concurrently on another stream can be checked for LDS writes outside its own
- * allocation. out (crnn_diag_lds_sentinel_words() u32, zeroed by the caller): [0] mismatching
- * words, [1] records taken, [2] waves that saw one, [3] checks done; then records of 8 words
- * {index, got, expected, HW_ID, LDS_ALLOC, XCC_ID, check, block}. */
-int crnn_diag_lds_sentinel(unsigned* out, int blocks, int lds_bytes, int iters, unsigned seed, int sleep,
-                           int mode, void* stream);
-int crnn_diag_lds_sentinel_words(void);
 
 #ifdef __cplusplus
 }

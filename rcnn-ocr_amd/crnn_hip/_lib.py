@@ -155,8 +155,6 @@ _SIGS = {
     "crnn_adamw": ([vp, vp, vp, vp, i64, f32, f32, f32, f32, f32, i32, f32, vp], i32),
     "crnn_adam_step": ([vp, vp, vp, vp, i64, f32, f32, f32, f32, f32, i32, f32, i32, vp, vp], i32),
     "crnn_sgd_step": ([vp, vp, vp, i64, f32, f32, f32, f32, i32, vp, vp], i32),
-    "crnn_diag_lds_sentinel": ([vp, i32, i32, i32, C.c_uint, i32, i32, vp], i32),
-    "crnn_diag_lds_sentinel_words": ([], i32),
 }
 
 _lib = None

@@ -156,9 +156,8 @@ template <class F> int chan_reduce(F f, long M, int C, float* p0, float* p1, int
 }
 
 // ------------------------------------------------------------ finalize
-// Up to FIN_FUSED_ROWS partial rows: one launch (fin_fused_kernel below, a <= 32-block ticket per
-// channel group). Beyond that, two launches (a ticket over up to 256 blocks costs more than the
-// launch boundary: the same-address atomics serialize):
+// Up to FIN_FUSED_ROWS partial rows (C % 8 == 0): one launch (fin_one_kernel below). Otherwise two
+// launches:
 //  (1) fin_chunk_kernel, grid (C/64, P): block y folds partial rows [y*chunk, ...) of 64 channels
 //      (4 row lanes per channel, 8 loads in flight per lane) into one chunk partial. Chan mode
 //      (forward): rows hold (sum, M2 about the row's own mean) covering rpp data rows, the chunk
@@ -335,148 +334,7 @@ __global__ __launch_bounds__(256) void fin_combine_kernel(const float* __restric
   }
 }
 
-// One-launch finalize for up to FIN_FUSED_ROWS partial rows: fin_chunk's fold over at most
-// FIN_PF chunks per 64-channel group, then a ticket — the group's last block to finish combines.
-// Cross-workgroup hand-off in the guide's first valid form (cdna_hip_programming.md Guideline 16):
-// chunk results by sc1 stores, vmcnt(0), workgroup barrier, ONE agent-scope atomic add per block;
-// the block whose add returns FIN_PF-1 (its own add returned) reads them with sc1 loads and re-arms
-// the counter. <= FIN_PF same-address atomics per group (256 of them serialized: the reason the
-// large-row case keeps two launches).
-constexpr int FIN_PF = 32;
 constexpr int FIN_FUSED_ROWS = 2048;
-
-__device__ __forceinline__ void st_sc1_f32(__amdgpu_buffer_rsrc_t r, uint32_t off, float v) {
-  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, off, 0, 16);
-}
-__device__ __forceinline__ float ld_sc1_f32(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 16));
-}
-
-template <bool CHAN, class A>
-__global__ __launch_bounds__(256) void fin_fused_kernel(const float* __restrict__ p0, const float* __restrict__ p1,
-                                                        int rows, long rpp, int C, long count, int chunk, float* o0,
-                                                        unsigned* cnt, A args) {
-  __shared__ float red[2][4][64];
-  __shared__ double dred[2][4][64];
-  __shared__ int last;
-  const int lc = threadIdx.x & 63, ln = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + lc;
-  const int P = gridDim.y;
-  const int r0 = blockIdx.y * chunk, r1 = min(rows, r0 + chunk);
-  // ---- stage 1: this block's chunk (as fin_chunk_kernel)
-  float s = 0.f, q = 0.f;
-  if (c < C)
-    for (int rb = r0 + ln; rb < r1; rb += 32) {
-      float a[8], b[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int r = rb + 4 * u;
-        a[u] = r < r1 ? p0[(size_t)r * C + c] : 0.f;
-        b[u] = (!CHAN && r < r1) ? p1[(size_t)r * C + c] : 0.f;
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        s += a[u];
-        q += b[u];
-      }
-    }
-  red[0][ln][lc] = s;
-  red[1][ln][lc] = q;
-  __syncthreads();
-  const float S = red[0][0][lc] + red[0][1][lc] + red[0][2][lc] + red[0][3][lc];
-  if (CHAN) {
-    const long n = span_rows(r0, r1, rpp, count);
-    const float mu = n > 0 ? S / (float)n : 0.f;
-    const float rr = 1.f / (float)rpp;
-    q = 0.f;
-    if (c < C)
-      for (int rb = r0 + ln; rb < r1; rb += 32) {
-        float a[8], b[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const int r = rb + 4 * u;
-          a[u] = r < r1 ? p0[(size_t)r * C + c] : 0.f;
-          b[u] = r < r1 ? p1[(size_t)r * C + c] : 0.f;
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const int r = rb + 4 * u;
-          const long nr = r < r1 ? span_rows(r, r + 1, rpp, count) : 0;
-          if (nr == 0) continue;
-          const float d = a[u] * (nr == rpp ? rr : 1.f / (float)nr) - mu;
-          q += b[u] + (float)nr * d * d;
-        }
-      }
-    __syncthreads();
-    red[1][ln][lc] = q;
-    __syncthreads();
-  }
-  // chunk results: o0[p][c] (sum), o0[FIN_PF * C + p * C + c] (M2 / second sum), sc1
-  const __amdgpu_buffer_rsrc_t ro = mk_rsrc(o0, (uint32_t)(2 * FIN_PF * C * sizeof(float)));
-  if (ln == 0 && c < C) {
-    st_sc1_f32(ro, (uint32_t)((blockIdx.y * C + c) * 4), S);
-    st_sc1_f32(ro, (uint32_t)(((FIN_PF + blockIdx.y) * C + c) * 4),
-               red[1][0][lc] + red[1][1][lc] + red[1][2][lc] + red[1][3][lc]);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned prev = __hip_atomic_fetch_add(cnt + blockIdx.x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = prev == (unsigned)(P - 1);
-    if (last) __hip_atomic_store(cnt + blockIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  __syncthreads();
-  if (!last) return;
-  // ---- stage 2 (last block of the group): fold the P <= 32 chunk results in double, 4 lanes
-  // per channel, 8 each; unconditional loads (out-of-range offsets read 0)
-  float v[8], w[8];
-#pragma unroll
-  for (int u = 0; u < 8; ++u) {
-    const int pp = ln + 4 * u;
-    const bool ok = c < C && pp < P;
-    v[u] = ld_sc1_f32(ro, ok ? (uint32_t)((pp * C + c) * 4) : OOB);
-    w[u] = ld_sc1_f32(ro, ok ? (uint32_t)(((FIN_PF + pp) * C + c) * 4) : OOB);
-  }
-  double ds = 0.0, dq = 0.0;
-#pragma unroll
-  for (int u = 0; u < 8; ++u) {
-    ds += v[u];
-    if (!CHAN) dq += w[u];
-  }
-  dred[0][ln][lc] = ds;
-  dred[1][ln][lc] = dq;
-  __syncthreads();
-  ds = dred[0][0][lc] + dred[0][1][lc] + dred[0][2][lc] + dred[0][3][lc];
-  dq = dred[1][0][lc] + dred[1][1][lc] + dred[1][2][lc] + dred[1][3][lc];
-  if constexpr (CHAN) {
-    const long crows = (long)chunk * rpp;
-    const double mean = ds / (double)count;
-    double m2 = 0.0;
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int pp = ln + 4 * u;
-      const long n = pp < P ? span_rows(pp, pp + 1, crows, count) : 0;
-      if (n == 0) continue;
-      const double d = (double)v[u] / (double)n - mean;
-      m2 += (double)w[u] + (double)n * d * d;
-    }
-    __syncthreads();
-    dred[1][ln][lc] = m2;
-    __syncthreads();
-    if (ln == 0 && c < C) {
-      double var = (dred[1][0][lc] + dred[1][1][lc] + dred[1][2][lc] + dred[1][3][lc]) / (double)count;
-      if (var < 0.0) var = 0.0;
-      write_affine(args, c, mean, var, true, count);
-    }
-  } else {
-    if (ln == 0 && c < C) {
-      if (args.dgamma) args.dgamma[c] = (float)(args.acc ? args.dgamma[c] + dq : dq);
-      if (args.dbeta) args.dbeta[c] = (float)(args.acc ? args.dbeta[c] + ds : ds);
-      args.mean_g[c] = (float)(ds / (double)count);
-      args.mean_gx[c] = (float)(dq / (double)count);
-    }
-  }
-}
 
 // One-launch finalize with NO inter-workgroup hand-off (r04, the default for <= FIN_FUSED_ROWS rows):
 // block = 8 channels; thread = (4-channel half h = tid & 1, row lane rl = tid >> 1 of 128). Each thread
@@ -486,9 +344,9 @@ __global__ __launch_bounds__(256) void fin_fused_kernel(const float* __restrict_
 // (every row holds rpp samples except at most the one at count / rpp). Block sums: an xor butterfly
 // over the wave's 32 row lanes (commutative adds: every lane ends with the same bits), then the four
 // waves' values from LDS in a fixed order. A block reads only what the previous kernel wrote, so the
-// launch boundary is the only hand-off. (fin_fused_kernel above handed its chunk results to the
-// group's last block by 4-B sc1 stores / loads + a ticket: a form the guide measures valid only at one
-// workgroup per CU; under load it read stale chunk results)
+// launch boundary is the only hand-off. (r01-r03 handed chunk results to the group's last block by
+// 4-B sc1 stores / loads + a ticket: a form the guide measures valid only at one workgroup per CU;
+// under load it read stale chunk results, DESIGN.md §6. Removed in r06.)
 constexpr int FIN1_RL = 128;
 
 template <int K>
@@ -597,7 +455,7 @@ __global__ void bn_eval_affine_kernel(int C, FinFwd a) {
 template <bool CHAN, class A>
 int launch_fin(const float* p0, const float* p1, int rows, long rpp, int C, long count, float* ws, const A& args,
                hipStream_t st) {
-  if (rows <= FIN_FUSED_ROWS && C % 8 == 0 && crnn_option(CRNN_OPT_FIN_TICKET) == 0) {
+  if (rows <= FIN_FUSED_ROWS && C % 8 == 0) {
     const dim3 g(C / 8), t(256);
     if (rows <= 2 * FIN1_RL)
       hipLaunchKernelGGL((fin_one_kernel<CHAN, 2, A>), g, t, 0, st, p0, p1, rows, rpp, C, count, args);
@@ -607,15 +465,6 @@ int launch_fin(const float* p0, const float* p1, int rows, long rpp, int C, long
       hipLaunchKernelGGL((fin_one_kernel<CHAN, 8, A>), g, t, 0, st, p0, p1, rows, rpp, C, count, args);
     else
       hipLaunchKernelGGL((fin_one_kernel<CHAN, 16, A>), g, t, 0, st, p0, p1, rows, rpp, C, count, args);
-    return (int)hipGetLastError();
-  }
-  if (rows <= FIN_FUSED_ROWS && C <= FIN_CNT * 64) {  // one launch, ticket per 64-channel group
-    int P = (rows + 15) / 16;
-    if (P > FIN_PF) P = FIN_PF;
-    const int chunk = (rows + P - 1) / P;
-    P = (rows + chunk - 1) / chunk;
-    hipLaunchKernelGGL((fin_fused_kernel<CHAN, A>), dim3((C + 63) / 64, P), dim3(256), 0, st, p0, p1, rows, rpp, C,
-                       count, chunk, ws + FIN_CNT, (unsigned*)ws, args);
     return (int)hipGetLastError();
   }
   int P = rows / 16;  // ~16 partial rows per stage-1 block (4 per lane)

@@ -513,238 +513,6 @@ __global__ __launch_bounds__(512) void gemm256_kernel(LA la, LB lb, EPI epi, int
   gemm256_item<BM, BN, SKIP>(la, lb, epi, M, K, klen, m_tile, n_tile, kz, stagger, ktk);
 }
 
-// Persistent variant (crnn_set_option CRNN_OPT_GEMM_PERSISTENT): grid <= CU count, every block
-// loops over work items with one continuous LDS-DMA pipeline across item boundaries. Measured no
-// faster on this path's shapes (the short-K stem conv included) and slower on some, so it is off
-// by default and kept for A/B.
-template <int BM, int BN, class LA, class LB, class EPI>
-__global__ __launch_bounds__(512) void gemm256p_kernel(LA la, LB lb, EPI epi, int M, int N, int K, int klen,
-                                                      int tiles_m, int tiles_n, int nsplit, int stagger,
-                                                      int nbatch) {
-  using T = bf16;
-  static_assert(BM == 256 && (BN == 256 || BN == 128), "tile");
-  constexpr int KS = 64;
-  constexpr int WM = BM / 2, WN = BN / 4;        // per-wave output block
-  constexpr int MI = WM / 16, NI = WN / 16;      // 16x16 fragments per wave
-  constexpr int MQ = MI / 2, NQ = NI / 2;        // fragments per quadrant
-  constexpr int QM = WM / 2, QN = WN / 2;        // quadrant extent
-  using OA = Op256<LA, BM, QM>;
-  using OB = Op256<LB, BN, QN>;
-  constexpr int STAGE = OA::TB + OB::TB;
-  constexpr int VM = OA::I + 2 * OB::I;          // DMA instructions of tile t+2 issued before the P4 wait
-  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
-
-  // Persistent over work items (tile, K-split): block lb takes items lb, lb + G, lb + 2G, ...
-  // (G = gridDim.x <= CU count) and runs their K-tiles as ONE flat sequence through the
-  // LDS-DMA ring, so the next item's first stages are in flight while the current item's last
-  // stages compute and while its epilogue runs. Positions u, u+1, u+2 of the sequence are
-  // tracked by cursors (item, K-tile index); the loaders' row contexts follow the item of the
-  // position being issued (re-initialised once per item, before the P2 issue that first needs it).
-  // item = ((batch * nsplit + split) * tiles_m + m_tile) * tiles_n + n_tile; a batch entry is an
-  // independent GEMM whose loaders / epilogue are selected by set_batch (nbatch > 1 only)
-  const int items = tiles_m * tiles_n * nsplit * nbatch;
-  const int G = gridDim.x;
-  const int lb_id = xcd_remap(blockIdx.x, G);
-  if (lb_id >= items) return;
-
-  const int lane = threadIdx.x & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wr = wid >> 2, wc = wid & 3;
-
-  struct Cur {
-    int it, t, nk, kb;  // item, K-tile within the item, K-tiles of the item, first k of the item
-  };
-  auto item_k = [&](Cur& c) {
-    const int kz = (c.it / (tiles_n * tiles_m)) % nsplit;
-    c.kb = kz * klen;
-    const int ke = min(K, c.kb + klen);
-    c.nk = ke > c.kb ? (ke - c.kb + KS - 1) / KS : 1;   // an empty split still owns one (masked) K-tile
-  };
-  auto advance = [&](Cur& c) {
-    if (++c.t == c.nk) {
-      c.it += G;
-      c.t = 0;
-      if (c.it < items) item_k(c);
-    }
-  };
-  auto tile_m0 = [&](int it) { return ((it / tiles_n) % tiles_m) * BM; };
-  auto tile_n0 = [&](int it) { return (it % tiles_n) * BN; };
-
-  auto item_b = [&](int it) { return it / (tiles_n * tiles_m * nsplit); };
-  auto select_batch = [&](int bz) {
-    if constexpr (has_set_batch<LA>::value) la.set_batch(bz);
-    if constexpr (has_set_batch<LB>::value) lb.set_batch(bz);
-  };
-  OA oa;
-  OB ob;
-  int ctx_it = lb_id;
-  if (nbatch > 1) select_batch(item_b(ctx_it));
-  oa.init(la, tile_m0(ctx_it), wid, lane, wr);
-  ob.init(lb, tile_n0(ctx_it), wid, lane, wc);
-  auto ensure_ctx = [&](int it) {
-    if (it != ctx_it) {
-      ctx_it = it;
-      if (nbatch > 1) select_batch(item_b(it));
-      oa.init(la, tile_m0(it), wid, lane, wr);
-      ob.init(lb, tile_n0(it), wid, lane, wc);
-    }
-  };
-  __amdgpu_buffer_rsrc_t ra = la.rsrc(), rb = lb.rsrc();
-  char* const sA0 = smem;
-  char* const sB0 = smem + OA::TB;
-
-  f32x4 acc[MI][NI];
-#pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  Cur cur{lb_id, 0, 1, 0};
-  item_k(cur);
-  // ---- prologue: position 0 whole, position 1 except its A-half1 (issued in P1 of position 0)
-  {
-    const typename LA::Prep pa = la.prep(cur.kb);
-    const typename LB::Prep pb = lb.prep(cur.kb);
-    oa.issue(la, ra, sA0, 0, pa);
-    ob.issue(lb, rb, sB0, 0, pb);
-    ob.issue(lb, rb, sB0, 1, pb);
-    oa.issue(la, ra, sA0, 1, pa);
-  }
-  Cur c1 = cur;
-  advance(c1);
-  if (c1.it < items) {
-    ensure_ctx(c1.it);
-    if (nbatch > 1) {
-      ra = la.rsrc();
-      rb = lb.rsrc();
-    }
-    const int k1 = c1.kb + c1.t * KS;
-    const typename LA::Prep pa = la.prep(k1);
-    const typename LB::Prep pb = lb.prep(k1);
-    oa.issue(la, ra, sA0 + STAGE, 0, pa);
-    ob.issue(lb, rb, sB0 + STAGE, 0, pb);
-    ob.issue(lb, rb, sB0 + STAGE, 1, pb);
-    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(VM) : "memory");
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  Cur c2 = c1;
-  if (c2.it < items) advance(c2);
-  raw_barrier();
-  // ping-pong: waves 4-7 (wr == 1, one per SIMD) run one barrier behind waves 0-3, so each SIMD
-  // alternates one wave's MFMA cluster with its partner's ds_read / LDS-DMA issue segment
-  if (stagger && wr == 1) raw_barrier();
-
-  bf16x8 af[MQ][2], bfr[NI][2];
-  for (int u = 0; cur.it < items; ++u) {
-    const int b = u & 1;
-    const char* As = smem + b * STAGE;
-    const char* Bs = As + OA::TB;
-    const uint32_t lA = lds_addr(As), lB = lds_addr(Bs);
-    const bool n1 = c1.it < items, n2 = c2.it < items;
-    typename LA::Prep pa2;
-    typename LB::Prep pb2;
-    typename LA::Prep pa1 = la.prep(c1.kb + c1.t * KS);   // A-half1 of position u+1 (ctx: c1's item)
-    if (n2) {
-      pa2 = la.prep(c2.kb + c2.t * KS);
-      pb2 = lb.prep(c2.kb + c2.t * KS);
-    }
-    // ---- P1: quadrant (0,0)
-    oa.template load<0, MQ>(af, As, lA, wr * WM, lane);
-    ob.template load<0, NQ>(*reinterpret_cast<bf16x8(*)[NQ][2]>(&bfr[0]), Bs, lB, wc * WN, lane);
-    if (n1) oa.issue(la, ra, sA0 + (b ^ 1) * STAGE, 1, pa1);
-    lds_wait_all();
-    raw_barrier();
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int i = 0; i < MQ; ++i)
-#pragma unroll
-        for (int j = 0; j < NQ; ++j) mma<T>(acc[i][j], bfr[j][kk], af[i][kk]);
-    __builtin_amdgcn_s_setprio(0);
-    raw_barrier();
-    // ---- P2: quadrant (0,1)
-    ob.template load<1, NQ>(*reinterpret_cast<bf16x8(*)[NQ][2]>(&bfr[NQ]), Bs, lB, wc * WN, lane);
-    if (n2) {
-      if (nbatch > 1 && c2.it != ctx_it) {
-        ensure_ctx(c2.it);
-        ra = la.rsrc();
-        rb = lb.rsrc();
-      } else {
-        ensure_ctx(c2.it);
-      }
-      oa.issue(la, ra, sA0 + b * STAGE, 0, pa2);
-    }
-    lds_wait_all();
-    raw_barrier();
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int i = 0; i < MQ; ++i)
-#pragma unroll
-        for (int j = NQ; j < NI; ++j) mma<T>(acc[i][j], bfr[j][kk], af[i][kk]);
-    __builtin_amdgcn_s_setprio(0);
-    raw_barrier();
-    // ---- P3: quadrant (1,1)
-    oa.template load<1, MQ>(af, As, lA, wr * WM, lane);
-    if (n2) ob.issue(lb, rb, sB0 + b * STAGE, 0, pb2);
-    lds_wait_all();
-    raw_barrier();
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int i = 0; i < MQ; ++i)
-#pragma unroll
-        for (int j = NQ; j < NI; ++j) mma<T>(acc[MQ + i][j], bfr[j][kk], af[i][kk]);
-    __builtin_amdgcn_s_setprio(0);
-    raw_barrier();
-    // ---- P4: quadrant (1,0)
-    if (n2) {
-      ob.issue(lb, rb, sB0 + b * STAGE, 1, pb2);
-      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(VM) : "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    raw_barrier();
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int i = 0; i < MQ; ++i)
-#pragma unroll
-        for (int j = 0; j < NQ; ++j) mma<T>(acc[MQ + i][j], bfr[j][kk], af[i][kk]);
-    __builtin_amdgcn_s_setprio(0);
-    raw_barrier();
-    // ---- item finished: epilogue (registers + global stores only; the next item's first
-    // stages are already in flight), then a fresh accumulator
-    if (cur.t == cur.nk - 1) {
-      const int m0 = tile_m0(cur.it), n0 = tile_n0(cur.it), kz = (cur.it / (tiles_n * tiles_m)) % nsplit;
-      if constexpr (has_set_batch<EPI>::value)
-        if (nbatch > 1) epi.set_batch(item_b(cur.it));
-      const int mr = lane & 15, nq = 4 * (lane >> 4);
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int j = 0; j < NI; ++j) epi.store(m0 + wr * WM + i * 16 + mr, n0 + wc * WN + j * 16 + nq, acc[i][j], kz);
-      if constexpr (EPI::kStats)
-        wave_col_stats<MI, NI>(acc, epi, M, m0 + wr * WM, (m0 / BM) * 2 + wr, n0 + wc * WN, lane);
-      if constexpr (has_tile_hook<EPI>::value)
-        epi.template tile<MI, NI>(acc, M, m0 + wr * WM, (m0 / BM) * 2 + wr, n0 + wc * WN, lane);
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-    cur = c1;
-    c1 = c2;
-    if (c2.it < items) advance(c2);
-  }
-  if (stagger && wr == 0) raw_barrier();
-}
-
 // 4-wave form helper: N fragments of one 32-deep k sub-step KK (see Op256::load), fragments
 // F0 .. F0+N-1 of quadrant half H
 template <class OP, int H, int N, int KK, int F0 = 0>
@@ -908,6 +676,20 @@ __device__ __forceinline__ void gemm4w_item(LA la, LB lb, EPI epi, int M, int K,
     for (; t < e1; ++t) ktile(std::integral_constant<uint32_t, 0xffu>{}, t);
     for (; t < nk; ++t) ktile(std::integral_constant<uint32_t, M2>{}, t);
   }
+  // The F0(nk) reads past the last K-tile are asm LDS loads (trd / frag), which hipcc neither counts nor
+  // keeps live: their registers are dead after the loop, so hipcc reused them for the epilogue's LDS
+  // addresses while the reads were still in flight, and a late LDS return (a co-resident workgroup
+  // slows the LDS) overwrote the address — the r05 co-scheduled wgrad mismatch (found by
+  // tools/asm_hazard_scan.py "pending"). Wait for them here with every F0 register named as an operand,
+  // so none is reused before the data has landed.
+  asm volatile("s_waitcnt lgkmcnt(0)"
+               : "+v"(a0[0]), "+v"(a0[1]), "+v"(a0[2]), "+v"(a0[3]), "+v"(a0[4]), "+v"(a0[5]), "+v"(a0[6]),
+                 "+v"(a0[7]));
+  if constexpr (NI == 8)
+    asm volatile("" : "+v"(b0[0]), "+v"(b0[1]), "+v"(b0[2]), "+v"(b0[3]), "+v"(b0[4]), "+v"(b0[5]), "+v"(b0[6]),
+                 "+v"(b0[7]));
+  else
+    asm volatile("" : "+v"(b0[0]), "+v"(b0[1]), "+v"(b0[2]), "+v"(b0[3]));
   // ... and the last MFMA's result 11+ wait states (8-pass XDL) ahead of its first VALU / LDS read
   asm volatile("s_nop 15\n\ts_nop 15" ::);
   __builtin_amdgcn_sched_barrier(0);
@@ -980,17 +762,10 @@ inline int launch256(const LA& la, const LB& lb, const EPI& epi, int M, int N, i
   const int klen = split_len(K, nsplit);
   nsplit = K > 0 ? (K + klen - 1) / klen : 1;
   const int items = tm * tn * nsplit * nbatch;
-  const int ncu = crnn_cu_count();
-  const int popt = crnn_option(CRNN_OPT_GEMM_PERSISTENT);   // 1: when items > CUs, 2: always
   const int f4 = crnn_option(CRNN_OPT_GEMM4W);
   if (f4 == 1 || (f4 & ~1 & prefers_4w<EPI>::value) != 0) {
     hipLaunchKernelGGL((gemm4w_kernel<BM, BN, SKIP, LA, LB, EPI>), dim3(items), dim3(256), 0, st, la, lb, epi, M, N, K,
                        klen, tm, tn, nsplit, nbatch, ktk);
-    return (int)hipGetLastError();
-  }
-  if (SKIP == 0 && ((popt == 1 && items > ncu) || popt == 2)) {
-    hipLaunchKernelGGL((gemm256p_kernel<BM, BN, LA, LB, EPI>), dim3(items < ncu ? items : ncu), dim3(512), 0, st, la,
-                       lb, epi, M, N, K, klen, tm, tn, nsplit, crnn_option(CRNN_OPT_GEMM_STAGGER), nbatch);
     return (int)hipGetLastError();
   }
     hipLaunchKernelGGL((gemm256_kernel<BM, BN, SKIP, LA, LB, EPI>), dim3(items), dim3(512), 0, st, la, lb, epi,

@@ -32,6 +32,9 @@ using namespace gemm;
 
 namespace {
 
+typedef bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+
 constexpr unsigned long long SEQ_TIMEOUT_TICKS = 50000000ull;  // s_memrealtime @100 MHz: 0.5 s per wait
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* p) {
@@ -355,309 +358,260 @@ __global__ __launch_bounds__(256) void lstm_seq_fwd_kernel(const bf16* __restric
   }
 }
 
-// ---------------------------------------------------------------- forward sweep, pipelined sample groups
-// (CRNN_OPT_LSTM_PIPE bit 0, granule hand-off). A workgroup owns G groups of 16 samples and U units
-// (one W_hh slice in VGPRs shared by the groups) and runs a step group after group: group g's hand-off
-// wait, MFMA, partial-sum exchange, cell and publish. The groups' recurrences are independent, so the
-// granules of group g for step s+1 travel while the workgroup computes the other groups of step s: the
-// hand-off latency, which the one-group kernel pays in full every step, hides under G - 1 half-steps of
-// compute. Same ring, tags, loads, arithmetic and summation order as lstm_seq_fwd_kernel<H, 16, U, true>
-// per group (results bit-identical to it).
-template <int H, int U, int G>
-__global__ __launch_bounds__(256) void lstm_seq_fwd_pipe_kernel(const bf16* __restrict__ xg,
-                                                                const bf16* __restrict__ whh, bf16* hseq,
-                                                                bf16* __restrict__ gsv, float* __restrict__ csv,
-                                                                unsigned* cnt, unsigned* err, uint2* ring, int B,
-                                                                int Tn) {
-  constexpr int S = 16, KW = H / 4, KK = KW / 32;
-  constexpr int GR = 4 * U, NJ = GR / 16;
-  constexpr int QB = NJ / 4;   // blocks finalised per wave (one 16-sample fragment row)
-  constexpr int H4 = 4 * H;
-  static_assert(H % 128 == 0 && U % 16 == 0 && NJ % 4 == 0 && S * U / 4 <= 256, "shape");
-  __shared__ __attribute__((aligned(16))) f32x4 part[4][NJ][64];
-  __shared__ __attribute__((aligned(16))) bf16 htile[G][S][U];   // per group: no barrier between groups' uses
 
-  const int nsl = H / U, nbs = B / (S * G);
+// ---------------------------------------------------------------- forward sweep, unit-complete waves
+// (CRNN_OPT_LSTM_HANDOFF = 2). Same workgroup tile (direction, S samples, U units) and the same
+// granule ring as above, but the K split is gone: wave w OWNS NT * 4 = U/4 whole units over the full
+// K = H (NT = U/16 gate-row fragments of 4 units x 4 gates, KK = H/32 k-steps in VGPRs/AGPRs: the same
+// 64 KB of W_hh per wave and the same MFMA count per wave as the K-split form). What moves instead is
+// h_{t-1}: each wave polls its K-quarter of the granules (as before) and writes it to a double-buffered
+// LDS image of the whole h row block [S][H]; ONE barrier; then every wave reads all of it as MFMA B
+// fragments. No fp32 partial tiles are exchanged (the K-split form wrote and re-read 64 KB of partials
+// per workgroup per step plus a second barrier before the publish).
+// Row order inside a wave: fragment jt, A row r -> unit NT*(r/4) + jt, gate r%4, so the accumulator
+// rows 4g..4g+3 of lane (c, g) are the four gates of unit NT*g + jt of sample c: a lane ends the step
+// with NT CONSECUTIVE units of one sample and publishes them straight from registers, NT/2 granules
+// in one 8- or 16-B store (no h tile in LDS, no barrier before the publish).
+// LDS image pitch H + 8 bf16 (16 B off a multiple of 256 B per row): the 16 lanes of a fragment read
+// group land on distinct 16-B bank groups.
+// Ring reuse (2 slots): a wave writes slot s & 1 at step s after its workgroup's step-s barrier, i.e.
+// after all 4 waves' polls of h_{s-1} returned, from every producer wave of the group; each of those
+// produced h_{s-1} after its own workgroup had read h_{s-2} (the slot's previous contents).
+template <int H, int S, int U, int W>
+__global__ __launch_bounds__(64 * W) void lstm_seq_fwd_uc_kernel(const bf16* __restrict__ xg,
+                                                              const bf16* __restrict__ whh, bf16* hseq,
+                                                              bf16* __restrict__ gsv, float* __restrict__ csv,
+                                                              unsigned* cnt, unsigned* err, uint2* ring, int B,
+                                                              int Tn, unsigned long long* stamps, unsigned* xtab) {
+  constexpr int UW = U / W;           // units per wave
+  constexpr int NT = UW / 4;          // fragments (and consecutive units per lane) per wave
+  constexpr int KK = H / 32;          // k-steps over the full K
+  constexpr int HW = H / W;           // one wave's poll slice of K
+  constexpr int KQ = HW / 32;         // its k-steps
+  constexpr int MI = S / 16, H4 = 4 * H, HP = H + 8;
+  static_assert(HW % 32 == 0 && S % 16 == 0 && (NT == 2 || NT == 4), "shape");
+  __shared__ __attribute__((aligned(16))) bf16 himg[2][S][HP];
+
+  const int nsl = H / U, nbs = B / S;
   int d, bs, ns;
   seq_coords(nsl, nbs, d, bs, ns);
   const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int n0 = ns * GR;
+  const int b0 = bs * S;
+  const int ul = ns * U + w * UW + NT * g;   // this lane's first unit (NT consecutive)
   unsigned* mycnt = cnt + d * nbs + bs;
+  if (stamps && threadIdx.x == 0) stamps[(size_t)blockIdx.x * Tn * 8 + 7] = __builtin_amdgcn_s_memrealtime();
 
-  const int rot = ns % KK;   // rotated K-chunk order (lstm_seq_fwd_kernel)
-  bf16x8 wf[NJ][KK];
+  // x-gate rows of (sample b0 + 16i + c, units ul .. ul+NT-1): 4*NT consecutive packed gate rows
+  bf16x8 xv[MI][NT / 2];
+  auto load_xg = [&](int t) {
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int h2 = 0; h2 < NT / 2; ++h2)
+        xv[i][h2] = *reinterpret_cast<const bf16x8*>(xg + ((size_t)(b0 + 16 * i + c) * Tn + t) * 2 * H4 + d * H4 +
+                                                      4 * ul + 8 * h2);
+  };
+  load_xg(d == 0 ? 0 : Tn - 1);
+
+  // W_hh' fragments: A row c of fragment jt = packed row 4 * (ns*U + w*UW + NT*(c>>2) + jt) + (c & 3)
+  bf16x8 wf[NT][KK];
   {
     const bf16* wb = whh + (size_t)d * H4 * H;
 #pragma unroll
-    for (int j = 0; j < NJ; ++j)
+    for (int jt = 0; jt < NT; ++jt) {
+      const int row = 4 * (ns * U + w * UW + NT * (c >> 2) + jt) + (c & 3);
 #pragma unroll
-      for (int kk = 0; kk < KK; ++kk) {
-        const int kc = kk + rot < KK ? kk + rot : kk + rot - KK;
-        wf[j][kk] = *reinterpret_cast<const bf16x8*>(wb + (size_t)(n0 + 16 * j + c) * H + w * KW + 32 * kc + 8 * g);
-      }
+      for (int kk = 0; kk < KK; ++kk)
+        wf[jt][kk] = *reinterpret_cast<const bf16x8*>(wb + (size_t)row * H + 32 * kk + 8 * g);
+    }
   }
   const __amdgpu_buffer_rsrc_t rr = rsrc_of(ring);
-  float cst[G][QB];
-  bf16x4 xv[G][QB];
+  const bool l2_handoff = xtab && seq_group_local(xtab, (d * nbs + bs) * nsl, nsl, ns, err);
+  const int rot = ns % KQ;   // rotated poll order: the group's workgroups spread their requests
+  float cst[MI][NT];
 #pragma unroll
-  for (int gi = 0; gi < G; ++gi)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
-    for (int q = 0; q < QB; ++q) cst[gi][q] = 0.f;
-  auto load_xg = [&](int gi, int t) {
-    const int b0 = (bs * G + gi) * S;
-#pragma unroll
-    for (int q = 0; q < QB; ++q) {
-      const int j = w * QB + q;
-      const int b = b0 + c, n = n0 + 16 * j + 4 * g;
-      xv[gi][q] = *reinterpret_cast<const bf16x4*>(xg + ((size_t)b * Tn + t) * 2 * H4 + d * H4 + n);
-    }
-  };
-#pragma unroll
-  for (int gi = 0; gi < G; ++gi) load_xg(gi, d == 0 ? 0 : Tn - 1);
+    for (int jt = 0; jt < NT; ++jt) cst[i][jt] = 0.f;
 
   for (int s = 0; s < Tn; ++s) {
     const int t = d == 0 ? s : Tn - 1 - s;
+    const int buf = s & 1;
+    bool ok = true;
+    // accumulators start at the x-gate rows (the recurrent product accumulates onto them), which frees xv
+    // for the next step's rows as soon as this step's hand-off has arrived
+    f32x4 acc[MI][NT];
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int jt = 0; jt < NT; ++jt) {
+        const bf16x8& x8 = xv[i][jt >> 1];
+        const int o = (jt & 1) * 4;
+        acc[i][jt] = f32x4{(float)x8[o], (float)x8[o + 1], (float)x8[o + 2], (float)x8[o + 3]};
+      }
     const int tn = s + 1 < Tn ? (d == 0 ? t + 1 : t - 1) : t;
+    bf16 hh[MI][NT];
+    f32x4 gq[MI][NT];
+    // cell update of fragment (i, jt): lane holds gates (i, f, g, o) of unit ul + jt of one sample
+    auto cell = [&](int i, int jt) {
+      const f32x4 v = acc[i][jt];
+      const float ig = sigmoid_fast(v[0]), fg = sigmoid_fast(v[1]), gg = tanh_fast(v[2]), og = sigmoid_fast(v[3]);
+      float cc = fg * cst[i][jt] + ig * gg;
+      float h = og * tanh_fast(cc);
+      if (!ok) h = cc = __builtin_nanf("");
+      cst[i][jt] = cc;
+      gq[i][jt] = f32x4{ig, fg, gg, og};
+      hh[i][jt] = (bf16)h;
+    };
+    SEQ_STAMP(0);
+    if (s > 0) {
+      // poll this wave's K-slice of h_{s-1}: row b0 + 16i + c, k = w*H/4 + 32kc + 8g .. +7 (4 granules)
+      const uint32_t want = (uint32_t)s;
+      const uint32_t gbase =
+          (uint32_t)((((size_t)((s - 1) & 1) * B + b0 + c) * H + (d * H + w * HW + 8 * g) / 2) * 8u);
+      unsigned long long t0 = 0;
+      u32x4 gv[MI][KQ][2];
+      for (;;) {
 #pragma unroll
-    for (int gi = 0; gi < G; ++gi) {
-      const int b0 = (bs * G + gi) * S;
-      f32x4 sum[QB];
-      bool ok = true;
-      if (s > 0) {
-        bf16x8 af[KK];
-        const uint32_t want = (uint32_t)s;
-        const uint32_t gbase =
-            (uint32_t)((((size_t)((s - 1) & 1) * B + b0 + c) * H + (d * H + w * KW + 8 * g) / 2) * 8u);
-        unsigned long long t0 = 0;
-        u32x4 gv[KK][2];
-        for (;;) {
+        for (int kq = 0; kq < KQ; ++kq)
 #pragma unroll
-          for (int kk = 0; kk < KK; ++kk) {
-            const int kc = kk + rot < KK ? kk + rot : kk + rot - KK;
-            const uint32_t off = gbase + (uint32_t)(kc * 128);
-            gv[kk][0] = __builtin_amdgcn_raw_buffer_load_b128(rr, off, 0, 16);
-            gv[kk][1] = __builtin_amdgcn_raw_buffer_load_b128(rr, off + 16, 0, 16);
+          for (int i = 0; i < MI; ++i) {
+            const int kc = kq + rot < KQ ? kq + rot : kq + rot - KQ;
+            const uint32_t off = gbase + (uint32_t)(i * 16 * H * 8 + kc * 128);
+            gv[i][kq][0] = __builtin_amdgcn_raw_buffer_load_b128(rr, off, 0, 16);
+            gv[i][kq][1] = __builtin_amdgcn_raw_buffer_load_b128(rr, off + 16, 0, 16);
           }
-          bool mine = true;
+        bool mine = true;
 #pragma unroll
-          for (int kk = 0; kk < KK; ++kk)
+        for (int kq = 0; kq < KQ; ++kq)
 #pragma unroll
-            for (int h2 = 0; h2 < 2; ++h2) mine &= (gv[kk][h2][1] == want) & (gv[kk][h2][3] == want);
-          if (__all(mine)) break;
-          const unsigned long long now = __builtin_amdgcn_s_memrealtime();
-          if (t0 == 0) t0 = now;
-          if (now - t0 > SEQ_TIMEOUT_TICKS || __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-            __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            ok = false;
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
+          for (int i = 0; i < MI; ++i)
+#pragma unroll
+            for (int h2 = 0; h2 < 2; ++h2) mine &= (gv[i][kq][h2][1] == want) & (gv[i][kq][h2][3] == want);
+        if (__all(mine)) break;
+        const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+        if (t0 == 0) t0 = now;
+        if (now - t0 > SEQ_TIMEOUT_TICKS || __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+          __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          ok = false;
+          break;
         }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      SEQ_STAMP(1);
 #pragma unroll
-        for (int kk = 0; kk < KK; ++kk)
-          af[kk] = __builtin_bit_cast(bf16x8, u32x4{gv[kk][0][0], gv[kk][0][2], gv[kk][1][0], gv[kk][1][2]});
-        f32x4 acc[NJ];
+      for (int kq = 0; kq < KQ; ++kq)
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int kk = 0; kk < KK; ++kk)
-#pragma unroll
-          for (int j = 0; j < NJ; ++j) mma<bf16>(acc[j], wf[j][kk], af[kk]);
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) part[w][j][lane] = acc[j];
-        __syncthreads();
-#pragma unroll
-        for (int q = 0; q < QB; ++q) {
-          const int j = w * QB + q;
-          sum[q] = f32x4{(float)xv[gi][q][0], (float)xv[gi][q][1], (float)xv[gi][q][2], (float)xv[gi][q][3]};
-#pragma unroll
-          for (int ww = 0; ww < 4; ++ww) sum[q] += part[ww][j][lane];
+        for (int i = 0; i < MI; ++i) {
+          const int kc = kq + rot < KQ ? kq + rot : kq + rot - KQ;
+          *reinterpret_cast<u32x4*>(&himg[buf][16 * i + c][w * HW + 32 * kc + 8 * g]) =
+              u32x4{gv[i][kq][0][0], gv[i][kq][0][2], gv[i][kq][1][0], gv[i][kq][1][2]};
         }
-      } else {
-#pragma unroll
-        for (int q = 0; q < QB; ++q)
-          sum[q] = f32x4{(float)xv[gi][q][0], (float)xv[gi][q][1], (float)xv[gi][q][2], (float)xv[gi][q][3]};
-      }
-      load_xg(gi, tn);   // this group's next input rows, a whole step ahead of their use
-      f32x4 gq[QB];
-#pragma unroll
-      for (int q = 0; q < QB; ++q) {
-        const int j = w * QB + q;
-        const f32x4 v = sum[q];
-        const float ig = sigmoid_fast(v[0]), fg = sigmoid_fast(v[1]), gg = tanh_fast(v[2]), og = sigmoid_fast(v[3]);
-        float cc = fg * cst[gi][q] + ig * gg;
-        float hh = og * tanh_fast(cc);
-        if (!ok) hh = cc = __builtin_nanf("");
-        cst[gi][q] = cc;
-        gq[q] = f32x4{ig, fg, gg, og};
-        htile[gi][c][4 * j + g] = (bf16)hh;
-      }
+      load_xg(tn);   // issued behind the hand-off loads, a whole step ahead of its use
+      SEQ_STAMP(2);
       __syncthreads();
-      if (threadIdx.x < S * U / 4) {   // publish: S rows x U/2 granules, two per 16-B sc1 store
-        const int row = threadIdx.x / (U / 4), gp = threadIdx.x % (U / 4);
-        const u32x4 hv = __builtin_bit_cast(u32x4, *reinterpret_cast<const bf16x8*>(&htile[gi][row][8 * (gp >> 1)]));
-        const uint32_t tag = (uint32_t)(s + 1);
-        const u32x4 v = (gp & 1) ? u32x4{hv[2], tag, hv[3], tag} : u32x4{hv[0], tag, hv[1], tag};
-        const uint32_t ro = (uint32_t)((((size_t)(s & 1) * B + b0 + row) * H + (d * H + ns * U + 4 * gp) / 2) * 8u);
-        __builtin_amdgcn_raw_buffer_store_b128(v, rr, ro, 0, 16);
-      }
-      if (threadIdx.x < S * U / 8) {   // h_t for the next layer / BPTT: plain stores
-        const int row = threadIdx.x / (U / 8), ch = threadIdx.x % (U / 8);
-        *reinterpret_cast<bf16x8*>(hseq + ((size_t)(b0 + row) * Tn + t) * 2 * H + d * H + ns * U + 8 * ch) =
-            *reinterpret_cast<const bf16x8*>(&htile[gi][row][8 * ch]);
-      }
-      if (gsv != nullptr) {
+      SEQ_STAMP(3);
+      if constexpr (MI == 1 && KK <= 16) {
+        // all B fragments in flight first, then fragment after fragment: fragment jt's 4 cells run in the
+        // shadow of fragment jt+1's MFMAs (an MFMA holds vector issue for 8 of its 16 cycles)
+        bf16x8 hb[KK];
 #pragma unroll
-        for (int q = 0; q < QB; ++q) {
-          const int j = w * QB + q;
-          const int b = b0 + c;
-          const int n = n0 + 16 * j + 4 * g, u = n >> 2;
-          csv[((size_t)(d * Tn + t) * B + b) * H + u] = cst[gi][q];
-          st4<bf16>(gsv + ((size_t)(d * Tn + t) * B + b) * H4 + n, gq[q]);
+        for (int kk = 0; kk < KK; ++kk) hb[kk] = *reinterpret_cast<const bf16x8*>(&himg[buf][c][32 * kk + 8 * g]);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int jt = 0; jt < NT; ++jt) {
+#pragma unroll
+          for (int kk = 0; kk < KK; ++kk) mma<bf16>(acc[0][jt], wf[jt][kk], hb[kk]);
+          if (jt > 0) {
+            cell(0, jt - 1);
+            // the scheduler keeps a fragment's MFMA chain together and the cell math after it: ask for
+            // one MFMA then ~3 VALU (the cell's ~45 instructions spread over the 16 MFMA gaps)
+#pragma unroll
+            for (int q = 0; q < KK; ++q) {
+              __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
+              __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);   // VALU
+            }
+          }
+          __builtin_amdgcn_sched_barrier(0);
         }
+        cell(0, NT - 1);
+      } else {
+        // B fragments in batches of up to 16 reads, all issued before the batch's MFMAs (one
+        // ds_read -> lgkmcnt(0) -> MFMA round trip per k-step would expose the LDS latency 16 times)
+        constexpr int CH = MI * KK <= 16 ? KK : 16 / MI;
+#pragma unroll
+        for (int k0 = 0; k0 < KK; k0 += CH) {
+          bf16x8 hb[MI][CH];
+#pragma unroll
+          for (int kk = 0; kk < CH; ++kk)
+#pragma unroll
+            for (int i = 0; i < MI; ++i)
+              if (k0 + kk < KK)
+                hb[i][kk] = *reinterpret_cast<const bf16x8*>(&himg[buf][16 * i + c][32 * (k0 + kk) + 8 * g]);
+          __builtin_amdgcn_sched_barrier(0);   // every read of the batch in flight before its first MFMA
+#pragma unroll
+          for (int kk = 0; kk < CH; ++kk)
+#pragma unroll
+            for (int i = 0; i < MI; ++i)
+#pragma unroll
+              for (int jt = 0; jt < NT; ++jt)
+                if (k0 + kk < KK) mma<bf16>(acc[i][jt], wf[jt][k0 + kk], hb[i][kk]);
+        }
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int jt = 0; jt < NT; ++jt) cell(i, jt);
+      }
+    } else {
+      load_xg(tn);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int jt = 0; jt < NT; ++jt) cell(i, jt);
+    }
+    SEQ_STAMP(4);
+    // publish: NT/2 granules {2 bf16, tag = s + 1} per (lane, sample tile), straight from registers
+    const uint32_t tag = (uint32_t)(s + 1);
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const uint32_t ro = (uint32_t)((((size_t)(s & 1) * B + b0 + 16 * i + c) * H + (d * H + ul) / 2) * 8u);
+      const uint32_t h01 = __builtin_bit_cast(uint32_t, bf16x2_t{hh[i][0], hh[i][1]});
+      if constexpr (NT == 4) {
+        const uint32_t h23 = __builtin_bit_cast(uint32_t, bf16x2_t{hh[i][2], hh[i][3]});
+        const u32x4 v = u32x4{h01, tag, h23, tag};
+        if (l2_handoff) __builtin_amdgcn_raw_buffer_store_b128(v, rr, ro, 0, 0);   // stays in the XCD's L2
+        else __builtin_amdgcn_raw_buffer_store_b128(v, rr, ro, 0, 16);            // sc1: written through
+      } else {
+        const u32x2_t v = u32x2_t{h01, tag};
+        if (l2_handoff) __builtin_amdgcn_raw_buffer_store_b64(v, rr, ro, 0, 0);
+        else __builtin_amdgcn_raw_buffer_store_b64(v, rr, ro, 0, 16);
       }
     }
+    SEQ_STAMP(5);
+    // h_t for the next layer / BPTT and the saved forward state: plain stores, off the critical path
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int b = b0 + 16 * i + c;
+      bf16* hp = hseq + ((size_t)b * Tn + t) * 2 * H + d * H + ul;
+      if constexpr (NT == 4) *reinterpret_cast<bf16x4*>(hp) = bf16x4{hh[i][0], hh[i][1], hh[i][2], hh[i][3]};
+      else *reinterpret_cast<bf16x2_t*>(hp) = bf16x2_t{hh[i][0], hh[i][1]};
+      if (gsv != nullptr) {
+        float* cp = csv + ((size_t)(d * Tn + t) * B + b) * H + ul;
+        bf16* gp = gsv + ((size_t)(d * Tn + t) * B + b) * H4 + 4 * ul;
+#pragma unroll
+        for (int h2 = 0; h2 < NT / 2; ++h2) {
+          const f32x4 a = gq[i][2 * h2], e = gq[i][2 * h2 + 1];
+          *reinterpret_cast<bf16x8*>(gp + 8 * h2) =
+              bf16x8{(bf16)a[0], (bf16)a[1], (bf16)a[2], (bf16)a[3], (bf16)e[0], (bf16)e[1], (bf16)e[2], (bf16)e[3]};
+        }
+        if constexpr (NT == 4) *reinterpret_cast<f32x4*>(cp) = f32x4{cst[i][0], cst[i][1], cst[i][2], cst[i][3]};
+        else *reinterpret_cast<float2*>(cp) = float2{cst[i][0], cst[i][1]};
+      }
+    }
+    SEQ_STAMP(6);
   }
   if (threadIdx.x == 0) __hip_atomic_fetch_add(mycnt, (unsigned)Tn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// ---------------------------------------------------------------- BPTT sweep, pipelined sample groups
-// (CRNN_OPT_LSTM_PIPE bit 1) The counter-form BPTT (lstm_seq_bwd_kernel) with G groups of 16 samples per
-// workgroup and U units: each group has its own step counter (slot (d * nbs + bs) * G + g) and its own
-// running dc, and a step runs the groups one after the other, so one group's dgates gather is in flight
-// while the workgroup computes another. Per group the arithmetic and summation order of the one-group
-// 16 x U kernel.
-template <int H, int U, int G>
-__global__ __launch_bounds__(256) void lstm_seq_bwd_pipe_kernel(const bf16* __restrict__ dhseq,
-                                                                const bf16* __restrict__ whh_t,
-                                                                const bf16* __restrict__ gsv,
-                                                                const float* __restrict__ csv, bf16* dgates,
-                                                                unsigned* cnt, unsigned* err, int B, int Tn,
-                                                                unsigned* xtab) {
-  constexpr int S = 16, KW = H, KK = KW / 32;
-  constexpr int H4 = 4 * H, NU = U / 16, NBLK = NU;
-  static_assert(H % 32 == 0 && NBLK <= 4 && U % 16 == 0, "shape");
-  __shared__ __attribute__((aligned(16))) f32x4 part[4][NU][64];
-
-  const int nsl = H / U, nbs = B / (S * G);
-  int d, bs, ns;
-  seq_coords(nsl, nbs, d, bs, ns);
-  const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int u0 = ns * U;
-
-  const int rot = (ns * KK / nsl) % KK;
-  bf16x8 wf[NU][KK];
-  {
-    const bf16* wb = whh_t + (size_t)d * H * H4;
-#pragma unroll
-    for (int j = 0; j < NU; ++j)
-#pragma unroll
-      for (int kk = 0; kk < KK; ++kk) {
-        const int kc = kk + rot < KK ? kk + rot : kk + rot - KK;
-        wf[j][kk] = *reinterpret_cast<const bf16x8*>(wb + (size_t)(u0 + 16 * j + c) * H4 + w * KW + 32 * kc + 8 * g);
-      }
-  }
-  const __amdgpu_buffer_rsrc_t rg = rsrc_of(dgates);
-  const bool l2_handoff = xtab && seq_group_local(xtab, (d * nbs + bs) * nsl, nsl, ns, err);
-  const bool fin = w < NBLK;
-  const int fj = fin ? w : 0;
-  const int u = u0 + 16 * fj + 4 * g;  // this lane's 4 units u..u+3
-  float dcs[G][4];
-  bf16x8 gv0[G], gv1[G];
-  f32x4 cv[G], cpv[G], dhv[G];
-  float has_prev_f[G];
-#pragma unroll
-  for (int gi = 0; gi < G; ++gi)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) dcs[gi][r] = 0.f;
-  auto load_in = [&](int gi, int t) {
-    const int b = (bs * G + gi) * S + c;
-    const size_t gix = ((size_t)(d * Tn + t) * B + b) * H4 + 4 * u;
-    gv0[gi] = *reinterpret_cast<const bf16x8*>(gsv + gix);
-    gv1[gi] = *reinterpret_cast<const bf16x8*>(gsv + gix + 8);
-    cv[gi] = *reinterpret_cast<const f32x4*>(csv + ((size_t)(d * Tn + t) * B + b) * H + u);
-    const int tf = d == 0 ? t - 1 : t + 1;
-    const bool has_prev = d == 0 ? t > 0 : t < Tn - 1;
-    const int tfc = has_prev ? tf : t;
-    cpv[gi] = *reinterpret_cast<const f32x4*>(csv + ((size_t)(d * Tn + tfc) * B + b) * H + u);
-    has_prev_f[gi] = has_prev ? 1.f : 0.f;
-    dhv[gi] = ld4f<bf16>(dhseq + ((size_t)b * Tn + t) * 2 * H + d * H + u);
-  };
-#pragma unroll
-  for (int gi = 0; gi < G; ++gi) load_in(gi, d == 0 ? Tn - 1 : 0);
-
-  for (int s = 0; s < Tn; ++s) {
-    const int t = d == 0 ? Tn - 1 - s : s;
-    const int tn = d == 0 ? t + 1 : t - 1;  // time of the previous BPTT step
-#pragma unroll
-    for (int gi = 0; gi < G; ++gi) {
-      const int b0 = (bs * G + gi) * S, b = b0 + c;
-      unsigned* mycnt = cnt + (d * nbs + bs) * G + gi;
-      f32x4 dh = dhv[gi];
-      bool ok = true;
-      if (s > 0) {
-        __shared__ int okflag;
-        if (threadIdx.x == 0) okflag = seq_wait(mycnt, (unsigned)(nsl * s), err) ? 1 : 0;
-        __syncthreads();
-        ok = okflag != 0;
-        bf16x8 af[KK];
-        const uint32_t abase = (uint32_t)((((size_t)(d * Tn + tn) * B + b0 + c) * H4 + w * KW + 8 * g) * 2u);
-#pragma unroll
-        for (int kk = 0; kk < KK; ++kk) {
-          const int kc = kk + rot < KK ? kk + rot : kk + rot - KK;
-          af[kk] = ld_sc1(rg, abase + (uint32_t)(kc * 64));
-        }
-        __builtin_amdgcn_sched_barrier(0);  // all loads issued first
-        f32x4 acc[NU];
-#pragma unroll
-        for (int j = 0; j < NU; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int kk = 0; kk < KK; ++kk)
-#pragma unroll
-          for (int j = 0; j < NU; ++j) mma<bf16>(acc[j], wf[j][kk], af[kk]);
-#pragma unroll
-        for (int j = 0; j < NU; ++j) part[w][j][lane] = acc[j];
-        __syncthreads();
-        if (fin)
-#pragma unroll
-          for (int ww = 0; ww < 4; ++ww) dh += part[ww][fj][lane];
-      }
-      if (fin) {
-        bf16x8 out0, out1;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const bf16x8& gv = r < 2 ? gv0[gi] : gv1[gi];
-          const int o = (r & 1) * 4;
-          const float ig = (float)gv[o], fg = (float)gv[o + 1], gg = (float)gv[o + 2], og = (float)gv[o + 3];
-          const float tc = tanh_fast(cv[gi][r]);
-          const float dcv = dcs[gi][r] + dh[r] * og * (1.f - tc * tc);
-          const float do_ = dh[r] * tc;
-          const float di = dcv * gg, dg = dcv * ig, df = dcv * cpv[gi][r] * has_prev_f[gi];
-          dcs[gi][r] = dcv * fg;
-          float q0 = di * ig * (1.f - ig), q1 = df * fg * (1.f - fg), q2 = dg * (1.f - gg * gg),
-                q3 = do_ * og * (1.f - og);
-          if (!ok) q0 = q1 = q2 = q3 = __builtin_nanf("");
-          bf16x8& ov = r < 2 ? out0 : out1;
-          ov[o] = (bf16)q0;
-          ov[o + 1] = (bf16)q1;
-          ov[o + 2] = (bf16)q2;
-          ov[o + 3] = (bf16)q3;
-        }
-        const uint32_t go = (uint32_t)((((size_t)(d * Tn + t) * B + b) * H4 + 4 * u) * sizeof(bf16));
-        if (l2_handoff) {
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, out0), rg, go, 0, 0);
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, out1), rg, go + 16, 0, 0);
-        } else {
-          st_sc1(rg, go, out0);
-          st_sc1(rg, go + 16, out1);
-        }
-      }
-      seq_publish(mycnt);
-      load_in(gi, s + 1 < Tn ? (d == 0 ? t - 1 : t + 1) : t);
-    }
-  }
 }
 
 // ---------------------------------------------------------------- BPTT sweep
@@ -1018,9 +972,22 @@ bool seq_config(int B, int H, bool bwd, int& S, int& U) {
 }
 
 template <int H, int S, int U>
-void launch_fwd_tile(bool tag, dim3 grid, hipStream_t st, const bf16* xg, const bf16* whh, bf16* hseq, bf16* gsv,
+void launch_fwd_tile(int form, dim3 grid, hipStream_t st, const bf16* xg, const bf16* whh, bf16* hseq, bf16* gsv,
                      float* csv, unsigned* cnt, unsigned* err, uint2* ring, int B, int T, unsigned* xtab) {
-  if (tag)
+  if constexpr (U == 64) {
+    if (form == 3) {   // 8 waves of 8 units: 2 waves per SIMD, weights without AGPR copies
+      hipLaunchKernelGGL((lstm_seq_fwd_uc_kernel<H, S, U, 8>), grid, dim3(512), 0, st, xg, whh, hseq, gsv, csv, cnt,
+                         err, ring, B, T, g_stamps, xtab);
+      return;
+    }
+  }
+  // form 3 on a 32-unit tile (H = 768): the K-split granule form, which measured faster there
+  // (3.29 vs 4.11 us per step at B = 64, profiles/r06/r06a_lstm_forms_ab.log)
+  if (form == 3) form = 1;
+  if (form == 2)
+    hipLaunchKernelGGL((lstm_seq_fwd_uc_kernel<H, S, U, 4>), grid, dim3(256), 0, st, xg, whh, hseq, gsv, csv, cnt, err,
+                       ring, B, T, g_stamps, xtab);
+  else if (form == 1)
     hipLaunchKernelGGL((lstm_seq_fwd_kernel<H, S, U, true>), grid, dim3(256), 0, st, xg, whh, hseq, gsv, csv, cnt, err,
                        ring, B, T, g_stamps, xtab);
   else
@@ -1028,20 +995,10 @@ void launch_fwd_tile(bool tag, dim3 grid, hipStream_t st, const bf16* xg, const 
                        err, ring, B, T, g_stamps, nullptr);
 }
 
-// the pipelined forward (lstm_seq_fwd_pipe_kernel: 2 groups of 16 samples x 32 units per workgroup), when
-// CRNN_OPT_LSTM_PIPE asks for it (bit 0 forward, bit 1 BPTT), the granule hand-off is on and the grid fits
-bool pipe_ok(int B, int H, bool bwd) {
-  if (!(crnn_option(CRNN_OPT_LSTM_PIPE) & (bwd ? 2 : 1))) return false;
-  if (!bwd && !crnn_option(CRNN_OPT_LSTM_HANDOFF)) return false;
-  if (bwd && crnn_option(CRNN_OPT_LSTM_BWD_PART)) return false;
-  if (!(H == 256 || H == 512 || H == 768) || B % 32) return false;
-  return 2 * (B / 32) * (H / 32) <= cu_count();
-}
-
 template <int H>
 int launch_fwd(int S, int U, dim3 grid, hipStream_t st, const bf16* xg, const bf16* whh, bf16* hseq, bf16* gsv,
                float* csv, unsigned* cnt, unsigned* err, uint2* ring, int B, int T, unsigned* xtab) {
-  const bool tag = crnn_option(CRNN_OPT_LSTM_HANDOFF) != 0;
+  const int tag = crnn_option(CRNN_OPT_LSTM_HANDOFF);
   if constexpr (H <= 512) {  // 16 x 64 would spill at H = 768 (seq_config never picks it)
     if (S == 16 && U == 64) {
       launch_fwd_tile<H, 16, 64>(tag, grid, st, xg, whh, hseq, gsv, csv, cnt, err, ring, B, T, xtab);
@@ -1106,10 +1063,6 @@ int crnn_lstm_seq_supported(int dtype, int B, int H) {
 int crnn_lstm_seq_config(int B, int H, int bwd, int* S, int* U) {
   int s = 0, u = 0;
   const int ok = seq_config(B, H, bwd != 0, s, u) ? 1 : 0;
-  if (ok && pipe_ok(B, H, bwd != 0)) {   // the pipelined sweep: 32 samples (2 groups) x 32 units per workgroup
-    s = 32;
-    u = 32;
-  }
   if (S) *S = ok ? s : 0;
   if (U) *U = ok ? u : 0;
   return ok;
@@ -1189,22 +1142,6 @@ int crnn_lstm_seq_fwd(const void* xg, const void* whh, void* hseq, void* gsv, fl
   unsigned* xtab = crnn_option(CRNN_OPT_LSTM_L2_HANDOFF) > 1 ? (unsigned*)((char*)ws + seq_tab_offset(B)) : nullptr;
   const bf16 *x = (const bf16*)xg, *w = (const bf16*)whh;
   int rc;
-  if (pipe_ok(B, H, false)) {   // two pipelined 16-sample groups x 32 units per workgroup
-    const dim3 pg(2 * (B / 32) * (H / 32));
-    seq_time_mark(st, 0);
-    if (H == 256)
-      hipLaunchKernelGGL((lstm_seq_fwd_pipe_kernel<256, 32, 2>), pg, dim3(256), 0, st, x, w, (bf16*)hseq,
-                         (bf16*)gsv, csv, cnt, err, ring, B, T);
-    else if (H == 512)
-      hipLaunchKernelGGL((lstm_seq_fwd_pipe_kernel<512, 32, 2>), pg, dim3(256), 0, st, x, w, (bf16*)hseq,
-                         (bf16*)gsv, csv, cnt, err, ring, B, T);
-    else
-      hipLaunchKernelGGL((lstm_seq_fwd_pipe_kernel<768, 32, 2>), pg, dim3(256), 0, st, x, w, (bf16*)hseq,
-                         (bf16*)gsv, csv, cnt, err, ring, B, T);
-    rc = (int)hipGetLastError();
-    seq_time_mark(st, 1);
-    return seq_accum_status(ws, B, st, rc);
-  }
   seq_time_mark(st, 0);
   if (H == 256) rc = launch_fwd<256>(S, U, grid, st, x, w, (bf16*)hseq, (bf16*)gsv, csv, cnt, err, ring, B, T, xtab);
   else if (H == 512) rc = launch_fwd<512>(S, U, grid, st, x, w, (bf16*)hseq, (bf16*)gsv, csv, cnt, err, ring, B, T, xtab);
@@ -1231,22 +1168,6 @@ int crnn_lstm_seq_bwd(const void* dhseq, const void* whh_t, const void* gsv, con
   unsigned* xtab = crnn_option(CRNN_OPT_LSTM_L2_HANDOFF) ? (unsigned*)((char*)ws + seq_tab_offset(B)) : nullptr;
   const bf16 *dh = (const bf16*)dhseq, *wt = (const bf16*)whh_t, *gv = (const bf16*)gsv;
   int rc;
-  if (pipe_ok(B, H, true) && !crnn_option(CRNN_OPT_LSTM_BWD_PART)) {   // two pipelined 16-sample groups x 32 units
-    const dim3 pg(2 * (B / 32) * (H / 32));
-    seq_time_mark(st, 0);
-    if (H == 256)
-      hipLaunchKernelGGL((lstm_seq_bwd_pipe_kernel<256, 32, 2>), pg, dim3(256), 0, st, dh, wt, gv, csv,
-                         (bf16*)dgates, cnt, err, B, T, xtab);
-    else if (H == 512)
-      hipLaunchKernelGGL((lstm_seq_bwd_pipe_kernel<512, 32, 2>), pg, dim3(256), 0, st, dh, wt, gv, csv,
-                         (bf16*)dgates, cnt, err, B, T, xtab);
-    else
-      hipLaunchKernelGGL((lstm_seq_bwd_pipe_kernel<768, 32, 2>), pg, dim3(256), 0, st, dh, wt, gv, csv,
-                         (bf16*)dgates, cnt, err, B, T, xtab);
-    rc = (int)hipGetLastError();
-    seq_time_mark(st, 1);
-    return seq_accum_status(ws, B, st, rc);
-  }
   seq_time_mark(st, 0);
   if (H == 256) rc = launch_bwd<256>(S, U, grid, st, dh, wt, gv, csv, (bf16*)dgates, cnt, err, ring, B, T, xtab);
   else if (H == 512) rc = launch_bwd<512>(S, U, grid, st, dh, wt, gv, csv, (bf16*)dgates, cnt, err, ring, B, T, xtab);

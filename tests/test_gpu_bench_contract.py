@@ -14,8 +14,9 @@ pytestmark = pytest.mark.gpu
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _run(*args):
+def _run(*args, env_extra=None):
     env = dict(os.environ)
+    env.update(env_extra or {})
     p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), *args], cwd=REPO, env=env,
                        capture_output=True, text=True, timeout=240)
     assert p.returncode == 0, p.stderr[-2000:]
@@ -49,3 +50,25 @@ def test_bench_line_contract():
     for k in ("value", "unit", "cores", "kind", "sample"):
         assert k in c, k
     assert c["kind"] in ("port", "reference") and c["value"] > 0 and c["cores"] >= 1
+
+
+def test_bench_gpus2_spawns_two_ranks():
+    """`python bench.py --gpus 2` with no launcher env starts its two ranks itself:
+    the line says n_gpus 2, the replicas end bit-identical and the DP overlap fields are there. One-device
+    rehearsal: both ranks on cuda:0, gloo over the GPU tensors, per-step BiLSTM launches (the persistent
+    sweeps want the whole chip to themselves)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    env = {"CRNN_SHARE_DEVICE": "1", "CRNN_DIST_BACKEND": "gloo", "CRNN_LSTM_PER_STEP": "1"}
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        os.environ.pop(k, None)
+    d = _run("--gpus", "2", "--steps", "2", "--warmup", "1", "--batch", "32", "--no-sub", env_extra=env)
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2" and d["config"]["global_batch"] == 64
+    assert abs(d["value"] - 64 / (d["ms_per_step"] / 1e3)) <= 0.02 * d["value"]
+    dp = d["dp"]
+    assert dp["param_checksum_spread"] == 0.0
+    for k in ("exposed_allreduce_ms_per_step_max_rank", "buckets_per_step", "allreduce_bytes_per_step", "bucket_mb"):
+        assert k in dp, k
+    assert dp["buckets_per_step"] >= 2 and dp["allreduce_bytes_per_step"] > 0
+    assert "cpu_baseline" not in d   # the CPU leg is rank 0 at N = 1 only
+

@@ -11,7 +11,9 @@ mkdir -p $obj
 skip=""
 for s in $srcs; do
   o=$obj/${s%.hip}.o
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I../../include -Wno-unused-result "$@" -c $s -o $o
+  # the Makefile's device flags (NOPK: no packed fp32 ops) so that a variant differs only in the flags under test
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I../../include -Wno-unused-result \
+    -Xclang -target-feature -Xclang -packed-fp32-ops "$@" -c $s -o $o
   skip="$skip|/${s%.hip}.o"
 done
 objs=$(ls ../../build/obj/*.o | grep -Ev "(${skip#|})$")

@@ -3,9 +3,7 @@ model of this library (its own engine, buffers and batch: the bf16 bench step wi
 the W-halo and halo stem convs) trains on a SIDE stream while the victim model repeats one bf16 train
 step (B=256, 32x256, hidden 512) on the compute stream. Every victim gradient must be bit-identical to
 the one it computed on an idle device; the aggressor's own gradients are checked the same way.
-    python tools/cohab_model.py [iters] [victim_seq 0|1] [aggressor_seq 0|1] [aggressor: model | hog:BLOCKS:LDS:ITERS]
-hog: instead of a second model, LDS sentinel workgroups (crnn_diag_lds_sentinel) that only sleep and re-check
-their LDS, co-resident with the victim's kernels (a resident spinner without any memory traffic).
+    python tools/cohab_model.py [iters] [victim_seq 0|1] [aggressor_seq 0|1]
 CRNN_OPTS="key=value,..." sets crnn_set_option switches first."""
 import os
 import sys
@@ -81,11 +79,6 @@ def main():
     for kv in os.environ.get("CRNN_OPTS", "").split(","):
         if kv:
             L.call("crnn_set_option", *[int(v) for v in kv.split("=")])
-    hog = None
-    if kind.startswith("hog"):
-        _, hb, hl, hi = kind.split(":")
-        hout = torch.zeros(L.lib().crnn_diag_lds_sentinel_words(), dtype=torch.int32, device="cuda")
-        hog = lambda st: L.call("crnn_diag_lds_sentinel", hout.data_ptr(), int(hb), int(hl), int(hi), 7, 1, 0, st)  # noqa
     vm, vx, vtg, vtl = make(5, 256, victim_seq)
     am, ax, atg, atl = make(6, 256, aggr_seq)
     probe = os.environ.get("COHAB_PROBE") == "1"
@@ -103,11 +96,8 @@ def main():
     for i in range(iters):
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
-            if hog is not None:
-                hog(side.cuda_stream)
-            else:
-                for _ in range(2):
-                    step(am, ax, atg, atl)   # the aggressor's forward + backward overlap the victim's step
+            for _ in range(2):
+                step(am, ax, atg, atl)   # the aggressor's forward + backward overlap the victim's step
         step(vm, vx, vtg, vtl)
         torch.cuda.synchronize()
         vg, ag = grads(vm), grads(am)

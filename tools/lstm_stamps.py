@@ -61,7 +61,7 @@ def run(kind, B, T, H, save=True):
     torch.cuda.synchronize()
     L.call("crnn_lstm_seq_debug_stamps", None)
     s = stamps.view(grid, T, 8).cpu().numpy().astype(np.int64)
-    ho = "granule" if HANDOFF else "counter"
+    ho = {0: "counter", 1: "granule", 2: "unit-complete", 3: "unit-complete 8w"}.get(HANDOFF, str(HANDOFF))
     print(f"{kind}: B={B} T={T} H={H} tile {S}x{U} grid={grid} hand-off {ho if kind == 'fwd' else 'counter'}: "
           f"{'' if save else '(inference, nothing saved) '}{us:.1f} us/sweep = {us / T:.2f} us/step (no stamps)")
     steps = slice(2, T - 1)
@@ -96,6 +96,17 @@ HANDOFF = 1
 if __name__ == "__main__":
     # forward under both hand-off forms (CRNN_OPT_LSTM_HANDOFF), each tile, in one process
     B, T, H = (int(a) for a in sys.argv[1:4]) if len(sys.argv) > 3 else (256, 32, 512)
+    if os.environ.get("STAMPS_FORMS"):
+        # the given forward forms (CRNN_OPT_LSTM_HANDOFF values) at the default tile, alternated twice, then the BPTT
+        # (phases of the unit-complete forms 2 / 3: waited = own K-slice polled, mfma+part = slice written to LDS,
+        # reduced = past the barrier, epilogue = MFMAs + cell done, stored = granules published)
+        forms = [int(v) for v in os.environ["STAMPS_FORMS"].split(",")]
+        for _ in range(2):
+            for HANDOFF in forms:
+                L.call("crnn_set_option", L.OPT_LSTM_HANDOFF, HANDOFF)
+                run("fwd", B, T, H)
+        run("bwd", B, T, H)
+        sys.exit(0)
     if os.environ.get("STAMPS_SAVE_AB"):
         # default tile and hand-off: saved-forward stores on / off (the BPTT operands' cost per step),
         # then the default BPTT
@@ -110,4 +121,4 @@ if __name__ == "__main__":
             run("fwd", B, T, H)
         run("bwd", B, T, H)
     L.call("crnn_set_option", L.OPT_LSTM_TILE, 0)
-    L.call("crnn_set_option", L.OPT_LSTM_HANDOFF, 1)
+    L.call("crnn_set_option", L.OPT_LSTM_HANDOFF, 3)
