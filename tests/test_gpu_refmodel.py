@@ -21,6 +21,13 @@ r05: tests/golden/make_refmodel2.py trains the same archite
 READS unseen lines, and records the reference's predictions on 10 000 held-out lines (refmodel2_attn.npz). On that
 set the bar is the north star's: fp32 gives the reference's strings, and bf16 exact-match accuracy is within
 0.001 of the reference's (10 lines in 10 000).
+r06: that model reads only 17 % of its lines, with an attention head on a frozen random CNN at
+hidden 256. tests/golden/make_refmodel3.py pins the bench's own configuration instead: RCNN(decoder="ctc"), hidden
+512, 2 BiLSTM layers, 32x256 crops, C = 194, trained WHOLE (CNN included) on the MI355X by this path's own
+training.train.run_training (tools/train_refmodel_ctc.py), and the reference's predictions for it on 10 000
+held-out lines (RCNN.encode + the CTC head + the reference's ctc_greedy_decoder, training/utils.py:122-150). Bars:
+fp32 gives the reference's strings line for line; bf16 exact-match accuracy within 0.001 of the reference's AND the
+reference's string on nearly every line (the bound below, set from the measurement).
 Reference: inference.py:126-195, training/utils.py:70-119, model/model.py:166-227."""
 import os
 
@@ -87,6 +94,40 @@ def refmodel2(tmp_path_factory):
 
 
 @pytest.fixture(scope="module")
+def refmodel3(tmp_path_factory):
+    """the bench-configuration CTC model (make_refmodel3.py): checkpoint path in the reference's save_checkpoint
+    format, (gray lines as 3-channel arrays, truth, reference predictions, reference accuracy), (img_h, img_w)"""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    z = np.load(os.path.join(GOLDEN, "refmodel3_ctc.npz"))
+    sd = {}
+    for k in z.files:
+        if k.startswith("q::"):
+            sd[k[3:]] = dequantize(torch.from_numpy(z[k]), torch.from_numpy(z["s::" + k[3:]]))
+        elif k.startswith("f::"):
+            sd[k[3:]] = torch.from_numpy(np.array(z[k]))
+    from data.transforms import load_charset
+    itos, stoi = load_charset(CHARSET)
+    H, W = int(z["img_h"]), int(z["img_w"])
+    ck = {"epoch": int(z["epochs"]), "global_step": 0, "model_state": sd, "optimizer_state": None,
+          "scheduler_state": None, "itos": itos, "stoi": stoi, "scaler_state": None, "best_val_loss": 0.0,
+          "best_val_acc": float(z["val_acc"]),
+          "config": {"hidden_size": int(z["hidden"]), "img_h": H, "img_w": W, "max_len": int(z["max_len"]),
+                     "decoder": "ctc"}}
+    path = str(tmp_path_factory.mktemp("refmodel3") / "ctc_ckpt.pth")
+    torch.save(ck, path)
+    widths, flat = z["test_widths"], z["test_pixels"]
+    imgs, off = [], 0
+    for w in widths.tolist():
+        imgs.append(np.repeat(flat[off:off + H * w].reshape(H, w)[:, :, None], 3, axis=2))
+        off += H * w
+    assert off == flat.size and len(imgs) == 10000
+    test = (imgs, [str(t) for t in z["test_truth"]], [str(t) for t in z["test_ref_pred"]],
+            float(z["test_ref_accuracy"]))
+    return path, {"test": test}, int(z["max_len"]), (H, W)
+
+
+@pytest.fixture(scope="module")
 def refmodel(tmp_path_factory):
     """(checkpoint path in the reference's save_checkpoint format, {set: (images, truth, reference
     predictions, reference accuracy)} for the fitted and the held-out lines, max_len, (img_h, img_w))"""
@@ -110,11 +151,11 @@ def refmodel(tmp_path_factory):
     return path, sets, int(z["max_len"]), (H, int(z["img_w"]))
 
 
-def _predict(refmodel, dtype, name):
+def _predict(refmodel, dtype, name, decoder="attn"):
     from inference import OCRInference
     path, sets, max_len, (H, W) = refmodel
     ocr = OCRInference(path, CHARSET, device="cuda", img_h=H, img_w=W, compute_dtype=dtype)
-    assert ocr.model.decoder == "attn"
+    assert ocr.model.decoder == decoder
     return ocr.predict(sets[name][0], max_length=max_len, batch_size=256)
 
 
@@ -179,3 +220,37 @@ def test_refmodel_load_crnn(refmodel):
     got = m.state_dict()
     for k in ("attn.generator.weight", "enc_rnn.1.rnn.weight_hh_l0", "cnn.layer4.2.bn2.running_var"):
         assert torch.equal(got[k].cpu(), sd[k]), k
+
+
+def test_refmodel3_reads(refmodel3):
+    """the fixture is a model that reads: the reference's own exact-match accuracy on the held-out lines"""
+    assert refmodel3[1]["test"][3] >= 0.85
+
+
+def test_refmodel3_fp32_reproduces_reference_strings(refmodel3):
+    """fp32, the bench's CTC model, 10 000 held-out lines: the reference's greedy-decoded strings, line for line
+    (north_star "identical greedy-decoded strings")"""
+    _, truth, ref, ref_acc = refmodel3[1]["test"]
+    got = _predict(refmodel3, torch.float32, "test", decoder="ctc")
+    diff = [(i, r, g) for i, (r, g) in enumerate(zip(ref, got)) if r != g]
+    acc = float(np.mean([g == t for g, t in zip(got, truth)]))
+    print(f"CTC held-out fp32: {len(diff)} of {len(ref)} strings differ from the reference's; accuracy {acc:.4f} "
+          f"(reference {ref_acc:.4f}); first differences {diff[:5]}")
+    assert not diff
+    assert acc == ref_acc
+
+
+REFMODEL3_BF16_AGREEMENT = 0.99   # bound on the bf16 string agreement (DESIGN.md r06: measured value there)
+
+
+def test_refmodel3_bf16_accuracy_and_agreement(refmodel3):
+    """bf16 (the performance mode) on the bench's CTC model: exact-match accuracy within 0.001 of the reference's
+    on 10 000 held-out lines, and the reference's string on at least REFMODEL3_BF16_AGREEMENT of them"""
+    _, truth, ref, ref_acc = refmodel3[1]["test"]
+    got = _predict(refmodel3, torch.bfloat16, "test", decoder="ctc")
+    same = float(np.mean([g == r for g, r in zip(got, ref)]))
+    acc = float(np.mean([g == t for g, t in zip(got, truth)]))
+    print(f"CTC held-out bf16: exact-match accuracy {acc:.4f} vs reference {ref_acc:.4f} (diff {acc - ref_acc:+.4f}); "
+          f"the reference's string on {same:.4f} of {len(ref)} lines")
+    assert abs(acc - ref_acc) <= 0.001 + 1e-9
+    assert same >= REFMODEL3_BF16_AGREEMENT

@@ -238,3 +238,34 @@ def test_oracle_reads_like_the_generalising_reference_model():
     oracle gives the reference's strings on the first 24 of its 10 000 held-out lines (the GPU test runs all
     10 000 on the HIP path and bounds the bf16 accuracy change at 0.1 %)."""
     _oracle_reads("refmodel2_attn.npz", ("test",), gray=True)
+
+
+def test_oracle_reads_like_the_bench_configuration_ctc_model():
+    """tests/golden/refmodel3_ctc.npz (make_refmodel3.py: RCNN(decoder="ctc") at hidden 512, 32x256, trained whole
+    by run_training on the MI355X; the reference's greedy strings on 10 000 held-out lines, 99.6 % correct): the
+    oracle's encode + CTC head + greedy collapse gives the reference's strings on the first 48 lines (the GPU test
+    runs all 10 000 on the HIP path in fp32 and bf16)."""
+    import preprocess_oracle as P
+    z = np.load(os.path.join(GOLDEN, "refmodel3_ctc.npz"))
+    assert float(z["test_ref_accuracy"]) >= 0.85
+    with open(os.path.join(GOLDEN, "charset.txt"), encoding="utf-8") as f:
+        itos = [l.rstrip("\n") for l in f if l.rstrip("\n") != ""]
+    p = {}
+    for k in z.files:
+        if k.startswith("q::"):
+            q, s = torch.from_numpy(z[k]), torch.from_numpy(z["s::" + k[3:]])
+            p[k[3:]] = (q.reshape(q.shape[0], -1).float() * s.reshape(-1, 1)).reshape(q.shape)
+        elif k.startswith("f::"):
+            p[k[3:]] = torch.from_numpy(np.array(z[k]))
+    H, W, n = int(z["img_h"]), int(z["img_w"]), 48
+    widths, flat = z["test_widths"], z["test_pixels"]
+    imgs, off = [], 0
+    for w in widths.tolist()[:n]:
+        imgs.append(np.repeat(flat[off:off + H * w].reshape(H, w)[:, :, None], 3, axis=2))
+        off += H * w
+    x = torch.from_numpy(np.stack([P.preprocess(im, H, W)[1] for im in imgs]))
+    with torch.no_grad():
+        lg = O.head(O.encode(x, p, O.Ctx(train=False)), p)
+    got = ["".join(itos[t] for t in seq) for seq in O.greedy_decode(lg.numpy())]   # training/utils.py:122-150
+    ref = [str(t) for t in z["test_ref_pred"][:n]]
+    assert got == ref, [(g, r) for g, r in zip(got, ref) if g != r][:4]
