@@ -95,7 +95,8 @@ int run(const LA& la, const LB& lb, const OutEpi<T>& ep, int M, int N, int K, in
       const long t256 = (long)((M + 255) / 256) * ((N + 255) / 256);
       const long t128 = (long)((M + 255) / 256) * ((N + 127) / 128);
       const OutEpi<T, true> ep8{ep.c, ep.ldc, ep.M, ep.N, ep.c_f32, ep.accumulate, ep.atomic, ep.bias};
-      const bool row8 = crnn_option(CRNN_OPT_LINEAR_ROW8) != 0;
+      // 16-B row stores need a 16-B aligned C and row pitch (a view offset by 4 elements is only 8-B aligned)
+      const bool row8 = crnn_option(CRNN_OPT_LINEAR_ROW8) != 0 && ep.ldc % 8 == 0 && ((uintptr_t)ep.c & 15) == 0;
       if (N >= 256 && t256 * 4 >= cu * 3)
         return row8 ? launch256<256, 256>(la, lb, ep8, M, N, K, st) : launch256<256, 256>(la, lb, ep, M, N, K, st);
       if (N >= 128 && t128 * 4 >= cu * 3)

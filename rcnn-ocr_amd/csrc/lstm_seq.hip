@@ -377,13 +377,7 @@ __global__ __launch_bounds__(256) void lstm_seq_fwd_kernel(const bf16* __restric
 // Ring reuse (2 slots): a wave writes slot s & 1 at step s after its workgroup's step-s barrier, i.e.
 // after all 4 waves' polls of h_{s-1} returned, from every producer wave of the group; each of those
 // produced h_{s-1} after its own workgroup had read h_{s-2} (the slot's previous contents).
-// tanh(x) = 2 sigmoid(2x) - 1: exp + add + rcp + fma (tanh_fast's |x| / sign restore cost 3 more VALU);
-// saturates to -1 / +1 through rcp(inf) = 0 / rcp(1) = 1
-__device__ __forceinline__ float tanh_sig(float x) {
-  return __builtin_fmaf(2.f, __builtin_amdgcn_rcpf(1.f + __expf(-2.f * x)), -1.f);
-}
-
-template <int H, int S, int U, int W, bool FT = false, bool SF = false>
+template <int H, int S, int U, int W>
 __global__ __launch_bounds__(64 * W) void lstm_seq_fwd_uc_kernel(const bf16* __restrict__ xg,
                                                               const bf16* __restrict__ whh, bf16* hseq,
                                                               bf16* __restrict__ gsv, float* __restrict__ csv,
@@ -396,15 +390,7 @@ __global__ __launch_bounds__(64 * W) void lstm_seq_fwd_uc_kernel(const bf16* __r
   constexpr int KQ = HW / 32;         // its k-steps
   constexpr int MI = S / 16, H4 = 4 * H, HP = H + 8;
   static_assert(HW % 32 == 0 && S % 16 == 0 && (NT == 2 || NT == 4), "shape");
-  static_assert(!SF || (MI == 1 && KK <= 16), "slice flags: one sample tile, B fragments of a slice in registers");
   __shared__ __attribute__((aligned(16))) bf16 himg[2][S][HP];
-  // SF: per-slice LDS flags instead of the step barrier — flag[buf][j] = the step whose K-slice j wave j
-  // has written; a wave runs the MFMAs of each slice as soon as its flag says so, own slice first
-  __shared__ unsigned sflag[2][W];
-  if constexpr (SF) {
-    if (threadIdx.x < 2 * W) (&sflag[0][0])[threadIdx.x] = 0xffffffffu;
-    __syncthreads();
-  }
 
   const int nsl = H / U, nbs = B / S;
   int d, bs, ns;
@@ -436,11 +422,8 @@ __global__ __launch_bounds__(64 * W) void lstm_seq_fwd_uc_kernel(const bf16* __r
     for (int jt = 0; jt < NT; ++jt) {
       const int row = 4 * (ns * U + w * UW + NT * (c >> 2) + jt) + (c & 3);
 #pragma unroll
-      for (int kk = 0; kk < KK; ++kk) {
-        // SF: slot kk holds k-step (kk + w KQ) mod KK, so slot jj KQ + kq belongs to slice (w + jj) mod W
-        const int ks = SF ? (kk + w * KQ) % KK : kk;
-        wf[jt][kk] = *reinterpret_cast<const bf16x8*>(wb + (size_t)row * H + 32 * ks + 8 * g);
-      }
+      for (int kk = 0; kk < KK; ++kk)
+        wf[jt][kk] = *reinterpret_cast<const bf16x8*>(wb + (size_t)row * H + 32 * kk + 8 * g);
     }
   }
   const __amdgpu_buffer_rsrc_t rr = rsrc_of(ring);
@@ -473,10 +456,9 @@ __global__ __launch_bounds__(64 * W) void lstm_seq_fwd_uc_kernel(const bf16* __r
     // cell update of fragment (i, jt): lane holds gates (i, f, g, o) of unit ul + jt of one sample
     auto cell = [&](int i, int jt) {
       const f32x4 v = acc[i][jt];
-      const float ig = sigmoid_fast(v[0]), fg = sigmoid_fast(v[1]), og = sigmoid_fast(v[3]);
-      const float gg = FT ? tanh_sig(v[2]) : tanh_fast(v[2]);
+      const float ig = sigmoid_fast(v[0]), fg = sigmoid_fast(v[1]), gg = tanh_fast(v[2]), og = sigmoid_fast(v[3]);
       float cc = fg * cst[i][jt] + ig * gg;
-      float h = og * (FT ? tanh_sig(cc) : tanh_fast(cc));
+      float h = og * tanh_fast(cc);
       if (!ok) h = cc = __builtin_nanf("");
       cst[i][jt] = cc;
       gq[i][jt] = f32x4{ig, fg, gg, og};
@@ -528,37 +510,6 @@ __global__ __launch_bounds__(64 * W) void lstm_seq_fwd_uc_kernel(const bf16* __r
         }
       load_xg(tn);   // issued behind the hand-off loads, a whole step ahead of its use
       SEQ_STAMP(2);
-      if constexpr (SF) {
-        // publish this wave's slice to the workgroup (its ds_writes are ordered before the flag: release),
-        // then consume the slices in ring order; the double-buffered image and flags are safe without a
-        // step barrier: a wave writing buffer b at step s + 2 has the step-(s+1) slices of every wave of
-        // the workgroup, each written after that wave finished its step-s reads
-        // LDS ops of one wave retire in order: the slice's ds_writes are complete before the flag write is
-        // issued (lgkmcnt(0) only: an atomic release here waited for vmcnt(0), i.e. for the x-gate prefetch)
-        __builtin_amdgcn_s_waitcnt(0xC07F);
-        __hip_atomic_store(&sflag[buf][w], (unsigned)s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        SEQ_STAMP(3);
-#pragma unroll
-        for (int jj = 0; jj < W; ++jj) {
-          const int j = (w + jj) % W;
-          if (jj > 0)
-            while (__hip_atomic_load(&sflag[buf][j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != (unsigned)s)
-              __builtin_amdgcn_s_sleep(0);
-          // the slice's reads stay behind the flag read (compiler order; the LDS keeps the wave's order)
-          asm volatile("" ::: "memory");
-          __builtin_amdgcn_sched_barrier(0);
-          bf16x8 hb[KQ];
-#pragma unroll
-          for (int kq = 0; kq < KQ; ++kq)
-            hb[kq] = *reinterpret_cast<const bf16x8*>(&himg[buf][c][j * HW + 32 * kq + 8 * g]);
-#pragma unroll
-          for (int kq = 0; kq < KQ; ++kq)
-#pragma unroll
-            for (int jt = 0; jt < NT; ++jt) mma<bf16>(acc[0][jt], wf[jt][jj * KQ + kq], hb[kq]);
-        }
-#pragma unroll
-        for (int jt = 0; jt < NT; ++jt) cell(0, jt);
-      } else {
       __syncthreads();
       SEQ_STAMP(3);
       if constexpr (MI == 1 && KK <= 16) {
@@ -612,7 +563,6 @@ __global__ __launch_bounds__(64 * W) void lstm_seq_fwd_uc_kernel(const bf16* __r
 #pragma unroll
           for (int jt = 0; jt < NT; ++jt) cell(i, jt);
       }
-      }   // SF
     } else {
       load_xg(tn);
 #pragma unroll
@@ -1028,16 +978,6 @@ void launch_fwd_tile(int form, dim3 grid, hipStream_t st, const bf16* xg, const 
     if (form == 3) {   // 8 waves of 8 units: 2 waves per SIMD, weights without AGPR copies
       hipLaunchKernelGGL((lstm_seq_fwd_uc_kernel<H, S, U, 8>), grid, dim3(512), 0, st, xg, whh, hseq, gsv, csv, cnt,
                          err, ring, B, T, g_stamps, xtab);
-      return;
-    }
-    if (form == 5) {   // form 4 with per-slice LDS flags instead of the step barrier (A/B)
-      hipLaunchKernelGGL((lstm_seq_fwd_uc_kernel<H, S, U, 8, true, true>), grid, dim3(512), 0, st, xg, whh, hseq, gsv,
-                         csv, cnt, err, ring, B, T, g_stamps, xtab);
-      return;
-    }
-    if (form == 4) {   // form 3 with tanh = 2 sigmoid(2x) - 1 (A/B)
-      hipLaunchKernelGGL((lstm_seq_fwd_uc_kernel<H, S, U, 8, true>), grid, dim3(512), 0, st, xg, whh, hseq, gsv, csv,
-                         cnt, err, ring, B, T, g_stamps, xtab);
       return;
     }
   }

@@ -27,7 +27,7 @@ for step in "$@"; do
   case "$step" in
   tests)
     sel=(); [ -n "$PYTEST_K" ] && sel=(-k "$PYTEST_K")
-    timeout -k 10 ${PYTEST_T:-1000} python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread \
+    timeout -k 10 ${PYTEST_T:-1000} python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread $PYTEST_EXTRA \
       "${sel[@]}" > ${O}_pytest.log 2>&1 || { grep -E "^FAILED|Error" ${O}_pytest.log | head -20; tail -30 ${O}_pytest.log; exit 1; }
     tail -2 ${O}_pytest.log ;;
   smoke)
