@@ -44,6 +44,10 @@ extern "C" {
 
 #define CRNN_F32 0
 #define CRNN_BF16 1
+/* crnn_gemm_nt / nn / tn only: fp32 operands in memory, converted to bf16 while staged, bf16 MFMA, fp32
+ * accumulation, fp32 C (c_f32 implied) — the attention decoder's training GEMMs (r06), the precision of the
+ * reference's fp16 autocast (training/train.py:499) */
+#define CRNN_F32_BF16MMA 2
 
 int crnn_version(void);
 const char* crnn_last_error_string(void);

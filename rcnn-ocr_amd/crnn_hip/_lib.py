@@ -18,6 +18,7 @@ LIB_PATH = os.environ.get("CRNN_HIP_LIB", os.path.join(HERE, "libcrnn_hip.so"))
 CSRC = os.path.join(PKG, "csrc")
 
 F32, BF16 = 0, 1
+F32_BF16MMA = 2   # gemm_nt / nn / tn: fp32 operands, bf16 MFMA, fp32 out (include/crnn_hip.h)
 
 vp = C.c_void_p
 i32 = C.c_int

@@ -24,11 +24,15 @@ from ._lib import call, ptr
 
 class AttnDecoderHIP:
     """params: the reference Attention state_dict (attention_cell.*, generator.*), any device
-    tensors; copied to fp32 device buffers (call refresh() after the weights change)."""
+    tensors; copied to fp32 device buffers (call refresh() after the weights change).
+    train_bf16: the training pass (run_train / backward) runs its GEMMs on bf16 MFMA with fp32 accumulation
+    over the fp32 operands (CRNN_F32_BF16MMA, converted while staged) — the reference trains this head under
+    fp16 autocast (training/train.py:499-505). Inference (run) keeps the exact-fp32 GEMMs."""
 
     def __init__(self, params: Dict[str, torch.Tensor], num_classes: int, sos_id: int,
-                 blank_id: Optional[int], device):
+                 blank_id: Optional[int], device, train_bf16: bool = False):
         self.device = torch.device(device)
+        self.tdt = L.F32_BF16MMA if train_bf16 else L.F32   # the training pass's GEMM dtype code
         self._saved = None
         self.V = num_classes
         self.Vpad = (num_classes + 7) // 8 * 8
@@ -55,9 +59,9 @@ class AttnDecoderHIP:
         self.b_gen = torch.zeros(self.Vpad, device=self.device)
         self.b_gen[: self.V] = gb
 
-    def _gemm(self, a, lda, w, ldw, out, ldo, bias, M, N, K):
-        call("crnn_gemm_nt", L.F32, ptr(a), lda, ptr(w), ldw, ptr(out), ldo, ptr(bias), M, N, K, 1, 0,
-             L.stream_ptr())
+    def _gemm(self, a, lda, w, ldw, out, ldo, bias, M, N, K, dt=None):
+        call("crnn_gemm_nt", L.F32 if dt is None else dt, ptr(a), lda, ptr(w), ldw, ptr(out), ldo, ptr(bias), M, N, K,
+             1, 0, L.stream_ptr())
 
     def run_train(self, enc: torch.Tensor, steps: int, text: torch.Tensor, drop_p: float = 0.0,
                   seed: int = 0) -> torch.Tensor:
@@ -72,7 +76,7 @@ class AttnDecoderHIP:
         if txt.shape[1] < steps:
             raise ValueError("text needs batch_max_length + 1 columns")
         projH = torch.empty(B * T, H, device=dev)
-        self._gemm(enc, C, self.w_i2h, C, projH, H, None, B * T, H, C)
+        self._gemm(enc, C, self.w_i2h, C, projH, H, None, B * T, H, C, self.tdt)
         LX = C + H + Vp                                     # [context_t | h_{t-1} | onehot(text_t)] per step
         Xs = torch.zeros(steps + 1, B, LX, device=dev)
         call("crnn_attn_onehot_rows", ptr(txt), txt.shape[1], steps, B, V, ptr(Xs), LX, C + H, s)
@@ -85,15 +89,15 @@ class AttnDecoderHIP:
         c = torch.zeros(B, H, device=dev)
         gates = torch.empty(B, 4 * H, device=dev)
         for t in range(steps):
-            self._gemm(h, H, self.w_h2h, H, Ph[t], H, self.b_h2h, B, H, H)
+            self._gemm(h, H, self.w_h2h, H, Ph[t], H, self.b_h2h, B, H, H, self.tdt)
             call("crnn_attn_context", ptr(projH), ptr(Ph[t]), ptr(self.score), ptr(enc), ptr(Xs[t]), LX,
                  ptr(As[t]), B, T, H, C, drop_p, (seed + t) & (2 ** 64 - 1), s)
-            self._gemm(Xs[t], LX, self.w_cat, C + H, gates, 4 * H, None, B, 4 * H, C + H)
+            self._gemm(Xs[t], LX, self.w_cat, C + H, gates, 4 * H, None, B, 4 * H, C + H, self.tdt)
             call("crnn_attn_cell", ptr(gates), ptr(self.b_ih), ptr(self.b_hh), ptr(self.w_ih), C + V, ptr(txt[:, t:]),
                  txt.shape[1], ptr(h), ptr(c), ptr(Xs[t + 1]), LX, ptr(hs[:, t]), steps * H, ptr(Gs[t]), ptr(Cs[t]),
                  B, H, C, s)
         lg = torch.empty(B * steps, Vp, device=dev)
-        self._gemm(hs, H, self.w_gen, H, lg, Vp, self.b_gen, B * steps, Vp, H)
+        self._gemm(hs, H, self.w_gen, H, lg, Vp, self.b_gen, B * steps, Vp, H, self.tdt)
         out = torch.empty(B, steps, V, device=dev)
         scratch = torch.empty(B * steps, dtype=torch.int32, device=dev)
         call("crnn_attn_out", ptr(lg), Vp, B * steps, V, self.blank, ptr(out), V, ptr(scratch), s)
@@ -113,7 +117,7 @@ class AttnDecoderHIP:
         drop_p, seed = sv["drop"]
         B, T, C = enc.shape
         H, V, Vp, dev, s = self.H, self.V, self.Vpad, self.device, L.stream_ptr()
-        F32 = L.F32
+        F32 = self.tdt   # GEMMs only (crnn_colsum keeps L.F32)
         dL = torch.zeros(B * steps, Vp, device=dev)
         dL[:, :V] = dlogits.reshape(B * steps, V).to(dev, torch.float32)
         if self.blank >= 0:
@@ -123,7 +127,7 @@ class AttnDecoderHIP:
         gw = torch.empty(Vp, H, device=dev)
         call("crnn_gemm_tn", F32, ptr(dL), Vp, ptr(hs), H, ptr(gw), H, Vp, H, B * steps, 0, s)
         gb = torch.empty(Vp, device=dev)
-        call("crnn_colsum", F32, ptr(dL), Vp, B * steps, Vp, ptr(gb), 0, 1, s)
+        call("crnn_colsum", L.F32, ptr(dL), Vp, B * steps, Vp, ptr(gb), 0, 1, s)
         dG = torch.empty(steps, B, 4 * H, device=dev)
         dPh = torch.empty(steps, B, H, device=dev)
         De = torch.empty(steps, B, T, device=dev)           # d attention logits per step
@@ -154,16 +158,16 @@ class AttnDecoderHIP:
         call("crnn_gemm_tn", F32, ptr(dG), 4 * H, ptr(Xs), LX, ptr(wfull), LX, 4 * H, LX, steps * B, 0, s)
         dwih = torch.cat([wfull[:, :C], wfull[:, C + H:C + H + V]], 1)
         db = torch.empty(4 * H, device=dev)
-        call("crnn_colsum", F32, ptr(dG), 4 * H, steps * B, 4 * H, ptr(db), 0, 1, s)
+        call("crnn_colsum", L.F32, ptr(dG), 4 * H, steps * B, 4 * H, ptr(db), 0, 1, s)
         wh2h = torch.empty(H, H, device=dev)
         call("crnn_gemm_tn", F32, ptr(dPh), H, ptr(Xs[:, :, C:]), LX, ptr(wh2h), H, H, H, steps * B, 0, s)
         bh2h = torch.empty(H, device=dev)
-        call("crnn_colsum", F32, ptr(dPh), H, steps * B, H, ptr(bh2h), 0, 1, s)
+        call("crnn_colsum", L.F32, ptr(dPh), H, steps * B, H, ptr(bh2h), 0, 1, s)
         wi2h = torch.empty(H, C, device=dev)
         call("crnn_gemm_tn", F32, ptr(dProjH), H, ptr(enc), C, ptr(wi2h), C, H, C, B * T, 0, s)
         call("crnn_gemm_nn", F32, ptr(dProjH), H, ptr(self.w_i2h), C, ptr(denc), C, B * T, C, H, 1, 1, s)
         dsc = torch.empty(H, device=dev)
-        call("crnn_colsum", F32, ptr(dscore), H, B, H, ptr(dsc), 0, 1, s)
+        call("crnn_colsum", L.F32, ptr(dscore), H, B, H, ptr(dsc), 0, 1, s)
         pre = "attention_cell."
         out = {pre + "i2h.weight": wi2h, pre + "h2h.weight": wh2h, pre + "h2h.bias": bh2h,
                pre + "score.weight": dsc.view(1, H), pre + "rnn.weight_ih": dwih, pre + "rnn.weight_hh": wfull[:, C:C + H],

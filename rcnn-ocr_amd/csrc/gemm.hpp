@@ -374,4 +374,21 @@ template <typename T> struct ColMajorK {
   }
 };
 
+// fp32 operands staged as bf16 (CRNN_F32_BF16MMA: the attention decoder's training GEMMs, fp32 in memory and
+// bf16 MFMA with fp32 accumulation, as the reference's fp16 autocast computes them): the register-staged
+// kernels' loaders convert 8 fp32 elements to bf16 on the way to LDS. No LDS-DMA form (nothing to convert
+// with), so these views run only on gemm_kernel.
+template <class L32> struct Bf16Of {
+  static constexpr bool kRowVec = L32::kRowVec;
+  using Ctx = typename L32::Ctx;
+  typedef int Prep;
+  L32 l;
+  __device__ __forceinline__ Ctx row_ctx(int r) const { return l.row_ctx(r); }
+  __device__ __forceinline__ Prep prep(int k0) const { return k0; }
+  __device__ __forceinline__ bf16x8 load(const Ctx& c, Prep k0, int kofs) const {
+    const f32x8 v = l.load(c, k0, kofs);
+    return bf16x8{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3], (bf16)v[4], (bf16)v[5], (bf16)v[6], (bf16)v[7]};
+  }
+};
+
 }  // namespace gemm

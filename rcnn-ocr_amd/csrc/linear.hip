@@ -85,10 +85,11 @@ template <typename T, bool ROW8 = false> struct OutEpi {
   __device__ __forceinline__ void stats(int, int, f32x4, f32x4) const {}
 };
 
-template <typename T, class LA, class LB>
+// DEEP = false: the register-staged kernels only (loaders without an LDS-DMA form, gemm::Bf16Of)
+template <typename T, bool DEEP = true, class LA, class LB>
 int run(const LA& la, const LB& lb, const OutEpi<T>& ep, int M, int N, int K, int splits, hipStream_t st) {
   long work = (long)M * N;
-  if constexpr (sizeof(T) == 2) {
+  if constexpr (sizeof(T) == 2 && DEEP) {
     // the deep 256-row kernel when the grid alone fills most CUs (no split-K for these outputs)
     const long cu = crnn_cu_count();
     if (crnn_option(CRNN_OPT_DEEP_LINEAR) && splits == 1 && K >= 256) {
@@ -149,6 +150,46 @@ int gemm_tn_t(const void* A, int lda, const void* B, int ldb, float* C, int ldc,
   if (b == 128) return launch<T, 128, 128>(la, lb, ep, M, N, K, splits, st);
   if (b == 64) return launch<T, 64, 64>(la, lb, ep, M, N, K, splits, st);
   return launch<T, 32, 32>(la, lb, ep, M, N, K, splits, st);
+}
+
+// CRNN_F32_BF16MMA: fp32 operands in memory, staged as bf16 (gemm::Bf16Of), bf16 MFMA, fp32 accumulation and
+// fp32 output — the attention decoder's training GEMMs (the reference's fp16 autocast, training/train.py:499)
+int gemm_nt_mix(const void* A, int lda, const void* B, int ldb, void* C, int ldc, const float* bias, int M, int N,
+                int K, int acc, hipStream_t st) {
+  Bf16Of<RowMajorK<float>> la{RowMajorK<float>{(const float*)A, lda, M, K}};
+  Bf16Of<RowMajorK<float>> lb{RowMajorK<float>{(const float*)B, ldb, N, K}};
+  OutEpi<bf16> ep{C, ldc, M, N, 1, acc, 0, bias};
+  return run<bf16, false>(la, lb, ep, M, N, K, 1, st);
+}
+
+int gemm_nn_mix(const void* A, int lda, const void* B, int ldb, void* C, int ldc, int M, int N, int K, int acc,
+                hipStream_t st) {
+  Bf16Of<RowMajorK<float>> la{RowMajorK<float>{(const float*)A, lda, M, K}};
+  Bf16Of<ColMajorK<float>> lb{ColMajorK<float>{(const float*)B, ldb, N, K}};
+  OutEpi<bf16> ep{C, ldc, M, N, 1, acc, 0, nullptr};
+  return run<bf16, false>(la, lb, ep, M, N, K, 1, st);
+}
+
+int gemm_tn_mix(const void* A, int lda, const void* B, int ldb, float* C, int ldc, int M, int N, int K, int acc,
+                hipStream_t st) {
+  Bf16Of<ColMajorK<float>> la{ColMajorK<float>{(const float*)A, lda, M, K}};
+  Bf16Of<ColMajorK<float>> lb{ColMajorK<float>{(const float*)B, ldb, N, K}};
+  int b = (M >= 128 && N >= 128) ? 128 : (M >= 64 && N >= 64 ? 64 : 32);
+  long tiles = (long)((M + b - 1) / b) * ((N + b - 1) / b);
+  long want = (512 + tiles - 1) / tiles;
+  long maxs = (K + 4 * BK - 1) / (4 * BK);
+  if (want > maxs) want = maxs;
+  if (want < 1) want = 1;
+  int splits = eff_splits(K, (int)want);
+  if (splits > 1 && !acc) {
+    hipError_t e = ldc == N ? hipMemsetAsync(C, 0, (size_t)M * N * sizeof(float), st)
+                            : hipMemset2DAsync(C, (size_t)ldc * sizeof(float), 0, (size_t)N * sizeof(float), M, st);
+    if (e != hipSuccess) return (int)e;
+  }
+  OutEpi<bf16> ep{C, ldc, M, N, 1, acc, splits > 1 ? 1 : 0, nullptr};
+  if (b == 128) return launch<bf16, 128, 128>(la, lb, ep, M, N, K, splits, st);
+  if (b == 64) return launch<bf16, 64, 64>(la, lb, ep, M, N, K, splits, st);
+  return launch<bf16, 32, 32>(la, lb, ep, M, N, K, splits, st);
 }
 
 // split-K partials of C = A^T B into fp32 slabs [S][M][N] (deterministic; fp32 atomics from every
@@ -251,6 +292,7 @@ int crnn_gemm_nt(int dtype, const void* A, int lda, const void* B, int ldb, void
                  int N, int K, int c_f32, int accumulate, void* stream) {
   if (K % 8 || lda % 8 || ldb % 8) return crnn_set_error(hipErrorInvalidValue, "gemm_nt: K/lda/ldb must be multiples of 8");
   hipStream_t st = (hipStream_t)stream;
+  if (dtype == CRNN_F32_BF16MMA) return gemm_nt_mix(A, lda, B, ldb, C, ldc, bias, M, N, K, accumulate, st);
   return dtype == CRNN_BF16 ? gemm_nt_t<bf16>(A, lda, B, ldb, C, ldc, bias, M, N, K, c_f32, accumulate, st)
                             : gemm_nt_t<float>(A, lda, B, ldb, C, ldc, bias, M, N, K, c_f32, accumulate, st);
 }
@@ -259,6 +301,7 @@ int crnn_gemm_nn(int dtype, const void* A, int lda, const void* B, int ldb, void
                  int c_f32, int accumulate, void* stream) {
   if (K % 8 || N % 8 || lda % 8 || ldb % 8) return crnn_set_error(hipErrorInvalidValue, "gemm_nn: K/N/ld must be multiples of 8");
   hipStream_t st = (hipStream_t)stream;
+  if (dtype == CRNN_F32_BF16MMA) return gemm_nn_mix(A, lda, B, ldb, C, ldc, M, N, K, accumulate, st);
   return dtype == CRNN_BF16 ? gemm_nn_t<bf16>(A, lda, B, ldb, C, ldc, M, N, K, c_f32, accumulate, st)
                             : gemm_nn_t<float>(A, lda, B, ldb, C, ldc, M, N, K, c_f32, accumulate, st);
 }
@@ -267,6 +310,7 @@ int crnn_gemm_tn(int dtype, const void* A, int lda, const void* B, int ldb, floa
                  int accumulate, void* stream) {
   if (M % 8 || N % 8 || lda % 8 || ldb % 8) return crnn_set_error(hipErrorInvalidValue, "gemm_tn: M/N/ld must be multiples of 8");
   hipStream_t st = (hipStream_t)stream;
+  if (dtype == CRNN_F32_BF16MMA) return gemm_tn_mix(A, lda, B, ldb, C, ldc, M, N, K, accumulate, st);
   return dtype == CRNN_BF16 ? gemm_tn_t<bf16>(A, lda, B, ldb, C, ldc, M, N, K, accumulate, st)
                             : gemm_tn_t<float>(A, lda, B, ldb, C, ldc, M, N, K, accumulate, st);
 }

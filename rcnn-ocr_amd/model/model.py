@@ -279,7 +279,8 @@ class RCNN(nn.Module):
             if self._attn_dec is not None and self._attn_dec.device == device:
                 self._attn_dec.refresh(params)
             else:
-                self._attn_dec = AttnDecoderHIP(params, self.num_classes, self.sos_id, self.blank_id, device)
+                self._attn_dec = AttnDecoderHIP(params, self.num_classes, self.sos_id, self.blank_id, device,
+                                                train_bf16=self.compute_dtype == torch.bfloat16)
             self._attn_version = ver
         return self._attn_dec
 

@@ -588,6 +588,45 @@ def test_attn_decoder_backward_matches_oracle(drop_p):
         assert rel(grads[k].cpu().double(), 2 * pr[k].grad) < 1e-4, k
 
 
+def test_attn_decoder_backward_bf16mma():
+    """The decoder's training pass with train_bf16 (GEMMs on bf16 MFMA over fp32 operands, CRNN_F32_BF16MMA — the
+    reference trains this head under fp16 autocast, training/train.py:499-505) vs fp64 autograd through the
+    oracle's attn_teacher at the bench configuration's widths (C = 1024, H = 256, V = 194): logits within 1e-2
+    and every gradient within 3e-2 (relative norm; bf16 operand rounding, 2^-9 per element)."""
+    from crnn_hip.attn import AttnDecoderHIP
+    B, T, C, H, steps, V, seed = 16, 32, 1024, 256, 12, 194, 77
+    g = torch.Generator().manual_seed(12)
+    p64 = {"attention_cell.i2h.weight": torch.randn(H, C, generator=g, dtype=torch.float64) / C ** 0.5,
+           "attention_cell.h2h.weight": torch.randn(H, H, generator=g, dtype=torch.float64) / H ** 0.5,
+           "attention_cell.h2h.bias": torch.randn(H, generator=g, dtype=torch.float64) * 0.1,
+           "attention_cell.score.weight": torch.randn(1, H, generator=g, dtype=torch.float64) / H ** 0.5,
+           "attention_cell.rnn.weight_ih": torch.randn(4 * H, C + V, generator=g, dtype=torch.float64) / (C + V) ** 0.5,
+           "attention_cell.rnn.weight_hh": torch.randn(4 * H, H, generator=g, dtype=torch.float64) / H ** 0.5,
+           "attention_cell.rnn.bias_ih": torch.randn(4 * H, generator=g, dtype=torch.float64) * 0.1,
+           "attention_cell.rnn.bias_hh": torch.randn(4 * H, generator=g, dtype=torch.float64) * 0.1,
+           "generator.weight": torch.randn(V, H, generator=g, dtype=torch.float64) / H ** 0.5,
+           "generator.bias": torch.randn(V, generator=g, dtype=torch.float64) * 0.1}
+    enc = torch.randn(B, T, C, generator=g, dtype=torch.float64)
+    text = torch.randint(4, V, (B, steps), generator=g)
+    text[:, 0] = 1
+    gout = torch.randn(B, steps, V, generator=g, dtype=torch.float64)
+    dec = AttnDecoderHIP({k: v.float() for k, v in p64.items()}, V, 1, 3, DEV, train_bf16=True)
+    lg = dec.run_train(enc.float().to(DEV), steps, text.to(DEV), drop_p=0.0, seed=seed)
+    grads = {k: torch.zeros(v.shape, device=DEV) for k, v in p64.items()}
+    denc = dec.backward(gout.float().to(DEV), grads, accumulate=False).cpu().double()
+    pr = {k: v.clone().requires_grad_(True) for k, v in p64.items()}
+    e = enc.clone().requires_grad_(True)
+    ref = O.attn_teacher(pr, e, text, steps, 3, V)
+    (ref * gout).sum().backward()
+    rel = lambda a, b: float((a - b).norm() / (b.norm() + 1e-30))  # noqa: E731
+    errs = {k: rel(grads[k].cpu().double(), pr[k].grad) for k in pr}
+    errs["enc"] = rel(denc, e.grad)
+    errs["logits"] = rel(lg.cpu().double(), ref.detach())
+    print("attn backward (bf16 MFMA) rel errors:", errs)
+    assert errs["logits"] < 1e-2, errs
+    assert max(errs.values()) < 3e-2, errs
+
+
 def test_rcnn_attn_train_step_matches_oracle():
     """RCNN(decoder='attn') training step end to end on the HIP path (fp32): encoder forward
     (train-mode BN) -> teacher-forced decoder -> cross-entropy -> decoder BPTT -> encoder

@@ -945,6 +945,41 @@ def test_gemm_nt_nn_tn(mnk, dtype):
             assert relerr(C4.cpu(), 2 * (At.t() @ Bt)) < tol
 
 
+@pytest.mark.parametrize("mnk", [(37, 48, 64), (1536, 256, 512), (48, 1024, 768), (4096, 200, 256)])
+def test_gemm_f32_bf16mma(mnk):
+    """CRNN_F32_BF16MMA (the attention decoder's training GEMMs): fp32 operands rounded to bf16 while staged,
+    bf16 MFMA, fp32 accumulation and fp32 output, for nt (bias, overwrite / accumulate), nn and tn — vs torch
+    fp32 on the bf16-rounded operands (the same products, only the summation order differs): rel 1e-5"""
+    L = _L()
+    M, N, K = mnk
+    g = torch.Generator().manual_seed(31)
+    A = torch.randn(M, K, generator=g)
+    Bm = torch.randn(N, K, generator=g)
+    bias = torch.randn(N, generator=g)
+    r = lambda t: t.to(torch.bfloat16).float()  # noqa: E731
+    st = L.stream_ptr()
+    Ad, Bd = A.to(DEV), Bm.to(DEV)
+    C = torch.full((M, N), 2.0, device=DEV)
+    L.call("crnn_gemm_nt", L.F32_BF16MMA, Ad.data_ptr(), K, Bd.data_ptr(), K, C.data_ptr(), N, bias.to(DEV).data_ptr(),
+           M, N, K, 1, 1, st)
+    assert relerr(C.cpu(), 2.0 + r(A) @ r(Bm).t() + bias) < 1e-5
+    if N % 8 == 0:
+        Bk = torch.randn(K, N, generator=g)
+        Bkd = Bk.to(DEV)
+        C2 = torch.empty(M, N, device=DEV)
+        L.call("crnn_gemm_nn", L.F32_BF16MMA, Ad.data_ptr(), K, Bkd.data_ptr(), N, C2.data_ptr(), N, M, N, K, 1, 0,
+               st)
+        assert relerr(C2.cpu(), r(A) @ r(Bk)) < 1e-5
+    if M % 8 == 0 and N % 8 == 0:
+        At = torch.randn(K, M, generator=g)
+        Bt = torch.randn(K, N, generator=g)
+        Atd, Btd = At.to(DEV), Bt.to(DEV)
+        C3 = torch.full((M, N), 3.0, device=DEV)
+        L.call("crnn_gemm_tn", L.F32_BF16MMA, Atd.data_ptr(), M, Btd.data_ptr(), N, C3.data_ptr(), N, M, N, K, 1, st)
+        assert relerr(C3.cpu(), 3.0 + r(At).t() @ r(Bt)) < 1e-5
+    torch.cuda.synchronize()
+
+
 def _pack_lstm(w_ih, w_hh, b_ih, b_hh, H, dtype, L):
     from crnn_hip.engine import gate_perm
     perm = torch.tensor(gate_perm(H))

@@ -208,14 +208,15 @@ def test_inference_bf16_b256_bench_selection():
     assert got == O.greedy_decode(hip_lg.numpy())
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_long_line_config4_end_to_end(dtype):
+@pytest.mark.parametrize("dtype,B", [(torch.float32, 16), (torch.bfloat16, 16), (torch.float32, 64),
+                                     (torch.bfloat16, 64)])
+def test_long_line_config4_end_to_end(dtype, B):
     """BASELINE configs[4] shapes on the HIP path: 4 x 768 BiLSTM (model/model.py:151-163 stacked,
-    SURVEY D4) on 32x1024 crops (T = 128), B = 16 (persistent BiLSTM in bf16), train-mode forward +
-    CTC + backward. fp32: logits within 1e-3 of the oracle, identical greedy strings, loss to 1e-4;
-    bf16: within the bf16-storage bar."""
+    SURVEY D4) on 32x1024 crops (T = 128), B = 16 and the configuration's own B = 64 per GPU (persistent
+    BiLSTM in bf16), train-mode forward + CTC + backward. fp32: logits within 1e-3 of the oracle, identical
+    greedy strings, loss to 1e-4; bf16: within the bf16-storage bar."""
     from crnn_hip.ctc import ctc_loss
-    B, H, W, hid, nl = 16, 32, 1024, 768, 4
+    H, W, hid, nl = 32, 1024, 768, 4
     sd = recipe_state_dict(O.param_shapes(hid, C, nl), 47, head_gain=HEAD_GAIN)
     x, _, tg, tl = synthetic_batch(B, H, W, W // 8, C, seed=48)
     m = hip_model(sd, hid, dtype, nl).train()

@@ -240,7 +240,7 @@ def test_refmodel3_fp32_reproduces_reference_strings(refmodel3):
     assert acc == ref_acc
 
 
-REFMODEL3_BF16_AGREEMENT = 0.99   # bound on the bf16 string agreement (measured value there)
+REFMODEL3_BF16_AGREEMENT = 0.999  # bound on the bf16 string agreement (measured value there)
 
 
 def test_refmodel3_bf16_accuracy_and_agreement(refmodel3):

@@ -1,5 +1,7 @@
 """In-process A/B of the persistent BiLSTM sweeps under crnn_set_option variants (interleaved rounds).
-    python tools/lstm_ab.py KEY=V0,V1[,...] [B T H]"""
+    python tools/lstm_ab.py KEY=V0,V1[,...] [B T H]
+    LSTM_AB_COLD=1: each timed launch alone, after a 1 GiB scratch write (weights, x-gates and workspace out of
+    L2 / MALL, as inside the train step) — the per-launch time then includes the cold prologue."""
 import os
 import sys
 
@@ -32,12 +34,26 @@ def main():
                               dg.data_ptr(), ws.data_ptr(), B, T, H, st),
     }
     res = {}
+    cold = os.environ.get("LSTM_AB_COLD") == "1"
+    scratch = torch.empty(1 << 28, device=dev) if cold else None
     for rnd in range(3):
         for v in vals:
             L.call("crnn_set_option", key, v)
             for name, fn in fns.items():
                 for _ in range(3):
                     fn()
+                if cold:
+                    ts = []
+                    for _ in range(10):
+                        scratch.fill_(float(rnd))
+                        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                        e0.record()
+                        fn()
+                        e1.record()
+                        torch.cuda.synchronize()
+                        ts.append(e0.elapsed_time(e1) * 1e3 / T)
+                    res.setdefault((name, v), []).append(sorted(ts)[len(ts) // 2])
+                    continue
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 for _ in range(20):
@@ -47,7 +63,7 @@ def main():
                 res.setdefault((name, v), []).append(e0.elapsed_time(e1) / 20 * 1e3 / T)
     L.call("crnn_set_option", key, vals[0])
     for (name, v), xs in sorted(res.items()):
-        print(f"B={B} T={T} H={H} {name} opt{key}={v}: us/step median {sorted(xs)[len(xs) // 2]:.3f} "
+        print(f"B={B} T={T} H={H} {'cold ' if cold else ''}{name} opt{key}={v}: us/step median {sorted(xs)[len(xs) // 2]:.3f} "
               f"(rounds {', '.join(f'{x:.3f}' for x in xs)})")
 
 

@@ -1,7 +1,9 @@
 """Phase timing of the persistent BiLSTM kernels (lstm_seq.hip) from in-kernel s_memrealtime
 stamps (10 ns ticks). Prints per-phase medians and the hand-off latency (last producer's signal of
 step s-1 -> consumer past its wait at step s), for every workgroup tile (CRNN_OPT_LSTM_TILE) the
-shape supports, in one process.   python tools/lstm_stamps.py [B T H]"""
+shape supports, in one process.   python tools/lstm_stamps.py [B T H]
+STAMPS_COLD=1: the stamped launch runs after a 1 GiB scratch write (weights, x-gates and ring out of L2 / MALL,
+as inside the train step)."""
 import ctypes
 import os
 import sys
@@ -57,8 +59,17 @@ def run(kind, B, T, H, save=True):
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) / 10 * 1e3
     L.call("crnn_lstm_seq_debug_stamps", stamps.data_ptr())
+    cold = os.environ.get("STAMPS_COLD") == "1"
+    if cold:
+        scratch = torch.empty(1 << 28, device=dev)
+        scratch.fill_(1.0)
+        torch.cuda.synchronize()
+    e0.record()
     fn()
+    e1.record()
     torch.cuda.synchronize()
+    if cold:
+        print(f"  (stamped launch after a 1 GiB scratch write: {e0.elapsed_time(e1) * 1e3:.1f} us)")
     L.call("crnn_lstm_seq_debug_stamps", None)
     s = stamps.view(grid, T, 8).cpu().numpy().astype(np.int64)
     ho = {0: "counter", 1: "granule", 2: "unit-complete", 3: "unit-complete 8w"}.get(HANDOFF, str(HANDOFF))
