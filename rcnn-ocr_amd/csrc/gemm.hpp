@@ -62,7 +62,7 @@ template <class E> struct EpiPair {
   __device__ __forceinline__ void stats(int r, int n, f32x4 s, f32x4 q) const { a.stats(r, n, s, q); }
 };
 
-constexpr int BK = 32;  // K per MFMA sub-step; a pipeline stage holds KS = 32 or 64
+constexpr int BK = 32;  // K per MFMA sub-step; a pipeline stage holds KS = 32 or 64 (128 / 256: linear.hip run_mix)
 constexpr int NT = 256;
 
 // K-contiguous tiles: bf16 rows are unpadded (KS elements) with the 16-byte chunks XOR-swizzled
@@ -73,7 +73,7 @@ template <typename T, int KS = BK> constexpr int kpitch() { return sizeof(T) == 
 // physical 16-byte chunk of logical chunk c in row r (bf16 K-contiguous tiles)
 template <typename T, int KS> __device__ __forceinline__ int swz(int r, int c) {
   if constexpr (sizeof(T) != 2) return c;
-  else if constexpr (KS == 64) return c ^ ((r >> 1) & 7);
+  else if constexpr (KS >= 64) return c ^ ((r >> 1) & 7);
   else {
     const int q = (r >> 2) & 3;
     return c ^ (q == 1 ? 3 : (q == 3 ? 1 : q));  // h = {0,3,2,1}

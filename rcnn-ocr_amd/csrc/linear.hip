@@ -17,9 +17,9 @@ template <typename T, bool ROW8 = false> struct OutEpi {
   void* c;
   int ldc, M, N, c_f32, accumulate, atomic;
   const float* bias;
-  __device__ __forceinline__ void store(int m, int n, f32x4 v, int) const {
+  __device__ __forceinline__ void store(int m, int n, f32x4 v, int kz) const {
     if (m >= M || n >= N) return;
-    if (bias) {
+    if (bias && (!atomic || kz == 0)) {   // split-K partials: the bias once, with the first K split
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[r] += (n + r < N) ? bias[n + r] : 0.f;
     }
@@ -154,20 +154,33 @@ int gemm_tn_t(const void* A, int lda, const void* B, int ldb, float* C, int ldc,
 
 // CRNN_F32_BF16MMA: fp32 operands in memory, staged as bf16 (gemm::Bf16Of), bf16 MFMA, fp32 accumulation and
 // fp32 output — the attention decoder's training GEMMs (the reference's fp16 autocast, training/train.py:499)
+// The decoder's per-step products are small (M = batch: 256 x 1280 x 1024 and 256 x 1024 x 1280 per step): one
+// K-serial tile per workgroup, and the fp32 operands cost twice the bytes of bf16 ones. Measured on the MI355X
+// (profiles/r06/r06w_gemm_mix_plans.log, us for nn / nt): 32 x 32 tiles with 128-deep stages 12.4 / 12.9, the same
+// with 64-deep stages 13.5 / 15.5, 256-deep 15.4 / 12.4, 64 x 64 x 128 13.8 / 13.6, 64 x 64 x 256 12.7 / 12.8;
+// split-K with fp32 atomics ~20 (and not bit-reproducible); bf16 operands on the LDS-DMA kernels 8.0 / 7.5;
+// hipBLASLt bf16 19.1 / 19.8. The 256^3 products stay on the default plan (~4 us, launch-bound).
+template <class LA, class LB>
+int run_mix(const LA& la, const LB& lb, void* C, int ldc, const float* bias, int M, int N, int K, int acc,
+            hipStream_t st) {
+  const OutEpi<bf16> ep{C, ldc, M, N, 1, acc, 0, bias};
+  const long t64 = (long)((M + 63) / 64) * ((N + 63) / 64);
+  if (t64 >= 2 * crnn_cu_count() || K < 512) return run<bf16, false>(la, lb, ep, M, N, K, 1, st);
+  return launch<bf16, 32, 32, 128>(la, lb, ep, M, N, K, 1, st);
+}
+
 int gemm_nt_mix(const void* A, int lda, const void* B, int ldb, void* C, int ldc, const float* bias, int M, int N,
                 int K, int acc, hipStream_t st) {
   Bf16Of<RowMajorK<float>> la{RowMajorK<float>{(const float*)A, lda, M, K}};
   Bf16Of<RowMajorK<float>> lb{RowMajorK<float>{(const float*)B, ldb, N, K}};
-  OutEpi<bf16> ep{C, ldc, M, N, 1, acc, 0, bias};
-  return run<bf16, false>(la, lb, ep, M, N, K, 1, st);
+  return run_mix(la, lb, C, ldc, bias, M, N, K, acc, st);
 }
 
 int gemm_nn_mix(const void* A, int lda, const void* B, int ldb, void* C, int ldc, int M, int N, int K, int acc,
                 hipStream_t st) {
   Bf16Of<RowMajorK<float>> la{RowMajorK<float>{(const float*)A, lda, M, K}};
   Bf16Of<ColMajorK<float>> lb{ColMajorK<float>{(const float*)B, ldb, N, K}};
-  OutEpi<bf16> ep{C, ldc, M, N, 1, acc, 0, nullptr};
-  return run<bf16, false>(la, lb, ep, M, N, K, 1, st);
+  return run_mix(la, lb, C, ldc, nullptr, M, N, K, acc, st);
 }
 
 int gemm_tn_mix(const void* A, int lda, const void* B, int ldb, float* C, int ldc, int M, int N, int K, int acc,

@@ -945,7 +945,8 @@ def test_gemm_nt_nn_tn(mnk, dtype):
             assert relerr(C4.cpu(), 2 * (At.t() @ Bt)) < tol
 
 
-@pytest.mark.parametrize("mnk", [(37, 48, 64), (1536, 256, 512), (48, 1024, 768), (4096, 200, 256)])
+@pytest.mark.parametrize("mnk", [(37, 48, 64), (1536, 256, 512), (48, 1024, 768), (4096, 200, 256), (256, 1280, 1024),
+                                 (256, 1024, 1280), (8192, 256, 1024)])
 def test_gemm_f32_bf16mma(mnk):
     """CRNN_F32_BF16MMA (the attention decoder's training GEMMs): fp32 operands rounded to bf16 while staged,
     bf16 MFMA, fp32 accumulation and fp32 output, for nt (bias, overwrite / accumulate), nn and tn — vs torch
