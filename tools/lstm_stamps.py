@@ -118,6 +118,17 @@ if __name__ == "__main__":
                 run("fwd", B, T, H)
         run("bwd", B, T, H)
         sys.exit(0)
+    if os.environ.get("STAMPS_BWD_FORMS"):
+        # the BPTT under CRNN_OPT_LSTM_BWD_PART values (0: counter form, 1: partial-sum form; phases of form 1:
+        # waited = partials gathered, mfma+part = cell done, reduced = past the barrier, epilogue = partial tiles
+        # multiplied and published)
+        for _ in range(2):
+            for v in (int(x) for x in os.environ["STAMPS_BWD_FORMS"].split(",")):
+                L.call("crnn_set_option", L.OPT_LSTM_BWD_PART, v)
+                print(f"BPTT form CRNN_OPT_LSTM_BWD_PART={v}")
+                run("bwd", B, T, H)
+        L.call("crnn_set_option", L.OPT_LSTM_BWD_PART, 0)
+        sys.exit(0)
     if os.environ.get("STAMPS_SAVE_AB"):
         # default tile and hand-off: saved-forward stores on / off (the BPTT operands' cost per step),
         # then the default BPTT
