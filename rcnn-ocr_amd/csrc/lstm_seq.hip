@@ -439,17 +439,21 @@ __global__ __launch_bounds__(64 * W) void lstm_seq_fwd_uc_kernel(const bf16* __r
     const int t = d == 0 ? s : Tn - 1 - s;
     const int buf = s & 1;
     bool ok = true;
-    // accumulators start at the x-gate rows (the recurrent product accumulates onto them), which frees xv
-    // for the next step's rows as soon as this step's hand-off has arrived
+    // accumulators start at the x-gate rows (the recurrent product accumulates onto them), initialised once the
+    // hand-off has arrived (the rows' load then never holds up the poll's start; before the poll the step measured
+    // 4.22-4.27 us inside the train step, after it 4.03, profiles/r06/r06u1_uc_variants_ab.log), which frees xv
+    // for the next step's rows
     f32x4 acc[MI][NT];
+    auto init_acc = [&]() {
 #pragma unroll
-    for (int i = 0; i < MI; ++i)
+      for (int i = 0; i < MI; ++i)
 #pragma unroll
-      for (int jt = 0; jt < NT; ++jt) {
-        const bf16x8& x8 = xv[i][jt >> 1];
-        const int o = (jt & 1) * 4;
-        acc[i][jt] = f32x4{(float)x8[o], (float)x8[o + 1], (float)x8[o + 2], (float)x8[o + 3]};
-      }
+        for (int jt = 0; jt < NT; ++jt) {
+          const bf16x8& x8 = xv[i][jt >> 1];
+          const int o = (jt & 1) * 4;
+          acc[i][jt] = f32x4{(float)x8[o], (float)x8[o + 1], (float)x8[o + 2], (float)x8[o + 3]};
+        }
+    };
     const int tn = s + 1 < Tn ? (d == 0 ? t + 1 : t - 1) : t;
     bf16 hh[MI][NT];
     f32x4 gq[MI][NT];
@@ -500,6 +504,7 @@ __global__ __launch_bounds__(64 * W) void lstm_seq_fwd_uc_kernel(const bf16* __r
         __builtin_amdgcn_s_sleep(1);
       }
       SEQ_STAMP(1);
+      init_acc();
 #pragma unroll
       for (int kq = 0; kq < KQ; ++kq)
 #pragma unroll
@@ -564,6 +569,7 @@ __global__ __launch_bounds__(64 * W) void lstm_seq_fwd_uc_kernel(const bf16* __r
           for (int jt = 0; jt < NT; ++jt) cell(i, jt);
       }
     } else {
+      init_acc();
       load_xg(tn);
 #pragma unroll
       for (int i = 0; i < MI; ++i)

@@ -41,7 +41,7 @@ def main():
                 e1.record()
                 torch.cuda.synchronize()
                 res.setdefault((form, save), []).append(e0.elapsed_time(e1) / 20 * 1e3 / T)
-    L.call("crnn_set_option", L.OPT_LSTM_HANDOFF, 1)   # the default
+    L.call("crnn_set_option", L.OPT_LSTM_HANDOFF, 3)   # the default
     for (form, save), xs in sorted(res.items()):
         print(f"B={B} T={T} H={H} form {form} {'saved stores' if save else 'no saved stores'}: us/step median "
               f"{sorted(xs)[len(xs) // 2]:.3f} ({', '.join(f'{x:.3f}' for x in xs)})")

@@ -54,7 +54,7 @@ def main():
         outs[form] = (hseq.float().cpu(), gsv.float().cpu(), csv.cpu())
         print(f"form {form}: err word {e}, counters min {cnt} (want {H // U.value * T}), finite "
               f"{all(torch.isfinite(x).all().item() for x in outs[form])}", flush=True)
-    L.call("crnn_set_option", L.OPT_LSTM_HANDOFF, 1)   # the default
+    L.call("crnn_set_option", L.OPT_LSTM_HANDOFF, 3)   # the default
     ref = host_ref(xg, whh, B, T, H)
     for form, (h, gs, cs) in outs.items():
         a = outs[min(outs)]

@@ -143,4 +143,4 @@ if __name__ == "__main__":
             run("fwd", B, T, H)
         run("bwd", B, T, H)
     L.call("crnn_set_option", L.OPT_LSTM_TILE, 0)
-    L.call("crnn_set_option", L.OPT_LSTM_HANDOFF, 1)   # the default
+    L.call("crnn_set_option", L.OPT_LSTM_HANDOFF, 3)   # the default
