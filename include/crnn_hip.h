@@ -469,6 +469,11 @@ int crnn_lstm_seq_bwd(const void* dhseq, const void* whh_t, const void* gsv, con
 int crnn_attn_context(const float* projH, const float* projh, const float* score, const float* enc, float* ctx,
                       int ldc, float* alpha, int B, int T, int H, int C, float drop_p, unsigned long long seed,
                       void* stream);
+/* the same with proj_H and enc stored as bf16 (the bf16 training pass, AttnDecoderHIP(train_bf16=True): the
+ * reference's fp16 autocast runs this attention on fp16 tensors, training/train.py:499-505); fp32 arithmetic */
+int crnn_attn_context_bf16(const void* projH, const float* projh, const float* score, const void* enc, float* ctx,
+                           int ldc, float* alpha, int B, int T, int H, int C, float drop_p, unsigned long long seed,
+                           void* stream);
 int crnn_attn_cell(const float* gates, const float* b_ih, const float* b_hh, const float* w_ih, int ldw, const int* ch,
                    int ch_stride, float* h, float* c, float* hx, int ldx, float* hs, int ld_hs, float* gact, float* cs,
                    int B, int H, int C, void* stream);
@@ -486,6 +491,10 @@ int crnn_attn_cell_bwd(const float* gact, const float* c_t, const float* c_prev,
 int crnn_attn_bwd(const float* dctx, int lddc, const float* alpha, const float* enc, const float* projH,
                   const float* projh, const float* score, float* de, float* dprojh, float* dscore_part, int B, int T,
                   int H, int C, float drop_p, unsigned long long seed, void* stream);
+/* the same with enc and proj_H stored as bf16 (pairs with crnn_attn_context_bf16) */
+int crnn_attn_bwd_bf16(const float* dctx, int lddc, const float* alpha, const void* enc, const void* projH,
+                       const float* projh, const float* score, float* de, float* dprojh, float* dscore_part, int B,
+                       int T, int H, int C, float drop_p, unsigned long long seed, void* stream);
 /* after the step loop: denc[b][t'][c] = sum_t alpha'_t[b][t'] dctx_t[b][c] (written; dctx rows
  * [steps][B] of stride lddc, alpha [steps][B][T], step t's mask from seed + t) */
 int crnn_attn_denc(const float* dctx, int lddc, const float* alpha, int steps, int B, int T, int C, float drop_p,

@@ -140,9 +140,11 @@ _SIGS = {
     "crnn_lstm_wgrad": ([vp, vp, vp, vp, vp, vp, vp, vp, sz, i32, i32, i32, i32, i32, vp], i32),
     "crnn_lstm_dx": ([i32, vp, vp, vp, i32, i32, i32, i32, vp], i32),
     "crnn_attn_context": ([vp, vp, vp, vp, vp, i32, vp, i32, i32, i32, i32, f32, u64, vp], i32),
+    "crnn_attn_context_bf16": ([vp, vp, vp, vp, vp, i32, vp, i32, i32, i32, i32, f32, u64, vp], i32),
     "crnn_attn_cell": ([vp, vp, vp, vp, i32, vp, i32, vp, vp, vp, i32, vp, i32, vp, vp, i32, i32, i32, vp], i32),
     "crnn_attn_cell_bwd": ([vp, vp, vp, vp, i32, vp, i32, vp, vp, vp, i32, i32, vp], i32),
     "crnn_attn_bwd": ([vp, i32, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, f32, u64, vp], i32),
+    "crnn_attn_bwd_bf16": ([vp, i32, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, f32, u64, vp], i32),
     "crnn_attn_denc": ([vp, i32, vp, i32, i32, i32, i32, f32, u64, vp, vp], i32),
     "crnn_attn_dproj_enc": ([vp, vp, vp, vp, i32, i32, i32, i32, vp, vp], i32),
     "crnn_attn_onehot_rows": ([vp, i32, i32, i32, i32, vp, i32, i32, vp], i32),

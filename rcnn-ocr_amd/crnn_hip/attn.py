@@ -63,11 +63,30 @@ class AttnDecoderHIP:
         call("crnn_gemm_nt", L.F32 if dt is None else dt, ptr(a), lda, ptr(w), ldw, ptr(out), ldo, ptr(bias), M, N, K,
              1, 0, L.stream_ptr())
 
+    def _bf16(self, x: torch.Tensor) -> torch.Tensor:
+        """bf16 copy of a contiguous fp32 tensor (crnn_cast_f32)"""
+        out = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device)
+        call("crnn_cast_f32", L.BF16, ptr(x), ptr(out), x.numel(), L.stream_ptr())
+        return out
+
+    def _tn(self, A, lda, Bm, ldb, C, ldc, M, N, K, bf=None):
+        """C (fp32) = A^T B over K rows. Training with train_bf16: bf16 operands (bf = their bf16 copies) through the
+        deterministic split-K slab GEMM (crnn_gemm_tn_slab, fp32 accumulation); else crnn_gemm_tn in fp32."""
+        s = L.stream_ptr()
+        if bf is None:
+            call("crnn_gemm_tn", L.F32, ptr(A), lda, ptr(Bm), ldb, ptr(C), ldc, M, N, K, 0, s)
+            return
+        need = L.lib().crnn_gemm_tn_workspace(M, N, K)
+        ws = torch.empty(need // 4 + 4, device=C.device)
+        call("crnn_gemm_tn_slab", bf[0], lda, bf[1], ldb, ptr(C), ldc, M, N, K, 0, ptr(ws), ws.numel() * 4, s)
+
     def run_train(self, enc: torch.Tensor, steps: int, text: torch.Tensor, drop_p: float = 0.0,
                   seed: int = 0) -> torch.Tensor:
         """teacher-forced forward that saves what backward() needs -> logits [B, steps, V].
         drop_p: the training-mode F.dropout on the attention weights (model/model.py:38; the
         reference's RCNN uses 0.1); step t's mask comes from the counter hash with seed + t."""
+        mix = self.tdt == L.F32_BF16MMA
+        enc_in = enc
         enc = enc.to(self.device, torch.float32).contiguous()
         B, T, C = enc.shape
         H, V, Vp, dev = self.H, self.V, self.Vpad, self.device
@@ -77,6 +96,10 @@ class AttnDecoderHIP:
             raise ValueError("text needs batch_max_length + 1 columns")
         projH = torch.empty(B * T, H, device=dev)
         self._gemm(enc, C, self.w_i2h, C, projH, H, None, B * T, H, C, self.tdt)
+        encb = projHb = None
+        if mix:   # the attention reads enc and proj_H as bf16 every step (crnn_attn_context_bf16)
+            encb = (enc_in.to(dev).contiguous() if enc_in.dtype == torch.bfloat16 else self._bf16(enc))
+            projHb = self._bf16(projH)
         LX = C + H + Vp                                     # [context_t | h_{t-1} | onehot(text_t)] per step
         Xs = torch.zeros(steps + 1, B, LX, device=dev)
         call("crnn_attn_onehot_rows", ptr(txt), txt.shape[1], steps, B, V, ptr(Xs), LX, C + H, s)
@@ -90,8 +113,12 @@ class AttnDecoderHIP:
         gates = torch.empty(B, 4 * H, device=dev)
         for t in range(steps):
             self._gemm(h, H, self.w_h2h, H, Ph[t], H, self.b_h2h, B, H, H, self.tdt)
-            call("crnn_attn_context", ptr(projH), ptr(Ph[t]), ptr(self.score), ptr(enc), ptr(Xs[t]), LX,
-                 ptr(As[t]), B, T, H, C, drop_p, (seed + t) & (2 ** 64 - 1), s)
+            if mix:
+                call("crnn_attn_context_bf16", ptr(projHb), ptr(Ph[t]), ptr(self.score), ptr(encb), ptr(Xs[t]), LX,
+                     ptr(As[t]), B, T, H, C, drop_p, (seed + t) & (2 ** 64 - 1), s)
+            else:
+                call("crnn_attn_context", ptr(projH), ptr(Ph[t]), ptr(self.score), ptr(enc), ptr(Xs[t]), LX,
+                     ptr(As[t]), B, T, H, C, drop_p, (seed + t) & (2 ** 64 - 1), s)
             self._gemm(Xs[t], LX, self.w_cat, C + H, gates, 4 * H, None, B, 4 * H, C + H, self.tdt)
             call("crnn_attn_cell", ptr(gates), ptr(self.b_ih), ptr(self.b_hh), ptr(self.w_ih), C + V, ptr(txt[:, t:]),
                  txt.shape[1], ptr(h), ptr(c), ptr(Xs[t + 1]), LX, ptr(hs[:, t]), steps * H, ptr(Gs[t]), ptr(Cs[t]),
@@ -101,7 +128,7 @@ class AttnDecoderHIP:
         out = torch.empty(B, steps, V, device=dev)
         scratch = torch.empty(B * steps, dtype=torch.int32, device=dev)
         call("crnn_attn_out", ptr(lg), Vp, B * steps, V, self.blank, ptr(out), V, ptr(scratch), s)
-        self._saved = dict(enc=enc, projH=projH, Xs=Xs, Gs=Gs, Cs=Cs, Ph=Ph, As=As, hs=hs, txt=txt, steps=steps,
+        self._saved = dict(enc=enc, encb=encb, projH=projH, projHb=projHb, Xs=Xs, Gs=Gs, Cs=Cs, Ph=Ph, As=As, hs=hs, txt=txt, steps=steps,
                            drop=(drop_p, seed))
         return out
 
@@ -124,8 +151,13 @@ class AttnDecoderHIP:
             dL[:, self.blank] = 0.0   # the masked column is a constant (model/model.py:87-89)
         dHs = torch.empty(B * steps, H, device=dev)
         call("crnn_gemm_nn", F32, ptr(dL), Vp, ptr(self.w_gen), H, ptr(dHs), H, B * steps, H, Vp, 1, 0, s)
+        mix = F32 == L.F32_BF16MMA
+        bfp = (lambda *xs: tuple(ptr(x) for x in xs)) if mix else (lambda *xs: None)  # noqa: E731
+        keep = []   # bf16 copies live until the stream has used them
+        if mix:
+            keep += [self._bf16(dL), self._bf16(hs)]
         gw = torch.empty(Vp, H, device=dev)
-        call("crnn_gemm_tn", F32, ptr(dL), Vp, ptr(hs), H, ptr(gw), H, Vp, H, B * steps, 0, s)
+        self._tn(dL, Vp, hs, H, gw, H, Vp, H, B * steps, bfp(*keep[-2:]) if mix else None)
         gb = torch.empty(Vp, device=dev)
         call("crnn_colsum", L.F32, ptr(dL), Vp, B * steps, Vp, ptr(gb), 0, 1, s)
         dG = torch.empty(steps, B, 4 * H, device=dev)
@@ -141,8 +173,13 @@ class AttnDecoderHIP:
             dc.reverse()
             call("crnn_gemm_nn", F32, ptr(dG[t]), 4 * H, ptr(self.w_cat), C + H, ptr(dX[t]), C + H, B, C + H, 4 * H, 1,
                  0, s)
-            call("crnn_attn_bwd", ptr(dX[t]), C + H, ptr(As[t]), ptr(enc), ptr(projH), ptr(Ph[t]), ptr(self.score),
-                 ptr(De[t]), ptr(dPh[t]), ptr(dscore), B, T, H, C, drop_p, (seed + t) & (2 ** 64 - 1), s)
+            if mix:
+                call("crnn_attn_bwd_bf16", ptr(dX[t]), C + H, ptr(As[t]), ptr(sv["encb"]), ptr(sv["projHb"]), ptr(Ph[t]),
+                     ptr(self.score), ptr(De[t]), ptr(dPh[t]), ptr(dscore), B, T, H, C, drop_p,
+                     (seed + t) & (2 ** 64 - 1), s)
+            else:
+                call("crnn_attn_bwd", ptr(dX[t]), C + H, ptr(As[t]), ptr(enc), ptr(projH), ptr(Ph[t]), ptr(self.score),
+                     ptr(De[t]), ptr(dPh[t]), ptr(dscore), B, T, H, C, drop_p, (seed + t) & (2 ** 64 - 1), s)
             # dh_{t-1} = d(h part of [context | h]) + dproj_h W_h2h   (accumulated into dX[t][:, C:])
             call("crnn_gemm_nn", F32, ptr(dPh[t]), H, ptr(self.w_h2h), H, ptr(dX[t][:, C:]), C + H, B, H, H, 1, 1, s)
             dh_rec, ld_rec = dX[t][:, C:], C + H
@@ -155,16 +192,21 @@ class AttnDecoderHIP:
         # [dW_ih[:, :C] | dW_hh | dW_ih[:, C:]] in one GEMM over the saved [context | h | onehot] rows
         LX = C + H + Vp
         wfull = torch.empty(4 * H, LX, device=dev)
-        call("crnn_gemm_tn", F32, ptr(dG), 4 * H, ptr(Xs), LX, ptr(wfull), LX, 4 * H, LX, steps * B, 0, s)
+        if mix:
+            keep += [self._bf16(dG), self._bf16(Xs[:steps]), self._bf16(dPh), self._bf16(dProjH)]
+            dGb, Xsb, dPhb, dPjb = keep[-4:]
+            encb = sv["encb"]
+        self._tn(dG, 4 * H, Xs, LX, wfull, LX, 4 * H, LX, steps * B, bfp(dGb, Xsb) if mix else None)
         dwih = torch.cat([wfull[:, :C], wfull[:, C + H:C + H + V]], 1)
         db = torch.empty(4 * H, device=dev)
         call("crnn_colsum", L.F32, ptr(dG), 4 * H, steps * B, 4 * H, ptr(db), 0, 1, s)
         wh2h = torch.empty(H, H, device=dev)
-        call("crnn_gemm_tn", F32, ptr(dPh), H, ptr(Xs[:, :, C:]), LX, ptr(wh2h), H, H, H, steps * B, 0, s)
+        self._tn(dPh, H, Xs[:, :, C:], LX, wh2h, H, H, H, steps * B,
+                 (ptr(dPhb), ptr(Xsb) + 2 * C) if mix else None)
         bh2h = torch.empty(H, device=dev)
         call("crnn_colsum", L.F32, ptr(dPh), H, steps * B, H, ptr(bh2h), 0, 1, s)
         wi2h = torch.empty(H, C, device=dev)
-        call("crnn_gemm_tn", F32, ptr(dProjH), H, ptr(enc), C, ptr(wi2h), C, H, C, B * T, 0, s)
+        self._tn(dProjH, H, enc, C, wi2h, C, H, C, B * T, bfp(dPjb, encb) if mix else None)
         call("crnn_gemm_nn", F32, ptr(dProjH), H, ptr(self.w_i2h), C, ptr(denc), C, B * T, C, H, 1, 1, s)
         dsc = torch.empty(H, device=dev)
         call("crnn_colsum", L.F32, ptr(dscore), H, B, H, ptr(dsc), 0, 1, s)

@@ -14,31 +14,61 @@
 
 namespace {
 
+__device__ __forceinline__ float ldf(const float* p) { return *p; }
+__device__ __forceinline__ float ldf(const bf16* p) { return (float)*p; }
+// the attention's tanh: libm's for the fp32 parity path, the exp / rcp form (tanh_fast, common.hpp) when the operands
+// are bf16 (its ~1e-7 error is far below their 2^-9 rounding)
+template <typename TE> __device__ __forceinline__ float att_tanh(float x) {
+  if constexpr (sizeof(TE) == 2) return tanh_fast(x);
+  else return tanhf(x);
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
   return v;
 }
+// the same sum without LDS round trips: DPP within each 16-lane row, then the four row sums read into a scalar
+// (the per-step attention kernels; __shfl_xor is a ds_bpermute per level)
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+  v = rowgroup_sum<16>(v);
+  const int i = __float_as_int(v);
+  return (__int_as_float(__builtin_amdgcn_readlane(i, 0)) + __int_as_float(__builtin_amdgcn_readlane(i, 16))) +
+         (__int_as_float(__builtin_amdgcn_readlane(i, 32)) + __int_as_float(__builtin_amdgcn_readlane(i, 48)));
+}
 
-// block (1024 threads) per sample: e[t] (wave per t), softmax over t, context over c (4 groups of
-// t per channel, combined in LDS in fixed order)
+// block (1024 threads) per sample: e[t] (wave per t), softmax over t, then context with a thread per channel c
+// summing over t from registers. The first 32 enc rows of every thread's channel are loaded before the scores, so
+// their round trip hides under the score and softmax phases (the r05 form loaded them after, 4 channel groups in
+// turn, 15 us per step at B = 256, T = 32, C = 1024). Loads use clamped indices and masked values (a load under
+// a runtime condition costs a branch and a full vmcnt wait).
 constexpr int ATT_NT = 1024;
-__global__ __launch_bounds__(ATT_NT) void attn_context_kernel(const float* __restrict__ projH,
+constexpr int ATT_TC = 32;   // enc rows per register pass
+// TE: how proj_H and enc are stored (fp32, or bf16 for the bf16 training pass: crnn_attn_context_bf16)
+template <typename TE>
+__global__ __launch_bounds__(ATT_NT) void attn_context_kernel(const TE* __restrict__ projH,
                                                               const float* __restrict__ projh,
                                                               const float* __restrict__ score,
-                                                              const float* __restrict__ enc, float* __restrict__ ctx,
+                                                              const TE* __restrict__ enc, float* __restrict__ ctx,
                                                               int ldc, float* __restrict__ alpha_out, int T, int H,
                                                               int C, uint32_t thr, float scale,
                                                               unsigned long long seed) {
   extern __shared__ float sm[];  // [T] scores -> weights (after the training-mode dropout)
-  __shared__ float red[4][256];
-  const int b = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int b = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6, tid = threadIdx.x;
+  const TE* eb = enc + (size_t)b * T * C;
+  float ev[ATT_TC];
+  {
+    const int cc = min(tid, C - 1);
+#pragma unroll
+    for (int u = 0; u < ATT_TC; ++u) ev[u] = ldf(eb + (size_t)min(u, T - 1) * C + cc);
+  }
   const float* ph = projh + (size_t)b * H;
   for (int t = w; t < T; t += ATT_NT / 64) {
-    const float* pH = projH + ((size_t)b * T + t) * H;
+    const TE* pH = projH + ((size_t)b * T + t) * H;
     float s = 0.f;
-    for (int k = lane; k < H; k += 64) s += score[k] * tanhf(pH[k] + ph[k]);
-    s = wave_sum(s);
+#pragma unroll 4
+    for (int k = lane; k < H; k += 64) s += score[k] * att_tanh<TE>(ldf(pH + k) + ph[k]);
+    s = wave_sum_dpp(s);
     if (lane == 0) sm[t] = s;
   }
   __syncthreads();
@@ -49,7 +79,7 @@ __global__ __launch_bounds__(ATT_NT) void attn_context_kernel(const float* __res
     for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
     float z = 0.f;
     for (int t = lane; t < T; t += 64) z += expf(sm[t] - m);
-    z = wave_sum(z);
+    z = wave_sum_dpp(z);
     const float rz = 1.f / z;
     for (int t = lane; t < T; t += 64) {
       const float a = expf(sm[t] - m) * rz;
@@ -59,17 +89,18 @@ __global__ __launch_bounds__(ATT_NT) void attn_context_kernel(const float* __res
     }
   }
   __syncthreads();
-  const float* eb = enc + (size_t)b * T * C;
-  const int cq = threadIdx.x & 255, tq = threadIdx.x >> 8;
-  for (int c0 = 0; c0 < C; c0 += 256) {
-    const int c = c0 + cq;
+  for (int c0 = 0; c0 < C; c0 += ATT_NT) {
+    const int c = c0 + tid, cc = min(c, C - 1);
     float s = 0.f;
-    if (c < C)
-      for (int t = tq; t < T; t += 4) s += sm[t] * eb[(size_t)t * C + c];
-    red[tq][cq] = s;
-    __syncthreads();
-    if (tq == 0 && c < C) ctx[(size_t)b * ldc + c] = ((red[0][cq] + red[1][cq]) + red[2][cq]) + red[3][cq];
-    __syncthreads();
+    for (int t0 = 0; t0 < T; t0 += ATT_TC) {
+      if (c0 > 0 || t0 > 0) {
+#pragma unroll
+        for (int u = 0; u < ATT_TC; ++u) ev[u] = ldf(eb + (size_t)min(t0 + u, T - 1) * C + cc);
+      }
+#pragma unroll
+      for (int u = 0; u < ATT_TC; ++u) s += (t0 + u < T ? sm[t0 + u] : 0.f) * ev[u];
+    }
+    if (c < C) ctx[(size_t)b * ldc + c] = s;
   }
 }
 
@@ -151,10 +182,11 @@ __device__ __forceinline__ float keep_scale(uint32_t thr, float scale, unsigned 
   return thr == 0u ? 1.f : (drop_hash(seed, i) >= thr ? scale : 0.f);
 }
 
+template <typename TE>
 __global__ __launch_bounds__(ATT_NT) void attn_step_bwd_kernel(const float* __restrict__ dctx, int lddc,
                                                                const float* __restrict__ alpha,
-                                                               const float* __restrict__ enc,
-                                                               const float* __restrict__ projH,
+                                                               const TE* __restrict__ enc,
+                                                               const TE* __restrict__ projH,
                                                                const float* __restrict__ projh,
                                                                const float* __restrict__ score,
                                                                float* __restrict__ de_out, float* __restrict__ dprojh,
@@ -166,19 +198,53 @@ __global__ __launch_bounds__(ATT_NT) void attn_step_bwd_kernel(const float* __re
   float* de = sm + T;
   const int b = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const float* dc = dctx + (size_t)b * lddc;
-  const float* eb = enc + (size_t)b * T * C;
+  const TE* eb = enc + (size_t)b * T * C;
   const float* al = alpha + (size_t)b * T;
-  for (int t = w; t < T; t += ATT_NT / 64) {
-    float s = 0.f;
-    for (int k = lane; k < C; k += 64) s += dc[k] * eb[(size_t)t * C + k];
-    s = wave_sum(s);
-    if (lane == 0) da[t] = s * keep_scale(thr, scale, seed, (unsigned long long)b * T + t);
+  // dalpha: wave w owns t = w, w + 16, ...; per pass over 512 channels a lane holds its 8 dctx values in
+  // registers and issues the enc loads of TWO rows before any sum (clamped indices, masked values; 16 channels
+  // per lane spilled at the 128-register budget of 1024-thread blocks)
+  constexpr int KC = 8;
+  for (int k0 = 0; k0 < C; k0 += 64 * KC) {
+    float dcr[KC];
+#pragma unroll
+    for (int j = 0; j < KC; ++j) {
+      const int k = k0 + lane + 64 * j;
+      const float v = dc[min(k, C - 1)];
+      dcr[j] = k < C ? v : 0.f;
+    }
+    for (int t = w; t < T; t += 2 * (ATT_NT / 64)) {
+      const int t2 = t + ATT_NT / 64;
+      const TE* e1 = eb + (size_t)t * C;
+      const TE* e2 = eb + (size_t)min(t2, T - 1) * C;
+      float x1[KC], x2[KC];
+#pragma unroll
+      for (int j = 0; j < KC; ++j) {
+        const int k = min(k0 + lane + 64 * j, C - 1);
+        x1[j] = ldf(e1 + k);
+        x2[j] = ldf(e2 + k);
+      }
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int j = 0; j < KC; ++j) {
+        s1 += dcr[j] * x1[j];
+        s2 += dcr[j] * x2[j];
+      }
+      s1 = wave_sum_dpp(s1);
+      s2 = wave_sum_dpp(s2);
+      if (lane == 0) {
+        da[t] = (k0 > 0 ? da[t] : 0.f) + s1;
+        if (t2 < T) da[t2] = (k0 > 0 ? da[t2] : 0.f) + s2;
+      }
+    }
   }
+  __syncthreads();
+  if (w == 0)
+    for (int t = lane; t < T; t += 64) da[t] *= keep_scale(thr, scale, seed, (unsigned long long)b * T + t);
   __syncthreads();
   if (w == 0) {
     float z = 0.f;
     for (int t = lane; t < T; t += 64) z += al[t] * da[t];
-    z = wave_sum(z);
+    z = wave_sum_dpp(z);
     for (int t = lane; t < T; t += 64) {
       const float v = al[t] * (da[t] - z);
       de[t] = v;
@@ -187,15 +253,16 @@ __global__ __launch_bounds__(ATT_NT) void attn_step_bwd_kernel(const float* __re
   }
   __syncthreads();
   const float* ph = projh + (size_t)b * H;
-  const float* pH = projH + (size_t)b * T * H;
+  const TE* pH = projH + (size_t)b * T * H;
   const int kq = threadIdx.x & 255, tq = threadIdx.x >> 8;
   for (int k0 = 0; k0 < H; k0 += 256) {
     const int k = k0 + kq;
     float acc_h = 0.f, acc_s = 0.f;
     if (k < H) {
       const float pk = ph[k];
+#pragma unroll 8
       for (int t = tq; t < T; t += 4) {
-        const float th = tanhf(pH[(size_t)t * H + k] + pk);
+        const float th = att_tanh<TE>(ldf(pH + (size_t)t * H + k) + pk);
         acc_h += de[t] * (1.f - th * th);
         acc_s += de[t] * th;
       }
@@ -236,22 +303,42 @@ __global__ __launch_bounds__(256) void attn_denc_kernel(const float* __restrict_
   }
 }
 
-// thread per (b, t', k)
-__global__ void attn_dprojH_kernel(const float* __restrict__ projh, const float* __restrict__ de,
-                                   const float* __restrict__ projH, const float* __restrict__ score, int steps,
-                                   int B, int T, int H, float* __restrict__ dprojH) {
-  const long n = (long)B * T * H;
-  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) {
-    const long bt = e / H;
-    const int k = (int)(e - bt * H);
-    const int b = (int)(bt / T);
-    const float u0 = projH[e];
-    float acc = 0.f;
-    for (int t = 0; t < steps; ++t) {
-      const float th = tanhf(u0 + projh[((size_t)t * B + b) * H + k]);
-      acc += de[(size_t)t * B * T + bt] * (1.f - th * th);
+// block per (sample b, 256 k): the sample's de rows of every step staged in LDS; a thread holds proj_H[b, t', k]
+// for 32 t' in registers and loops over the steps (one proj_h load per step), summing in step order as before.
+// (The r05 form, a thread per (b, t', k) re-reading proj_h for every t', took 137 us at B = 256, T = 32.)
+__global__ __launch_bounds__(256) void attn_dprojH_kernel(const float* __restrict__ projh, const float* __restrict__ de,
+                                                          const float* __restrict__ projH,
+                                                          const float* __restrict__ score, int steps, int B, int T,
+                                                          int H, float* __restrict__ dprojH) {
+  extern __shared__ float sde[];  // [steps][T]
+  const int b = blockIdx.x, k = blockIdx.y * 256 + threadIdx.x;
+  for (int i = threadIdx.x; i < steps * T; i += 256) {
+    const int t = i / T, tp = i - t * T;
+    sde[i] = de[((size_t)t * B + b) * T + tp];
+  }
+  __syncthreads();
+  if (k >= H) return;
+  const int kc = min(k, H - 1);
+  for (int t0 = 0; t0 < T; t0 += 32) {
+    float u[32], acc[32];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+      u[j] = projH[((size_t)b * T + min(t0 + j, T - 1)) * H + kc];
+      acc[j] = 0.f;
     }
-    dprojH[e] = acc * score[k];
+    for (int t = 0; t < steps; ++t) {
+      const float p = projh[((size_t)t * B + b) * H + kc];
+      const float* d = sde + t * T + t0;
+#pragma unroll
+      for (int j = 0; j < 32; ++j) {
+        const float th = tanhf(u[j] + p);
+        acc[j] += (t0 + j < T ? d[j] : 0.f) * (1.f - th * th);
+      }
+    }
+    const float sk = score[k];
+#pragma unroll
+    for (int j = 0; j < 32; ++j)
+      if (t0 + j < T) dprojH[((size_t)b * T + t0 + j) * H + k] = acc[j] * sk;
   }
 }
 
@@ -361,8 +448,20 @@ int crnn_attn_context(const float* projH, const float* projh, const float* score
                       void* stream) {
   if (T <= 0 || T > 4096) return crnn_set_error(hipErrorInvalidValue, "attn_context: T out of range");
   if (!(drop_p >= 0.f && drop_p < 1.f)) return crnn_set_error(hipErrorInvalidValue, "attn_context: p not in [0, 1)");
-  hipLaunchKernelGGL(attn_context_kernel, dim3(B), dim3(ATT_NT), (size_t)T * sizeof(float), (hipStream_t)stream, projH,
-                     projh, score, enc, ctx, ldc, alpha, T, H, C, drop_threshold(drop_p), 1.f / (1.f - drop_p), seed);
+  hipLaunchKernelGGL(attn_context_kernel<float>, dim3(B), dim3(ATT_NT), (size_t)T * sizeof(float), (hipStream_t)stream,
+                     projH, projh, score, enc, ctx, ldc, alpha, T, H, C, drop_threshold(drop_p), 1.f / (1.f - drop_p),
+                     seed);
+  return (int)hipGetLastError();
+}
+
+int crnn_attn_context_bf16(const void* projH, const float* projh, const float* score, const void* enc, float* ctx,
+                           int ldc, float* alpha, int B, int T, int H, int C, float drop_p, unsigned long long seed,
+                           void* stream) {
+  if (T <= 0 || T > 4096) return crnn_set_error(hipErrorInvalidValue, "attn_context: T out of range");
+  if (!(drop_p >= 0.f && drop_p < 1.f)) return crnn_set_error(hipErrorInvalidValue, "attn_context: p not in [0, 1)");
+  hipLaunchKernelGGL(attn_context_kernel<bf16>, dim3(B), dim3(ATT_NT), (size_t)T * sizeof(float), (hipStream_t)stream,
+                     (const bf16*)projH, projh, score, (const bf16*)enc, ctx, ldc, alpha, T, H, C,
+                     drop_threshold(drop_p), 1.f / (1.f - drop_p), seed);
   return (int)hipGetLastError();
 }
 
@@ -387,9 +486,20 @@ int crnn_attn_bwd(const float* dctx, int lddc, const float* alpha, const float* 
                   int H, int C, float drop_p, unsigned long long seed, void* stream) {
   if (T <= 0 || T > 4096) return crnn_set_error(hipErrorInvalidValue, "attn_bwd: T out of range");
   if (!(drop_p >= 0.f && drop_p < 1.f)) return crnn_set_error(hipErrorInvalidValue, "attn_bwd: p not in [0, 1)");
-  hipLaunchKernelGGL(attn_step_bwd_kernel, dim3(B), dim3(ATT_NT), (size_t)2 * T * sizeof(float), (hipStream_t)stream,
-                     dctx, lddc, alpha, enc, projH, projh, score, de, dprojh, dscore_part, T, H, C,
+  hipLaunchKernelGGL(attn_step_bwd_kernel<float>, dim3(B), dim3(ATT_NT), (size_t)2 * T * sizeof(float),
+                     (hipStream_t)stream, dctx, lddc, alpha, enc, projH, projh, score, de, dprojh, dscore_part, T, H, C,
                      drop_threshold(drop_p), 1.f / (1.f - drop_p), seed);
+  return (int)hipGetLastError();
+}
+
+int crnn_attn_bwd_bf16(const float* dctx, int lddc, const float* alpha, const void* enc, const void* projH,
+                       const float* projh, const float* score, float* de, float* dprojh, float* dscore_part, int B,
+                       int T, int H, int C, float drop_p, unsigned long long seed, void* stream) {
+  if (T <= 0 || T > 4096) return crnn_set_error(hipErrorInvalidValue, "attn_bwd: T out of range");
+  if (!(drop_p >= 0.f && drop_p < 1.f)) return crnn_set_error(hipErrorInvalidValue, "attn_bwd: p not in [0, 1)");
+  hipLaunchKernelGGL(attn_step_bwd_kernel<bf16>, dim3(B), dim3(ATT_NT), (size_t)2 * T * sizeof(float),
+                     (hipStream_t)stream, dctx, lddc, alpha, (const bf16*)enc, (const bf16*)projH, projh, score, de,
+                     dprojh, dscore_part, T, H, C, drop_threshold(drop_p), 1.f / (1.f - drop_p), seed);
   return (int)hipGetLastError();
 }
 
@@ -406,8 +516,11 @@ int crnn_attn_denc(const float* dctx, int lddc, const float* alpha, int steps, i
 
 int crnn_attn_dproj_enc(const float* projh, const float* de, const float* projH, const float* score, int steps, int B,
                      int T, int H, float* dprojH, void* stream) {
-  hipLaunchKernelGGL(attn_dprojH_kernel, dim3(grid_for((long)B * T * H)), dim3(256), 0, (hipStream_t)stream, projh,
-                     de, projH, score, steps, B, T, H, dprojH);
+  const size_t lds = (size_t)steps * T * sizeof(float);
+  if (steps <= 0 || T <= 0 || lds > 64 * 1024)
+    return crnn_set_error(hipErrorInvalidValue, "attn_dproj_enc: steps * T exceeds the LDS stage");
+  hipLaunchKernelGGL(attn_dprojH_kernel, dim3(B, (H + 255) / 256), dim3(256), lds, (hipStream_t)stream, projh, de,
+                     projH, score, steps, B, T, H, dprojH);
   return (int)hipGetLastError();
 }
 
