@@ -503,6 +503,9 @@ int crnn_attn_denc(const float* dctx, int lddc, const float* alpha, int steps, i
  * (proj_h [steps][B][H], de [steps][B][T]; written) */
 int crnn_attn_dproj_enc(const float* projh, const float* de, const float* projH, const float* score, int steps, int B,
                      int T, int H, float* dprojH, void* stream);
+/* the same with proj_H stored as bf16 (pairs with crnn_attn_context_bf16) */
+int crnn_attn_dproj_enc_bf16(const float* projh, const float* de, const void* projH, const float* score, int steps,
+                             int B, int T, int H, float* dprojH, void* stream);
 /* teacher-forcing one-hot rows: X[t][b][col0 + text[b][t]] = 1 (rows [steps][B] of stride ldx,
  * zeroed by the caller; ids outside [0, V) leave the row zero) — the saved [context | h | onehot]
  * rows make dW_ih (both parts) and dW_hh one GEMM in the backward */

@@ -147,6 +147,7 @@ _SIGS = {
     "crnn_attn_bwd_bf16": ([vp, i32, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, f32, u64, vp], i32),
     "crnn_attn_denc": ([vp, i32, vp, i32, i32, i32, i32, f32, u64, vp, vp], i32),
     "crnn_attn_dproj_enc": ([vp, vp, vp, vp, i32, i32, i32, i32, vp, vp], i32),
+    "crnn_attn_dproj_enc_bf16": ([vp, vp, vp, vp, i32, i32, i32, i32, vp, vp], i32),
     "crnn_attn_onehot_rows": ([vp, i32, i32, i32, i32, vp, i32, i32, vp], i32),
     "crnn_attn_out": ([vp, i32, i32, i32, i32, vp, i32, vp, vp], i32),
     "crnn_preprocess": ([vp, vp, i32, i32, i32, i32, i32, vp, vp, i64, vp], i32),

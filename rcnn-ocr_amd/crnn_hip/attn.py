@@ -187,7 +187,11 @@ class AttnDecoderHIP:
         denc = torch.empty(B, T, C, device=dev)
         call("crnn_attn_denc", ptr(dX), C + H, ptr(As), steps, B, T, C, drop_p, seed & (2 ** 64 - 1), ptr(denc), s)
         dProjH = torch.empty(B * T, H, device=dev)
-        call("crnn_attn_dproj_enc", ptr(Ph), ptr(De), ptr(projH), ptr(self.score), steps, B, T, H, ptr(dProjH), s)
+        if mix:
+            call("crnn_attn_dproj_enc_bf16", ptr(Ph), ptr(De), ptr(sv["projHb"]), ptr(self.score), steps, B, T, H,
+                 ptr(dProjH), s)
+        else:
+            call("crnn_attn_dproj_enc", ptr(Ph), ptr(De), ptr(projH), ptr(self.score), steps, B, T, H, ptr(dProjH), s)
         # weight gradients, batched over steps
         # [dW_ih[:, :C] | dW_hh | dW_ih[:, C:]] in one GEMM over the saved [context | h | onehot] rows
         LX = C + H + Vp

@@ -304,10 +304,12 @@ __global__ __launch_bounds__(256) void attn_denc_kernel(const float* __restrict_
 }
 
 // block per (sample b, 256 k): the sample's de rows of every step staged in LDS; a thread holds proj_H[b, t', k]
-// for 32 t' in registers and loops over the steps (one proj_h load per step), summing in step order as before.
-// (The r05 form, a thread per (b, t', k) re-reading proj_h for every t', took 137 us at B = 256, T = 32.)
+// for 32 t' and proj_h[t][b][k] for 32 steps in registers (all loads issued before any tanh) and sums over the steps
+// in step order. (The r05 form, a thread per (b, t', k) re-reading proj_h for every t', took 137 us at B = 256,
+// T = 32.) TE = bf16: proj_H stored as bf16 and the exp / rcp tanh (the bf16 training pass).
+template <typename TE>
 __global__ __launch_bounds__(256) void attn_dprojH_kernel(const float* __restrict__ projh, const float* __restrict__ de,
-                                                          const float* __restrict__ projH,
+                                                          const TE* __restrict__ projH,
                                                           const float* __restrict__ score, int steps, int B, int T,
                                                           int H, float* __restrict__ dprojH) {
   extern __shared__ float sde[];  // [steps][T]
@@ -318,21 +320,25 @@ __global__ __launch_bounds__(256) void attn_dprojH_kernel(const float* __restric
   }
   __syncthreads();
   if (k >= H) return;
-  const int kc = min(k, H - 1);
   for (int t0 = 0; t0 < T; t0 += 32) {
     float u[32], acc[32];
 #pragma unroll
     for (int j = 0; j < 32; ++j) {
-      u[j] = projH[((size_t)b * T + min(t0 + j, T - 1)) * H + kc];
+      u[j] = ldf(projH + ((size_t)b * T + min(t0 + j, T - 1)) * H + k);
       acc[j] = 0.f;
     }
-    for (int t = 0; t < steps; ++t) {
-      const float p = projh[((size_t)t * B + b) * H + kc];
-      const float* d = sde + t * T + t0;
+    for (int s0 = 0; s0 < steps; s0 += 32) {
+      float p[32];
 #pragma unroll
-      for (int j = 0; j < 32; ++j) {
-        const float th = tanhf(u[j] + p);
-        acc[j] += (t0 + j < T ? d[j] : 0.f) * (1.f - th * th);
+      for (int q = 0; q < 32; ++q) p[q] = projh[((size_t)min(s0 + q, steps - 1) * B + b) * H + k];
+      const int ns = min(32, steps - s0);
+      for (int q = 0; q < ns; ++q) {
+        const float* d = sde + (s0 + q) * T + t0;
+#pragma unroll
+        for (int j = 0; j < 32; ++j) {
+          const float th = att_tanh<TE>(u[j] + p[q]);
+          acc[j] += (t0 + j < T ? d[j] : 0.f) * (1.f - th * th);
+        }
       }
     }
     const float sk = score[k];
@@ -519,8 +525,18 @@ int crnn_attn_dproj_enc(const float* projh, const float* de, const float* projH,
   const size_t lds = (size_t)steps * T * sizeof(float);
   if (steps <= 0 || T <= 0 || lds > 64 * 1024)
     return crnn_set_error(hipErrorInvalidValue, "attn_dproj_enc: steps * T exceeds the LDS stage");
-  hipLaunchKernelGGL(attn_dprojH_kernel, dim3(B, (H + 255) / 256), dim3(256), lds, (hipStream_t)stream, projh, de,
-                     projH, score, steps, B, T, H, dprojH);
+  hipLaunchKernelGGL(attn_dprojH_kernel<float>, dim3(B, (H + 255) / 256), dim3(256), lds, (hipStream_t)stream, projh,
+                     de, projH, score, steps, B, T, H, dprojH);
+  return (int)hipGetLastError();
+}
+
+int crnn_attn_dproj_enc_bf16(const float* projh, const float* de, const void* projH, const float* score, int steps,
+                             int B, int T, int H, float* dprojH, void* stream) {
+  const size_t lds = (size_t)steps * T * sizeof(float);
+  if (steps <= 0 || T <= 0 || lds > 64 * 1024)
+    return crnn_set_error(hipErrorInvalidValue, "attn_dproj_enc: steps * T exceeds the LDS stage");
+  hipLaunchKernelGGL(attn_dprojH_kernel<bf16>, dim3(B, (H + 255) / 256), dim3(256), lds, (hipStream_t)stream, projh,
+                     de, (const bf16*)projH, score, steps, B, T, H, dprojH);
   return (int)hipGetLastError();
 }
 
