@@ -643,6 +643,12 @@ __global__ __launch_bounds__(256) void lstm_seq_bwd_kernel(const bf16* __restric
   unsigned* mycnt = cnt + d * nbs + bs;
 
   if (stamps && threadIdx.x == 0) stamps[(size_t)blockIdx.x * Tn * 8 + 7] = __builtin_amdgcn_s_memrealtime();
+  // dgates payload: plain stores + the drained counter when the group is on one XCD (the
+  // consumers' sc1 loads then hit the shared L2), sc1 stores otherwise (seq_group_local). Checked
+  // BEFORE the prologue's loads: the check is a call, and a non-kernel function starts with a full
+  // s_waitcnt, which after the W_hh slice loads held every workgroup ~8 us (r06 stamps: 11 us from
+  // entry to step 0)
+  const bool l2_handoff = xtab && seq_group_local(xtab, (d * nbs + bs) * nsl, nsl, ns, err);
   const bool fin = w < NBLK;
   const int fi = fin ? w % MI : 0, fj = fin ? w / MI : 0;
   const int bl = 16 * fi + c, b = b0 + bl;
@@ -682,9 +688,6 @@ __global__ __launch_bounds__(256) void lstm_seq_bwd_kernel(const bf16* __restric
       }
   }
   const __amdgpu_buffer_rsrc_t rg = rsrc_of(dgates);
-  // dgates payload: plain stores + the drained counter when the group is on one XCD (the
-  // consumers' sc1 loads then hit the shared L2), sc1 stores otherwise (seq_group_local)
-  const bool l2_handoff = xtab && seq_group_local(xtab, (d * nbs + bs) * nsl, nsl, ns, err);
 
   for (int s = 0; s < Tn; ++s) {
     const int t = d == 0 ? Tn - 1 - s : s;
