@@ -360,6 +360,22 @@ def main():
                          if k in r}
             torch.cuda.empty_cache()
         out["sub_measurements"] = subs
+    if world > 1 and args.mode == "train" and args.config is None and not args.no_sub:
+        # BASELINE configs[4] in its own multi-GPU form (32x1024 crops, 4x768 BiLSTM, batch 64 per GPU, DP over the
+        # same ranks) as a sub-measurement of the N-rank line, so that the driver's scaling runs observe it. Every
+        # rank takes part (the timed region is collective); rank 0 attaches the result
+        import copy
+        a = copy.copy(args)
+        a.mode, a.config, a.steps, a.warmup = "train", "long", min(args.steps, 10), min(args.warmup, 3)
+        a.width, a.hidden, a.layers, a.batch = 1024, 768, 4, 64
+        torch.cuda.empty_cache()
+        t0 = time.perf_counter()
+        r = measure(a, world, rank, dev)
+        if rank == 0:
+            r["wall_s"] = round(time.perf_counter() - t0, 1)
+            out["sub_measurements"] = {"configs4_long_dp": {k: r[k] for k in (
+                "metric", "value", "unit", "n_gpus", "ms_per_step", "steps", "warmup", "dtype", "config", "roofline",
+                "roofline_lstm", "dp", "wall_s") if k in r}}
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

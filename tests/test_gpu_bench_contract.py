@@ -20,7 +20,7 @@ def _run(*args, env_extra=None):
     p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), *args], cwd=REPO, env=env,
                        capture_output=True, text=True, timeout=240)
     assert p.returncode == 0, p.stderr[-2000:]
-    lines = [l for l in p.stdout.splitlines() if l.strip().startswith("{")]
+    lines = [l for l in p.stdout.splitlines() if l.strip().startswith("{")]   # (gloo prints "[Gloo] ..." lines)
     assert len(lines) == 1, p.stdout[-2000:]
     return json.loads(lines[0])
 
@@ -72,3 +72,20 @@ def test_bench_gpus2_spawns_two_ranks():
     assert dp["buckets_per_step"] >= 2 and dp["allreduce_bytes_per_step"] > 0
     assert "cpu_baseline" not in d   # the CPU leg is rank 0 at N = 1 only
 
+
+
+def test_bench_gpus2_attaches_configs4_dp_line():
+    """An N-rank line also times BASELINE configs[4] in its multi-GPU form (32x1024 crops, 4x768 BiLSTM, batch 64
+    per GPU, DP over the same ranks) as sub_measurements.configs4_long_dp, so that the driver's scaling runs observe
+    it. One-device rehearsal as above (gloo, per-step BiLSTM launches), one timed step."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    env = {"CRNN_SHARE_DEVICE": "1", "CRNN_DIST_BACKEND": "gloo", "CRNN_LSTM_PER_STEP": "1"}
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        os.environ.pop(k, None)
+    d = _run("--gpus", "2", "--steps", "1", "--warmup", "1", "--batch", "16", env_extra=env)
+    s = d["sub_measurements"]["configs4_long_dp"]
+    assert s["n_gpus"] == 2 and s["config"]["parallelism"] == "dp2"
+    assert s["config"]["per_gpu_batch"] == 64 and s["config"]["global_batch"] == 128
+    assert s["config"]["crop"] == "32x1024" and s["config"]["hidden"] == 768 and s["config"]["rnn_layers"] == 4
+    assert s["value"] > 0 and s["dp"]["param_checksum_spread"] == 0.0
