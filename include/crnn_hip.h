@@ -477,6 +477,15 @@ int crnn_attn_context_bf16(const void* projH, const float* projh, const float* s
 int crnn_attn_cell(const float* gates, const float* b_ih, const float* b_hh, const float* w_ih, int ldw, const int* ch,
                    int ch_stride, float* h, float* c, float* hx, int ldx, float* hs, int ld_hs, float* gact, float* cs,
                    int B, int H, int C, void* stream);
+/* the gate GEMM and the cell in one launch: gates = X[B][C+H] W^T (+ b_ih + b_hh + the one-hot column) -> LSTMCell,
+ * with W [4H][C+H] (ldw), b_ih / b_hh [4H] and wv [V][4H] (wv[ch][r] = W_ih[r][C + ch]) in GATE-INTERLEAVED row order
+ * (row 4u + q = the reference's row q*H + u, q = i f g o); writes h, c, hx[b][C + j] (row stride ldhx; must not be X),
+ * hs (optional) and gact / cs (optional, the reference's gate-block order) as crnn_attn_cell does, bit for bit.
+ * dtype CRNN_F32 or CRNN_F32_BF16MMA (the GEMM of crnn_gemm_nt with that dtype) */
+int crnn_attn_gates_cell(int dtype, const float* X, int ldx, const float* W, int ldw, const float* b_ih,
+                         const float* b_hh, const float* wv, const int* ch, int ch_stride, float* h, float* c,
+                         float* hx, int ldhx, float* hs, int ld_hs, float* gact, float* cs, int B, int H, int C,
+                         void* stream);
 /* backward (teacher forcing; host loop in crnn_hip/attn.py): gact = the activated gates
  * (i f g o) and cs = c_t the forward saved (crnn_attn_cell's optional outputs), c_prev NULL at
  * t = 0; dh = dh1 + dh2 (row strides ld1, ld2; either NULL), dc NULL = 0 -> dgates

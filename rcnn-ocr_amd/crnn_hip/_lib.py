@@ -143,6 +143,8 @@ _SIGS = {
     "crnn_attn_context_bf16": ([vp, vp, vp, vp, vp, i32, vp, i32, i32, i32, i32, f32, u64, vp], i32),
     "crnn_attn_cell": ([vp, vp, vp, vp, i32, vp, i32, vp, vp, vp, i32, vp, i32, vp, vp, i32, i32, i32, vp], i32),
     "crnn_attn_cell_bwd": ([vp, vp, vp, vp, i32, vp, i32, vp, vp, vp, i32, i32, vp], i32),
+    "crnn_attn_gates_cell": ([i32, vp, i32, vp, i32, vp, vp, vp, vp, i32, vp, vp, vp, i32, vp, i32, vp, vp, i32, i32,
+                              i32, vp], i32),
     "crnn_attn_bwd": ([vp, i32, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, f32, u64, vp], i32),
     "crnn_attn_bwd_bf16": ([vp, i32, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, f32, u64, vp], i32),
     "crnn_attn_denc": ([vp, i32, vp, i32, i32, i32, i32, f32, u64, vp, vp], i32),

@@ -53,6 +53,13 @@ class AttnDecoderHIP:
         self.b_hh = f(pre + "rnn.bias_hh")
         w_hh = f(pre + "rnn.weight_hh")               # [4H, H]
         self.w_cat = torch.cat([self.w_ih[:, : self.C], w_hh], 1).contiguous()  # [4H, C + H]
+        # gate-interleaved copies for the fused gate GEMM + cell (crnn_attn_gates_cell): row 4u + q = row q*H + u
+        H = self.H
+        il = torch.arange(4 * H, device=self.device).view(4, H).t().reshape(-1)
+        self.w_cat_il = self.w_cat.index_select(0, il).contiguous()
+        self.b_ih_il = self.b_ih.index_select(0, il).contiguous()
+        self.b_hh_il = self.b_hh.index_select(0, il).contiguous()
+        self.wv_il = self.w_ih[:, self.C:].index_select(0, il).t().contiguous()   # [V][4H]
         gw, gb = f("generator.weight"), f("generator.bias")
         self.w_gen = torch.zeros(self.Vpad, self.H, device=self.device)
         self.w_gen[: self.V] = gw
@@ -110,7 +117,6 @@ class AttnDecoderHIP:
         hs = torch.empty(B, steps, H, device=dev)
         h = torch.zeros(B, H, device=dev)
         c = torch.zeros(B, H, device=dev)
-        gates = torch.empty(B, 4 * H, device=dev)
         for t in range(steps):
             self._gemm(h, H, self.w_h2h, H, Ph[t], H, self.b_h2h, B, H, H, self.tdt)
             if mix:
@@ -119,10 +125,10 @@ class AttnDecoderHIP:
             else:
                 call("crnn_attn_context", ptr(projH), ptr(Ph[t]), ptr(self.score), ptr(enc), ptr(Xs[t]), LX,
                      ptr(As[t]), B, T, H, C, drop_p, (seed + t) & (2 ** 64 - 1), s)
-            self._gemm(Xs[t], LX, self.w_cat, C + H, gates, 4 * H, None, B, 4 * H, C + H, self.tdt)
-            call("crnn_attn_cell", ptr(gates), ptr(self.b_ih), ptr(self.b_hh), ptr(self.w_ih), C + V, ptr(txt[:, t:]),
-                 txt.shape[1], ptr(h), ptr(c), ptr(Xs[t + 1]), LX, ptr(hs[:, t]), steps * H, ptr(Gs[t]), ptr(Cs[t]),
-                 B, H, C, s)
+            # gate GEMM + LSTM cell in one launch (gate-interleaved weights); h_t into the next step's X row
+            call("crnn_attn_gates_cell", self.tdt, ptr(Xs[t]), LX, ptr(self.w_cat_il), C + H, ptr(self.b_ih_il),
+                 ptr(self.b_hh_il), ptr(self.wv_il), ptr(txt[:, t:]), txt.shape[1], ptr(h), ptr(c), ptr(Xs[t + 1]), LX,
+                 ptr(hs[:, t]), steps * H, ptr(Gs[t]), ptr(Cs[t]), B, H, C, s)
         lg = torch.empty(B * steps, Vp, device=dev)
         self._gemm(hs, H, self.w_gen, H, lg, Vp, self.b_gen, B * steps, Vp, H, self.tdt)
         out = torch.empty(B, steps, V, device=dev)
@@ -240,15 +246,16 @@ class AttnDecoderHIP:
         self._gemm(enc, C, self.w_i2h, C, projH, H, None, B * T, H, C)
         h = torch.zeros(B, H, device=dev)
         c = torch.zeros(B, H, device=dev)
-        hx = torch.zeros(B, C + H, device=dev)           # [context | h] rows of the gates GEMM
+        # [context | h] rows of the gate GEMM, two buffers: step t reads hxs[t % 2] while its fused cell writes h_t
+        # into hxs[(t + 1) % 2]
+        hxs = torch.zeros(2, B, C + H, device=dev)
         projh = torch.empty(B, H, device=dev)
-        gates = torch.empty(B, 4 * H, device=dev)
         if text is None:
             ch = torch.full((B,), self.sos_id, dtype=torch.int32, device=dev)
             logits_t = torch.empty(B, Vp, device=dev)
             out = torch.empty(B, steps, V, device=dev)
             for t in range(steps):
-                self._step(enc, projH, h, c, hx, projh, gates, ch, 1, None, 0, B, T)
+                self._step(enc, projH, h, c, hxs[t % 2], hxs[(t + 1) % 2], projh, ch, 1, None, 0, B, T)
                 self._gemm(h, H, self.w_gen, H, logits_t, Vp, self.b_gen, B, Vp, H)
                 call("crnn_attn_out", ptr(logits_t), Vp, B, V, self.blank, ptr(out[:, t]), steps * V, ptr(ch), s)
             return out
@@ -257,7 +264,8 @@ class AttnDecoderHIP:
             raise ValueError("text needs batch_max_length + 1 columns")
         hs = torch.empty(B, steps, H, device=dev)
         for t in range(steps):
-            self._step(enc, projH, h, c, hx, projh, gates, txt[:, t:], txt.shape[1], hs[:, t], steps * H, B, T)
+            self._step(enc, projH, h, c, hxs[t % 2], hxs[(t + 1) % 2], projh, txt[:, t:], txt.shape[1], hs[:, t],
+                       steps * H, B, T)
         lg = torch.empty(B * steps, Vp, device=dev)
         self._gemm(hs, H, self.w_gen, H, lg, Vp, self.b_gen, B * steps, Vp, H)
         out = torch.empty(B, steps, V, device=dev)
@@ -265,14 +273,14 @@ class AttnDecoderHIP:
         call("crnn_attn_out", ptr(lg), Vp, B * steps, V, self.blank, ptr(out), V, ptr(scratch), s)
         return out
 
-    def _step(self, enc, projH, h, c, hx, projh, gates, ch, ch_stride, hs, ld_hs, B, T):
+    def _step(self, enc, projH, h, c, hx, hx_next, projh, ch, ch_stride, hs, ld_hs, B, T):
         H, C, s = self.H, self.C, L.stream_ptr()
         self._gemm(h, H, self.w_h2h, H, projh, H, self.b_h2h, B, H, H)
         call("crnn_attn_context", ptr(projH), ptr(projh), ptr(self.score), ptr(enc), ptr(hx), C + H, None,
              B, T, H, C, 0.0, 0, s)
-        self._gemm(hx, C + H, self.w_cat, C + H, gates, 4 * H, None, B, 4 * H, C + H)
-        call("crnn_attn_cell", ptr(gates), ptr(self.b_ih), ptr(self.b_hh), ptr(self.w_ih), C + self.V, ptr(ch),
-             ch_stride, ptr(h), ptr(c), ptr(hx), C + H, ptr(hs), ld_hs, None, None, B, H, C, s)
+        call("crnn_attn_gates_cell", L.F32, ptr(hx), C + H, ptr(self.w_cat_il), C + H, ptr(self.b_ih_il),
+             ptr(self.b_hh_il), ptr(self.wv_il), ptr(ch), ch_stride, ptr(h), ptr(c), ptr(hx_next), C + H, ptr(hs),
+             ld_hs, None, None, B, H, C, s)
 
 
 class _XentFn(torch.autograd.Function):

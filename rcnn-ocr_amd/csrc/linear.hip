@@ -205,6 +205,59 @@ int gemm_tn_mix(const void* A, int lda, const void* B, int ldb, float* C, int ld
   return launch<bf16, 32, 32>(la, lb, ep, M, N, K, splits, st);
 }
 
+// ---- the attention decoder's gate GEMM with its LSTM cell in the epilogue (crnn_attn_gates_cell)
+// W rows gate-interleaved (row 4u + q = the reference's row q*H + u, q = i f g o): the MFMA epilogue hands a lane 4
+// consecutive columns of one row, i.e. the four gates of one unit of one sample, and the cell runs right there. The
+// arithmetic is attn.hip attn_cell_kernel's, in the same order, so the fused step equals GEMM + cell bit for bit.
+struct AttnCellEpi {
+  static constexpr bool kStats = false;
+  const float *b_ih, *b_hh;   // [4H] interleaved
+  const float* wv;            // [V][4H] interleaved one-hot columns of W_ih
+  const int* ch;
+  int ch_stride;
+  float *h, *c, *hx;
+  int ldx;
+  float* hs;
+  int ld_hs;
+  float *gact, *cs;
+  int B, H, C;
+  __device__ __forceinline__ void store(int m, int n, f32x4 v, int) const {
+    if (m >= B || n >= 4 * H) return;
+    const int u = n >> 2;
+    const float* wr = wv + (size_t)ch[(size_t)m * ch_stride] * 4 * H + n;
+    float g[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) g[q] = v[q] + b_ih[n + q] + b_hh[n + q] + wr[q];
+    const float ig = 1.f / (1.f + expf(-g[0])), fg = 1.f / (1.f + expf(-g[1])), gg = tanhf(g[2]),
+                og = 1.f / (1.f + expf(-g[3]));
+    const size_t e = (size_t)m * H + u;
+    const float cn = fg * c[e] + ig * gg;
+    const float hn = og * tanhf(cn);
+    c[e] = cn;
+    h[e] = hn;
+    hx[(size_t)m * ldx + C + u] = hn;
+    if (hs) hs[(size_t)m * ld_hs + u] = hn;
+    if (gact) {   // saved for the backward in the reference's gate-block order
+      float* gr = gact + (size_t)m * 4 * H;
+      gr[u] = ig;
+      gr[H + u] = fg;
+      gr[2 * H + u] = gg;
+      gr[3 * H + u] = og;
+      cs[e] = cn;
+    }
+  }
+  __device__ __forceinline__ void stats(int, int, f32x4, f32x4) const {}
+};
+
+// the tile plans of crnn_gemm_nt (run / run_mix) with another epilogue
+template <typename T, class LA, class LB, class EPI>
+int run_plain(const LA& la, const LB& lb, const EPI& ep, int M, int N, int K, hipStream_t st) {
+  const long work = (long)M * N;
+  if (M >= 128 && N >= 128 && work >= 128L * 128 * 128) return launch<T, 128, 128>(la, lb, ep, M, N, K, 1, st);
+  if (work >= 64L * 64 * 128) return launch<T, 64, 64>(la, lb, ep, M, N, K, 1, st);
+  return launch<T, 32, 32>(la, lb, ep, M, N, K, 1, st);
+}
+
 // split-K partials of C = A^T B into fp32 slabs [S][M][N] (deterministic; fp32 atomics from every
 // split are several times slower on this chip), then one fixed-order reduce into C (ldc, +=)
 struct TnSlabEpi {
@@ -361,6 +414,28 @@ int crnn_gemm_tn_slab(const void* A, int lda, const void* B, int ldb, float* C, 
   if (blocks > 2048) blocks = 2048;
   hipLaunchKernelGGL(tn_reduce_kernel, dim3(blocks), dim3(256), 0, st, ws, S, M, N, C, ldc, accumulate);
   return (int)hipGetLastError();
+}
+
+int crnn_attn_gates_cell(int dtype, const float* X, int ldx, const float* W, int ldw, const float* b_ih,
+                         const float* b_hh, const float* wv, const int* ch, int ch_stride, float* h, float* c,
+                         float* hx, int ldhx, float* hs, int ld_hs, float* gact, float* cs, int B, int H, int C,
+                         void* stream) {
+  const int K = C + H;
+  if (K % 8 || ldx % 8 || ldw % 8) return crnn_set_error(hipErrorInvalidValue, "attn_gates_cell: K/ld must be multiples of 8");
+  if (hx == X) return crnn_set_error(hipErrorInvalidValue, "attn_gates_cell: hx must not alias X (read by the GEMM)");
+  hipStream_t st = (hipStream_t)stream;
+  const AttnCellEpi ep{b_ih, b_hh, wv, ch, ch_stride, h, c, hx, ldhx, hs, ld_hs, gact, cs, B, H, C};
+  const int M = B, N = 4 * H;
+  if (dtype == CRNN_F32_BF16MMA) {   // crnn_gemm_nt's run_mix plan
+    Bf16Of<RowMajorK<float>> la{RowMajorK<float>{X, ldx, M, K}};
+    Bf16Of<RowMajorK<float>> lb{RowMajorK<float>{W, ldw, N, K}};
+    const long t64 = (long)((M + 63) / 64) * ((N + 63) / 64);
+    if (t64 >= 2 * crnn_cu_count() || K < 512) return run_plain<bf16>(la, lb, ep, M, N, K, st);
+    return launch<bf16, 32, 32, 128>(la, lb, ep, M, N, K, 1, st);
+  }
+  RowMajorK<float> la{X, ldx, M, K};
+  RowMajorK<float> lb{W, ldw, N, K};
+  return run_plain<float>(la, lb, ep, M, N, K, st);
 }
 
 }  // extern "C"
