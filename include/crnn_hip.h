@@ -109,7 +109,11 @@ enum { CRNN_OPT_GEMM_STAGGER = 0,    /* 256-row conv GEMM: waves 4-7 one barrier
                                         the MFMA layout */
        CRNN_OPT_HALO_WG2 = 22,       /* the stem input conv's weight gradient (halo kernel, streaming): 1 = one workgroup
                                         per band (two per CU, one slab each; default), 0 = min(bands, CUs) workgroups */
-       CRNN_OPT_COUNT = 23 };
+       CRNN_OPT_WGRAD_SLAB_BF16 = 23, /* bf16 conv weight gradients on the GEMM kernels: 1 (default) = split-K
+                                        partial slabs stored as bf16 (half the slab bytes written and re-read by
+                                        the reduce; each partial rounded once, fp32 sum), 0 = fp32 slabs. fp32
+                                        convs and the halo stem kernels always use fp32 slabs */
+       CRNN_OPT_COUNT = 24 };
 int crnn_set_option(int key, int value);
 /* current value of a tuning switch (0 for an unknown key) */
 int crnn_get_option(int key);

@@ -49,7 +49,7 @@ class PackJob(C.Structure):  # crnn_pack_job
 (OPT_GEMM_STAGGER, OPT_GEMM_PERSISTENT, OPT_DEEP_LINEAR, OPT_WGRAD_TILE, OPT_LSTM_TILE, OPT_HALO_CONV, OPT_LSTM_HANDOFF,
  OPT_WGRAD_REDUCE, OPT_WGRAD_FAST, OPT_ROW_CLASS, OPT_QUANT_TILE, OPT_PAD_SKIP, OPT_LSTM_BWD_PART,
  OPT_LSTM_L2_HANDOFF, OPT_GEMM4W, OPT_DIAG, OPT_DGRAD_GROUP, OPT_FIN_TICKET,
- OPT_CONV_HALO_W, OPT_LSTM_PIPE, OPT_LINEAR_ROW8, OPT_HALO_ROW16, OPT_HALO_WG2) = range(23)
+ OPT_CONV_HALO_W, OPT_LSTM_PIPE, OPT_LINEAR_ROW8, OPT_HALO_ROW16, OPT_HALO_WG2, OPT_WGRAD_SLAB_BF16) = range(24)
 
 PACK_CONV, PACK_ROWS, PACK_ROWS_SUM, PACK_TRANSPOSE, PACK_CONV_T = 0, 1, 2, 3, 4
 

@@ -14,7 +14,7 @@ int crnn_set_error(int code, const char* msg) {
 extern "C" int crnn_version(void) { return 100; }
 
 // tuning switches (A/B in one process); defaults are the measured-best settings
-static int g_opts[CRNN_OPT_COUNT] = {1, 0, 1, 0, 0, 1, 3, 1, 1, 1, 1, 1, 0, 1, 2, 0, 2, 0, 1, 0, 1, 1, 1};
+static int g_opts[CRNN_OPT_COUNT] = {1, 0, 1, 0, 0, 1, 3, 1, 1, 1, 1, 1, 0, 1, 2, 0, 2, 0, 1, 0, 1, 1, 1, 1};
 
 int crnn_cu_count() {
   static int n = -1;

@@ -650,11 +650,13 @@ template <typename T> struct DgradBnEpi {
 struct SlabEpi {
   static constexpr bool kStats = false;
   static constexpr int kPrefer4W = 2;
-  float* ws;  // [nsplit][Mrows][N]
-  int M, N;
+  float* ws;  // [nsplit][Mrows][N], fp32 or (bf != 0, CRNN_OPT_WGRAD_SLAB_BF16) bf16
+  int M, N, bf;
   __device__ __forceinline__ void store(int m, int n, f32x4 v, int kz) const {
     if (m >= M || n >= N) return;
-    *reinterpret_cast<f32x4*>(ws + ((size_t)kz * M + m) * N + n) = v;
+    const size_t o = ((size_t)kz * M + m) * N + n;
+    if (bf) st4<bf16>(reinterpret_cast<bf16*>(ws) + o, v);
+    else *reinterpret_cast<f32x4*>(ws + o) = v;
   }
   __device__ __forceinline__ void stats(int, int, f32x4, f32x4) const {}
 };
@@ -662,6 +664,13 @@ struct SlabEpi {
 // sum split-K slabs [S][Co][KH*KW*Cip] and scatter into an OIHW fp32 gradient. A thread owns 4
 // consecutive k' (one tap, 4 channels: Cip % 8 == 0) of one output row: 16-B slab loads, 8 slabs
 // in flight per batch (the loop is otherwise latency-bound), fixed summation order.
+// slab element loads: 4 consecutive fp32, or 4 bf16 (CRNN_OPT_WGRAD_SLAB_BF16) widened
+template <bool BF> __device__ __forceinline__ f32x4 slab4(const float* ws, size_t o) {
+  if constexpr (BF) return ld4f<bf16>(reinterpret_cast<const bf16*>(ws) + o);
+  else return *reinterpret_cast<const f32x4*>(ws + o);
+}
+
+template <bool BF>
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ ws, int S,
                                                            float* __restrict__ dw, int Co, int Ci, int Cip, int KH,
                                                            int KW, float beta) {
@@ -674,11 +683,11 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
     for (; z + 8 <= S; z += 8) {
       f32x4 v[8];
 #pragma unroll
-      for (int q = 0; q < 8; ++q) v[q] = *reinterpret_cast<const f32x4*>(ws + (size_t)(z + q) * total + i);
+      for (int q = 0; q < 8; ++q) v[q] = slab4<BF>(ws, (size_t)(z + q) * total + i);
 #pragma unroll
       for (int q = 0; q < 8; ++q) s += v[q];
     }
-    for (; z < S; ++z) s += *reinterpret_cast<const f32x4*>(ws + (size_t)z * total + i);
+    for (; z < S; ++z) s += slab4<BF>(ws, (size_t)z * total + i);
     const int co = (int)(i / Kp), k = (int)(i - (long)co * Kp);
     const int tap = k / Cip, ci = k - tap * Cip;
     const int kh = tap / KW, kw = tap - kh * KW;
@@ -696,6 +705,7 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
 // when the tile is narrow), partial sums transposed through LDS (pitch cc + 1: taps of one channel
 // on different banks), then the OIHW rows [ci][kh][kw] of the chunk written contiguously. The
 // flat kernel's 4-B stores land KH*KW floats apart; here every store is a coalesced run.
+template <bool BF>
 __global__ __launch_bounds__(256) void wgrad_reduce_tiled_kernel(const float* __restrict__ ws, int S,
                                                                  float* __restrict__ dw, int Ci, int Cip, int T,
                                                                  float beta) {
@@ -708,17 +718,17 @@ __global__ __launch_bounds__(256) void wgrad_reduce_tiled_kernel(const float* __
   const int t = threadIdx.x, g = t / nv, v = t - g * nv;
   if (g < G) {
     const int tap = v / cv, c = 4 * (v - tap * cv);
-    const float* src = ws + (long)co * Kp + (long)tap * Cip + c0 + c;
+    const size_t src = (size_t)co * Kp + (size_t)tap * Cip + c0 + c;
     f32x4 s = {0.f, 0.f, 0.f, 0.f};
     int z = g;
     for (; z + 7 * G < S; z += 8 * G) {
       f32x4 r[8];
 #pragma unroll
-      for (int q = 0; q < 8; ++q) r[q] = *reinterpret_cast<const f32x4*>(src + (size_t)(z + q * G) * total);
+      for (int q = 0; q < 8; ++q) r[q] = slab4<BF>(ws, src + (size_t)(z + q * G) * total);
 #pragma unroll
       for (int q = 0; q < 8; ++q) s += r[q];
     }
-    for (; z < S; z += G) s += *reinterpret_cast<const f32x4*>(src + (size_t)z * total);
+    for (; z < S; z += G) s += slab4<BF>(ws, src + (size_t)z * total);
     float* d = red + (g * T + tap) * P + c;
 #pragma unroll
     for (int e = 0; e < 4; ++e) d[e] = s[e];
@@ -1100,6 +1110,14 @@ int conv_dgrad_tw_launch(const crnn_conv_desc* d, const void* dy, const void* wt
   return launch_fwd256(g, la, lb, ep, M, N, K, bn, st, true);
 }
 
+// bf16 partial slabs (CRNN_OPT_WGRAD_SLAB_BF16, default on): only for bf16 operands on the GEMM forms (the
+// halo stem kernels write their own fp32 slabs; fp32 convs keep fp32 slabs). Each partial is rounded to bf16
+// once and the reduce sums in fp32: about one bf16 rounding of the gradient, as a bf16 weight gradient under
+// the reference's AMP has, for half the slab bytes written and re-read.
+template <typename T> bool wgrad_slab_bf16(int bm) {
+  return sizeof(T) == 2 && bm != 0 && crnn_option(CRNN_OPT_WGRAD_SLAB_BF16) != 0;
+}
+
 // phases: bit 0 = the split-K GEMM into the fp32 slabs, bit 1 = the slab reduce into the OIHW gradient
 // (crnn_conv_wgrad_gemm / _reduce run them apart, so the reduce can go to another stream)
 template <typename T> int conv_wgrad_t(const crnn_conv_desc* d, const void* dy, const void* x, float* dw,
@@ -1117,7 +1135,7 @@ template <typename T> int conv_wgrad_t(const crnn_conv_desc* d, const void* dy, 
   } else {
   WgradA<T> la{(const T*)dy, g.Co, Mp, nbytes((long)Mp * g.Co, sizeof(T))};
   WgradB<T> lb{(const T*)x, g, Kp, Mp, nbytes((long)g.B * g.Hi * g.Wi * g.Ci, sizeof(T))};
-  SlabEpi ep{ws, g.Co, Kp};
+  SlabEpi ep{ws, g.Co, Kp, wgrad_slab_bf16<T>(bm) ? 1 : 0};
   if (crnn_option(CRNN_OPT_DIAG) & 1) ep.M = 0;   // diagnostic: no slab stores
   if constexpr (sizeof(T) == 2) {
     const int fk = bm == 256 ? wgrad_fast_kind(g) : 0;
@@ -1141,15 +1159,24 @@ template <typename T> int conv_wgrad_t(const crnn_conv_desc* d, const void* dy, 
   if (rc || !(phases & 2)) return rc;
   int ci_real = d->Ci_real > 0 ? d->Ci_real : g.Ci;
   long total = (long)g.Co * Kp;
+  const bool bfr = wgrad_slab_bf16<T>(bm);   // as the GEMM phase wrote them
   if (crnn_option(CRNN_OPT_WGRAD_REDUCE) != 0 && g.KH * g.KW <= 16 && g.Ci % 8 == 0) {
-    hipLaunchKernelGGL(wgrad_reduce_tiled_kernel, dim3(g.Co * ((g.Ci + 63) / 64)), dim3(256), 0, st, ws, splits,
-                       dw, ci_real, g.Ci, g.KH * g.KW, beta);
+    if (bfr)
+      hipLaunchKernelGGL(wgrad_reduce_tiled_kernel<true>, dim3(g.Co * ((g.Ci + 63) / 64)), dim3(256), 0, st, ws,
+                         splits, dw, ci_real, g.Ci, g.KH * g.KW, beta);
+    else
+      hipLaunchKernelGGL(wgrad_reduce_tiled_kernel<false>, dim3(g.Co * ((g.Ci + 63) / 64)), dim3(256), 0, st, ws,
+                         splits, dw, ci_real, g.Ci, g.KH * g.KW, beta);
     return (int)hipGetLastError();
   }
   int blocks = (int)((total / 4 + 255) / 256);
   if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, ws, splits, dw, g.Co, ci_real,
-                     g.Ci, g.KH, g.KW, beta);
+  if (bfr)
+    hipLaunchKernelGGL(wgrad_reduce_kernel<true>, dim3(blocks), dim3(256), 0, st, ws, splits, dw, g.Co, ci_real,
+                       g.Ci, g.KH, g.KW, beta);
+  else
+    hipLaunchKernelGGL(wgrad_reduce_kernel<false>, dim3(blocks), dim3(256), 0, st, ws, splits, dw, g.Co, ci_real,
+                       g.Ci, g.KH, g.KW, beta);
   return (int)hipGetLastError();
 }
 

@@ -290,6 +290,19 @@ def test_conv_fwd_dgrad_wgrad(cfg, dtype):
     finally:
         L.call("crnn_set_option", L.OPT_WGRAD_REDUCE, 1)
     assert relerr(dw_flat.cpu(), dw.cpu()) < 1e-6
+    # bf16 partial slabs (CRNN_OPT_WGRAD_SLAB_BF16, default for bf16) vs fp32 slabs: one bf16 rounding apart
+    # (fp32 operands always keep fp32 slabs: bit-identical)
+    dw_f32s = torch.empty_like(dw)
+    try:
+        L.call("crnn_set_option", L.OPT_WGRAD_SLAB_BF16, 0)
+        L.call("crnn_conv_wgrad", dt, d, dyd.data_ptr(), xd.data_ptr(), dw_f32s.data_ptr(), ws.data_ptr(), need, 0.0, st)
+    finally:
+        L.call("crnn_set_option", L.OPT_WGRAD_SLAB_BF16, 1)
+    if dtype == torch.float32:
+        assert torch.equal(dw_f32s, dw)
+    else:
+        assert relerr(dw_f32s.cpu(), dw.cpu()) < 4e-3
+        assert relerr(dw_f32s.cpu(), wr.grad) < 1e-2
     # the per-tile pixel decode of 64-aligned tiles (CRNN_OPT_WGRAD_FAST, default) vs the per-lane
     # decode: the same bytes in the same order, so bit-identical
     dw_gen = torch.empty_like(dw)
@@ -389,6 +402,7 @@ def test_conv_halo_vs_gemm():
     out = {}
     for opt in (1, 0):
         L.call("crnn_set_option", L.OPT_HALO_CONV, opt)
+        L.call("crnn_set_option", L.OPT_WGRAD_SLAB_BF16, 0)   # fp32 slabs on the GEMM leg: same sums both ways
         try:
             rows = L.lib().crnn_conv_stat_rows(dt, d)
             rpp = L.lib().crnn_conv_stat_rows_per_partial(dt, d)
@@ -410,6 +424,16 @@ def test_conv_halo_vs_gemm():
             out[opt] = (y.float(), mean, var, dx.float(), rows, rpp, dw.clone())
         finally:
             L.call("crnn_set_option", L.OPT_HALO_CONV, 1)
+            L.call("crnn_set_option", L.OPT_WGRAD_SLAB_BF16, 1)
+    # the GEMM leg with its default bf16 partial slabs: about one bf16 rounding from the fp32-slab sums
+    L.call("crnn_set_option", L.OPT_HALO_CONV, 0)
+    try:
+        dwb = torch.full((Co, Ci, 3, 3), 0.25, device=DEV)
+        L.call("crnn_conv_wgrad", dt, d, dy.data_ptr(), x.data_ptr(), dwb.data_ptr(), wsb.data_ptr(), need, 1.0, st)
+        torch.cuda.synchronize()
+    finally:
+        L.call("crnn_set_option", L.OPT_HALO_CONV, 1)
+    assert relerr(dwb, out[0][6]) < 4e-3
     (y1, m1, v1, dx1, r1, p1, w1), (y0, m0, v0, dx0, r0, p0, w0) = out[1], out[0]
     assert r1 * p1 == r0 * p0 == B * H * W
     assert float((y1 - y0).abs().max()) <= 2 ** -7 * float(y0.abs().max())
