@@ -7,7 +7,13 @@ emulation of the same job: the same batches dealt to the two "ranks", each step'
 accumulated in one process and applied as their mean. BN keeps per-shard batch statistics in both, so
 the emulation is the DP step's definition: measured |dp - emulation| / |update| = 1.5e-10 after two
 epochs (profiles/r04o_dp.log). The emulation also keeps one copy of the BN running statistics per rank and
-averages them at each epoch end, as sync_bn_stats does; rank 0's checkpoint must hold that average. Reference: training/train.py:179-235, :493-518."""
+averages them at each epoch end, as sync_bn_stats does; rank 0's checkpoint must hold that average. Reference: training/train.py:179-235, :493-518.
+
+Both sides run the conv weight gradients with fp32 split-K slabs (CRNN_OPT_WGRAD_SLAB_BF16 = 0): the default
+bf16 slabs round each partial once, which turns the all-reduce's last-ulp differences from the emulation's
+in-place accumulation (the 1.5e-10 above) into bf16-ulp jumps of whole partials, measured 2.8e-4 after two
+epochs (r06f6). The bf16-slab kernel itself is pinned by tests/test_gpu_kernels.py (one-rounding bound,
+accumulate mode)."""
 import json
 import os
 import socket
@@ -51,6 +57,8 @@ def _worker(rank, world, port, cfg_path, q):
     for sub in ("../rcnn-ocr_amd", "../oracle"):
         sys.path.insert(0, os.path.join(here, sub))
     try:
+        from crnn_hip import _lib as L
+        L.call("crnn_set_option", L.OPT_WGRAD_SLAB_BF16, 0)
         from training.train import Config, run_training
         out = run_training(Config(cfg_path), device="cuda")
         q.put((rank, out, None))
@@ -150,7 +158,12 @@ def test_run_training_world2_matches_single_process_emulation(tmp_path):
     assert len(spreads) == 2 and all(s == 0.0 for s in spreads), spreads
     # rank 0's weights vs the single-process emulation of the same DP job
     cfg = Config(str(cfg_path))
-    p0, model = _emulate(cfg, 2)
+    from crnn_hip import _lib as L
+    L.call("crnn_set_option", L.OPT_WGRAD_SLAB_BF16, 0)
+    try:
+        p0, model = _emulate(cfg, 2)
+    finally:
+        L.call("crnn_set_option", L.OPT_WGRAD_SLAB_BF16, 1)
     sd = torch.load(os.path.join(exp, "last_weights.pth"), map_location="cpu", weights_only=True)
     dp = torch.cat([sd[k].float().reshape(-1) for k, _ in model.named_parameters()])
     em = model._flat_param.detach().float().cpu()
